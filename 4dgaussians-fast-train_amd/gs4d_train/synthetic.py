@@ -1,0 +1,63 @@
+"""Seeded synthetic scenes of BASELINE.md §2 / SURVEY.md §8(d).
+
+One generator serves the parity tests, the fixtures, smoke() and bench.py, so every leg sees the
+same bytes for a given (P, W, H, seed).  Draw order is fixed: z, x, y, scales, rotations,
+opacities, SH DC, SH rest; the upstream image gradient uses its own generator (seed + 1).
+"""
+import math
+
+import numpy as np
+
+from .camera import Camera
+
+SH_C0 = 0.28209479177387814
+
+# name -> (P, W, H): the BASELINE.json configs that the rasterizer benchmark/parity tests use
+CONFIGS = {
+    "c1_plumbing": (20_000, 400, 400),
+    "c2_800": (100_000, 800, 800),
+    "metric": (100_000, 1352, 1014),
+    "c4_per_view": (300_000, 1352, 1014),
+    "c5_broom": (1_000_000, 960, 536),
+}
+
+
+def make_camera(W, H, fovx_deg=60.0, R=None, T=None, time=0.0):
+    fovx = math.radians(fovx_deg)
+    fovy = 2.0 * math.atan(math.tan(fovx / 2.0) * H / W)
+    R = np.eye(3) if R is None else R
+    T = np.zeros(3) if T is None else T
+    return Camera(R, T, fovx, fovy, W, H, time=time)
+
+
+def make_scene(P, W, H, seed=0, sh_degree=3, z_range=(2.0, 10.0), spread=1.1, log_scale=math.log(0.02),
+               log_scale_sigma=0.5):
+    """Return a dict of float32 numpy arrays + camera settings for one view."""
+    cam = make_camera(W, H)
+    rng = np.random.default_rng(seed)
+    tx, ty = cam.tanfovx, cam.tanfovy
+    z = rng.uniform(z_range[0], z_range[1], P)
+    x = rng.uniform(-spread, spread, P) * z * tx
+    y = rng.uniform(-spread, spread, P) * z * ty
+    means3D = np.stack([x, y, z], 1).astype(np.float32)
+    scales = np.exp(rng.normal(log_scale, log_scale_sigma, (P, 3))).astype(np.float32)
+    q = rng.normal(0, 1, (P, 4))
+    rotations = (q / np.linalg.norm(q, axis=1, keepdims=True)).astype(np.float32)
+    opacities = (1.0 / (1.0 + np.exp(-rng.normal(0, 1, (P, 1))))).astype(np.float32)
+    K = (sh_degree + 1) ** 2
+    shs = np.zeros((P, 16 if sh_degree <= 3 else K, 3), np.float32)
+    shs[:, 0, :] = (rng.uniform(0, 1, (P, 3)) - 0.5) / SH_C0
+    shs[:, 1:, :] = rng.normal(0, 0.1, (P, shs.shape[1] - 1, 3))
+    return dict(
+        means3D=means3D, scales=scales, rotations=rotations, opacities=opacities, shs=shs.astype(np.float32),
+        bg=np.ones(3, np.float32), viewmatrix=cam.world_view_transform.numpy().astype(np.float32),
+        projmatrix=cam.full_proj_transform.numpy().astype(np.float32),
+        campos=cam.camera_center.numpy().astype(np.float32), tanfovx=cam.tanfovx, tanfovy=cam.tanfovy,
+        W=W, H=H, sh_degree=sh_degree, scale_modifier=1.0, camera=cam)
+
+
+def make_upstream_grad(color, seed=1):
+    """L1 gradient of train.py:244 against a uniform-random ground truth: sign(color-gt)/(3HW)."""
+    C, H, W = color.shape
+    gt = np.random.default_rng(seed).uniform(0, 1, (C, H, W)).astype(np.float32)
+    return (np.sign(color - gt) / (C * H * W)).astype(np.float32), gt

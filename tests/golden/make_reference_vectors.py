@@ -1,0 +1,76 @@
+"""Generate golden vectors by RUNNING the reference's own importable Python (this container only).
+
+The reference's CUDA rasterizer cannot be built here (no nvcc/CUB), so the parts of
+the path that exist as runnable reference Python pin the oracle:
+  * utils/sh_utils.py:57-112  eval_sh          -> SH -> RGB (forward.cu:20-71 restates the same
+                                                   polynomial; the rasterizer adds +0.5 and clamps)
+  * utils/graphics_utils.py:38-71 getWorld2View2 / getProjectionMatrix, composed as
+    scene/cameras.py:61-66 does  -> viewmatrix / projmatrix / campos handed to the rasterizer.
+
+Usage (from the repo root, in the build container where /root/reference exists):
+    python tests/golden/make_reference_vectors.py
+Writes tests/golden/ref_sh_vectors.npz and tests/golden/ref_camera_vectors.npz (inputs + outputs).
+"""
+import math
+import os
+import sys
+
+import numpy as np
+import torch
+
+REF = "/root/reference"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def main():
+    sys.path.insert(0, REF)
+    from utils.sh_utils import eval_sh  # noqa: E402  (reference code, run as-is)
+    from utils.graphics_utils import getWorld2View2, getProjectionMatrix  # noqa: E402
+
+    rng = np.random.default_rng(1234)
+    # --- SH vectors: means/campos -> dir; sh (P,16,3) in the rasterizer's layout -------------
+    P = 512
+    means = rng.normal(0, 3, (P, 3)).astype(np.float32)
+    campos = rng.normal(0, 1, 3).astype(np.float32)
+    shs = rng.normal(0, 0.5, (P, 16, 3)).astype(np.float32)
+    rgb = {}
+    for deg in range(4):
+        d = torch.from_numpy(means) - torch.from_numpy(campos)
+        d = d / d.norm(dim=1, keepdim=True)
+        # gaussian_renderer/__init__.py:106-110 layout: (P, 3, K)
+        sh_view = torch.from_numpy(shs).transpose(1, 2).contiguous()
+        val = eval_sh(deg, sh_view, d)
+        rgb[f"deg{deg}"] = torch.clamp_min(val + 0.5, 0.0).numpy().astype(np.float32)
+        rgb[f"raw{deg}"] = val.numpy().astype(np.float32)
+    np.savez_compressed(os.path.join(OUT, "ref_sh_vectors.npz"), means=means, campos=campos, shs=shs, **rgb)
+
+    # --- camera vectors ---------------------------------------------------------------------
+    cams = []
+    for i in range(6):
+        W, H = [(400, 400), (800, 800), (1352, 1014), (960, 536), (97, 61), (1352, 1014)][i]
+        fovx = math.radians([60, 50, 60, 70, 45, 30][i])
+        fovy = 2 * math.atan(math.tan(fovx / 2) * H / W)
+        q = rng.normal(0, 1, 4)
+        q /= np.linalg.norm(q)
+        r, x, y, z = q
+        R = np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - r * z), 2 * (x * z + r * y)],
+                      [2 * (x * y + r * z), 1 - 2 * (x * x + z * z), 2 * (y * z - r * x)],
+                      [2 * (x * z - r * y), 2 * (y * z + r * x), 1 - 2 * (x * x + y * y)]])
+        if i == 0:
+            R = np.eye(3)
+        T = rng.normal(0, 2, 3) if i else np.zeros(3)
+        # scene/cameras.py:61-66
+        wv = torch.tensor(getWorld2View2(R, T, np.array([0.0, 0.0, 0.0]), 1.0)).transpose(0, 1)
+        pr = getProjectionMatrix(znear=0.01, zfar=100.0, fovX=fovx, fovY=fovy).transpose(0, 1)
+        full = wv.unsqueeze(0).bmm(pr.unsqueeze(0)).squeeze(0)
+        center = wv.inverse()[3, :3]
+        cams.append(dict(R=R, T=T, fovx=fovx, fovy=fovy, W=W, H=H, view=wv.numpy(), proj=full.numpy(),
+                         center=center.numpy()))
+    np.savez_compressed(os.path.join(OUT, "ref_camera_vectors.npz"),
+                        **{f"{k}_{i}": np.asarray(v) for i, c in enumerate(cams) for k, v in c.items()},
+                        n=np.array(len(cams)))
+    print("wrote ref_sh_vectors.npz, ref_camera_vectors.npz")
+
+
+if __name__ == "__main__":
+    main()
