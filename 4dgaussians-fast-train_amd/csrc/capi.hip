@@ -1,0 +1,309 @@
+// capi.hip -- the extern "C" boundary of libgs4d (include/gs4d.h) and the forward/backward
+// orchestration that replaces CudaRasterizer::Rasterizer (rasterizer_impl.cu:141-437).
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/gs4d.h"
+#include "gs4d_internal.h"
+
+namespace gs4d {
+
+static thread_local std::string g_last_error;
+static thread_local bool g_profiling = false;
+static thread_local std::vector<std::pair<const char *, hipEvent_t>> g_marks;
+static thread_local std::vector<std::pair<const char *, float>> g_timings;
+
+static int fail(int code, const std::string &msg) {
+    g_last_error = msg;
+    return code;
+}
+
+#define GS4D_HIP(expr)                                                                                                  \
+    do {                                                                                                               \
+        hipError_t e_ = (expr);                                                                                        \
+        if (e_ != hipSuccess)                                                                                          \
+            return fail(GS4D_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));                               \
+    } while (0)
+
+// Debug mode = the reference's CHECK_CUDA (auxiliary.h:166-173): synchronise after every stage.
+#define GS4D_STAGE(name, expr)                                                                                          \
+    do {                                                                                                               \
+        GS4D_HIP(expr);                                                                                                \
+        if (debug) {                                                                                                   \
+            hipError_t e_ = hipStreamSynchronize(stream);                                                              \
+            if (e_ != hipSuccess)                                                                                      \
+                return fail(GS4D_ERR_HIP, std::string("[HIP ERROR] in stage ") + name + ": " + hipGetErrorString(e_)); \
+        }                                                                                                              \
+        mark(name, stream);                                                                                            \
+    } while (0)
+
+static void mark(const char *name, hipStream_t s) {
+    if (!g_profiling) return;
+    hipEvent_t ev;
+    if (hipEventCreate(&ev) != hipSuccess) return;
+    hipEventRecord(ev, s);
+    g_marks.emplace_back(name, ev);
+}
+static void begin_marks(hipStream_t s) {
+    for (auto &m : g_marks) hipEventDestroy(m.second);
+    g_marks.clear();
+    mark("begin", s);
+}
+static void end_marks() {
+    if (!g_profiling || g_marks.empty()) return;
+    hipEventSynchronize(g_marks.back().second);
+    g_timings.clear();
+    for (size_t i = 1; i < g_marks.size(); i++) {
+        float ms = 0.f;
+        hipEventElapsedTime(&ms, g_marks[i - 1].second, g_marks[i].second);
+        g_timings.emplace_back(g_marks[i].first, ms);
+    }
+    for (auto &m : g_marks) hipEventDestroy(m.second);
+    g_marks.clear();
+}
+
+static char *carve(char *&p, size_t bytes) {
+    char *r = p;
+    p += align_up(bytes, 256);
+    return r;
+}
+
+size_t GeomState::required(int P) {
+    const size_t nb = (size_t)(P + kPreprocessBlock - 1) / kPreprocessBlock + 1;
+    return align_up(4 * (size_t)P, 256) * 2 + align_up(8 * (size_t)P, 256) + align_up(16 * (size_t)P, 256) * 2 +
+           align_up(24 * (size_t)P, 256) + align_up((size_t)P, 256) + align_up(4 * (size_t)P, 256) * 2 +
+           align_up(4 * nb, 256) + 256;
+}
+GeomState GeomState::carve(char *base, int P) {
+    char *p = (char *)align_up((size_t)base, 256);
+    const size_t nb = (size_t)(P + kPreprocessBlock - 1) / kPreprocessBlock + 1;
+    GeomState g;
+    g.depths = (float *)gs4d::carve(p, 4 * (size_t)P);
+    g.radii = (int *)gs4d::carve(p, 4 * (size_t)P);
+    g.xy = (float2 *)gs4d::carve(p, 8 * (size_t)P);
+    g.conic_opacity = (float4 *)gs4d::carve(p, 16 * (size_t)P);
+    g.rgbd = (float4 *)gs4d::carve(p, 16 * (size_t)P);
+    g.cov3D = (float *)gs4d::carve(p, 24 * (size_t)P);
+    g.clamped = (uint8_t *)gs4d::carve(p, (size_t)P);
+    g.tiles_touched = (uint32_t *)gs4d::carve(p, 4 * (size_t)P);
+    g.point_offsets = (uint32_t *)gs4d::carve(p, 4 * (size_t)P);
+    g.block_sums = (uint32_t *)gs4d::carve(p, 4 * nb);
+    return g;
+}
+
+size_t ImageState::required(int W, int H) {
+    const size_t N = (size_t)W * H;
+    const size_t T = (size_t)((W + kBlockX - 1) / kBlockX) * ((H + kBlockY - 1) / kBlockY);
+    return align_up(4 * N, 256) * 2 + align_up(8 * T, 256) + 256;
+}
+ImageState ImageState::carve(char *base, int W, int H) {
+    char *p = (char *)align_up((size_t)base, 256);
+    const size_t N = (size_t)W * H;
+    const size_t T = (size_t)((W + kBlockX - 1) / kBlockX) * ((H + kBlockY - 1) / kBlockY);
+    ImageState s;
+    s.final_T = (float *)gs4d::carve(p, 4 * N);
+    s.n_contrib = (uint32_t *)gs4d::carve(p, 4 * N);
+    s.ranges = (uint2 *)gs4d::carve(p, 8 * T);
+    return s;
+}
+
+size_t BinningState::required(int L) {
+    const size_t nb = (size_t)(L + kSortBlockItems - 1) / kSortBlockItems;
+    return align_up(8 * (size_t)L, 256) * 2 + align_up(4 * (size_t)L, 256) * 4 + align_up(4 * 256 * nb, 256) + 256;
+}
+BinningState BinningState::carve(char *base, int L) {
+    char *p = (char *)align_up((size_t)base, 256);
+    const size_t nb = (size_t)(L + kSortBlockItems - 1) / kSortBlockItems;
+    BinningState b;
+    b.keys[0] = (uint64_t *)gs4d::carve(p, 8 * (size_t)L);
+    b.keys[1] = (uint64_t *)gs4d::carve(p, 8 * (size_t)L);
+    b.vals[0] = (uint32_t *)gs4d::carve(p, 4 * (size_t)L);
+    b.vals[1] = (uint32_t *)gs4d::carve(p, 4 * (size_t)L);
+    b.gid_by_upos = (uint32_t *)gs4d::carve(p, 4 * (size_t)L);
+    b.point_list = (uint32_t *)gs4d::carve(p, 4 * (size_t)L);
+    b.sorted_upos = nullptr;
+    b.hist = (uint32_t *)gs4d::carve(p, 4 * 256 * nb);
+    return b;
+}
+
+// rasterizer_impl.cu:35-50
+static uint32_t higher_msb(uint32_t n) {
+    uint32_t msb = sizeof(n) * 4;
+    uint32_t step = msb;
+    while (step > 1) {
+        step /= 2;
+        if (n >> msb) msb += step; else msb -= step;
+    }
+    if (n >> msb) msb++;
+    return msb;
+}
+static int sort_bits(int T) { return 32 + (int)higher_msb((uint32_t)T); }
+// buffer index that holds the sorted result: one swap per 8-bit pass
+static int sorted_buffer(int T) { return ((sort_bits(T) + 7) / 8) & 1; }
+
+static Args make_args(int P, int D, int M, int W, int H, const float *bg, float scale_modifier, const float *view,
+                      const float *proj, const float *campos, float tan_fovx, float tan_fovy, int prefiltered) {
+    Args a;
+    memset(&a, 0, sizeof(a));
+    a.P = P; a.D = D; a.M = M; a.W = W; a.H = H;
+    a.gx = (W + kBlockX - 1) / kBlockX;
+    a.gy = (H + kBlockY - 1) / kBlockY;
+    a.scale_modifier = scale_modifier;
+    a.tan_fovx = tan_fovx;
+    a.tan_fovy = tan_fovy;
+    a.focal_y = H / (2.0f * tan_fovy);  // rasterizer_impl.cu:223-224
+    a.focal_x = W / (2.0f * tan_fovx);
+    a.viewmatrix = view;
+    a.projmatrix = proj;
+    a.campos = campos;
+    a.bg = bg;
+    a.prefiltered = prefiltered;
+    return a;
+}
+
+}  // namespace gs4d
+
+using namespace gs4d;
+
+extern "C" {
+
+const char *gs4d_last_error(void) { return g_last_error.c_str(); }
+const char *gs4d_version(void) { return "gs4d 0.1.0 gfx950"; }
+void gs4d_set_profiling(int enabled) { g_profiling = enabled != 0; }
+int gs4d_last_timings(const char **names, float *ms, int max_entries) {
+    int n = (int)g_timings.size();
+    for (int i = 0; i < n && i < max_entries; i++) {
+        if (names) names[i] = g_timings[i].first;
+        if (ms) ms[i] = g_timings[i].second;
+    }
+    return n;
+}
+
+int gs4d_mark_visible(int P, const float *means3D, const float *viewmatrix, const float *projmatrix,
+                      uint8_t *present, void *stream_) {
+    hipStream_t stream = (hipStream_t)stream_;
+    if (P < 0 || (P > 0 && (!means3D || !viewmatrix || !present))) return fail(GS4D_ERR_ARG, "mark_visible: bad args");
+    if (P == 0) return GS4D_OK;
+    GS4D_HIP(launch_mark_visible(P, means3D, viewmatrix, present, stream));
+    return GS4D_OK;
+}
+
+int gs4d_forward(gs4d_alloc_fn geometry_alloc, void *geometry_ctx, gs4d_alloc_fn binning_alloc, void *binning_ctx,
+                 gs4d_alloc_fn image_alloc, void *image_ctx, int P, int D, int M, const float *background, int width,
+                 int height, const float *means3D, const float *shs, const float *colors_precomp,
+                 const float *opacities, const float *scales, float scale_modifier, const float *rotations,
+                 const float *cov3D_precomp, const float *viewmatrix, const float *projmatrix, const float *cam_pos,
+                 float tan_fovx, float tan_fovy, int prefiltered, float *out_color, float *out_depth, int *radii,
+                 int debug, void *stream_, int *num_rendered) {
+    hipStream_t stream = (hipStream_t)stream_;
+    *num_rendered = 0;
+    if (P < 0 || width <= 0 || height <= 0) return fail(GS4D_ERR_ARG, "forward: P must be >= 0 and the image non-empty");
+    if (P == 0) return GS4D_OK;
+    if (!means3D || !opacities || !viewmatrix || !projmatrix || !background || !out_color || !out_depth)
+        return fail(GS4D_ERR_ARG, "forward: missing required input");
+    if (!colors_precomp && (!shs || !cam_pos))
+        return fail(GS4D_ERR_ARG, "forward: provide either SHs (+campos) or precomputed colors");
+    if (!colors_precomp && (D < 0 || D > 3 || (D + 1) * (D + 1) > M))
+        return fail(GS4D_ERR_ARG, "forward: SH degree must be in [0,3] with (D+1)^2 <= M coefficients");
+    if (!cov3D_precomp && (!scales || !rotations))
+        return fail(GS4D_ERR_ARG, "forward: provide either scales+rotations or precomputed 3D covariances");
+    if (((size_t)rotations & 15) != 0 && rotations) return fail(GS4D_ERR_ARG, "forward: rotations must be 16-byte aligned");
+
+    Args a = make_args(P, D, M, width, height, background, scale_modifier, viewmatrix, projmatrix, cam_pos, tan_fovx,
+                       tan_fovy, prefiltered);
+    begin_marks(stream);
+
+    char *gbuf = geometry_alloc(geometry_ctx, GeomState::required(P) + 16);
+    if (!gbuf) return fail(GS4D_ERR_ALLOC, "forward: geometry buffer allocation failed");
+    GeomState g = GeomState::carve(gbuf, P);
+    char *ibuf = image_alloc(image_ctx, ImageState::required(width, height));
+    if (!ibuf) return fail(GS4D_ERR_ALLOC, "forward: image buffer allocation failed");
+    ImageState img = ImageState::carve(ibuf, width, height);
+    int *radii_ptr = radii ? radii : g.radii;
+
+    // the prefiltered error flag lives in the (zeroed) first word of ranges until binning starts
+    int *flag = (int *)img.ranges;
+    if (prefiltered) GS4D_HIP(hipMemsetAsync(flag, 0, sizeof(int), stream));
+
+    GS4D_STAGE("preprocess", launch_preprocess(a, means3D, scales, rotations, opacities, shs, cov3D_precomp,
+                                               colors_precomp, radii_ptr, g, flag, stream));
+    GS4D_STAGE("scan", launch_scan_blocks(P, g, stream));
+
+    // H1: the single device->host synchronisation of the forward (rasterizer_impl.cu:282)
+    static thread_local uint32_t *pinned = nullptr;
+    if (!pinned) GS4D_HIP(hipHostMalloc((void **)&pinned, 16, hipHostMallocDefault));
+    const int nblk = (P + kPreprocessBlock - 1) / kPreprocessBlock;
+    GS4D_HIP(hipMemcpyAsync(pinned, g.block_sums + nblk, 4, hipMemcpyDeviceToHost, stream));
+    if (prefiltered) GS4D_HIP(hipMemcpyAsync(pinned + 1, flag, 4, hipMemcpyDeviceToHost, stream));
+    GS4D_HIP(hipStreamSynchronize(stream));
+    if (prefiltered && pinned[1] != 0)
+        return fail(GS4D_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
+    const uint32_t L32 = pinned[0];
+    if (L32 > 0x7fffffffu) return fail(GS4D_ERR_ARG, "forward: more than 2^31 tile instances");
+    const int L = (int)L32;
+    *num_rendered = L;
+
+    char *bbuf = binning_alloc(binning_ctx, BinningState::required(L));
+    if (!bbuf) return fail(GS4D_ERR_ALLOC, "forward: binning buffer allocation failed");
+    BinningState b = BinningState::carve(bbuf, L);
+    const int T = a.gx * a.gy;
+    int buf = 0;
+    if (L > 0) {
+        GS4D_STAGE("duplicate", launch_duplicate(a, g, radii_ptr, b, stream));
+        GS4D_STAGE("sort", launch_radix_sort(b, L, sort_bits(T), &buf, stream));
+    }
+    GS4D_STAGE("tile_ranges", launch_tile_ranges(b, L, buf, img, T, stream));
+    GS4D_STAGE("render", launch_render_forward(a, g, b, img, out_color, out_depth, stream));
+    end_marks();
+    return GS4D_OK;
+}
+
+int gs4d_backward(int P, int D, int M, int R, const float *background, int width, int height, const float *means3D,
+                  const float *shs, const float *colors_precomp, const float *scales, float scale_modifier,
+                  const float *rotations, const float *cov3D_precomp, const float *viewmatrix,
+                  const float *projmatrix, const float *campos, float tan_fovx, float tan_fovy, const int *radii,
+                  char *geom_buffer, char *binning_buffer, char *image_buffer, const float *dL_dpix,
+                  float *dL_dmean2D, float *dL_dconic, float *dL_dopacity, float *dL_dcolor, float *dL_dmean3D,
+                  float *dL_dcov3D, float *dL_dsh, float *dL_dscale, float *dL_drot, gs4d_alloc_fn scratch_alloc,
+                  void *scratch_ctx, int debug, void *stream_) {
+    hipStream_t stream = (hipStream_t)stream_;
+    if (P < 0 || R < 0) return fail(GS4D_ERR_ARG, "backward: bad sizes");
+    if (P == 0) return GS4D_OK;
+    if (!geom_buffer || !image_buffer || (R > 0 && !binning_buffer) || !dL_dpix || !means3D)
+        return fail(GS4D_ERR_ARG, "backward: missing buffers");
+    if (shs && (D < 0 || D > 3 || (D + 1) * (D + 1) > M))
+        return fail(GS4D_ERR_ARG, "backward: SH degree must be in [0,3] with (D+1)^2 <= M coefficients");
+    if (rotations && ((size_t)rotations & 15) != 0) return fail(GS4D_ERR_ARG, "backward: rotations must be 16-byte aligned");
+    if (((size_t)dL_drot & 15) != 0) return fail(GS4D_ERR_ARG, "backward: dL_drot must be 16-byte aligned");
+    if (!viewmatrix || !projmatrix || !background || (shs && !campos))
+        return fail(GS4D_ERR_ARG, "backward: missing camera inputs");
+    Args a = make_args(P, D, M, width, height, background, scale_modifier, viewmatrix, projmatrix, campos, tan_fovx,
+                       tan_fovy, 0);
+    begin_marks(stream);
+    GeomState g = GeomState::carve(geom_buffer, P);
+    ImageState img = ImageState::carve(image_buffer, width, height);
+    const int *radii_ptr = radii ? radii : g.radii;
+    const int T = a.gx * a.gy;
+    float *contrib = nullptr;
+    if (R > 0) {
+        BinningState b = BinningState::carve(binning_buffer, R);
+        const uint32_t *sorted_upos = b.vals[sorted_buffer(T)];
+        contrib = (float *)scratch_alloc(scratch_ctx, (size_t)R * kContribStride * sizeof(float));
+        if (!contrib) return fail(GS4D_ERR_ALLOC, "backward: scratch allocation failed");
+        const float *color_ptr = colors_precomp;  // NULL -> the forward's rgb (rasterizer_impl.cu:392)
+        GS4D_STAGE("render_backward", launch_render_backward(a, g, b.point_list, sorted_upos, img, color_ptr, dL_dpix,
+                                                             contrib, stream));
+    }
+    const float *cov3D_ptr = cov3D_precomp ? cov3D_precomp : g.cov3D;  // rasterizer_impl.cu:414
+    GS4D_STAGE("preprocess_backward",
+               launch_preprocess_backward(a, g, radii_ptr, contrib, means3D, shs, scales, rotations, cov3D_ptr,
+                                          dL_dmean2D, dL_dconic, dL_dopacity, dL_dcolor, dL_dmean3D, dL_dcov3D,
+                                          dL_dsh, dL_dscale, dL_drot, stream));
+    end_marks();
+    return GS4D_OK;
+}
+
+}  // extern "C"

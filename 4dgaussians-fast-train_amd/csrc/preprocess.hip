@@ -1,0 +1,165 @@
+// preprocess.hip -- per-Gaussian forward preprocess (K1), markVisible (K10) and the block-offset scan
+// that replaces cub::DeviceScan::InclusiveSum (K2).
+//
+// Reference: cuda_rasterizer/forward.cu:155-256 (preprocessCUDA), auxiliary.h:139-164 (in_frustum),
+// rasterizer_impl.cu:54-66 (checkFrustum), rasterizer_impl.cu:278-282 (scan + num_rendered).
+#include "gs4d_internal.h"
+
+namespace gs4d {
+
+// One thread per Gaussian.  Besides the reference's outputs it produces the per-workgroup sum of
+// tiles_touched (block_sums), so that the prefix sum needs only one more single-workgroup pass.
+__global__ __launch_bounds__(kPreprocessBlock) void preprocess_kernel(
+    Args a, const float *__restrict__ means3D, const float *__restrict__ scales, const float *__restrict__ rotations,
+    const float *__restrict__ opacities, const float *__restrict__ shs, const float *__restrict__ cov3D_precomp,
+    const float *__restrict__ colors_precomp, int *__restrict__ radii, GeomState g, int *__restrict__ err_flag) {
+    __shared__ uint32_t s_wave[kPreprocessBlock / 64];
+    const int idx = blockIdx.x * kPreprocessBlock + threadIdx.x;
+    const Mat4 view = load_mat4(a.viewmatrix), proj = load_mat4(a.projmatrix);
+    uint32_t touched = 0;
+    if (idx < a.P) {
+        int my_r = 0;
+        V3 p_orig = v3(means3D[3 * idx], means3D[3 * idx + 1], means3D[3 * idx + 2]);
+        // in_frustum (auxiliary.h:146-154): only the near plane culls
+        V3 p_view = transformPoint4x3(p_orig, view);
+        bool ok = !(p_view.z <= 0.2f);
+        if (!ok && a.prefiltered) atomicOr(err_flag, 1);
+        float cov3[6];
+        float3 cov;
+        float det = 0.f;
+        if (ok) {
+            float4 p_hom = transformPoint4x4(p_orig, proj);
+            float p_w = 1.0f / (p_hom.w + 0.0000001f);
+            float p_proj_x = p_hom.x * p_w, p_proj_y = p_hom.y * p_w;
+            if (cov3D_precomp != nullptr) {
+#pragma unroll
+                for (int i = 0; i < 6; i++) cov3[i] = cov3D_precomp[6 * (size_t)idx + i];
+            } else {
+                V3 sc = v3(scales[3 * idx], scales[3 * idx + 1], scales[3 * idx + 2]);
+                float4 rot = reinterpret_cast<const float4 *>(rotations)[idx];
+                computeCov3D(sc, a.scale_modifier, rot, cov3);
+#pragma unroll
+                for (int i = 0; i < 6; i++) g.cov3D[6 * (size_t)idx + i] = cov3[i];
+            }
+            cov = computeCov2D(p_orig, a.focal_x, a.focal_y, a.tan_fovx, a.tan_fovy, cov3, view);
+            det = (cov.x * cov.z - cov.y * cov.y);
+            ok = det != 0.0f;
+            if (ok) {
+                float det_inv = 1.f / det;
+                float3 conic = make_float3(cov.z * det_inv, -cov.y * det_inv, cov.x * det_inv);
+                float mid = 0.5f * (cov.x + cov.z);
+                float lambda1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
+                float lambda2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
+                float my_radius = ceilf(3.f * sqrtf(fmaxf(lambda1, lambda2)));
+                float2 point_image = make_float2(ndc2Pix(p_proj_x, a.W), ndc2Pix(p_proj_y, a.H));
+                int x0, y0, x1, y1;
+                getRect(point_image.x, point_image.y, (int)my_radius, a.gx, a.gy, x0, y0, x1, y1);
+                uint32_t area = (uint32_t)((y1 - y0) * (x1 - x0));
+                if (area != 0) {
+                    float3 rgb;
+                    uint8_t cl = 0;
+                    if (colors_precomp == nullptr) {
+                        const float *sh = shs + (size_t)idx * a.M * 3;
+                        V3 dir = p_orig - load_v3(a.campos);
+                        float len = sqrtf(dot(dir, dir));
+                        dir = v3(dir.x / len, dir.y / len, dir.z / len);
+                        V3 res = sh_eval(a.D, sh, dir);
+                        cl = (uint8_t)((res.x < 0) | ((res.y < 0) << 1) | ((res.z < 0) << 2));
+                        rgb = make_float3(fmaxf(res.x, 0.0f), fmaxf(res.y, 0.0f), fmaxf(res.z, 0.0f));
+                    } else {
+                        rgb = make_float3(colors_precomp[3 * idx], colors_precomp[3 * idx + 1],
+                                          colors_precomp[3 * idx + 2]);
+                    }
+                    g.clamped[idx] = cl;
+                    g.depths[idx] = p_view.z;
+                    g.xy[idx] = point_image;
+                    g.conic_opacity[idx] = make_float4(conic.x, conic.y, conic.z, opacities[idx]);
+                    g.rgbd[idx] = make_float4(rgb.x, rgb.y, rgb.z, p_view.z);
+                    my_r = (int)my_radius;
+                    touched = area;
+                }
+            }
+        }
+        radii[idx] = my_r;
+        g.tiles_touched[idx] = touched;
+    }
+    // workgroup sum of tiles_touched
+    uint32_t v = touched;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    if ((threadIdx.x & 63) == 0) s_wave[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+#pragma unroll
+        for (int w = 0; w < kPreprocessBlock / 64; w++) t += s_wave[w];
+        g.block_sums[blockIdx.x] = t;
+    }
+}
+
+hipError_t launch_preprocess(const Args &a, const float *means3D, const float *scales, const float *rotations,
+                             const float *opacities, const float *shs, const float *cov3D_precomp,
+                             const float *colors_precomp, int *radii, GeomState g, int *err_flag, hipStream_t s) {
+    const int nblk = (a.P + kPreprocessBlock - 1) / kPreprocessBlock;
+    hipLaunchKernelGGL(preprocess_kernel, dim3(nblk), dim3(kPreprocessBlock), 0, s, a, means3D, scales, rotations,
+                       opacities, shs, cov3D_precomp, colors_precomp, radii, g, err_flag);
+    return hipGetLastError();
+}
+
+// Exclusive scan of the per-workgroup sums in place; block_sums[nblk] receives the total (L).
+// One workgroup of 1024 threads; each thread scans a contiguous chunk serially.
+__global__ __launch_bounds__(1024) void scan_blocks_kernel(uint32_t *__restrict__ sums, int n) {
+    __shared__ uint32_t s_tot[1024 / 64];
+    const int tid = threadIdx.x;
+    const int chunk = (n + 1023) / 1024;
+    const int b = tid * chunk, e = min(n, b + chunk);
+    uint32_t local = 0;
+    for (int i = b; i < e; i++) local += sums[i];
+    // inclusive wave scan
+    const int lane = tid & 63;
+    uint32_t x = local;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        uint32_t y = __shfl_up(x, off);
+        if (lane >= off) x += y;
+    }
+    if (lane == 63) s_tot[tid >> 6] = x;
+    __syncthreads();
+    uint32_t wave_base = 0;
+    for (int w = 0; w < (tid >> 6); w++) wave_base += s_tot[w];
+    uint32_t run = wave_base + x - local;  // exclusive prefix of this thread's chunk
+    for (int i = b; i < e; i++) {
+        uint32_t v = sums[i];
+        sums[i] = run;
+        run += v;
+    }
+    if (tid == 1023) {
+        uint32_t tot = 0;
+        for (int w = 0; w < 1024 / 64; w++) tot += s_tot[w];
+        sums[n] = tot;
+    }
+}
+
+hipError_t launch_scan_blocks(int P, GeomState g, hipStream_t s) {
+    const int nblk = (P + kPreprocessBlock - 1) / kPreprocessBlock;
+    hipLaunchKernelGGL(scan_blocks_kernel, dim3(1), dim3(1024), 0, s, g.block_sums, nblk);
+    return hipGetLastError();
+}
+
+// rasterizer_impl.cu:54-66 checkFrustum
+__global__ void mark_visible_kernel(int P, const float *__restrict__ means3D, const float *__restrict__ viewmatrix,
+                                    uint8_t *__restrict__ present) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= P) return;
+    const Mat4 view = load_mat4(viewmatrix);
+    V3 p = v3(means3D[3 * idx], means3D[3 * idx + 1], means3D[3 * idx + 2]);
+    V3 pv = transformPoint4x3(p, view);
+    present[idx] = !(pv.z <= 0.2f);
+}
+
+hipError_t launch_mark_visible(int P, const float *means3D, const float *viewmatrix, uint8_t *present, hipStream_t s) {
+    hipLaunchKernelGGL(mark_visible_kernel, dim3((P + 255) / 256), dim3(256), 0, s, P, means3D, viewmatrix, present);
+    return hipGetLastError();
+}
+
+}  // namespace gs4d
