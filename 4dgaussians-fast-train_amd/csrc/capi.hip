@@ -71,34 +71,32 @@ static char *carve(char *&p, size_t bytes) {
     return r;
 }
 
-size_t GeomState::required(int P) {
-    const size_t nb = (size_t)(P + kPreprocessBlock - 1) / kPreprocessBlock + 1;
-    return align_up(4 * (size_t)P, 256) * 2 + align_up(8 * (size_t)P, 256) + align_up(16 * (size_t)P, 256) * 2 +
-           align_up(24 * (size_t)P, 256) + align_up((size_t)P, 256) + align_up(4 * (size_t)P, 256) * 2 +
-           align_up(4 * nb, 256) + 256;
-}
+// Sizes are computed by carving from a null base, so required() and carve() cannot disagree.
+size_t GeomState::required(int P) { return (size_t)carve(nullptr, P).sort_scratch + 4 * radix_scratch_words(P) + 512; }
 GeomState GeomState::carve(char *base, int P) {
     char *p = (char *)align_up((size_t)base, 256);
-    const size_t nb = (size_t)(P + kPreprocessBlock - 1) / kPreprocessBlock + 1;
+    const size_t n = (size_t)P, nb = (n + kPreprocessBlock - 1) / kPreprocessBlock + 1;
     GeomState g;
-    g.depths = (float *)gs4d::carve(p, 4 * (size_t)P);
-    g.radii = (int *)gs4d::carve(p, 4 * (size_t)P);
-    g.xy = (float2 *)gs4d::carve(p, 8 * (size_t)P);
-    g.conic_opacity = (float4 *)gs4d::carve(p, 16 * (size_t)P);
-    g.rgbd = (float4 *)gs4d::carve(p, 16 * (size_t)P);
-    g.cov3D = (float *)gs4d::carve(p, 24 * (size_t)P);
-    g.clamped = (uint8_t *)gs4d::carve(p, (size_t)P);
-    g.tiles_touched = (uint32_t *)gs4d::carve(p, 4 * (size_t)P);
-    g.point_offsets = (uint32_t *)gs4d::carve(p, 4 * (size_t)P);
+    g.depths = (float *)gs4d::carve(p, 4 * n);
+    g.radii = (int *)gs4d::carve(p, 4 * n);
+    g.xy = (float2 *)gs4d::carve(p, 8 * n);
+    g.conic_opacity = (float4 *)gs4d::carve(p, 16 * n);
+    g.rgbd = (float4 *)gs4d::carve(p, 16 * n);
+    g.cov3D = (float *)gs4d::carve(p, 24 * n);
+    g.clamped = (uint8_t *)gs4d::carve(p, n);
+    g.tiles_touched = (uint32_t *)gs4d::carve(p, 4 * n);
+    g.point_offsets = (uint32_t *)gs4d::carve(p, 4 * n);
     g.block_sums = (uint32_t *)gs4d::carve(p, 4 * nb);
+    g.dkeys[0] = (uint32_t *)gs4d::carve(p, 4 * n);
+    g.dkeys[1] = (uint32_t *)gs4d::carve(p, 4 * n);
+    g.dvals[0] = (uint32_t *)gs4d::carve(p, 4 * n);
+    g.dvals[1] = (uint32_t *)gs4d::carve(p, 4 * n);
+    g.rank = (uint32_t *)gs4d::carve(p, 4 * n);
+    g.sort_scratch = (uint32_t *)gs4d::carve(p, 4 * radix_scratch_words(P));
     return g;
 }
 
-size_t ImageState::required(int W, int H) {
-    const size_t N = (size_t)W * H;
-    const size_t T = (size_t)((W + kBlockX - 1) / kBlockX) * ((H + kBlockY - 1) / kBlockY);
-    return align_up(4 * N, 256) * 2 + align_up(8 * T, 256) + 256;
-}
+size_t ImageState::required(int W, int H) { return (size_t)carve(nullptr, W, H).ranges + 8 * (size_t)((W + 15) / 16) * ((H + 15) / 16) + 512; }
 ImageState ImageState::carve(char *base, int W, int H) {
     char *p = (char *)align_up((size_t)base, 256);
     const size_t N = (size_t)W * H;
@@ -108,25 +106,6 @@ ImageState ImageState::carve(char *base, int W, int H) {
     s.n_contrib = (uint32_t *)gs4d::carve(p, 4 * N);
     s.ranges = (uint2 *)gs4d::carve(p, 8 * T);
     return s;
-}
-
-size_t BinningState::required(int L) {
-    const size_t nb = (size_t)(L + kSortBlockItems - 1) / kSortBlockItems;
-    return align_up(8 * (size_t)L, 256) * 2 + align_up(4 * (size_t)L, 256) * 4 + align_up(4 * 256 * nb, 256) + 256;
-}
-BinningState BinningState::carve(char *base, int L) {
-    char *p = (char *)align_up((size_t)base, 256);
-    const size_t nb = (size_t)(L + kSortBlockItems - 1) / kSortBlockItems;
-    BinningState b;
-    b.keys[0] = (uint64_t *)gs4d::carve(p, 8 * (size_t)L);
-    b.keys[1] = (uint64_t *)gs4d::carve(p, 8 * (size_t)L);
-    b.vals[0] = (uint32_t *)gs4d::carve(p, 4 * (size_t)L);
-    b.vals[1] = (uint32_t *)gs4d::carve(p, 4 * (size_t)L);
-    b.gid_by_upos = (uint32_t *)gs4d::carve(p, 4 * (size_t)L);
-    b.point_list = (uint32_t *)gs4d::carve(p, 4 * (size_t)L);
-    b.sorted_upos = nullptr;
-    b.hist = (uint32_t *)gs4d::carve(p, 4 * 256 * nb);
-    return b;
 }
 
 // rasterizer_impl.cu:35-50
@@ -140,9 +119,38 @@ static uint32_t higher_msb(uint32_t n) {
     if (n >> msb) msb++;
     return msb;
 }
-static int sort_bits(int T) { return 32 + (int)higher_msb((uint32_t)T); }
-// buffer index that holds the sorted result: one swap per 8-bit pass
-static int sorted_buffer(int T) { return ((sort_bits(T) + 7) / 8) & 1; }
+static int bits_for(uint32_t n) {  // smallest b with (n >> b) == 0
+    int b = 0;
+    while (b < 32 && (n >> b) != 0) b++;
+    return b;
+}
+
+}  // namespace gs4d
+
+namespace gs4d {
+
+// instance key = (tile << rank_bits) | depth rank; tile ids need msb(T) bits (rasterizer_impl.cu:301)
+void BinningState::geometry(int P, int T, int &rank_bits, int &key_bits, bool &wide) {
+    rank_bits = P > 1 ? bits_for((uint32_t)(P - 1)) : 1;
+    key_bits = rank_bits + (int)higher_msb((uint32_t)T);
+    wide = key_bits > 32;
+}
+size_t BinningState::required(int L, int P, int T) {
+    BinningState b = carve(nullptr, L, P, T);
+    return (size_t)b.scratch + 4 * radix_scratch_words(L) + 512;
+}
+BinningState BinningState::carve(char *base, int L, int P, int T) {
+    char *p = (char *)align_up((size_t)base, 256);
+    BinningState b;
+    geometry(P, T, b.rank_bits, b.key_bits, b.wide);
+    const size_t kb = b.wide ? 8 : 4;
+    b.keys[0] = gs4d::carve(p, kb * (size_t)L);
+    b.keys[1] = gs4d::carve(p, kb * (size_t)L);
+    b.point_list = (uint32_t *)gs4d::carve(p, 4 * (size_t)L);
+    b.upos = (uint32_t *)gs4d::carve(p, 4 * (size_t)L);
+    b.scratch = (uint32_t *)gs4d::carve(p, 4 * radix_scratch_words(L));
+    return b;
+}
 
 static Args make_args(int P, int D, int M, int W, int H, const float *bg, float scale_modifier, const float *view,
                       const float *proj, const float *campos, float tan_fovx, float tan_fovy, int prefiltered) {
@@ -232,13 +240,18 @@ int gs4d_forward(gs4d_alloc_fn geometry_alloc, void *geometry_ctx, gs4d_alloc_fn
                                                colors_precomp, radii_ptr, g, flag, stream));
     GS4D_STAGE("scan", launch_scan_blocks(P, g, stream));
 
-    // H1: the single device->host synchronisation of the forward (rasterizer_impl.cu:282)
+    // H1: the single device->host synchronisation of the forward (rasterizer_impl.cu:282).  The depth
+    // ordering is enqueued before the host waits, so the GPU keeps working during the round trip.
     static thread_local uint32_t *pinned = nullptr;
+    static thread_local hipEvent_t copied = nullptr;
     if (!pinned) GS4D_HIP(hipHostMalloc((void **)&pinned, 16, hipHostMallocDefault));
+    if (!copied) GS4D_HIP(hipEventCreateWithFlags(&copied, hipEventDisableTiming));
     const int nblk = (P + kPreprocessBlock - 1) / kPreprocessBlock;
     GS4D_HIP(hipMemcpyAsync(pinned, g.block_sums + nblk, 4, hipMemcpyDeviceToHost, stream));
     if (prefiltered) GS4D_HIP(hipMemcpyAsync(pinned + 1, flag, 4, hipMemcpyDeviceToHost, stream));
-    GS4D_HIP(hipStreamSynchronize(stream));
+    GS4D_HIP(hipEventRecord(copied, stream));
+    GS4D_STAGE("depth_order", launch_depth_order(a, g, stream));
+    GS4D_HIP(hipEventSynchronize(copied));
     if (prefiltered && pinned[1] != 0)
         return fail(GS4D_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
     const uint32_t L32 = pinned[0];
@@ -246,16 +259,11 @@ int gs4d_forward(gs4d_alloc_fn geometry_alloc, void *geometry_ctx, gs4d_alloc_fn
     const int L = (int)L32;
     *num_rendered = L;
 
-    char *bbuf = binning_alloc(binning_ctx, BinningState::required(L));
-    if (!bbuf) return fail(GS4D_ERR_ALLOC, "forward: binning buffer allocation failed");
-    BinningState b = BinningState::carve(bbuf, L);
     const int T = a.gx * a.gy;
-    int buf = 0;
-    if (L > 0) {
-        GS4D_STAGE("duplicate", launch_duplicate(a, g, radii_ptr, b, stream));
-        GS4D_STAGE("sort", launch_radix_sort(b, L, sort_bits(T), &buf, stream));
-    }
-    GS4D_STAGE("tile_ranges", launch_tile_ranges(b, L, buf, img, T, stream));
+    char *bbuf = binning_alloc(binning_ctx, BinningState::required(L, P, T));
+    if (!bbuf) return fail(GS4D_ERR_ALLOC, "forward: binning buffer allocation failed");
+    BinningState b = BinningState::carve(bbuf, L, P, T);
+    GS4D_STAGE("binning", launch_binning(a, g, radii_ptr, b, L, img, stream));
     GS4D_STAGE("render", launch_render_forward(a, g, b, img, out_color, out_depth, stream));
     end_marks();
     return GS4D_OK;
@@ -287,21 +295,27 @@ int gs4d_backward(int P, int D, int M, int R, const float *background, int width
     ImageState img = ImageState::carve(image_buffer, width, height);
     const int *radii_ptr = radii ? radii : g.radii;
     const int T = a.gx * a.gy;
-    float *contrib = nullptr;
+    // backward scratch: per-instance gradient records (R x 48 B) + per-Gaussian conic gradients
+    const size_t rec_bytes = align_up((size_t)R * kContribStride * sizeof(float), 256);
+    char *scratch = scratch_alloc(scratch_ctx, rec_bytes + 16 * (size_t)P + 512);
+    if (!scratch) return fail(GS4D_ERR_ALLOC, "backward: scratch allocation failed");
+    float *contrib = (float *)align_up((size_t)scratch, 256);
+    float4 *dconic = (dL_dconic && ((size_t)dL_dconic & 15) == 0) ? (float4 *)dL_dconic
+                                                                   : (float4 *)((char *)contrib + rec_bytes);
     if (R > 0) {
-        BinningState b = BinningState::carve(binning_buffer, R);
-        const uint32_t *sorted_upos = b.vals[sorted_buffer(T)];
-        contrib = (float *)scratch_alloc(scratch_ctx, (size_t)R * kContribStride * sizeof(float));
-        if (!contrib) return fail(GS4D_ERR_ALLOC, "backward: scratch allocation failed");
+        BinningState b = BinningState::carve(binning_buffer, R, P, T);
         const float *color_ptr = colors_precomp;  // NULL -> the forward's rgb (rasterizer_impl.cu:392)
-        GS4D_STAGE("render_backward", launch_render_backward(a, g, b.point_list, sorted_upos, img, color_ptr, dL_dpix,
-                                                             contrib, stream));
+        GS4D_STAGE("render_backward",
+                   launch_render_backward(a, g, b.point_list, b.upos, img, color_ptr, dL_dpix, contrib, stream));
     }
+    GS4D_STAGE("contrib_reduce", launch_contrib_reduce(a, g, contrib, dL_dmean2D, dconic, dL_dopacity, dL_dcolor,
+                                                       stream));
+    if (dL_dconic && (float *)dconic != dL_dconic)
+        GS4D_HIP(hipMemcpyAsync(dL_dconic, dconic, 16 * (size_t)P, hipMemcpyDeviceToDevice, stream));
     const float *cov3D_ptr = cov3D_precomp ? cov3D_precomp : g.cov3D;  // rasterizer_impl.cu:414
-    GS4D_STAGE("preprocess_backward",
-               launch_preprocess_backward(a, g, radii_ptr, contrib, means3D, shs, scales, rotations, cov3D_ptr,
-                                          dL_dmean2D, dL_dconic, dL_dopacity, dL_dcolor, dL_dmean3D, dL_dcov3D,
-                                          dL_dsh, dL_dscale, dL_drot, stream));
+    GS4D_STAGE("gaussian_backward",
+               launch_gaussian_backward(a, g, radii_ptr, means3D, shs, scales, rotations, cov3D_ptr, dL_dmean2D,
+                                        dconic, dL_dcolor, dL_dmean3D, dL_dcov3D, dL_dsh, dL_dscale, dL_drot, stream));
     end_marks();
     return GS4D_OK;
 }

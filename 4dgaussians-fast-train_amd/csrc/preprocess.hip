@@ -82,6 +82,8 @@ __global__ __launch_bounds__(kPreprocessBlock) void preprocess_kernel(
         }
         radii[idx] = my_r;
         g.tiles_touched[idx] = touched;
+        // depth-sort key (binning.hip): positive depths order as their bits; culled sort last
+        g.dkeys[0][idx] = touched ? __float_as_uint(p_view.z) : 0xFFFFFFFFu;
     }
     // workgroup sum of tiles_touched
     uint32_t v = touched;

@@ -3,23 +3,50 @@
 // Reference: cuda_rasterizer/forward.cu:261-379 (renderCUDA forward) and backward.cu:399-557
 // (renderCUDA backward).
 //
-// MI355X mapping (not the reference's): ONE wave64 per 16x16 tile, each lane owns a column of 4
-// pixels (rows r, r+4, r+8, r+12 with r = lane/16).  A tile's sorted splats are fetched 64 at a
-// time, one per lane, into registers, then broadcast to the whole wave with v_readlane (scalar
-// registers) -- no LDS and no workgroup barriers.  The 4 pixels of a lane share the splat's dx,
-// so part of the Gaussian falloff is computed once per lane.  In the backward pass the 9 gradient
-// terms of each splat are first summed over the lane's 4 pixels in registers, then over the wave
-// with DPP row operations, and stored once per (tile, splat) instance with a plain store; a
-// per-Gaussian pass later sums a Gaussian's instances in a fixed order (no float atomics, so the
-// result is bitwise reproducible).
+// MI355X mapping (not the reference's): ONE wave64 per 16x16 tile; each lane owns a column of 4
+// pixels (rows r, r+4, r+8, r+12 with r = lane/16), so a splat's dx and the dx-only part of the
+// Gaussian falloff are computed once per lane.  A tile's sorted splats are fetched 64 at a time,
+// one per lane (the next batch is prefetched while the current one is blended), and broadcast to
+// the wave with v_readlane into scalar registers: no LDS, no workgroup barriers.  The per-pixel
+// body is branch-free (predicated with lane masks); a splat that reaches no pixel of the tile is
+// skipped with one wave-uniform branch.  Terminated pixels are marked by a negative transmittance.
+//
+// Backward: per pixel the reference keeps accum_rec[3] and last_color[3] only to form
+// dL/dalpha = sum_c (c_c - accum_rec_c) * dL/dpix_c; since dL/dpix is constant per pixel this is
+// carried as one scalar (accum_rec . dL/dpix), which is algebraically identical.  The 9 gradient
+// terms of a splat (backward.cu:523,545-554) are rewritten as uniform combinations of 6 per-lane
+// moments (sum u, sum u dx, sum u dy, sum u dx^2, sum u dx dy, sum u dy^2 with u = G dL/dalpha)
+// plus the 3 colour terms; these 9 values are reduced over the wave with two v_permlane swaps and
+// a 16-lane DPP tree (reduce-scatter), and the splat's record is stored once per (tile, splat)
+// instance at its sorted position (coalesced 48-byte records, no float atomics); a per-Gaussian
+// pass sums a Gaussian's records in a fixed order (bitwise reproducible).
 #include "gs4d_internal.h"
 
 namespace gs4d {
 
 constexpr int kPix = 4;  // pixels per lane
 
-__device__ __forceinline__ float readlane_f(float v, int l) {
+__device__ __forceinline__ float rl(float v, int l) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+struct SplatRegs {
+    float2 xy;
+    float4 co;
+    float4 cd;
+};
+
+__device__ __forceinline__ void load_splat(SplatRegs &r, bool valid, uint32_t gid, const float2 *__restrict__ xy,
+                                           const float4 *__restrict__ conic_opacity, const float4 *__restrict__ rgbd) {
+    if (valid) {
+        r.xy = xy[gid];
+        r.co = conic_opacity[gid];
+        r.cd = rgbd[gid];
+    } else {
+        r.xy = make_float2(0.f, 0.f);
+        r.co = make_float4(0.f, 0.f, 0.f, 0.f);
+        r.cd = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -38,74 +65,83 @@ __global__ __launch_bounds__(64) void render_forward_kernel(Args a, const uint2 
     const int px = tx * kBlockX + (lane & 15);
     const int py0 = ty * kBlockY + (lane >> 4);
     const float pfx = (float)px;
-    const V3 bg = load_v3(a.bg);
-    float T[kPix], C[kPix][3], Dp[kPix];
+    float pfy[kPix], T[kPix], C0[kPix], C1[kPix], C2[kPix], Dp[kPix];
     uint32_t last[kPix];
-    bool done[kPix];
 #pragma unroll
     for (int k = 0; k < kPix; k++) {
-        T[k] = 1.0f;
-        C[k][0] = C[k][1] = C[k][2] = 0.f;
-        Dp[k] = 0.f;
+        pfy[k] = (float)(py0 + 4 * k);
+        // outside pixels never blend (forward.cu:287-289): they start "terminated" (T < 0)
+        T[k] = (px < a.W && py0 + 4 * k < a.H) ? 1.0f : -1.0f;
+        C0[k] = C1[k] = C2[k] = Dp[k] = 0.f;
         last[k] = 0;
-        done[k] = !(px < a.W && py0 + 4 * k < a.H);  // outside pixels never blend (forward.cu:287-289)
     }
-    const uint2 range = ranges[tile];
+    uint2 range = ranges[tile];
+    range.x = __builtin_amdgcn_readfirstlane(range.x);
+    range.y = __builtin_amdgcn_readfirstlane(range.y);
+    SplatRegs cur, nxt;
+    if (range.x < range.y) {
+        const bool v = range.x + lane < range.y;
+        load_splat(cur, v, v ? point_list[range.x + lane] : 0u, xy, conic_opacity, rgbd);
+    }
     for (uint32_t base = range.x; base < range.y; base += 64) {
-        bool any_live = false;
+        bool live = false;
 #pragma unroll
-        for (int k = 0; k < kPix; k++) any_live |= !done[k];
-        if (!__any(any_live)) break;   // forward.cu:312-314
+        for (int k = 0; k < kPix; k++) live |= T[k] > 0.f;
+        if (!__any(live)) break;  // every pixel of the tile is done (forward.cu:312-314)
         const uint32_t n = min(64u, range.y - base);
-        float2 m_xy = make_float2(0.f, 0.f);
-        float4 m_co = make_float4(0.f, 0.f, 0.f, 0.f), m_cd = make_float4(0.f, 0.f, 0.f, 0.f);
-        if ((uint32_t)lane < n) {
-            const uint32_t gid = point_list[base + lane];
-            m_xy = xy[gid];
-            m_co = conic_opacity[gid];
-            m_cd = rgbd[gid];
+        {
+            const uint32_t nb = base + 64;
+            const bool v = nb + lane < range.y;
+            if (nb < range.y) load_splat(nxt, v, v ? point_list[nb + lane] : 0u, xy, conic_opacity, rgbd);
         }
         for (uint32_t j = 0; j < n; j++) {
-            const float sx = readlane_f(m_xy.x, j), sy = readlane_f(m_xy.y, j);
-            const float ca = readlane_f(m_co.x, j), cb = readlane_f(m_co.y, j), cc = readlane_f(m_co.z, j);
-            const float op = readlane_f(m_co.w, j);
-            const float cr = readlane_f(m_cd.x, j), cg = readlane_f(m_cd.y, j), cbl = readlane_f(m_cd.z, j);
-            const float dep = readlane_f(m_cd.w, j);
-            const uint32_t contributor = base - range.x + j + 1;
+            const float sx = rl(cur.xy.x, j), sy = rl(cur.xy.y, j);
+            const float ca = rl(cur.co.x, j), cb = rl(cur.co.y, j), cc = rl(cur.co.z, j), op = rl(cur.co.w, j);
             const float dx = sx - pfx;
+            const float pa = -0.5f * ca * dx * dx, pb = -cb * dx, pc = -0.5f * cc;
+            float alpha[kPix];
+            bool valid[kPix];
+            uint64_t any = 0;
 #pragma unroll
             for (int k = 0; k < kPix; k++) {
-                if (done[k]) continue;
-                const float dy = sy - (float)(py0 + 4 * k);
-                const float power = -0.5f * (ca * dx * dx + cc * dy * dy) - cb * dx * dy;
-                if (power > 0.0f) continue;
-                const float alpha = fminf(0.99f, op * __expf(power));
-                if (alpha < 1.0f / 255.0f) continue;
-                const float test_T = T[k] * (1 - alpha);
-                if (test_T < 0.0001f) {
-                    done[k] = true;
-                    continue;
-                }
-                C[k][0] += cr * alpha * T[k];
-                C[k][1] += cg * alpha * T[k];
-                C[k][2] += cbl * alpha * T[k];
-                Dp[k] += dep * alpha * T[k];
-                T[k] = test_T;
-                last[k] = contributor;
+                const float dy = sy - pfy[k];
+                const float power = pa + dy * (pb + pc * dy);  // = -0.5(a dx^2 + c dy^2) - b dx dy
+                alpha[k] = fminf(0.99f, op * __expf(power));
+                valid[k] = (power <= 0.0f) && (alpha[k] >= 1.0f / 255.0f) && (T[k] > 0.f);
+                any |= __ballot(valid[k]);
+            }
+            if (any == 0) continue;  // this splat reaches no pixel of the wave
+            const float cr = rl(cur.cd.x, j), cg = rl(cur.cd.y, j), cbl = rl(cur.cd.z, j), dep = rl(cur.cd.w, j);
+            const uint32_t contributor = base - range.x + j + 1;
+#pragma unroll
+            for (int k = 0; k < kPix; k++) {
+                const float test_T = T[k] * (1 - alpha[k]);
+                const bool term = valid[k] && (test_T < 0.0001f);   // forward.cu:349-354
+                const bool blend = valid[k] && !term;
+                const float w = blend ? alpha[k] * T[k] : 0.f;
+                C0[k] += cr * w;
+                C1[k] += cg * w;
+                C2[k] += cbl * w;
+                Dp[k] += dep * w;
+                T[k] = blend ? test_T : (term ? -T[k] : T[k]);
+                last[k] = blend ? contributor : last[k];
             }
         }
+        cur = nxt;
     }
     const size_t HW = (size_t)a.W * a.H;
+    const V3 bg = load_v3(a.bg);
 #pragma unroll
     for (int k = 0; k < kPix; k++) {
         const int py = py0 + 4 * k;
         if (px < a.W && py < a.H) {
+            const float t = fabsf(T[k]);
             const size_t pix = (size_t)py * a.W + px;
-            final_T[pix] = T[k];
+            final_T[pix] = t;
             n_contrib[pix] = last[k];
-            out_color[pix] = C[k][0] + T[k] * bg.x;
-            out_color[HW + pix] = C[k][1] + T[k] * bg.y;
-            out_color[2 * HW + pix] = C[k][2] + T[k] * bg.z;
+            out_color[pix] = C0[k] + t * bg.x;
+            out_color[HW + pix] = C1[k] + t * bg.y;
+            out_color[2 * HW + pix] = C2[k] + t * bg.z;
             out_depth[pix] = Dp[k];
         }
     }
@@ -120,26 +156,53 @@ hipError_t launch_render_forward(const Args &a, GeomState g, BinningState b, Ima
 }
 
 // ---------------------------------------------------------------------------------------------
-// Wave64 sum into lane 63 with DPP row operations (quad_perm, row_half_mirror, row_mirror,
-// row_bcast15/31): six v_add_f32 with DPP source modifiers, no LDS.
-template <int CTRL, int ROW_MASK>
+// 16-lane DPP row sum: every lane of each row ends with its row's total.
+template <int CTRL>
 __device__ __forceinline__ float dpp_add(float v) {
-    const int moved = __builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROW_MASK, 0xF, false);
-    return v + __int_as_float(moved);
+    return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
 }
-__device__ __forceinline__ float wave_sum_lane63(float v) {
-    v = dpp_add<0xB1, 0xF>(v);   // quad_perm [1,0,3,2]
-    v = dpp_add<0x4E, 0xF>(v);   // quad_perm [2,3,0,1]
-    v = dpp_add<0x141, 0xF>(v);  // row_half_mirror
-    v = dpp_add<0x140, 0xF>(v);  // row_mirror
-    v = dpp_add<0x142, 0xA>(v);  // row_bcast15 into rows 1,3
-    v = dpp_add<0x143, 0xC>(v);  // row_bcast31 into rows 2,3
+__device__ __forceinline__ float row_sum(float v) {
+    v = dpp_add<0xB1>(v);   // quad_perm [1,0,3,2]
+    v = dpp_add<0x4E>(v);   // quad_perm [2,3,0,1]
+    v = dpp_add<0x141>(v);  // row_half_mirror
+    v = dpp_add<0x140>(v);  // row_mirror
     return v;
+}
+// lanes 0-31 of the result hold a's half-wave sums, lanes 32-63 b's (v_permlane32_swap)
+__device__ __forceinline__ float swap32_add(float a, float b) {
+    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+// rows (0,1,2,3) of the result hold (a rows 0+1, b rows 0+1, a rows 2+3, b rows 2+3) (v_permlane16_swap)
+__device__ __forceinline__ float swap16_add(float a, float b) {
+    auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// Wave64 totals of 9 per-lane values, returned as wave-uniform scalars.
+__device__ __forceinline__ void wave_sum9(const float v[9], float out[9]) {
+    const float h0 = swap32_add(v[0], v[1]);  // lo: v0, hi: v1
+    const float h1 = swap32_add(v[2], v[3]);  // lo: v2, hi: v3
+    const float h2 = swap32_add(v[4], v[5]);
+    const float h3 = swap32_add(v[6], v[7]);
+    const float h4 = swap32_add(v[8], 0.f);   // lo: v8, hi: 0
+    const float q0 = row_sum(swap16_add(h0, h1));  // rows: v0, v2, v1, v3
+    const float q1 = row_sum(swap16_add(h2, h3));  // rows: v4, v6, v5, v7
+    const float q2 = row_sum(swap16_add(h4, 0.f)); // rows: v8, 0, 0, 0
+    out[0] = rl(q0, 0);
+    out[2] = rl(q0, 16);
+    out[1] = rl(q0, 32);
+    out[3] = rl(q0, 48);
+    out[4] = rl(q1, 0);
+    out[6] = rl(q1, 16);
+    out[5] = rl(q1, 32);
+    out[7] = rl(q1, 48);
+    out[8] = rl(q2, 0);
 }
 
 __global__ __launch_bounds__(64) void render_backward_kernel(Args a, const uint2 *__restrict__ ranges,
                                                              const uint32_t *__restrict__ point_list,
-                                                             const uint32_t *__restrict__ sorted_upos,
+                                                             const uint32_t *__restrict__ upos,
                                                              const float2 *__restrict__ xy,
                                                              const float4 *__restrict__ conic_opacity,
                                                              const float4 *__restrict__ rgbd,
@@ -155,134 +218,140 @@ __global__ __launch_bounds__(64) void render_backward_kernel(Args a, const uint2
     const int py0 = ty * kBlockY + (lane >> 4);
     const float pfx = (float)px;
     const size_t HW = (size_t)a.W * a.H;
-    const uint2 range = ranges[tile];
+    uint2 range = ranges[tile];
+    range.x = __builtin_amdgcn_readfirstlane(range.x);
+    range.y = __builtin_amdgcn_readfirstlane(range.y);
     if (range.y <= range.x) return;
-    const float bgc[3] = {a.bg[0], a.bg[1], a.bg[2]};
+    const V3 bg = load_v3(a.bg);
 
-    float T[kPix], T_final[kPix], dpix[kPix][3], accum[kPix][3], last_color[kPix][3], last_alpha[kPix], bgdot[kPix];
-    uint32_t last_contrib[kPix];
+    // per-pixel state: T (recovered backwards), A = accum_rec . dL/dpix, LCD = last_color . dL/dpix
+    float pfy[kPix], T[kPix], Tf[kPix], dp0[kPix], dp1[kPix], dp2[kPix], bgdot[kPix], A[kPix], LCD[kPix], la[kPix];
+    uint32_t lastc[kPix];
+    uint32_t max_last = 0;
 #pragma unroll
     for (int k = 0; k < kPix; k++) {
         const int py = py0 + 4 * k;
+        pfy[k] = (float)py;
         const bool inside = px < a.W && py < a.H;
         const size_t pix = (size_t)py * a.W + px;
-        T_final[k] = inside ? final_Ts[pix] : 0.f;
-        T[k] = T_final[k];
-        last_contrib[k] = inside ? n_contrib[pix] : 0;
-#pragma unroll
-        for (int c = 0; c < 3; c++) {
-            dpix[k][c] = inside ? dL_dpixels[c * HW + pix] : 0.f;
-            accum[k][c] = 0.f;
-            last_color[k][c] = 0.f;
-        }
-        last_alpha[k] = 0.f;
-        bgdot[k] = 0.f;
-#pragma unroll
-        for (int c = 0; c < 3; c++) bgdot[k] += bgc[c] * dpix[k][c];
+        Tf[k] = inside ? final_Ts[pix] : 0.f;
+        T[k] = Tf[k];
+        lastc[k] = inside ? n_contrib[pix] : 0u;
+        dp0[k] = inside ? dL_dpixels[pix] : 0.f;
+        dp1[k] = inside ? dL_dpixels[HW + pix] : 0.f;
+        dp2[k] = inside ? dL_dpixels[2 * HW + pix] : 0.f;
+        bgdot[k] = bg.x * dp0[k] + bg.y * dp1[k] + bg.z * dp2[k];
+        A[k] = 0.f;
+        LCD[k] = 0.f;
+        la[k] = 0.f;
+        max_last = max(max_last, lastc[k]);
     }
-    uint32_t max_last = 0;
+    // splats at list position >= every pixel's n_contrib never contribute: the walk starts there
 #pragma unroll
-    for (int k = 0; k < kPix; k++) max_last = max(max_last, last_contrib[k]);
-    // splats at list position >= every pixel's n_contrib never contribute: start the walk there
     for (int off = 32; off > 0; off >>= 1) max_last = max(max_last, (uint32_t)__shfl_xor((int)max_last, off));
-    const float ddelx_dx = 0.5f * a.W, ddely_dy = 0.5f * a.H;
+    const float hw = 0.5f * a.W, hh = 0.5f * a.H;  // ddelx_dx, ddely_dy (backward.cu:460-461)
 
     const uint32_t len = range.y - range.x;
-    // instances past max_last get zero gradient terms
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
     for (uint32_t p = max_last + lane; p < len; p += 64) {
-        const uint32_t u = sorted_upos[range.x + p];
-#pragma unroll
-        for (int q = 0; q < kContribStride; q++) contrib[(size_t)u * kContribStride + q] = 0.f;
+        float4 *rec = reinterpret_cast<float4 *>(contrib + (size_t)upos[range.x + p] * kContribStride);
+        rec[0] = z4;
+        rec[1] = z4;
+        rec[2] = z4;
     }
-    // walk positions max_last-1 ... 0 in batches of 64 (back to front)
+    SplatRegs cur, nxt;
+    float4 ccur, cnxt;  // colour operand (colors_precomp or the forward's rgb)
+    uint32_t ucur = 0, unxt = 0;  // where this lane's splat record goes (unsorted instance position)
+    auto fetch = [&](SplatRegs &r, float4 &c, uint32_t &u, int end) {
+        const int n = min(64, end);
+        const bool v = lane < n;
+        const uint32_t gid = v ? point_list[range.x + end - 1 - lane] : 0u;
+        u = v ? upos[range.x + end - 1 - lane] : 0u;
+        load_splat(r, v, gid, xy, conic_opacity, rgbd);
+        c = r.cd;
+        if (colors && v) c = make_float4(colors[3 * gid], colors[3 * gid + 1], colors[3 * gid + 2], 0.f);
+    };
+    if (max_last > 0) fetch(cur, ccur, ucur, (int)max_last);
     for (int end = (int)max_last; end > 0; end -= 64) {
         const int n = min(64, end);
-        // lane l holds the splat at position end-1-l
-        float2 m_xy = make_float2(0.f, 0.f);
-        float4 m_co = make_float4(0.f, 0.f, 0.f, 0.f);
-        float3 m_c = make_float3(0.f, 0.f, 0.f);
-        uint32_t m_upos = 0;
-        if (lane < n) {
-            const uint32_t si = range.x + end - 1 - lane;
-            const uint32_t gid = point_list[si];
-            m_upos = sorted_upos[si];
-            m_xy = xy[gid];
-            m_co = conic_opacity[gid];
-            if (colors) {
-                m_c = make_float3(colors[3 * gid], colors[3 * gid + 1], colors[3 * gid + 2]);
-            } else {
-                float4 t4 = rgbd[gid];
-                m_c = make_float3(t4.x, t4.y, t4.z);
-            }
-        }
-        float acc[kContribStride];
+        if (end - 64 > 0) fetch(nxt, cnxt, unxt, end - 64);
+        float acc[9];
 #pragma unroll
-        for (int q = 0; q < kContribStride; q++) acc[q] = 0.f;
+        for (int q = 0; q < 9; q++) acc[q] = 0.f;
         for (int j = 0; j < n; j++) {
             const uint32_t contributor = (uint32_t)(end - 1 - j);
-            const float sx = readlane_f(m_xy.x, j), sy = readlane_f(m_xy.y, j);
-            const float ca = readlane_f(m_co.x, j), cb = readlane_f(m_co.y, j), cc = readlane_f(m_co.z, j);
-            const float op = readlane_f(m_co.w, j);
-            const float col[3] = {readlane_f(m_c.x, j), readlane_f(m_c.y, j), readlane_f(m_c.z, j)};
+            const float sx = rl(cur.xy.x, j), sy = rl(cur.xy.y, j);
+            const float ca = rl(cur.co.x, j), cb = rl(cur.co.y, j), cc = rl(cur.co.z, j), op = rl(cur.co.w, j);
             const float dx = sx - pfx;
-            float g[kContribStride];
-#pragma unroll
-            for (int q = 0; q < kContribStride; q++) g[q] = 0.f;
-            bool any = false;
+            const float pa = -0.5f * ca * dx * dx, pb = -cb * dx, pc = -0.5f * cc;
+            float G[kPix], alpha[kPix], dy[kPix];
+            bool valid[kPix];
+            uint64_t any = 0;
 #pragma unroll
             for (int k = 0; k < kPix; k++) {
-                if (contributor >= last_contrib[k]) continue;
-                const float dy = sy - (float)(py0 + 4 * k);
-                const float power = -0.5f * (ca * dx * dx + cc * dy * dy) - cb * dx * dy;
-                if (power > 0.0f) continue;
-                const float G = __expf(power);
-                const float alpha = fminf(0.99f, op * G);
-                if (alpha < 1.0f / 255.0f) continue;
-                any = true;
-                T[k] = T[k] / (1.f - alpha);
-                const float dchannel_dcolor = alpha * T[k];
-                float dL_dalpha = 0.0f;
-#pragma unroll
-                for (int c = 0; c < 3; c++) {
-                    accum[k][c] = last_alpha[k] * last_color[k][c] + (1.f - last_alpha[k]) * accum[k][c];
-                    last_color[k][c] = col[c];
-                    dL_dalpha += (col[c] - accum[k][c]) * dpix[k][c];
-                    g[6 + c] += dchannel_dcolor * dpix[k][c];
-                }
-                dL_dalpha *= T[k];
-                last_alpha[k] = alpha;
-                dL_dalpha += (-T_final[k] / (1.f - alpha)) * bgdot[k];
-                const float dL_dG = op * dL_dalpha;
-                const float gdx = G * dx, gdy = G * dy;
-                const float dG_ddelx = -gdx * ca - gdy * cb;
-                const float dG_ddely = -gdy * cc - gdx * cb;
-                g[0] += dL_dG * dG_ddelx * ddelx_dx;
-                g[1] += dL_dG * dG_ddely * ddely_dy;
-                g[2] += -0.5f * gdx * dx * dL_dG;
-                g[3] += -0.5f * gdx * dy * dL_dG;
-                g[4] += -0.5f * gdy * dy * dL_dG;
-                g[5] += G * dL_dalpha;
+                dy[k] = sy - pfy[k];
+                const float power = pa + dy[k] * (pb + pc * dy[k]);
+                G[k] = __expf(power);
+                alpha[k] = fminf(0.99f, op * G[k]);
+                valid[k] = (contributor < lastc[k]) && (power <= 0.0f) && (alpha[k] >= 1.0f / 255.0f);
+                any |= __ballot(valid[k]);
             }
-            if (__any(any)) {
+            if (any == 0) continue;
+            const float cr = rl(ccur.x, j), cg = rl(ccur.y, j), cbl = rl(ccur.z, j);
+            float U0 = 0.f, U1 = 0.f, U2 = 0.f, W0 = 0.f, W1 = 0.f, W2 = 0.f;
 #pragma unroll
-                for (int q = 0; q < kContribStride; q++) {
-                    const float s = readlane_f(wave_sum_lane63(g[q]), 63);
-                    acc[q] = (lane == j) ? s : acc[q];
-                }
+            for (int k = 0; k < kPix; k++) {
+                const float inv = __builtin_amdgcn_rcpf(1.f - alpha[k]);
+                const float Tn = T[k] * inv;                                  // backward.cu:503
+                const float CD = cr * dp0[k] + cg * dp1[k] + cbl * dp2[k];
+                const float An = la[k] * LCD[k] + (1.f - la[k]) * A[k];       // backward.cu:515 dotted
+                const float dLda = (CD - An) * Tn + (-Tf[k] * inv) * bgdot[k];  // :519,525,534
+                const float u = valid[k] ? G[k] * dLda : 0.f;
+                const float w = valid[k] ? alpha[k] * Tn : 0.f;               // dchannel_dcolor
+                T[k] = valid[k] ? Tn : T[k];
+                A[k] = valid[k] ? An : A[k];
+                LCD[k] = valid[k] ? CD : LCD[k];
+                la[k] = valid[k] ? alpha[k] : la[k];
+                U0 += u;
+                U1 += u * dy[k];
+                U2 += u * dy[k] * dy[k];
+                W0 += w * dp0[k];
+                W1 += w * dp1[k];
+                W2 += w * dp2[k];
             }
+            const float v[9] = {U0, dx * U0, U1, dx * dx * U0, dx * U1, U2, W0, W1, W2};
+            float R[9];
+            wave_sum9(v, R);
+            // backward.cu:545-554 in terms of the moments (dL_dG = op * dL_dalpha)
+            const float g[9] = {hw * op * (-ca * R[1] - cb * R[2]),
+                                hh * op * (-cc * R[2] - cb * R[1]),
+                                -0.5f * op * R[3],
+                                -0.5f * op * R[4],
+                                -0.5f * op * R[5],
+                                R[0],
+                                R[6],
+                                R[7],
+                                R[8]};
+#pragma unroll
+            for (int q = 0; q < 9; q++) acc[q] = (lane == j) ? g[q] : acc[q];
         }
         if (lane < n) {
-#pragma unroll
-            for (int q = 0; q < kContribStride; q++) contrib[(size_t)m_upos * kContribStride + q] = acc[q];
+            float4 *rec = reinterpret_cast<float4 *>(contrib + (size_t)ucur * kContribStride);
+            rec[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+            rec[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
+            rec[2] = make_float4(acc[8], 0.f, 0.f, 0.f);
         }
+        cur = nxt;
+        ccur = cnxt;
+        ucur = unxt;
     }
 }
 
-hipError_t launch_render_backward(const Args &a, GeomState g, const uint32_t *point_list, const uint32_t *sorted_upos,
+hipError_t launch_render_backward(const Args &a, GeomState g, const uint32_t *point_list, const uint32_t *upos,
                                   ImageState img, const float *colors, const float *dL_dpix, float *contrib,
                                   hipStream_t s) {
     const int T = a.gx * a.gy;
-    hipLaunchKernelGGL(render_backward_kernel, dim3(T), dim3(64), 0, s, a, img.ranges, point_list, sorted_upos, g.xy,
+    hipLaunchKernelGGL(render_backward_kernel, dim3(T), dim3(64), 0, s, a, img.ranges, point_list, upos, g.xy,
                        g.conic_opacity, g.rgbd, colors, img.final_T, img.n_contrib, dL_dpix, contrib);
     return hipGetLastError();
 }
