@@ -22,7 +22,7 @@ HIP_SOURCES = ["preprocess.hip", "binning.hip", "render.hip", "preprocess_backwa
 # Per-Gaussian math (K1, K8/K9) is compiled without FMA contraction: it costs nothing measurable
 # (those kernels are tiny) and keeps radii / tile rects -- discrete decisions -- bit-identical to the
 # oracle.  The per-pixel blend kernels keep contraction for throughput.
-NO_CONTRACT = {"preprocess.hip", "preprocess_backward.hip"}
+NO_CONTRACT = {"preprocess.hip", "preprocess_backward.hip", "binning.hip"}
 HIPCC_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics", "-Wall",
                "-Wno-unused-result", "-I" + INCLUDE]
 

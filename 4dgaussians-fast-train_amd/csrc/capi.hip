@@ -85,8 +85,10 @@ GeomState GeomState::carve(char *base, int P) {
     g.cov3D = (float *)gs4d::carve(p, 24 * n);
     g.clamped = (uint8_t *)gs4d::carve(p, n);
     g.tiles_touched = (uint32_t *)gs4d::carve(p, 4 * n);
+    g.n_inst = (uint32_t *)gs4d::carve(p, 4 * n);
     g.point_offsets = (uint32_t *)gs4d::carve(p, 4 * n);
     g.block_sums = (uint32_t *)gs4d::carve(p, 4 * nb);
+    g.block_area = (uint32_t *)gs4d::carve(p, 4 * nb);
     g.dkeys[0] = (uint32_t *)gs4d::carve(p, 4 * n);
     g.dkeys[1] = (uint32_t *)gs4d::carve(p, 4 * n);
     g.dvals[0] = (uint32_t *)gs4d::carve(p, 4 * n);
@@ -210,6 +212,7 @@ int gs4d_forward(gs4d_alloc_fn geometry_alloc, void *geometry_ctx, gs4d_alloc_fn
     *num_rendered = 0;
     if (P < 0 || width <= 0 || height <= 0) return fail(GS4D_ERR_ARG, "forward: P must be >= 0 and the image non-empty");
     if (P == 0) return GS4D_OK;
+    if (P >= (1 << 30)) return fail(GS4D_ERR_ARG, "forward: at most 2^30 Gaussians");
     if (!means3D || !opacities || !viewmatrix || !projmatrix || !background || !out_color || !out_depth)
         return fail(GS4D_ERR_ARG, "forward: missing required input");
     if (!colors_precomp && (!shs || !cam_pos))
@@ -247,23 +250,26 @@ int gs4d_forward(gs4d_alloc_fn geometry_alloc, void *geometry_ctx, gs4d_alloc_fn
     if (!pinned) GS4D_HIP(hipHostMalloc((void **)&pinned, 16, hipHostMallocDefault));
     if (!copied) GS4D_HIP(hipEventCreateWithFlags(&copied, hipEventDisableTiming));
     const int nblk = (P + kPreprocessBlock - 1) / kPreprocessBlock;
-    GS4D_HIP(hipMemcpyAsync(pinned, g.block_sums + nblk, 4, hipMemcpyDeviceToHost, stream));
+    GS4D_HIP(hipMemcpyAsync(pinned, g.block_area + nblk, 4, hipMemcpyDeviceToHost, stream));
+    GS4D_HIP(hipMemcpyAsync(pinned + 2, g.block_sums + nblk, 4, hipMemcpyDeviceToHost, stream));
     if (prefiltered) GS4D_HIP(hipMemcpyAsync(pinned + 1, flag, 4, hipMemcpyDeviceToHost, stream));
     GS4D_HIP(hipEventRecord(copied, stream));
     GS4D_STAGE("depth_order", launch_depth_order(a, g, stream));
     GS4D_HIP(hipEventSynchronize(copied));
     if (prefiltered && pinned[1] != 0)
         return fail(GS4D_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
-    const uint32_t L32 = pinned[0];
-    if (L32 > 0x7fffffffu) return fail(GS4D_ERR_ARG, "forward: more than 2^31 tile instances");
-    const int L = (int)L32;
+    // num_rendered keeps the reference's meaning (all 3-sigma rect instances, rasterizer_impl.cu:282)
+    // and sizes the binning buffer; only the Lc <= L instances that reach a pixel are materialised.
+    const uint32_t L32 = pinned[0], Lc32 = pinned[2];
+    if (L32 >= (1u << 30)) return fail(GS4D_ERR_ARG, "forward: more than 2^30 tile instances");
+    const int L = (int)L32, Lc = (int)Lc32;
     *num_rendered = L;
 
     const int T = a.gx * a.gy;
     char *bbuf = binning_alloc(binning_ctx, BinningState::required(L, P, T));
     if (!bbuf) return fail(GS4D_ERR_ALLOC, "forward: binning buffer allocation failed");
     BinningState b = BinningState::carve(bbuf, L, P, T);
-    GS4D_STAGE("binning", launch_binning(a, g, radii_ptr, b, L, img, stream));
+    GS4D_STAGE("binning", launch_binning(a, g, radii_ptr, b, Lc, img, stream));
     GS4D_STAGE("render", launch_render_forward(a, g, b, img, out_color, out_depth, stream));
     end_marks();
     return GS4D_OK;

@@ -27,9 +27,11 @@ struct GeomState {
     float4 *rgbd;             // P   (r, g, b, depth) render attributes
     float *cov3D;             // 6P  world covariance (forward.cu:211)
     uint8_t *clamped;         // P   bit c set when channel c was clamped (forward.cu:67-69)
-    uint32_t *tiles_touched;  // P
-    uint32_t *point_offsets;  // P   exclusive offsets of each Gaussian's instances
-    uint32_t *block_sums;     // nblk_pre + 1 (last entry: total L)
+    uint32_t *tiles_touched;  // P   3-sigma rect area (the reference's tiles_touched, forward.cu:255)
+    uint32_t *n_inst;         // P   tiles of the rect actually reached (tile_reached), <= tiles_touched
+    uint32_t *point_offsets;  // P   exclusive offsets of each Gaussian's instances (over n_inst)
+    uint32_t *block_sums;     // nblk_pre + 1: exclusive per-workgroup offsets of n_inst, [nblk] = L'
+    uint32_t *block_area;     // nblk_pre + 1: same over tiles_touched, [nblk] = num_rendered
     uint32_t *dkeys[2];       // P   depth-sort keys (ping-pong)
     uint32_t *dvals[2];       // P   depth-sort ids; dvals[0] = Gaussian id by depth rank after the sort
     uint32_t *rank;           // P   depth rank of each Gaussian
@@ -75,6 +77,51 @@ __device__ __forceinline__ Mat4 load_mat4(const float *__restrict__ p) {
 __device__ __forceinline__ V3 load_v3(const float *__restrict__ p) { return v3(p[0], p[1], p[2]); }
 
 size_t radix_scratch_words(int n);
+
+// ---- exact tile culling ------------------------------------------------------------------------
+// The reference bins a splat into every tile of its 3-sigma rectangle (forward.cu:232-237), but a
+// pixel only blends a splat when alpha = min(0.99, o * exp(power)) >= 1/255 (forward.cu:346-348).
+// tile_reached() is false only when NO pixel centre of the tile (clipped to the image) can reach that
+// threshold: the minimum of the quadratic form q = a dx^2 + 2b dx dy + c dy^2 (power = -q/2) over
+// the tile's centre rectangle is taken in closed form (convex q: interior minimum or clamped
+// stationary point on an edge) and compared with a 0.1% margin.  Dropping such (tile, splat) pairs
+// changes no output bit: the reference skips every one of their pixel evaluations.  Splats with a
+// rectangle larger than kTightMaxArea tiles, or a conic that is not positive definite, are not culled.
+constexpr uint32_t kTightMaxArea = 64;
+
+__device__ __forceinline__ bool tile_reached(float mx, float my, float4 co, int tx, int ty, int W, int H) {
+    // evaluated identically wherever it is inlined (preprocess, duplicate, tile ranges)
+#pragma clang fp contract(off)
+    const float a = co.x, b = co.y, c = co.z, o = co.w;
+    if (!(a > 0.f && c > 0.f && a * c - b * b > 0.f)) return true;
+    // d = mean - pixel centre, over the tile's pixel centres inside the image
+    const float X0 = mx - (float)min(tx * kBlockX + kBlockX - 1, W - 1), X1 = mx - (float)(tx * kBlockX);
+    const float Y0 = my - (float)min(ty * kBlockY + kBlockY - 1, H - 1), Y1 = my - (float)(ty * kBlockY);
+    float q = 0.f;
+    if (!(X0 <= 0.f && X1 >= 0.f && Y0 <= 0.f && Y1 >= 0.f)) {
+        const float ia = 1.f / a, ic = 1.f / c;
+        float y = fminf(fmaxf(-b * X0 * ic, Y0), Y1);
+        float q0 = a * X0 * X0 + 2.f * b * X0 * y + c * y * y;
+        y = fminf(fmaxf(-b * X1 * ic, Y0), Y1);
+        float q1 = a * X1 * X1 + 2.f * b * X1 * y + c * y * y;
+        float x = fminf(fmaxf(-b * Y0 * ia, X0), X1);
+        float q2 = a * x * x + 2.f * b * x * Y0 + c * Y0 * Y0;
+        x = fminf(fmaxf(-b * Y1 * ia, X0), X1);
+        float q3 = a * x * x + 2.f * b * x * Y1 + c * Y1 * Y1;
+        q = fminf(fminf(q0, q1), fminf(q2, q3));
+    }
+    return !(o * __expf(-0.5f * q) * 1.001f < 1.0f / 255.0f);
+}
+// number of tiles of the rect [x0,x1)x[y0,y1) reached by the splat (all of them when not culled)
+__device__ __forceinline__ uint32_t count_reached(float mx, float my, float4 co, int x0, int y0, int x1, int y1, int W,
+                                                  int H) {
+    const uint32_t area = (uint32_t)((x1 - x0) * (y1 - y0));
+    if (area > kTightMaxArea) return area;
+    uint32_t n = 0;
+    for (int ty = y0; ty < y1; ty++)
+        for (int tx = x0; tx < x1; tx++) n += tile_reached(mx, my, co, tx, ty, W, H) ? 1u : 0u;
+    return n;
+}
 
 // ---- launchers (each enqueues on `stream`, returns hipError_t of the launch) ------------------
 hipError_t launch_preprocess(const Args &a, const float *means3D, const float *scales, const float *rotations,

@@ -5,7 +5,7 @@
 // :20-139 (SH backward), :278-341 (cov3D backward); rasterize_points.cu:153-161 (zeroed outputs).
 //
 // 1. contrib_reduce: each Gaussian sums the per-(tile, Gaussian) records the render backward stored
-//    at its unsorted instance positions [point_offsets[g], +tiles_touched[g]) -- in tile-rect order,
+//    at its unsorted instance positions [point_offsets[g], +n_inst[g]) -- in tile-rect order,
 //    which replaces the reference's float atomics (backward.cu:523,545-554) by a fixed-order sum.
 //    A workgroup's 256 Gaussians own one contiguous record range, streamed through LDS in chunks
 //    with coalesced 16-byte loads.
@@ -30,7 +30,7 @@ __global__ __launch_bounds__(256) void contrib_reduce_kernel(int P, GeomState g,
     uint32_t lo = 0, hi = 0;
     if (idx < P) {
         lo = g.point_offsets[idx];
-        hi = lo + g.tiles_touched[idx];
+        hi = lo + g.n_inst[idx];
     }
     float acc[9];
 #pragma unroll
