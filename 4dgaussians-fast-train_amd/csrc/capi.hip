@@ -72,7 +72,7 @@ static char *carve(char *&p, size_t bytes) {
 }
 
 // Sizes are computed by carving from a null base, so required() and carve() cannot disagree.
-size_t GeomState::required(int P) { return (size_t)carve(nullptr, P).sort_scratch + 4 * radix_scratch_words(P) + 512; }
+size_t GeomState::required(int P) { return (size_t)carve(nullptr, P).sort_scratch + 4 * geom_scratch_words(P) + 512; }
 GeomState GeomState::carve(char *base, int P) {
     char *p = (char *)align_up((size_t)base, 256);
     const size_t n = (size_t)P, nb = (n + kPreprocessBlock - 1) / kPreprocessBlock + 1;
@@ -86,15 +86,14 @@ GeomState GeomState::carve(char *base, int P) {
     g.clamped = (uint8_t *)gs4d::carve(p, n);
     g.tiles_touched = (uint32_t *)gs4d::carve(p, 4 * n);
     g.n_inst = (uint32_t *)gs4d::carve(p, 4 * n);
-    g.point_offsets = (uint32_t *)gs4d::carve(p, 4 * n);
-    g.block_sums = (uint32_t *)gs4d::carve(p, 4 * nb);
     g.block_area = (uint32_t *)gs4d::carve(p, 4 * nb);
     g.dkeys[0] = (uint32_t *)gs4d::carve(p, 4 * n);
     g.dkeys[1] = (uint32_t *)gs4d::carve(p, 4 * n);
     g.dvals[0] = (uint32_t *)gs4d::carve(p, 4 * n);
     g.dvals[1] = (uint32_t *)gs4d::carve(p, 4 * n);
-    g.rank = (uint32_t *)gs4d::carve(p, 4 * n);
-    g.sort_scratch = (uint32_t *)gs4d::carve(p, 4 * radix_scratch_words(P));
+    g.area_rank = (uint32_t *)gs4d::carve(p, 4 * n);
+    g.cand_off = (uint32_t *)gs4d::carve(p, 4 * n + 4);
+    g.sort_scratch = (uint32_t *)gs4d::carve(p, 4 * geom_scratch_words(P));
     return g;
 }
 
@@ -121,36 +120,28 @@ static uint32_t higher_msb(uint32_t n) {
     if (n >> msb) msb++;
     return msb;
 }
-static int bits_for(uint32_t n) {  // smallest b with (n >> b) == 0
-    int b = 0;
-    while (b < 32 && (n >> b) != 0) b++;
-    return b;
-}
 
 }  // namespace gs4d
 
 namespace gs4d {
 
-// instance key = (tile << rank_bits) | depth rank; tile ids need msb(T) bits (rasterizer_impl.cu:301)
-void BinningState::geometry(int P, int T, int &rank_bits, int &key_bits, bool &wide) {
-    rank_bits = P > 1 ? bits_for((uint32_t)(P - 1)) : 1;
-    key_bits = rank_bits + (int)higher_msb((uint32_t)T);
-    wide = key_bits > 32;
+// instances are sorted by tile id only; tile ids need msb(T) bits (rasterizer_impl.cu:301)
+size_t BinningState::required(int L, int T) {
+    BinningState b = carve(nullptr, L, T);
+    return (size_t)b.scratch + 4 * binning_scratch_words(L) + 512;
 }
-size_t BinningState::required(int L, int P, int T) {
-    BinningState b = carve(nullptr, L, P, T);
-    return (size_t)b.scratch + 4 * radix_scratch_words(L) + 512;
-}
-BinningState BinningState::carve(char *base, int L, int P, int T) {
+BinningState BinningState::carve(char *base, int L, int T) {
     char *p = (char *)align_up((size_t)base, 256);
     BinningState b;
-    geometry(P, T, b.rank_bits, b.key_bits, b.wide);
-    const size_t kb = b.wide ? 8 : 4;
-    b.keys[0] = gs4d::carve(p, kb * (size_t)L);
-    b.keys[1] = gs4d::carve(p, kb * (size_t)L);
+    b.key_bits = (int)higher_msb((uint32_t)T);
+    for (int i = 0; i < 2; i++) {
+        b.keys[i] = (uint32_t *)gs4d::carve(p, 4 * (size_t)L);
+        b.vals[i] = (uint32_t *)gs4d::carve(p, 4 * (size_t)L);
+    }
+    b.gid_by_e = (uint32_t *)gs4d::carve(p, 4 * (size_t)L);
     b.point_list = (uint32_t *)gs4d::carve(p, 4 * (size_t)L);
     b.upos = (uint32_t *)gs4d::carve(p, 4 * (size_t)L);
-    b.scratch = (uint32_t *)gs4d::carve(p, 4 * radix_scratch_words(L));
+    b.scratch = (uint32_t *)gs4d::carve(p, 4 * binning_scratch_words(L));
     return b;
 }
 
@@ -251,7 +242,6 @@ int gs4d_forward(gs4d_alloc_fn geometry_alloc, void *geometry_ctx, gs4d_alloc_fn
     if (!copied) GS4D_HIP(hipEventCreateWithFlags(&copied, hipEventDisableTiming));
     const int nblk = (P + kPreprocessBlock - 1) / kPreprocessBlock;
     GS4D_HIP(hipMemcpyAsync(pinned, g.block_area + nblk, 4, hipMemcpyDeviceToHost, stream));
-    GS4D_HIP(hipMemcpyAsync(pinned + 2, g.block_sums + nblk, 4, hipMemcpyDeviceToHost, stream));
     if (prefiltered) GS4D_HIP(hipMemcpyAsync(pinned + 1, flag, 4, hipMemcpyDeviceToHost, stream));
     GS4D_HIP(hipEventRecord(copied, stream));
     GS4D_STAGE("depth_order", launch_depth_order(a, g, stream));
@@ -259,17 +249,18 @@ int gs4d_forward(gs4d_alloc_fn geometry_alloc, void *geometry_ctx, gs4d_alloc_fn
     if (prefiltered && pinned[1] != 0)
         return fail(GS4D_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
     // num_rendered keeps the reference's meaning (all 3-sigma rect instances, rasterizer_impl.cu:282)
-    // and sizes the binning buffer; only the Lc <= L instances that reach a pixel are materialised.
-    const uint32_t L32 = pinned[0], Lc32 = pinned[2];
+    // and sizes the binning buffer; only the L' <= L instances that reach a pixel are materialised,
+    // and L' stays on the device.
+    const uint32_t L32 = pinned[0];
     if (L32 >= (1u << 30)) return fail(GS4D_ERR_ARG, "forward: more than 2^30 tile instances");
-    const int L = (int)L32, Lc = (int)Lc32;
+    const int L = (int)L32;
     *num_rendered = L;
 
     const int T = a.gx * a.gy;
-    char *bbuf = binning_alloc(binning_ctx, BinningState::required(L, P, T));
+    char *bbuf = binning_alloc(binning_ctx, BinningState::required(L, T));
     if (!bbuf) return fail(GS4D_ERR_ALLOC, "forward: binning buffer allocation failed");
-    BinningState b = BinningState::carve(bbuf, L, P, T);
-    GS4D_STAGE("binning", launch_binning(a, g, radii_ptr, b, Lc, img, stream));
+    BinningState b = BinningState::carve(bbuf, L, T);
+    GS4D_STAGE("binning", launch_binning(a, g, radii_ptr, b, L, img, stream));
     GS4D_STAGE("render", launch_render_forward(a, g, b, img, out_color, out_depth, stream));
     end_marks();
     return GS4D_OK;
@@ -301,21 +292,25 @@ int gs4d_backward(int P, int D, int M, int R, const float *background, int width
     ImageState img = ImageState::carve(image_buffer, width, height);
     const int *radii_ptr = radii ? radii : g.radii;
     const int T = a.gx * a.gy;
-    // backward scratch: per-instance gradient records (R x 48 B) + per-Gaussian conic gradients
+    // backward scratch: per-instance gradient records (R x 48 B) | per-Gaussian conic gradients |
+    // segmented-reduction partials
     const size_t rec_bytes = align_up((size_t)R * kContribStride * sizeof(float), 256);
-    char *scratch = scratch_alloc(scratch_ctx, rec_bytes + 16 * (size_t)P + 512);
+    const size_t dconic_bytes = align_up(16 * (size_t)P, 256);
+    char *scratch = scratch_alloc(scratch_ctx, rec_bytes + dconic_bytes + contrib_scratch_bytes(R) + 256);
     if (!scratch) return fail(GS4D_ERR_ALLOC, "backward: scratch allocation failed");
     float *contrib = (float *)align_up((size_t)scratch, 256);
+    char *reduce_scratch = (char *)contrib + rec_bytes + dconic_bytes;
     float4 *dconic = (dL_dconic && ((size_t)dL_dconic & 15) == 0) ? (float4 *)dL_dconic
                                                                    : (float4 *)((char *)contrib + rec_bytes);
+    BinningState b = {};
     if (R > 0) {
-        BinningState b = BinningState::carve(binning_buffer, R, P, T);
+        b = BinningState::carve(binning_buffer, R, T);
         const float *color_ptr = colors_precomp;  // NULL -> the forward's rgb (rasterizer_impl.cu:392)
         GS4D_STAGE("render_backward",
                    launch_render_backward(a, g, b.point_list, b.upos, img, color_ptr, dL_dpix, contrib, stream));
     }
-    GS4D_STAGE("contrib_reduce", launch_contrib_reduce(a, g, contrib, dL_dmean2D, dconic, dL_dopacity, dL_dcolor,
-                                                       stream));
+    GS4D_STAGE("contrib_reduce", launch_contrib_reduce(a, g, b, R, contrib, reduce_scratch, dL_dmean2D, dconic,
+                                                       dL_dopacity, dL_dcolor, stream));
     if (dL_dconic && (float *)dconic != dL_dconic)
         GS4D_HIP(hipMemcpyAsync(dL_dconic, dconic, 16 * (size_t)P, hipMemcpyDeviceToDevice, stream));
     const float *cov3D_ptr = cov3D_precomp ? cov3D_precomp : g.cov3D;  // rasterizer_impl.cu:414

@@ -10,8 +10,7 @@ namespace gs4d {
 
 constexpr int kTilePixels = kBlockX * kBlockY;  // 256 pixels per 16x16 tile
 constexpr int kPreprocessBlock = 256;           // Gaussians per preprocess / duplicate workgroup
-constexpr int kSortBlockItems = 4096;           // keys per radix-sort workgroup (256 threads x 16)
-// Per-instance gradient record written by the render backward at the instance's sorted position:
+// Per-instance gradient record written by the render backward at the instance's emission slot:
 // m2x m2y conic_a conic_b conic_c opacity r g b + 3 pad (48 bytes = three 16-byte stores)
 constexpr int kContribStride = 12;
 
@@ -29,13 +28,12 @@ struct GeomState {
     uint8_t *clamped;         // P   bit c set when channel c was clamped (forward.cu:67-69)
     uint32_t *tiles_touched;  // P   3-sigma rect area (the reference's tiles_touched, forward.cu:255)
     uint32_t *n_inst;         // P   tiles of the rect actually reached (tile_reached), <= tiles_touched
-    uint32_t *point_offsets;  // P   exclusive offsets of each Gaussian's instances (over n_inst)
-    uint32_t *block_sums;     // nblk_pre + 1: exclusive per-workgroup offsets of n_inst, [nblk] = L'
-    uint32_t *block_area;     // nblk_pre + 1: same over tiles_touched, [nblk] = num_rendered
+    uint32_t *block_area;     // nblk_pre + 1: exclusive offsets of tiles_touched per id workgroup, [nblk] = L
     uint32_t *dkeys[2];       // P   depth-sort keys (ping-pong)
     uint32_t *dvals[2];       // P   depth-sort ids; dvals[0] = Gaussian id by depth rank after the sort
-    uint32_t *rank;           // P   depth rank of each Gaussian
-    uint32_t *sort_scratch;   // radix_scratch_words(P)
+    uint32_t *area_rank;      // P   tiles_touched by depth rank
+    uint32_t *cand_off;       // P+1 exclusive scan of area_rank: first candidate instance of each rank
+    uint32_t *sort_scratch;   // geom_scratch_words(P)
     static size_t required(int P);
     static GeomState carve(char *base, int P);
 };
@@ -48,16 +46,17 @@ struct ImageState {
     static ImageState carve(char *base, int W, int H);
 };
 
+// Sized for L = num_rendered instances; only the L' <= L reached ones are used (L' lives on the device).
 struct BinningState {
-    void *keys[2];          // L each: u32 or u64 instance keys (tile << rank_bits | depth rank)
+    uint32_t *keys[2];      // L each: tile id of each instance (ping-pong)
+    uint32_t *vals[2];      // L each: emission slot of each instance (ping-pong)
+    uint32_t *gid_by_e;     // L   Gaussian id of each emission slot
     uint32_t *point_list;   // L   Gaussian id of each sorted instance (render order)
-    uint32_t *upos;         // L   unsorted position (point_offsets[g] + k) of each sorted instance
-    uint32_t *scratch;      // radix_scratch_words(L)
-    int rank_bits, key_bits;
-    bool wide;              // u64 keys
-    static void geometry(int P, int T, int &rank_bits, int &key_bits, bool &wide);
-    static size_t required(int L, int P, int T);
-    static BinningState carve(char *base, int L, int P, int T);
+    uint32_t *upos;         // L   emission slot of each sorted instance (where its gradient record goes)
+    uint32_t *scratch;      // binning_scratch_words(L); word 0 = L' (emitted instances)
+    int key_bits;           // msb(T) (rasterizer_impl.cu:301)
+    static size_t required(int L, int T);
+    static BinningState carve(char *base, int L, int T);
 };
 
 // Camera constants stay in device memory (the caller's tensors) and are read by each kernel with
@@ -76,7 +75,8 @@ __device__ __forceinline__ Mat4 load_mat4(const float *__restrict__ p) {
 }
 __device__ __forceinline__ V3 load_v3(const float *__restrict__ p) { return v3(p[0], p[1], p[2]); }
 
-size_t radix_scratch_words(int n);
+size_t geom_scratch_words(int P);
+size_t binning_scratch_words(int L);
 
 // ---- exact tile culling ------------------------------------------------------------------------
 // The reference bins a splat into every tile of its 3-sigma rectangle (forward.cu:232-237), but a
@@ -90,7 +90,7 @@ size_t radix_scratch_words(int n);
 constexpr uint32_t kTightMaxArea = 64;
 
 __device__ __forceinline__ bool tile_reached(float mx, float my, float4 co, int tx, int ty, int W, int H) {
-    // evaluated identically wherever it is inlined (preprocess, duplicate, tile ranges)
+    // evaluated identically wherever it is inlined (count and emit passes)
 #pragma clang fp contract(off)
     const float a = co.x, b = co.y, c = co.z, o = co.w;
     if (!(a > 0.f && c > 0.f && a * c - b * b > 0.f)) return true;
@@ -112,17 +112,6 @@ __device__ __forceinline__ bool tile_reached(float mx, float my, float4 co, int 
     }
     return !(o * __expf(-0.5f * q) * 1.001f < 1.0f / 255.0f);
 }
-// number of tiles of the rect [x0,x1)x[y0,y1) reached by the splat (all of them when not culled)
-__device__ __forceinline__ uint32_t count_reached(float mx, float my, float4 co, int x0, int y0, int x1, int y1, int W,
-                                                  int H) {
-    const uint32_t area = (uint32_t)((x1 - x0) * (y1 - y0));
-    if (area > kTightMaxArea) return area;
-    uint32_t n = 0;
-    for (int ty = y0; ty < y1; ty++)
-        for (int tx = x0; tx < x1; tx++) n += tile_reached(mx, my, co, tx, ty, W, H) ? 1u : 0u;
-    return n;
-}
-
 // ---- launchers (each enqueues on `stream`, returns hipError_t of the launch) ------------------
 hipError_t launch_preprocess(const Args &a, const float *means3D, const float *scales, const float *rotations,
                              const float *opacities, const float *shs, const float *cov3D_precomp,
@@ -136,8 +125,10 @@ hipError_t launch_render_forward(const Args &a, GeomState g, BinningState b, Ima
                                  float *out_depth, hipStream_t s);
 hipError_t launch_render_backward(const Args &a, GeomState g, const uint32_t *point_list, const uint32_t *upos, ImageState img,
                                   const float *colors, const float *dL_dpix, float *contrib, hipStream_t s);
-hipError_t launch_contrib_reduce(const Args &a, GeomState g, const float *contrib, float *dL_dmean2D,
-                                 float4 *dL_dconic, float *dL_dopacity, float *dL_dcolor, hipStream_t s);
+size_t contrib_scratch_bytes(int R);
+hipError_t launch_contrib_reduce(const Args &a, GeomState g, BinningState b, int R, const float *contrib,
+                                 char *scratch, float *dL_dmean2D, float4 *dL_dconic, float *dL_dopacity,
+                                 float *dL_dcolor, hipStream_t s);
 hipError_t launch_gaussian_backward(const Args &a, GeomState g, const int *radii, const float *means3D,
                                     const float *shs, const float *scales, const float *rotations, const float *cov3D,
                                     const float *dL_dmean2D, const float4 *dL_dconic, const float *dL_dcolor,

@@ -8,15 +8,16 @@
 namespace gs4d {
 
 // One thread per Gaussian.  Besides the reference's outputs it produces the per-workgroup sum of
-// tiles_touched (block_sums), so that the prefix sum needs only one more single-workgroup pass.
+// tiles_touched (block_area), so that the prefix sum needs only one more single-workgroup pass, and
+// the depth-sort key of the Gaussian (binning.hip).
 __global__ __launch_bounds__(kPreprocessBlock) void preprocess_kernel(
     Args a, const float *__restrict__ means3D, const float *__restrict__ scales, const float *__restrict__ rotations,
     const float *__restrict__ opacities, const float *__restrict__ shs, const float *__restrict__ cov3D_precomp,
     const float *__restrict__ colors_precomp, int *__restrict__ radii, GeomState g, int *__restrict__ err_flag) {
-    __shared__ uint32_t s_wave[2][kPreprocessBlock / 64];
+    __shared__ uint32_t s_wave[kPreprocessBlock / 64];
     const int idx = blockIdx.x * kPreprocessBlock + threadIdx.x;
     const Mat4 view = load_mat4(a.viewmatrix), proj = load_mat4(a.projmatrix);
-    uint32_t touched = 0, reached = 0;
+    uint32_t touched = 0;
     if (idx < a.P) {
         int my_r = 0;
         V3 p_orig = v3(means3D[3 * idx], means3D[3 * idx + 1], means3D[3 * idx + 2]);
@@ -75,7 +76,6 @@ __global__ __launch_bounds__(kPreprocessBlock) void preprocess_kernel(
                     g.depths[idx] = p_view.z;
                     g.xy[idx] = point_image;
                     g.conic_opacity[idx] = co;
-                    reached = count_reached(point_image.x, point_image.y, co, x0, y0, x1, y1, a.W, a.H);
                     g.rgbd[idx] = make_float4(rgb.x, rgb.y, rgb.z, p_view.z);
                     my_r = (int)my_radius;
                     touched = area;
@@ -84,27 +84,20 @@ __global__ __launch_bounds__(kPreprocessBlock) void preprocess_kernel(
         }
         radii[idx] = my_r;
         g.tiles_touched[idx] = touched;
-        g.n_inst[idx] = reached;
         // depth-sort key (binning.hip): positive depths order as their bits; unbinned sort last
-        g.dkeys[0][idx] = reached ? __float_as_uint(p_view.z) : 0xFFFFFFFFu;
+        g.dkeys[0][idx] = touched ? __float_as_uint(p_view.z) : 0xFFFFFFFFu;
     }
-    // workgroup sums of tiles_touched and n_inst
-    uint32_t v = touched, u = reached;
+    // workgroup sum of tiles_touched
+    uint32_t v = touched;
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        v += __shfl_xor(v, off);
-        u += __shfl_xor(u, off);
-    }
-    if ((threadIdx.x & 63) == 0) {
-        s_wave[0][threadIdx.x >> 6] = v;
-        s_wave[1][threadIdx.x >> 6] = u;
-    }
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    if ((threadIdx.x & 63) == 0) s_wave[threadIdx.x >> 6] = v;
     __syncthreads();
-    if (threadIdx.x < 2) {
+    if (threadIdx.x == 0) {
         uint32_t t = 0;
 #pragma unroll
-        for (int w = 0; w < kPreprocessBlock / 64; w++) t += s_wave[threadIdx.x][w];
-        (threadIdx.x ? g.block_sums : g.block_area)[blockIdx.x] = t;
+        for (int w = 0; w < kPreprocessBlock / 64; w++) t += s_wave[w];
+        g.block_area[blockIdx.x] = t;
     }
 }
 
@@ -117,12 +110,10 @@ hipError_t launch_preprocess(const Args &a, const float *means3D, const float *s
     return hipGetLastError();
 }
 
-// Exclusive scan of the per-workgroup sums in place; block_sums[nblk] receives the total (L).
+// Exclusive scan of per-workgroup sums in place; sums[n] receives the total.
 // One workgroup of 1024 threads; each thread scans a contiguous chunk serially.
-__global__ __launch_bounds__(1024) void scan_blocks_kernel(uint32_t *__restrict__ sums0, uint32_t *__restrict__ sums1,
-                                                           int n) {
+__global__ __launch_bounds__(1024) void scan_blocks_kernel(uint32_t *__restrict__ sums, int n) {
     __shared__ uint32_t s_tot[1024 / 64];
-    uint32_t *__restrict__ sums = blockIdx.x ? sums1 : sums0;
     const int tid = threadIdx.x;
     const int chunk = (n + 1023) / 1024;
     const int b = tid * chunk, e = min(n, b + chunk);
@@ -153,12 +144,12 @@ __global__ __launch_bounds__(1024) void scan_blocks_kernel(uint32_t *__restrict_
     }
 }
 
+// block_area -> offsets of the 3-sigma instances, [nblk] = num_rendered
 hipError_t launch_scan_blocks(int P, GeomState g, hipStream_t s) {
     const int nblk = (P + kPreprocessBlock - 1) / kPreprocessBlock;
-    hipLaunchKernelGGL(scan_blocks_kernel, dim3(2), dim3(1024), 0, s, g.block_sums, g.block_area, nblk);
+    hipLaunchKernelGGL(scan_blocks_kernel, dim3(1), dim3(1024), 0, s, g.block_area, nblk);
     return hipGetLastError();
 }
-
 // rasterizer_impl.cu:54-66 checkFrustum
 __global__ void mark_visible_kernel(int P, const float *__restrict__ means3D, const float *__restrict__ viewmatrix,
                                     uint8_t *__restrict__ present) {

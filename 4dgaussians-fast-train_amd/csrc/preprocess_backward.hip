@@ -5,62 +5,135 @@
 // :20-139 (SH backward), :278-341 (cov3D backward); rasterize_points.cu:153-161 (zeroed outputs).
 //
 // 1. contrib_reduce: each Gaussian sums the per-(tile, Gaussian) records the render backward stored
-//    at its unsorted instance positions [point_offsets[g], +n_inst[g]) -- in tile-rect order,
-//    which replaces the reference's float atomics (backward.cu:523,545-554) by a fixed-order sum.
-//    A workgroup's 256 Gaussians own one contiguous record range, streamed through LDS in chunks
-//    with coalesced 16-byte loads.
+//    at its emission slots -- consecutive, in tile-rect order -- with a fixed-order segmented
+//    reduction, which replaces the reference's float atomics (backward.cu:523,545-554): bitwise
+//    deterministic, and balanced (one lane per record, whatever the splat sizes).
 // 2. gaussian_backward: K8 + K9 per Gaussian.  Every output element is written (zeros for culled
 //    Gaussians and for SH coefficients >= (D+1)^2), so no zero-fill pass is needed.
+#include <algorithm>
+
 #include "gs4d_internal.h"
 
 namespace gs4d {
 
-constexpr int kReduceChunk = 1024;  // records per LDS chunk (48 KB)
+// render-level gradients of Gaussian g, returned as dL_dmeans2D (.z stays 0), dL_dcolors, dL_dopacity;
+// the conic gradient uses the reference's float4 slots .x .y .w (backward.cu:549-551, read at :165)
+struct GradOut {
+    float *mean2D;
+    float4 *conic;
+    float *opacity;
+    float *color;
+};
+__device__ __forceinline__ void write_grads(const GradOut &o, uint32_t g, const float *acc) {
+    o.mean2D[3 * g + 0] = acc[0];
+    o.mean2D[3 * g + 1] = acc[1];
+    o.mean2D[3 * g + 2] = 0.f;
+    o.conic[g] = make_float4(acc[2], acc[3], 0.f, acc[4]);
+    o.opacity[g] = acc[5];
+    o.color[3 * g + 0] = acc[6];
+    o.color[3 * g + 1] = acc[7];
+    o.color[3 * g + 2] = acc[8];
+}
+__device__ __forceinline__ void store9(float4 *p, const float *acc) {
+    p[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    p[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
+    p[2] = make_float4(acc[8], 0.f, 0.f, 0.f);
+}
+__device__ __forceinline__ void add9(float *acc, const float4 *p) {
+    const float4 a = p[0], b = p[1], c = p[2];
+    acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
+    acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
+    acc[8] += c.x;
+}
 
-__global__ __launch_bounds__(256) void contrib_reduce_kernel(int P, GeomState g, const float *__restrict__ contrib,
-                                                             float *__restrict__ dL_dmean2D,
-                                                             float4 *__restrict__ dL_dconic,
-                                                             float *__restrict__ dL_dopacity,
-                                                             float *__restrict__ dL_dcolor) {
-    __shared__ float4 s_rec[kReduceChunk * 3];
-    const int tid = threadIdx.x;
-    const int idx = blockIdx.x * 256 + tid;
-    // the workgroup's record range (block_sums holds exclusive per-workgroup offsets, [nblk] = L)
-    const uint32_t R0 = g.block_sums[blockIdx.x], R1 = g.block_sums[blockIdx.x + 1];
-    uint32_t lo = 0, hi = 0;
-    if (idx < P) {
-        lo = g.point_offsets[idx];
-        hi = lo + g.n_inst[idx];
-    }
+// Pass 1: one lane per emission slot, one wave per 64 slots.  A Gaussian's records occupy consecutive
+// slots, so a segmented inclusive scan (fixed shuffle tree) sums each Gaussian's piece of the wave.
+// Pieces that are a whole Gaussian are written out; a piece continuing from the previous wave goes
+// to part[w][0], a piece that starts a Gaussian and continues into the next wave to part[w][1].
+// flags[w]: bit 0 = the wave's first piece ends its Gaussian, bit 1 = part[w][1] starts a chain.
+__global__ __launch_bounds__(256) void contrib_segments_kernel(const uint32_t *__restrict__ n_dev,
+                                                               const uint32_t *__restrict__ gid_by_e,
+                                                               const float4 *__restrict__ rec, GradOut o,
+                                                               float4 *__restrict__ part,
+                                                               uint32_t *__restrict__ flags) {
+    const int n = (int)__builtin_amdgcn_readfirstlane(*n_dev);
+    const int lane = threadIdx.x & 63;
+    const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (w * 64 >= n) return;
+    const int e = w * 64 + lane;
+    const bool valid = e < n;
+    const uint32_t key = valid ? gid_by_e[e] : 0xFFFFFFFFu;
     float acc[9];
-#pragma unroll
-    for (int q = 0; q < 9; q++) acc[q] = 0.f;
-    const float4 *src = reinterpret_cast<const float4 *>(contrib);
-    for (uint32_t cs = R0; cs < R1; cs += kReduceChunk) {
-        const uint32_t ce = min(R1, cs + kReduceChunk);
-        const uint32_t nq = (ce - cs) * 3;
-        __syncthreads();
-        for (uint32_t q = tid; q < nq; q += 256) s_rec[q] = src[(size_t)cs * 3 + q];
-        __syncthreads();
-        const uint32_t a = max(lo, cs), b = min(hi, ce);
-        for (uint32_t r = a; r < b; r++) {
-            const float4 r0 = s_rec[(r - cs) * 3], r1 = s_rec[(r - cs) * 3 + 1], r2 = s_rec[(r - cs) * 3 + 2];
-            acc[0] += r0.x; acc[1] += r0.y; acc[2] += r0.z; acc[3] += r0.w;
-            acc[4] += r1.x; acc[5] += r1.y; acc[6] += r1.z; acc[7] += r1.w;
-            acc[8] += r2.x;
+    {
+        float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a, c = a;
+        if (valid) {
+            a = rec[3 * (size_t)e];
+            b = rec[3 * (size_t)e + 1];
+            c = rec[3 * (size_t)e + 2];
         }
+        acc[0] = a.x; acc[1] = a.y; acc[2] = a.z; acc[3] = a.w;
+        acc[4] = b.x; acc[5] = b.y; acc[6] = b.z; acc[7] = b.w;
+        acc[8] = c.x;
     }
-    if (idx >= P) return;
-    // render-level gradients, returned as dL_dmeans2D (.z stays 0), dL_dcolors, dL_dopacity; the conic
-    // gradient uses the reference's float4 slots .x .y .w (backward.cu:549-551, read at :165)
-    dL_dmean2D[3 * idx + 0] = acc[0];
-    dL_dmean2D[3 * idx + 1] = acc[1];
-    dL_dmean2D[3 * idx + 2] = 0.f;
-    dL_dconic[idx] = make_float4(acc[2], acc[3], 0.f, acc[4]);
-    dL_dopacity[idx] = acc[5];
-    dL_dcolor[3 * idx + 0] = acc[6];
-    dL_dcolor[3 * idx + 1] = acc[7];
-    dL_dcolor[3 * idx + 2] = acc[8];
+    uint32_t kp = __shfl_up(key, 1), kn = __shfl_down(key, 1);
+    if (lane == 0) kp = e > 0 ? gid_by_e[e - 1] : 0xFFFFFFFFu;
+    if (lane == 63) kn = e + 1 < n ? gid_by_e[e + 1] : 0xFFFFFFFFu;
+    const bool head = valid && key != kp;  // first slot of its Gaussian
+    const bool tail = valid && key != kn;  // last slot of its Gaussian
+    bool f = head || lane == 0;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        float up[9];
+#pragma unroll
+        for (int q = 0; q < 9; q++) up[q] = __shfl_up(acc[q], off);
+        const bool fu = __shfl_up((int)f, off) != 0;
+        if (lane >= off && !f) {
+#pragma unroll
+            for (int q = 0; q < 9; q++) acc[q] += up[q];
+        }
+        f = f || (lane >= off && fu);
+    }
+    const uint64_t vmask = __ballot(valid), tailm = __ballot(tail), headm = __ballot(head);
+    const uint64_t endm = __ballot(valid && (tail || lane == 63));
+    const int fe = __ffsll((unsigned long long)endm) - 1;  // end lane of the first piece
+    const int le = 63 - __clzll(vmask);                    // end lane of the last piece
+    const bool head0 = headm & 1ull;
+    const bool pend = valid && (tail || lane == 63);
+    if (pend) {
+        const bool starts = lane != fe || head0;  // the piece starts at its Gaussian's first slot
+        if (starts && tail) write_grads(o, key, acc);
+        else if (!starts) store9(part + ((size_t)w * 2) * 3, acc);
+        else store9(part + ((size_t)w * 2 + 1) * 3, acc);
+    }
+    if (lane == 0) {
+        const bool last_starts = le != fe || head0;
+        const bool last_open = !((tailm >> le) & 1ull);
+        flags[w] = (uint32_t)((tailm >> fe) & 1ull) | ((last_starts && last_open) ? 2u : 0u);
+    }
+}
+
+// Pass 2: Gaussians spanning several waves (summed in wave order from their chain start), and zeros
+// for Gaussians without instances.
+__global__ __launch_bounds__(256) void contrib_finish_kernel(int P, const uint32_t *__restrict__ n_dev,
+                                                             const uint32_t *__restrict__ n_inst,
+                                                             const uint32_t *__restrict__ gid_by_e,
+                                                             const float4 *__restrict__ part,
+                                                             const uint32_t *__restrict__ flags, GradOut o) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int nw = n_dev ? ((int)*n_dev + 63) / 64 : 0;
+    if (i < nw && (flags[i] & 2u)) {
+        float acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+        add9(acc, part + ((size_t)i * 2 + 1) * 3);
+        for (int w = i + 1; w < nw; w++) {
+            add9(acc, part + ((size_t)w * 2) * 3);
+            if (flags[w] & 1u) break;
+        }
+        write_grads(o, gid_by_e[(size_t)i * 64 + 63], acc);
+    }
+    if (i < P && n_inst[i] == 0) {
+        const float z[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+        write_grads(o, (uint32_t)i, z);
+    }
 }
 
 __global__ __launch_bounds__(256) void gaussian_backward_kernel(
@@ -134,10 +207,25 @@ __global__ __launch_bounds__(256) void gaussian_backward_kernel(
     reinterpret_cast<float4 *>(dL_drot)[idx] = drot;
 }
 
-hipError_t launch_contrib_reduce(const Args &a, GeomState g, const float *contrib, float *dL_dmean2D,
-                                 float4 *dL_dconic, float *dL_dopacity, float *dL_dcolor, hipStream_t s) {
-    hipLaunchKernelGGL(contrib_reduce_kernel, dim3((a.P + 255) / 256), dim3(256), 0, s, a.P, g, contrib, dL_dmean2D,
-                       dL_dconic, dL_dopacity, dL_dcolor);
+size_t contrib_scratch_bytes(int R) {
+    const size_t nw = ((size_t)R + 63) / 64;
+    return align_up(nw * 2 * 3 * sizeof(float4), 256) + 4 * nw + 256;
+}
+
+hipError_t launch_contrib_reduce(const Args &a, GeomState g, BinningState b, int R, const float *contrib,
+                                 char *scratch, float *dL_dmean2D, float4 *dL_dconic, float *dL_dopacity,
+                                 float *dL_dcolor, hipStream_t s) {
+    const GradOut o = {dL_dmean2D, dL_dconic, dL_dopacity, dL_dcolor};
+    const size_t nw = ((size_t)R + 63) / 64;
+    float4 *part = (float4 *)scratch;
+    uint32_t *flags = (uint32_t *)(scratch + align_up(nw * 2 * 3 * sizeof(float4), 256));
+    const uint32_t *n_dev = R > 0 ? b.scratch : nullptr;  // L' (binning.hip)
+    if (R > 0)
+        hipLaunchKernelGGL(contrib_segments_kernel, dim3((unsigned)((nw + 3) / 4)), dim3(256), 0, s, n_dev,
+                           b.gid_by_e, reinterpret_cast<const float4 *>(contrib), o, part, flags);
+    const size_t nthreads = std::max<size_t>((size_t)a.P, R > 0 ? nw : 0);
+    hipLaunchKernelGGL(contrib_finish_kernel, dim3((unsigned)((nthreads + 255) / 256)), dim3(256), 0, s, a.P,
+                       R > 0 ? n_dev : nullptr, g.n_inst, R > 0 ? b.gid_by_e : nullptr, part, flags, o);
     return hipGetLastError();
 }
 
