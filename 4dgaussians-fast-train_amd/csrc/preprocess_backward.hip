@@ -16,23 +16,39 @@
 
 namespace gs4d {
 
-// render-level gradients of Gaussian g, returned as dL_dmeans2D (.z stays 0), dL_dcolors, dL_dopacity;
-// the conic gradient uses the reference's float4 slots .x .y .w (backward.cu:549-551, read at :165)
+// Render-level gradients of Gaussian g from its summed moments R (render.hip): backward.cu:545-554
+// with dL/dG = opacity dL/dalpha, ddelx_dx = W/2, ddely_dy = H/2.  Returned as dL_dmeans2D (.z stays
+// 0), dL_dcolors, dL_dopacity; the conic gradient uses the reference's float4 slots .x .y .w
+// (backward.cu:549-551, read at :165).
 struct GradOut {
     float *mean2D;
     float4 *conic;
     float *opacity;
     float *color;
+    const float4 *conic_opacity;
+    float hw, hh;
 };
-__device__ __forceinline__ void write_grads(const GradOut &o, uint32_t g, const float *acc) {
-    o.mean2D[3 * g + 0] = acc[0];
-    o.mean2D[3 * g + 1] = acc[1];
+__device__ __forceinline__ void write_grads(const GradOut &o, uint32_t g, const float *R) {
+    const float4 co = o.conic_opacity[g];
+    const float op = co.w;
+    o.mean2D[3 * g + 0] = o.hw * op * (-co.x * R[1] - co.y * R[2]);
+    o.mean2D[3 * g + 1] = o.hh * op * (-co.z * R[2] - co.y * R[1]);
     o.mean2D[3 * g + 2] = 0.f;
-    o.conic[g] = make_float4(acc[2], acc[3], 0.f, acc[4]);
-    o.opacity[g] = acc[5];
-    o.color[3 * g + 0] = acc[6];
-    o.color[3 * g + 1] = acc[7];
-    o.color[3 * g + 2] = acc[8];
+    o.conic[g] = make_float4(-0.5f * op * R[3], -0.5f * op * R[4], 0.f, -0.5f * op * R[5]);
+    o.opacity[g] = R[0];
+    o.color[3 * g + 0] = R[6];
+    o.color[3 * g + 1] = R[7];
+    o.color[3 * g + 2] = R[8];
+}
+__device__ __forceinline__ void write_zero_grads(const GradOut &o, uint32_t g) {
+    o.mean2D[3 * g + 0] = 0.f;
+    o.mean2D[3 * g + 1] = 0.f;
+    o.mean2D[3 * g + 2] = 0.f;
+    o.conic[g] = make_float4(0.f, 0.f, 0.f, 0.f);
+    o.opacity[g] = 0.f;
+    o.color[3 * g + 0] = 0.f;
+    o.color[3 * g + 1] = 0.f;
+    o.color[3 * g + 2] = 0.f;
 }
 __device__ __forceinline__ void store9(float4 *p, const float *acc) {
     p[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
@@ -130,10 +146,7 @@ __global__ __launch_bounds__(256) void contrib_finish_kernel(int P, const uint32
         }
         write_grads(o, gid_by_e[(size_t)i * 64 + 63], acc);
     }
-    if (i < P && n_inst[i] == 0) {
-        const float z[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-        write_grads(o, (uint32_t)i, z);
-    }
+    if (i < P && n_inst[i] == 0) write_zero_grads(o, (uint32_t)i);
 }
 
 __global__ __launch_bounds__(256) void gaussian_backward_kernel(
@@ -215,7 +228,7 @@ size_t contrib_scratch_bytes(int R) {
 hipError_t launch_contrib_reduce(const Args &a, GeomState g, BinningState b, int R, const float *contrib,
                                  char *scratch, float *dL_dmean2D, float4 *dL_dconic, float *dL_dopacity,
                                  float *dL_dcolor, hipStream_t s) {
-    const GradOut o = {dL_dmean2D, dL_dconic, dL_dopacity, dL_dcolor};
+    const GradOut o = {dL_dmean2D, dL_dconic, dL_dopacity, dL_dcolor, g.conic_opacity, 0.5f * a.W, 0.5f * a.H};
     const size_t nw = ((size_t)R + 63) / 64;
     float4 *part = (float4 *)scratch;
     uint32_t *flags = (uint32_t *)(scratch + align_up(nw * 2 * 3 * sizeof(float4), 256));

@@ -4,50 +4,81 @@
 // (renderCUDA backward).
 //
 // MI355X mapping (not the reference's): ONE wave64 per 16x16 tile; each lane owns a column of 4
-// pixels (rows r, r+4, r+8, r+12 with r = lane/16), so a splat's dx and the dx-only part of the
-// Gaussian falloff are computed once per lane.  A tile's sorted splats are fetched 64 at a time,
-// one per lane (the next batch is prefetched while the current one is blended), and broadcast to
-// the wave with v_readlane into scalar registers: no LDS, no workgroup barriers.  The per-pixel
-// body is branch-free (predicated with lane masks); a splat that reaches no pixel of the tile is
-// skipped with one wave-uniform branch.  Terminated pixels are marked by a negative transmittance.
+// pixels (rows r, r+4, r+8, r+12 with r = lane/16), processed as two pairs with packed-f32 VALU
+// (v_pk_fma/mul/add_f32: two pixels per instruction).  A tile's sorted splats are fetched 64 at a
+// time, one per lane (the next batch is prefetched while the current one is blended), converted to
+// blend-ready constants and staged in LDS; the blend loop reads each splat with wave-uniform
+// (broadcast) ds_read_b128.  The Gaussian falloff is evaluated in base 2 (log2(e) folded into the
+// conic once per splat) so each pixel costs one v_exp_f32.  Which pixels a splat touches is kept in
+// 64-bit lane masks (scalar unit); pixels are retired by a mask, and termination (T < 1e-4, rare)
+// takes a wave-uniform side path, so the common path is branch- and select-light.
 //
 // Backward: per pixel the reference keeps accum_rec[3] and last_color[3] only to form
 // dL/dalpha = sum_c (c_c - accum_rec_c) * dL/dpix_c; since dL/dpix is constant per pixel this is
-// carried as one scalar (accum_rec . dL/dpix), which is algebraically identical.  The 9 gradient
-// terms of a splat (backward.cu:523,545-554) are rewritten as uniform combinations of 6 per-lane
-// moments (sum u, sum u dx, sum u dy, sum u dx^2, sum u dx dy, sum u dy^2 with u = G dL/dalpha)
-// plus the 3 colour terms; these 9 values are reduced over the wave with two v_permlane swaps and
-// a 16-lane DPP tree (reduce-scatter), and the splat's record is stored once per (tile, splat)
-// instance at its sorted position (coalesced 48-byte records, no float atomics); a per-Gaussian
-// pass sums a Gaussian's records in a fixed order (bitwise reproducible).
+// carried as one scalar A = accum_rec . dL/dpix, updated eagerly after each contributing splat
+// (A = alpha CD + (1 - alpha) A, the same recurrence as backward.cu:515-517).  The 9 gradient terms of
+// a splat (backward.cu:523,545-554) are linear in 6 per-pixel moments (sum u, sum u dx, sum u dy,
+// sum u dx^2, sum u dx dy, sum u dy^2 with u = G dL/dalpha) and 3 colour sums; these 9 values are
+// reduced over the wave with two v_permlane swaps and a 16-lane DPP tree (reduce-scatter), staged in
+// LDS, and stored once per (tile, splat) instance at its emission slot (coalesced 48-byte records,
+// no float atomics).  The per-Gaussian pass (preprocess_backward.hip) sums a Gaussian's records in
+// a fixed order and applies the moment -> gradient map once (bitwise reproducible).
 #include "gs4d_internal.h"
 
 namespace gs4d {
 
-constexpr int kPix = 4;  // pixels per lane
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2 bc2(float x) { return f2{x, x}; }
 
-__device__ __forceinline__ float rl(float v, int l) {
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
-}
+constexpr float kLog2e = 1.4426950408889634f;
 
+// Blend-ready splat constants.  geo = (x, y, -a/2 log2e, -b log2e), opc = (-c/2 log2e, opacity, -, -),
+// col = (r, g, b, depth).  power2 = log2(e) * power (forward.cu:340-342) at offset d = mean - pixel.
+struct SplatLDS {
+    float4 geo, opc, col;
+};
 struct SplatRegs {
-    float2 xy;
-    float4 co;
-    float4 cd;
+    float4 geo, opc, col;
 };
 
 __device__ __forceinline__ void load_splat(SplatRegs &r, bool valid, uint32_t gid, const float2 *__restrict__ xy,
-                                           const float4 *__restrict__ conic_opacity, const float4 *__restrict__ rgbd) {
+                                           const float4 *__restrict__ conic_opacity, const float4 *__restrict__ rgbd,
+                                           const float *__restrict__ colors) {
     if (valid) {
-        r.xy = xy[gid];
-        r.co = conic_opacity[gid];
-        r.cd = rgbd[gid];
+        const float2 p = xy[gid];
+        const float4 co = conic_opacity[gid];
+        r.geo = make_float4(p.x, p.y, (-0.5f * co.x) * kLog2e, (-co.y) * kLog2e);
+        r.opc = make_float4((-0.5f * co.z) * kLog2e, co.w, 0.f, 0.f);
+        r.col = rgbd[gid];
+        if (colors) r.col = make_float4(colors[3 * gid], colors[3 * gid + 1], colors[3 * gid + 2], r.col.w);
     } else {
-        r.xy = make_float2(0.f, 0.f);
-        r.co = make_float4(0.f, 0.f, 0.f, 0.f);
-        r.cd = make_float4(0.f, 0.f, 0.f, 0.f);
+        r.geo = r.opc = r.col = make_float4(0.f, 0.f, 0.f, 0.f);
     }
 }
+
+// Falloff of one splat at a pixel pair: exponent (base 2) and G = 2^power2.  Forward and backward use
+// this one sequence, so they take identical blend decisions.
+struct Falloff {
+    f2 dy, pw, G, alpha;
+};
+__device__ __forceinline__ Falloff falloff(const float4 &geo, const float4 &opc, float pa, float pb, f2 pfy) {
+    Falloff f;
+    f.dy = bc2(geo.y) - pfy;
+    f.pw = fma2(f.dy, fma2(bc2(opc.x), f.dy, bc2(pb)), bc2(pa));
+    f.G = f2{__builtin_amdgcn_exp2f(f.pw.x), __builtin_amdgcn_exp2f(f.pw.y)};
+    const f2 al = bc2(opc.y) * f.G;
+    f.alpha = f2{fminf(0.99f, al.x), fminf(0.99f, al.y)};
+    return f;
+}
+__device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+// lanes where the splat blends into the pixel: power <= 0 and alpha >= 1/255 (forward.cu:341-348);
+// two ballots of plain compares, combined on the scalar unit
+__device__ __forceinline__ uint64_t blend_mask(float pw, float alpha) {
+    return ballot(pw <= 0.0f) & ballot(alpha >= 1.0f / 255.0f);
+}
+// this lane's bit of a wave mask, used directly as the select condition (no VALU shift)
+__device__ __forceinline__ bool lane_bit(uint64_t m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
 
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void render_forward_kernel(Args a, const uint2 *__restrict__ ranges,
@@ -59,90 +90,112 @@ __global__ __launch_bounds__(64) void render_forward_kernel(Args a, const uint2 
                                                             uint32_t *__restrict__ n_contrib,
                                                             float *__restrict__ out_color,
                                                             float *__restrict__ out_depth) {
+    __shared__ SplatLDS s_sp[64];
     const int tile = blockIdx.x;
     const int tx = tile % a.gx, ty = tile / a.gx;
     const int lane = threadIdx.x;
     const int px = tx * kBlockX + (lane & 15);
     const int py0 = ty * kBlockY + (lane >> 4);
     const float pfx = (float)px;
-    float pfy[kPix], T[kPix], C0[kPix], C1[kPix], C2[kPix], Dp[kPix];
-    uint32_t last[kPix];
+    const f2 pfy[2] = {f2{(float)py0, (float)(py0 + 4)}, f2{(float)(py0 + 8), (float)(py0 + 12)}};
+    // live pixels (forward.cu:287-289: pixels outside the image never blend)
+    uint64_t alive[4];
 #pragma unroll
-    for (int k = 0; k < kPix; k++) {
-        pfy[k] = (float)(py0 + 4 * k);
-        // outside pixels never blend (forward.cu:287-289): they start "terminated" (T < 0)
-        T[k] = (px < a.W && py0 + 4 * k < a.H) ? 1.0f : -1.0f;
-        C0[k] = C1[k] = C2[k] = Dp[k] = 0.f;
-        last[k] = 0;
-    }
+    for (int k = 0; k < 4; k++) alive[k] = ballot(px < a.W && py0 + 4 * k < a.H);
+    f2 T[2] = {bc2(1.f), bc2(1.f)};
+    f2 C0[2] = {bc2(0.f), bc2(0.f)}, C1[2] = {bc2(0.f), bc2(0.f)}, C2[2] = {bc2(0.f), bc2(0.f)},
+       Dp[2] = {bc2(0.f), bc2(0.f)};
+    uint32_t stop[4] = {0, 0, 0, 0};  // list position of the terminating splat (retired pixels)
+    uint32_t seen = 0;                // 1 + list position of the last splat that touched a pixel
     uint2 range = ranges[tile];
     range.x = __builtin_amdgcn_readfirstlane(range.x);
     range.y = __builtin_amdgcn_readfirstlane(range.y);
-    SplatRegs cur, nxt;
+    SplatRegs nxt;
     if (range.x < range.y) {
         const bool v = range.x + lane < range.y;
-        load_splat(cur, v, v ? point_list[range.x + lane] : 0u, xy, conic_opacity, rgbd);
+        load_splat(nxt, v, v ? point_list[range.x + lane] : 0u, xy, conic_opacity, rgbd, nullptr);
     }
     for (uint32_t base = range.x; base < range.y; base += 64) {
-        bool live = false;
-#pragma unroll
-        for (int k = 0; k < kPix; k++) live |= T[k] > 0.f;
-        if (!__any(live)) break;  // every pixel of the tile is done (forward.cu:312-314)
+        if ((alive[0] | alive[1] | alive[2] | alive[3]) == 0) break;  // forward.cu:312-314
         const uint32_t n = min(64u, range.y - base);
+        __syncthreads();
+        s_sp[lane].geo = nxt.geo;
+        s_sp[lane].opc = nxt.opc;
+        s_sp[lane].col = nxt.col;
+        __syncthreads();
         {
             const uint32_t nb = base + 64;
             const bool v = nb + lane < range.y;
-            if (nb < range.y) load_splat(nxt, v, v ? point_list[nb + lane] : 0u, xy, conic_opacity, rgbd);
+            if (nb < range.y) load_splat(nxt, v, v ? point_list[nb + lane] : 0u, xy, conic_opacity, rgbd, nullptr);
         }
+        const uint32_t pos0 = base - range.x;
+        // software pipeline: splat j+1's constants are read from LDS while splat j is blended
+        float4 geo_n = s_sp[0].geo, opc_n = s_sp[0].opc, col_n = s_sp[0].col;
         for (uint32_t j = 0; j < n; j++) {
-            const float sx = rl(cur.xy.x, j), sy = rl(cur.xy.y, j);
-            const float ca = rl(cur.co.x, j), cb = rl(cur.co.y, j), cc = rl(cur.co.z, j), op = rl(cur.co.w, j);
-            const float dx = sx - pfx;
-            const float pa = -0.5f * ca * dx * dx, pb = -cb * dx, pc = -0.5f * cc;
-            float alpha[kPix];
-            bool valid[kPix];
-            uint64_t any = 0;
-#pragma unroll
-            for (int k = 0; k < kPix; k++) {
-                const float dy = sy - pfy[k];
-                const float power = pa + dy * (pb + pc * dy);  // = -0.5(a dx^2 + c dy^2) - b dx dy
-                alpha[k] = fminf(0.99f, op * __expf(power));
-                valid[k] = (power <= 0.0f) && (alpha[k] >= 1.0f / 255.0f) && (T[k] > 0.f);
-                any |= __ballot(valid[k]);
+            const float4 geo = geo_n, opc = opc_n, col = col_n;
+            {
+                const uint32_t jn = (j + 1) & 63;
+                geo_n = s_sp[jn].geo;
+                opc_n = s_sp[jn].opc;
+                col_n = s_sp[jn].col;
             }
-            if (any == 0) continue;  // this splat reaches no pixel of the wave
-            const float cr = rl(cur.cd.x, j), cg = rl(cur.cd.y, j), cbl = rl(cur.cd.z, j), dep = rl(cur.cd.w, j);
-            const uint32_t contributor = base - range.x + j + 1;
+            const float dx = geo.x - pfx;
+            const float pa = geo.z * dx * dx, pb = geo.w * dx;
+            f2 ae[2], tT[2];
+            uint64_t any = 0, term[4];
 #pragma unroll
-            for (int k = 0; k < kPix; k++) {
-                const float test_T = T[k] * (1 - alpha[k]);
-                const bool term = valid[k] && (test_T < 0.0001f);   // forward.cu:349-354
-                const bool blend = valid[k] && !term;
-                const float w = blend ? alpha[k] * T[k] : 0.f;
-                C0[k] += cr * w;
-                C1[k] += cg * w;
-                C2[k] += cbl * w;
-                Dp[k] += dep * w;
-                T[k] = blend ? test_T : (term ? -T[k] : T[k]);
-                last[k] = blend ? contributor : last[k];
+            for (int h = 0; h < 2; h++) {
+                const Falloff f = falloff(geo, opc, pa, pb, pfy[h]);
+                const uint64_t m0 = blend_mask(f.pw.x, f.alpha.x) & alive[2 * h];
+                const uint64_t m1 = blend_mask(f.pw.y, f.alpha.y) & alive[2 * h + 1];
+                any |= m0 | m1;
+                ae[h] = f2{lane_bit(m0) ? f.alpha.x : 0.f, lane_bit(m1) ? f.alpha.y : 0.f};
+                tT[h] = T[h] * (bc2(1.f) - ae[h]);  // forward.cu:349
+                term[2 * h] = ballot(tT[h].x < 0.0001f);
+                term[2 * h + 1] = ballot(tT[h].y < 0.0001f);
+            }
+            seen = any ? pos0 + j + 1 : seen;
+            if ((term[0] | term[1] | term[2] | term[3]) != 0) {
+                // forward.cu:350-354: the splat that would drop T below 1e-4 is not blended; the pixel retires
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const bool t0 = lane_bit(term[2 * h]), t1 = lane_bit(term[2 * h + 1]);
+                    ae[h] = f2{t0 ? 0.f : ae[h].x, t1 ? 0.f : ae[h].y};
+                    tT[h] = f2{t0 ? T[h].x : tT[h].x, t1 ? T[h].y : tT[h].y};
+                    stop[2 * h] = t0 ? pos0 + j : stop[2 * h];
+                    stop[2 * h + 1] = t1 ? pos0 + j : stop[2 * h + 1];
+                }
+#pragma unroll
+                for (int k = 0; k < 4; k++) alive[k] &= ~term[k];
+            }
+            // every live pixel takes the update; pixels the splat does not touch have ae = 0
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const f2 w = ae[h] * T[h];  // forward.cu:357-358
+                C0[h] = fma2(bc2(col.x), w, C0[h]);
+                C1[h] = fma2(bc2(col.y), w, C1[h]);
+                C2[h] = fma2(bc2(col.z), w, C2[h]);
+                Dp[h] = fma2(bc2(col.w), w, Dp[h]);
+                T[h] = tT[h];
             }
         }
-        cur = nxt;
     }
     const size_t HW = (size_t)a.W * a.H;
     const V3 bg = load_v3(a.bg);
 #pragma unroll
-    for (int k = 0; k < kPix; k++) {
+    for (int k = 0; k < 4; k++) {
         const int py = py0 + 4 * k;
         if (px < a.W && py < a.H) {
-            const float t = fabsf(T[k]);
+            const int h = k >> 1;
+            const float t = (k & 1) ? T[h].y : T[h].x;
             const size_t pix = (size_t)py * a.W + px;
             final_T[pix] = t;
-            n_contrib[pix] = last[k];
-            out_color[pix] = C0[k] + t * bg.x;
-            out_color[HW + pix] = C1[k] + t * bg.y;
-            out_color[2 * HW + pix] = C2[k] + t * bg.z;
-            out_depth[pix] = Dp[k];
+            // splats at positions >= n_contrib never blended into this pixel (the backward's bound)
+            n_contrib[pix] = lane_bit(alive[k]) ? seen : stop[k];
+            out_color[pix] = ((k & 1) ? C0[h].y : C0[h].x) + t * bg.x;
+            out_color[HW + pix] = ((k & 1) ? C1[h].y : C1[h].x) + t * bg.y;
+            out_color[2 * HW + pix] = ((k & 1) ? C2[h].y : C2[h].x) + t * bg.z;
+            out_depth[pix] = (k & 1) ? Dp[h].y : Dp[h].x;
         }
     }
 }
@@ -179,8 +232,10 @@ __device__ __forceinline__ float swap16_add(float a, float b) {
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
-// Wave64 totals of 9 per-lane values, returned as wave-uniform scalars.
-__device__ __forceinline__ void wave_sum9(const float v[9], float out[9]) {
+// Wave64 totals of 9 per-lane values, left in LDS: dst[q] = sum over lanes of v[q].  After the two
+// swap stages and the row sums, row r of q0 holds the total of v0,v2,v1,v3 (r = 0..3), of q1 v4,v6,
+// v5,v7 and of q2 v8; the first lane of each row stores it.
+__device__ __forceinline__ void wave_sum9_to_lds(const float v[9], float *dst, int lane) {
     const float h0 = swap32_add(v[0], v[1]);  // lo: v0, hi: v1
     const float h1 = swap32_add(v[2], v[3]);  // lo: v2, hi: v3
     const float h2 = swap32_add(v[4], v[5]);
@@ -189,15 +244,13 @@ __device__ __forceinline__ void wave_sum9(const float v[9], float out[9]) {
     const float q0 = row_sum(swap16_add(h0, h1));  // rows: v0, v2, v1, v3
     const float q1 = row_sum(swap16_add(h2, h3));  // rows: v4, v6, v5, v7
     const float q2 = row_sum(swap16_add(h4, 0.f)); // rows: v8, 0, 0, 0
-    out[0] = rl(q0, 0);
-    out[2] = rl(q0, 16);
-    out[1] = rl(q0, 32);
-    out[3] = rl(q0, 48);
-    out[4] = rl(q1, 0);
-    out[6] = rl(q1, 16);
-    out[5] = rl(q1, 32);
-    out[7] = rl(q1, 48);
-    out[8] = rl(q2, 0);
+    if ((lane & 15) == 0) {
+        const int r = lane >> 4;
+        const int slot = ((r & 1) << 1) | (r >> 1);  // row -> value index {0, 2, 1, 3}
+        dst[slot] = q0;
+        dst[4 + slot] = q1;
+        if (r == 0) dst[8] = q2;
+    }
 }
 
 __global__ __launch_bounds__(64) void render_backward_kernel(Args a, const uint2 *__restrict__ ranges,
@@ -211,6 +264,8 @@ __global__ __launch_bounds__(64) void render_backward_kernel(Args a, const uint2
                                                              const uint32_t *__restrict__ n_contrib,
                                                              const float *__restrict__ dL_dpixels,
                                                              float *__restrict__ contrib) {
+    __shared__ SplatLDS s_sp[64];
+    __shared__ float4 s_rec[64][3];  // reduced moments of the batch's splats
     const int tile = blockIdx.x;
     const int tx = tile % a.gx, ty = tile / a.gx;
     const int lane = threadIdx.x;
@@ -223,33 +278,36 @@ __global__ __launch_bounds__(64) void render_backward_kernel(Args a, const uint2
     range.y = __builtin_amdgcn_readfirstlane(range.y);
     if (range.y <= range.x) return;
     const V3 bg = load_v3(a.bg);
+    const f2 pfy[2] = {f2{(float)py0, (float)(py0 + 4)}, f2{(float)(py0 + 8), (float)(py0 + 12)}};
 
-    // per-pixel state: T (recovered backwards), A = accum_rec . dL/dpix, LCD = last_color . dL/dpix
-    float pfy[kPix], T[kPix], Tf[kPix], dp0[kPix], dp1[kPix], dp2[kPix], bgdot[kPix], A[kPix], LCD[kPix], la[kPix];
-    uint32_t lastc[kPix];
+    // per-pixel state (pairs): T (recovered backwards), A = accum_rec . dL/dpix, dL/dpix, and the
+    // background term -T_final (bg . dL/dpix) (backward.cu:534)
+    f2 T[2], A[2], dp0[2], dp1[2], dp2[2], nTb[2];
+    uint32_t lastc[4];
     uint32_t max_last = 0;
 #pragma unroll
-    for (int k = 0; k < kPix; k++) {
+    for (int k = 0; k < 4; k++) {
         const int py = py0 + 4 * k;
-        pfy[k] = (float)py;
         const bool inside = px < a.W && py < a.H;
         const size_t pix = (size_t)py * a.W + px;
-        Tf[k] = inside ? final_Ts[pix] : 0.f;
-        T[k] = Tf[k];
+        const float tf = inside ? final_Ts[pix] : 0.f;
+        const float d0 = inside ? dL_dpixels[pix] : 0.f;
+        const float d1 = inside ? dL_dpixels[HW + pix] : 0.f;
+        const float d2 = inside ? dL_dpixels[2 * HW + pix] : 0.f;
         lastc[k] = inside ? n_contrib[pix] : 0u;
-        dp0[k] = inside ? dL_dpixels[pix] : 0.f;
-        dp1[k] = inside ? dL_dpixels[HW + pix] : 0.f;
-        dp2[k] = inside ? dL_dpixels[2 * HW + pix] : 0.f;
-        bgdot[k] = bg.x * dp0[k] + bg.y * dp1[k] + bg.z * dp2[k];
-        A[k] = 0.f;
-        LCD[k] = 0.f;
-        la[k] = 0.f;
+        const float nb = -tf * (bg.x * d0 + bg.y * d1 + bg.z * d2);
+        const int h = k >> 1;
+        if (k & 1) {
+            T[h].y = tf; dp0[h].y = d0; dp1[h].y = d1; dp2[h].y = d2; nTb[h].y = nb; A[h].y = 0.f;
+        } else {
+            T[h].x = tf; dp0[h].x = d0; dp1[h].x = d1; dp2[h].x = d2; nTb[h].x = nb; A[h].x = 0.f;
+        }
         max_last = max(max_last, lastc[k]);
     }
     // splats at list position >= every pixel's n_contrib never contribute: the walk starts there
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) max_last = max(max_last, (uint32_t)__shfl_xor((int)max_last, off));
-    const float hw = 0.5f * a.W, hh = 0.5f * a.H;  // ddelx_dx, ddely_dy (backward.cu:460-461)
+    max_last = __builtin_amdgcn_readfirstlane(max_last);
 
     const uint32_t len = range.y - range.x;
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -259,91 +317,78 @@ __global__ __launch_bounds__(64) void render_backward_kernel(Args a, const uint2
         rec[1] = z4;
         rec[2] = z4;
     }
-    SplatRegs cur, nxt;
-    float4 ccur, cnxt;  // colour operand (colors_precomp or the forward's rgb)
-    uint32_t ucur = 0, unxt = 0;  // where this lane's splat record goes (unsorted instance position)
-    auto fetch = [&](SplatRegs &r, float4 &c, uint32_t &u, int end) {
+    SplatRegs nxt;
+    uint32_t unxt = 0;  // where this lane's splat record goes (the instance's emission slot)
+    auto fetch = [&](int end) {
         const int n = min(64, end);
         const bool v = lane < n;
         const uint32_t gid = v ? point_list[range.x + end - 1 - lane] : 0u;
-        u = v ? upos[range.x + end - 1 - lane] : 0u;
-        load_splat(r, v, gid, xy, conic_opacity, rgbd);
-        c = r.cd;
-        if (colors && v) c = make_float4(colors[3 * gid], colors[3 * gid + 1], colors[3 * gid + 2], 0.f);
+        unxt = v ? upos[range.x + end - 1 - lane] : 0u;
+        load_splat(nxt, v, gid, xy, conic_opacity, rgbd, colors);  // colour: colors_precomp or rgb
     };
-    if (max_last > 0) fetch(cur, ccur, ucur, (int)max_last);
+    if (max_last > 0) fetch((int)max_last);
     for (int end = (int)max_last; end > 0; end -= 64) {
         const int n = min(64, end);
-        if (end - 64 > 0) fetch(nxt, cnxt, unxt, end - 64);
-        float acc[9];
-#pragma unroll
-        for (int q = 0; q < 9; q++) acc[q] = 0.f;
+        const uint32_t ucur = unxt;
+        __syncthreads();
+        s_sp[lane].geo = nxt.geo;
+        s_sp[lane].opc = nxt.opc;
+        s_sp[lane].col = nxt.col;
+        __syncthreads();
+        if (end - 64 > 0) fetch(end - 64);
+        float4 geo_n = s_sp[0].geo, opc_n = s_sp[0].opc, col_n = s_sp[0].col;
         for (int j = 0; j < n; j++) {
             const uint32_t contributor = (uint32_t)(end - 1 - j);
-            const float sx = rl(cur.xy.x, j), sy = rl(cur.xy.y, j);
-            const float ca = rl(cur.co.x, j), cb = rl(cur.co.y, j), cc = rl(cur.co.z, j), op = rl(cur.co.w, j);
-            const float dx = sx - pfx;
-            const float pa = -0.5f * ca * dx * dx, pb = -cb * dx, pc = -0.5f * cc;
-            float G[kPix], alpha[kPix], dy[kPix];
-            bool valid[kPix];
-            uint64_t any = 0;
-#pragma unroll
-            for (int k = 0; k < kPix; k++) {
-                dy[k] = sy - pfy[k];
-                const float power = pa + dy[k] * (pb + pc * dy[k]);
-                G[k] = __expf(power);
-                alpha[k] = fminf(0.99f, op * G[k]);
-                valid[k] = (contributor < lastc[k]) && (power <= 0.0f) && (alpha[k] >= 1.0f / 255.0f);
-                any |= __ballot(valid[k]);
+            const float4 geo = geo_n, opc = opc_n, col = col_n;
+            {
+                const int jn = (j + 1) & 63;
+                geo_n = s_sp[jn].geo;
+                opc_n = s_sp[jn].opc;
+                col_n = s_sp[jn].col;
             }
-            if (any == 0) continue;
-            const float cr = rl(ccur.x, j), cg = rl(ccur.y, j), cbl = rl(ccur.z, j);
-            float U0 = 0.f, U1 = 0.f, U2 = 0.f, W0 = 0.f, W1 = 0.f, W2 = 0.f;
+            const float dx = geo.x - pfx;
+            const float pa = geo.z * dx * dx, pb = geo.w * dx;
+            f2 U0 = bc2(0.f), U1 = bc2(0.f), U2 = bc2(0.f), W0 = bc2(0.f), W1 = bc2(0.f), W2 = bc2(0.f);
+            // every pixel takes the update; pixels the splat does not touch have alpha = G = 0, which
+            // leaves T and A unchanged and adds nothing
 #pragma unroll
-            for (int k = 0; k < kPix; k++) {
-                const float inv = __builtin_amdgcn_rcpf(1.f - alpha[k]);
-                const float Tn = T[k] * inv;                                  // backward.cu:503
-                const float CD = cr * dp0[k] + cg * dp1[k] + cbl * dp2[k];
-                const float An = la[k] * LCD[k] + (1.f - la[k]) * A[k];       // backward.cu:515 dotted
-                const float dLda = (CD - An) * Tn + (-Tf[k] * inv) * bgdot[k];  // :519,525,534
-                const float u = valid[k] ? G[k] * dLda : 0.f;
-                const float w = valid[k] ? alpha[k] * Tn : 0.f;               // dchannel_dcolor
-                T[k] = valid[k] ? Tn : T[k];
-                A[k] = valid[k] ? An : A[k];
-                LCD[k] = valid[k] ? CD : LCD[k];
-                la[k] = valid[k] ? alpha[k] : la[k];
+            for (int h = 0; h < 2; h++) {
+                const Falloff f = falloff(geo, opc, pa, pb, pfy[h]);
+                const uint64_t m0 = blend_mask(f.pw.x, f.alpha.x) & ballot(contributor < lastc[2 * h]);
+                const uint64_t m1 = blend_mask(f.pw.y, f.alpha.y) & ballot(contributor < lastc[2 * h + 1]);
+                const bool b0 = lane_bit(m0), b1 = lane_bit(m1);
+                const f2 ae = f2{b0 ? f.alpha.x : 0.f, b1 ? f.alpha.y : 0.f};
+                const f2 Ge = f2{b0 ? f.G.x : 0.f, b1 ? f.G.y : 0.f};
+                const f2 om = bc2(1.f) - ae;
+                const f2 inv = f2{__builtin_amdgcn_rcpf(om.x), __builtin_amdgcn_rcpf(om.y)};
+                const f2 Tn = T[h] * inv;  // backward.cu:503
+                T[h] = Tn;
+                const f2 CD = fma2(bc2(col.z), dp2[h], fma2(bc2(col.y), dp1[h], bc2(col.x) * dp0[h]));
+                const f2 diff = CD - A[h];
+                const f2 dLda = fma2(diff, Tn, nTb[h] * inv);  // backward.cu:519-534
+                A[h] = fma2(ae, diff, A[h]);                   // accum_rec for the next splat in front
+                const f2 u = Ge * dLda;
+                const f2 w = ae * Tn;                          // dchannel_dcolor (backward.cu:521)
+                const f2 ud = u * f.dy;
                 U0 += u;
-                U1 += u * dy[k];
-                U2 += u * dy[k] * dy[k];
-                W0 += w * dp0[k];
-                W1 += w * dp1[k];
-                W2 += w * dp2[k];
+                U1 += ud;
+                U2 = fma2(ud, f.dy, U2);
+                W0 = fma2(w, dp0[h], W0);
+                W1 = fma2(w, dp1[h], W1);
+                W2 = fma2(w, dp2[h], W2);
             }
-            const float v[9] = {U0, dx * U0, U1, dx * dx * U0, dx * U1, U2, W0, W1, W2};
-            float R[9];
-            wave_sum9(v, R);
-            // backward.cu:545-554 in terms of the moments (dL_dG = op * dL_dalpha)
-            const float g[9] = {hw * op * (-ca * R[1] - cb * R[2]),
-                                hh * op * (-cc * R[2] - cb * R[1]),
-                                -0.5f * op * R[3],
-                                -0.5f * op * R[4],
-                                -0.5f * op * R[5],
-                                R[0],
-                                R[6],
-                                R[7],
-                                R[8]};
-#pragma unroll
-            for (int q = 0; q < 9; q++) acc[q] = (lane == j) ? g[q] : acc[q];
+            const float u0 = U0.x + U0.y, u1 = U1.x + U1.y;
+            const float v[9] = {u0, dx * u0, u1, dx * dx * u0, dx * u1, U2.x + U2.y, W0.x + W0.y, W1.x + W1.y,
+                                W2.x + W2.y};
+            wave_sum9_to_lds(v, reinterpret_cast<float *>(s_rec[j]), lane);
         }
+        __syncthreads();
         if (lane < n) {
             float4 *rec = reinterpret_cast<float4 *>(contrib + (size_t)ucur * kContribStride);
-            rec[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
-            rec[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
-            rec[2] = make_float4(acc[8], 0.f, 0.f, 0.f);
+            rec[0] = s_rec[lane][0];
+            rec[1] = s_rec[lane][1];
+            rec[2] = s_rec[lane][2];
         }
-        cur = nxt;
-        ccur = cnxt;
-        ucur = unxt;
     }
 }
 
