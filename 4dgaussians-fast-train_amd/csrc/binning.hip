@@ -16,11 +16,13 @@
 //   3. the emitted sequence is already depth-ordered, so a STABLE sort by tile id alone yields the
 //      reference's (tile, depth, id) order: ceil(msb(T)/8) passes over u32 keys (2 at the metric
 //      config instead of 6 over 12-byte pairs).
-// Scan, compaction and every sort pass are single launches that chain workgroups by decoupled
-// look-back: workgroups take chunk ids from an atomic counter in launch order, publish their chunk
-// aggregate, and find their global offset from lower chunk ids only (one 32-bit status+count word per
-// chunk (and digit), stored and polled with agent-scope relaxed atomics, so each word is its own
-// flag; a chunk only waits on chunks that already started, and spins are bounded).
+// Every pass is one launch.  Digit histograms are accumulated by the kernel that produces the keys
+// (preprocess for depths, emission for tiles).  Scan, compaction and sort passes chain their
+// workgroups by decoupled look-back in launch order (workgroup i waits only on workgroups < i, which
+// the in-order dispatcher has already placed; waits are bounded): one 32-bit status+count word per
+// chunk (and digit), stored and polled with agent-scope relaxed atomics, so each word is its own flag.
+#include <algorithm>
+
 #include "gs4d_internal.h"
 
 namespace gs4d {
@@ -28,12 +30,10 @@ namespace gs4d {
 constexpr int kSortThreads = 256;
 constexpr int kItemsL = 8;     // keys per lane for the instance sort (2048 per workgroup)
 constexpr int kItemsP = 4;     // keys per lane for the Gaussian depth sort (1024 per workgroup)
-constexpr int kMaxPasses = 4;  // u32 keys
 constexpr int kScanItems = 4;  // area scan: 1024 per workgroup
-constexpr int kEmitItems = 8;  // candidates per lane in the emission pass (2048 per workgroup)
-constexpr int kEmitChunk = 256 * kEmitItems;
+constexpr int kEmitPer = kEmitChunk / 256;  // candidates per lane in the emission pass
 constexpr uint32_t kAgg = 1u << 30, kPrefix = 2u << 30, kValMask = (1u << 30) - 1;
-constexpr uint32_t kSpinLimit = 1u << 22;
+constexpr uint32_t kSpinLimit = 1u << 20;
 
 __device__ __forceinline__ void store_word(uint32_t *p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -46,8 +46,8 @@ __device__ __forceinline__ int count_of(int n_host, const uint32_t *n_dev) {
     return n_dev ? (int)__builtin_amdgcn_readfirstlane(*n_dev) : n_host;
 }
 
-// Decoupled look-back for one value of chunk b (words look[p * stride]): publishes c, returns the
-// exclusive prefix over chunks 0..b-1.
+// Decoupled look-back by one thread for one value (words look[p * stride]): publishes c and returns
+// the exclusive prefix over chunks 0..b-1.  Predecessor words are polled 4 at a time.
 __device__ __forceinline__ uint32_t look_back(uint32_t *look, size_t stride, uint32_t b, uint32_t c, uint32_t *err) {
     uint32_t *mine = look + (size_t)b * stride;
     if (b == 0) {
@@ -56,117 +56,143 @@ __device__ __forceinline__ uint32_t look_back(uint32_t *look, size_t stride, uin
     }
     store_word(mine, kAgg | c);
     uint32_t excl = 0, spins = 0;
-    for (int p = (int)b - 1; p >= 0;) {
-        const uint32_t v = load_word(look + (size_t)p * stride);
-        if ((v & ~kValMask) == 0) {
+    int p = (int)b - 1;
+    while (p >= 0) {
+        uint32_t v[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) v[i] = p - i >= 0 ? load_word(look + (size_t)(p - i) * stride) : kPrefix;
+        // consume the batch up to the first prefix or the first not-yet-published word
+        int used = 0;
+        bool done = false;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            if (done || used != i) continue;
+            if ((v[i] & ~kValMask) == 0) continue;  // not published yet: poll again from here
+            excl += v[i] & kValMask;
+            used = i + 1;
+            if (v[i] & kPrefix) done = true;
+        }
+        if (done) break;
+        p -= used;
+        if (used == 0) {
             if (++spins > kSpinLimit) {
                 atomicOr(err, 1u);
                 break;
             }
             __builtin_amdgcn_s_sleep(1);
-            continue;
         }
-        excl += v & kValMask;
-        if (v & kPrefix) break;
-        p--;
     }
     store_word(mine, kPrefix | (excl + c));
     return excl;
 }
 
-// ---------------------------------------------------------------------------------------------
-// Scratch layouts (u32 words, each zeroed by one memset).
-// Sort: 256*kMaxPasses digit histograms | kMaxPasses chunk counters | error flag | pad |
-//       npass x (nblk*256) look-back words
-static int sort_nblk(int n, int items) { return (n + kSortThreads * items - 1) / (kSortThreads * items); }
-static size_t sort_header_words() { return 256 * kMaxPasses + kMaxPasses + 60; }
-static size_t sort_words(int n, int items, int npass) {
-    return sort_header_words() + (size_t)npass * 256 * (size_t)sort_nblk(n, items);
-}
-struct SortScratch {
-    uint32_t *ghist, *counters, *err, *look;
-    int nblk;
-};
-static SortScratch sort_scratch(uint32_t *base, int n, int items) {
-    SortScratch s;
-    s.ghist = base;
-    s.counters = base + 256 * kMaxPasses;
-    s.err = s.counters + kMaxPasses;
-    s.look = base + sort_header_words();
-    s.nblk = sort_nblk(n, items);
-    return s;
-}
-// Chained single-pass kernels (scan, emission): [0] chunk counter | [1] error flag | pad |
-// [64 + j] word of chunk j.
-static size_t chain_words(int nchunks) { return 64 + (size_t)nchunks; }
-
-// Geometry scratch: [area scan chain | depth sort], zeroed together before the depth sort.
-size_t geom_scratch_words(int P) {
-    return chain_words((P + 256 * kScanItems - 1) / (256 * kScanItems)) + sort_words(P, kItemsP, 4) + 64;
-}
-// Binning scratch: [counters (L' at [0]) | emission chain | instance sort], zeroed together.
-size_t binning_scratch_words(int L) {
-    return 64 + chain_words((L + kEmitChunk - 1) / kEmitChunk) + sort_words(L, kItemsL, kMaxPasses) + 64;
-}
-
-// ---------------------------------------------------------------------------------------------
-// One read of the keys: the global histogram of every 8-bit digit position of the sort.
-template <int ITEMS>
-__global__ __launch_bounds__(kSortThreads) void global_hist_kernel(const uint32_t *__restrict__ keys, int n_host,
-                                                                   const uint32_t *__restrict__ n_dev, int npass,
-                                                                   uint32_t *__restrict__ ghist) {
-    __shared__ uint32_t s_h[kMaxPasses][256];
-    const int tid = threadIdx.x;
-    const int n = count_of(n_host, n_dev);
-    for (int p = 0; p < npass; p++) s_h[p][tid] = 0;
-    __syncthreads();
-    const size_t base = (size_t)blockIdx.x * (kSortThreads * ITEMS);
-#pragma unroll
-    for (int r = 0; r < ITEMS; r++) {
-        const size_t i = base + (size_t)r * kSortThreads + tid;
-        if (i < (size_t)n) {
-            const uint32_t k = keys[i];
-            for (int p = 0; p < npass; p++) atomicAdd(&s_h[p][(k >> (8 * p)) & 0xFFu], 1u);
+// Same, by one full wave: 64 predecessors polled per step (lane i <-> chunk b-1-i).  Wave-uniform.
+__device__ __forceinline__ uint32_t look_back_wave(uint32_t *look, uint32_t b, uint32_t c, uint32_t *err) {
+    const int lane = threadIdx.x & 63;
+    if (lane == 0) store_word(look + b, b == 0 ? (kPrefix | c) : (kAgg | c));
+    if (b == 0) return 0;
+    uint32_t excl = 0, spins = 0;
+    int p = (int)b - 1;
+    while (true) {
+        const int q = p - lane;
+        const uint32_t v = q >= 0 ? load_word(look + q) : kPrefix;  // before chunk 0: prefix 0
+        const uint64_t pref = __builtin_amdgcn_ballot_w64((v & kPrefix) != 0);
+        const uint64_t ready = __builtin_amdgcn_ballot_w64((v & ~kValMask) != 0);
+        // lanes needed: up to and including the nearest prefix (all 64 if none)
+        const int last = pref ? __builtin_ctzll(pref) : 63;
+        const uint64_t need = last == 63 ? ~0ull : ((2ull << last) - 1);
+        if ((ready & need) != need) {
+            if (++spins > kSpinLimit) {
+                if (lane == 0) atomicOr(err, 1u);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            continue;
         }
+        uint32_t x = lane <= last ? (v & kValMask) : 0u;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+        excl += x;
+        if (pref) break;
+        p -= 64;
     }
-    __syncthreads();
-    for (int p = 0; p < npass; p++)
-        if (s_h[p][tid]) atomicAdd(&ghist[p * 256 + tid], s_h[p][tid]);
+    if (lane == 0) store_word(look + b, kPrefix | (excl + c));
+    return excl;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Zero-region layouts (u32 words).
+static int sort_nblk(int n, int items) { return (n + kSortThreads * items - 1) / (kSortThreads * items); }
+static size_t nchunk_scan(int P) { return ((size_t)P + 256 * kScanItems - 1) / (256 * kScanItems); }
+static size_t nchunk_emit(int L) { return ((size_t)L + kEmitChunk - 1) / kEmitChunk; }
+// geometry: counters | depth histograms | area-scan chain (+ err) | depth-sort look-back
+__host__ __device__ static size_t geom_chain_off() { return kZeroHist + kHistWords; }
+static size_t geom_look_off(int P) { return geom_chain_off() + nchunk_scan(P) + 64; }
+size_t geom_zero_words(int P) { return geom_look_off(P) + (size_t)4 * 256 * sort_nblk(P, kItemsP) + 64; }
+// binning: counters | tile histograms | emission chain (+ err) | instance-sort look-back
+__host__ __device__ static size_t bin_chain_off() { return kZeroHist + kHistWords; }
+static size_t bin_look_off(int L) { return bin_chain_off() + nchunk_emit(L) + 64; }
+size_t binning_zero_words(int L) { return bin_look_off(L) + (size_t)kMaxPasses * 256 * sort_nblk(L, kItemsL) + 64; }
+size_t max_emit_chunks(int P, int T) {
+    // L < 2^30 is enforced by the caller
+    const size_t bound = ((size_t)P * (size_t)T + kEmitChunk - 1) / kEmitChunk;
+    return std::min<size_t>(bound, ((size_t)1 << 30) / kEmitChunk) + 1;
 }
 
 enum Epilogue { kEpiDepth = 1, kEpiInstances = 2 };
-// Last-pass side outputs (see onesweep_kernel); o2 == nullptr disables them.
+// Last-pass side outputs (see onesweep_kernel); `on` == false disables them.
 struct EpiPtrs {
-    uint32_t *o0;
-    const uint32_t *i1;
-    uint32_t *o2, *o3;
+    bool on;
+    // kEpiInstances: point_list, gid_by_e, upos
+    uint32_t *point_list;
+    const uint32_t *gid_by_e;
+    uint32_t *upos;
+    // kEpiDepth
+    const uint32_t *tiles_touched;
+    uint32_t *area_rank, *n_inst;
+    const float2 *xy;
+    const int *radii;
+    const float4 *conic_opacity;
+    float4 *rank_geo, *rank_co;
 };
 
-// One LSD pass over 8 bits at `shift`.  Values: vin == nullptr -> identity (the item's index).
+// One LSD pass over 8 bits at `shift` (chunk = blockIdx.x).  Values: vin == nullptr -> identity (the
+// item's index).  hist: the 8 shards of the producer's digit histogram for this pass.
 // Epilogue on the last pass:
-//   kEpiDepth:     o2[pos] = i1[value] (rect area by depth rank), o3[value] = 0 (reached-tile count)
-//   kEpiInstances: o0[pos] = i1[value] (Gaussian id, render order), o2[pos] = value (emission slot,
-//                  where the backward stores the instance's gradient record)
+//   kEpiDepth:     per depth rank pos of Gaussian v: area_rank[pos], rank_geo[pos], rank_co[pos];
+//                  n_inst[v] = 0
+//   kEpiInstances: point_list[pos] = gid_by_e[v] (Gaussian id, render order), upos[pos] = v (the
+//                  emission slot, where the backward stores the instance's gradient record)
 template <int ITEMS, int EPI>
 __global__ __launch_bounds__(kSortThreads) void onesweep_kernel(const uint32_t *__restrict__ kin,
                                                                 const uint32_t *__restrict__ vin,
                                                                 uint32_t *__restrict__ kout,
                                                                 uint32_t *__restrict__ vout, int n_host,
                                                                 const uint32_t *__restrict__ n_dev, int shift,
-                                                                const uint32_t *__restrict__ ghist,
+                                                                const uint32_t *__restrict__ hist,
                                                                 uint32_t *__restrict__ look,
-                                                                uint32_t *__restrict__ counter,
                                                                 uint32_t *__restrict__ err, EpiPtrs e) {
     __shared__ uint32_t s_cnt[kSortThreads / 64][256];
     __shared__ uint32_t s_wsum[kSortThreads / 64];
-    __shared__ uint32_t s_bid;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int n = count_of(n_host, n_dev);
-    if (tid == 0) s_bid = atomicAdd(counter, 1u);
+    const uint32_t b = blockIdx.x;
+    const size_t wbase = (size_t)b * (kSortThreads * ITEMS) + (size_t)w * (64 * ITEMS);
+    uint32_t key[ITEMS], val[ITEMS], lrank[ITEMS];
+    // issue every load of the chunk first
+#pragma unroll
+    for (int r = 0; r < ITEMS; r++) {
+        const size_t i = wbase + (size_t)r * 64 + lane;
+        const bool valid = i < (size_t)n;
+        key[r] = valid ? kin[i] : 0u;
+        val[r] = valid ? (vin ? vin[i] : (uint32_t)i) : 0u;
+    }
+    uint32_t gcount = 0;
+#pragma unroll
+    for (int s = 0; s < kHistShards; s++) gcount += hist[s * (kMaxPasses * 256) + tid];
 #pragma unroll
     for (int q = 0; q < kSortThreads / 64; q++) s_cnt[q][tid] = 0;
     // exclusive scan of the global digit histogram (thread tid <-> digit tid)
-    const uint32_t gcount = ghist[tid];
     uint32_t gx = gcount;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
@@ -177,27 +203,16 @@ __global__ __launch_bounds__(kSortThreads) void onesweep_kernel(const uint32_t *
     __syncthreads();
     uint32_t gbase = gx - gcount;
     for (int q = 0; q < w; q++) gbase += s_wsum[q];
-    const uint32_t b = s_bid;
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    const size_t wbase = (size_t)b * (kSortThreads * ITEMS) + (size_t)w * (64 * ITEMS);
-    uint32_t key[ITEMS], val[ITEMS], lrank[ITEMS];
-    // issue every load of the chunk before ranking
-#pragma unroll
-    for (int r = 0; r < ITEMS; r++) {
-        const size_t i = wbase + (size_t)r * 64 + lane;
-        const bool valid = i < (size_t)n;
-        key[r] = valid ? kin[i] : 0u;
-        val[r] = valid ? (vin ? vin[i] : (uint32_t)i) : 0u;
-    }
 #pragma unroll
     for (int r = 0; r < ITEMS; r++) {
         const bool valid = wbase + (size_t)r * 64 + lane < (size_t)n;
         const uint32_t d = (key[r] >> shift) & 0xFFu;
-        uint64_t peers = __ballot(valid);
+        uint64_t peers = __builtin_amdgcn_ballot_w64(valid);
 #pragma unroll
         for (int bit = 0; bit < 8; bit++) {
             const bool set = (d >> bit) & 1u;
-            const uint64_t m = __ballot(set);
+            const uint64_t m = __builtin_amdgcn_ballot_w64(set);
             peers &= set ? m : ~m;
         }
         const uint32_t below = __popcll(peers & lt_mask);
@@ -229,39 +244,41 @@ __global__ __launch_bounds__(kSortThreads) void onesweep_kernel(const uint32_t *
             const uint32_t pos = s_cnt[w][d] + lrank[r];
             kout[pos] = key[r];
             if (vout) vout[pos] = val[r];
-            if (EPI == kEpiDepth && e.o2) {
-                e.o2[pos] = e.i1[val[r]];
-                e.o3[val[r]] = 0u;
+            if (EPI == kEpiDepth && e.on) {
+                const uint32_t g = val[r];
+                e.area_rank[pos] = e.tiles_touched[g];
+                e.n_inst[g] = 0u;
+                const float2 p = e.xy[g];
+                e.rank_geo[pos] = make_float4(p.x, p.y, __int_as_float(e.radii[g]), __uint_as_float(g));
+                e.rank_co[pos] = e.conic_opacity[g];
             }
-            if (EPI == kEpiInstances && e.o2) {
-                e.o0[pos] = e.i1[val[r]];
-                e.o2[pos] = val[r];
+            if (EPI == kEpiInstances && e.on) {
+                e.point_list[pos] = e.gid_by_e[val[r]];
+                e.upos[pos] = val[r];
             }
         }
     }
 }
 
-// Stable LSD sort of u32 keys[0] (+ values, identity in pass 0) on bits [0, nbits): one histogram
-// launch and one onesweep launch per pass over `scratch` (already zeroed by the caller).  n = n_host,
-// or *n_dev when n_dev != nullptr (then n_host is only the grid-sizing upper bound).  Returns the
-// buffer index holding the sorted keys.
+// Stable LSD sort of u32 keys[0] (+ values, identity in pass 0) on bits [0, nbits): one onesweep
+// launch per pass.  hist = the producer's sharded digit histograms, look = zeroed look-back words.
+// n = n_host, or *n_dev when n_dev != nullptr (then n_host is only the grid-sizing upper bound).
+// Returns the buffer index holding the sorted keys.
 template <int ITEMS, int EPI>
 static int onesweep_sort(uint32_t *keys[2], uint32_t *vals[2], int n_host, const uint32_t *n_dev, int nbits,
-                         uint32_t *scratch, EpiPtrs epi, hipStream_t s) {
+                         const uint32_t *hist, uint32_t *look, uint32_t *err, EpiPtrs epi, hipStream_t s) {
     const int npass = (nbits + 7) / 8;
-    SortScratch ss = sort_scratch(scratch, n_host, ITEMS);
-    hipLaunchKernelGGL((global_hist_kernel<ITEMS>), dim3(ss.nblk), dim3(kSortThreads), 0, s, keys[0], n_host, n_dev,
-                       npass, ss.ghist);
+    const int nblk = sort_nblk(n_host, ITEMS);
     int cur = 0;
-    const EpiPtrs none = {nullptr, nullptr, nullptr, nullptr};
+    EpiPtrs none = epi;
+    none.on = false;
     for (int p = 0; p < npass; p++) {
         const bool last = p == npass - 1;
         // the instance sort's last pass writes render-order ids instead of sorted values
         uint32_t *vout = (last && EPI == kEpiInstances) ? nullptr : vals[cur ^ 1];
-        hipLaunchKernelGGL((onesweep_kernel<ITEMS, EPI>), dim3(ss.nblk), dim3(kSortThreads), 0, s, keys[cur],
-                           p == 0 ? nullptr : vals[cur], keys[cur ^ 1], vout, n_host, n_dev, 8 * p,
-                           ss.ghist + 256 * p, ss.look + (size_t)p * 256 * ss.nblk, ss.counters + p, ss.err,
-                           last ? epi : none);
+        hipLaunchKernelGGL((onesweep_kernel<ITEMS, EPI>), dim3(nblk), dim3(kSortThreads), 0, s, keys[cur],
+                           p == 0 ? nullptr : vals[cur], keys[cur ^ 1], vout, n_host, n_dev, 8 * p, hist + 256 * p,
+                           look + (size_t)p * 256 * nblk, err, last ? epi : none);
         cur ^= 1;
     }
     return cur;
@@ -269,15 +286,14 @@ static int onesweep_sort(uint32_t *keys[2], uint32_t *vals[2], int n_host, const
 
 // ---------------------------------------------------------------------------------------------
 // Exclusive scan of the rect areas in depth-rank order: cand_off[r] = first candidate of rank r,
-// cand_off[P] = num_rendered.  Single pass, chained by look-back.
+// cand_off[P] = num_rendered; and first_rank[j] = the rank owning candidate j * kEmitChunk.
 __global__ __launch_bounds__(256) void area_scan_kernel(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
+                                                        uint32_t *__restrict__ first_rank, uint32_t jmax,
                                                         int n, uint32_t *__restrict__ chain) {
     __shared__ uint32_t s_w[4];
-    __shared__ uint32_t s_bid, s_prefix;
+    __shared__ uint32_t s_prefix;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    if (tid == 0) s_bid = atomicAdd(chain, 1u);
-    __syncthreads();
-    const uint32_t b = s_bid;
+    const uint32_t b = blockIdx.x;
     const size_t base = (size_t)b * (256 * kScanItems) + (size_t)tid * kScanItems;
     uint32_t v[kScanItems], t = 0;
 #pragma unroll
@@ -299,135 +315,173 @@ __global__ __launch_bounds__(256) void area_scan_kernel(const uint32_t *__restri
         before += q < w ? s_w[q] : 0u;
         total += s_w[q];
     }
-    if (tid == 0) s_prefix = look_back(chain + 64, 1, b, total, chain + 1);
+    if (w == 0) {
+        const uint32_t p = look_back_wave(chain + 64, b, total, chain + 1);
+        if (lane == 0) s_prefix = p;
+    }
     __syncthreads();
     uint32_t run = s_prefix + before + x - t;
 #pragma unroll
     for (int i = 0; i < kScanItems; i++) {
-        if (base + i < (size_t)n) out[base + i] = run;
+        if (base + i < (size_t)n) {
+            out[base + i] = run;
+            // chunk starts inside this rank's candidates
+            for (uint32_t j = (run + kEmitChunk - 1) / kEmitChunk; j * (uint32_t)kEmitChunk < run + v[i] && j < jmax;
+                 j++)
+                first_rank[j] = (uint32_t)(base + i);
+        }
         run += v[i];
     }
     if (base < (size_t)n && base + kScanItems >= (size_t)n) out[n] = run;
 }
 
-hipError_t launch_depth_order(const Args &a, GeomState g, hipStream_t s) {
-    const int nchunk = (a.P + 256 * kScanItems - 1) / (256 * kScanItems);
-    uint32_t *chain = g.sort_scratch;
-    uint32_t *sort_base = chain + chain_words(nchunk);
-    hipError_t e = hipMemsetAsync(g.sort_scratch, 0, 4 * geom_scratch_words(a.P), s);
-    if (e != hipSuccess) return e;
-    // dkeys[0] = depth bits (unbinned: ~0u, last); afterwards dvals[0] = Gaussian id by depth rank,
-    // area_rank[r] = tiles_touched of rank r, n_inst = 0
+hipError_t launch_depth_order(const Args &a, GeomState g, const int *radii, hipStream_t s) {
     uint32_t *keys[2] = {g.dkeys[0], g.dkeys[1]};
     uint32_t *vals[2] = {g.dvals[0], g.dvals[1]};
-    const EpiPtrs epi = {nullptr, g.tiles_touched, g.area_rank, g.n_inst};
-    onesweep_sort<kItemsP, kEpiDepth>(keys, vals, a.P, nullptr, 32, sort_base, epi, s);
-    hipLaunchKernelGGL(area_scan_kernel, dim3(nchunk), dim3(256), 0, s, g.area_rank, g.cand_off, a.P, chain);
+    EpiPtrs epi = {};
+    epi.on = true;
+    epi.tiles_touched = g.tiles_touched;
+    epi.area_rank = g.area_rank;
+    epi.n_inst = g.n_inst;
+    epi.xy = g.xy;
+    epi.radii = radii;
+    epi.conic_opacity = g.conic_opacity;
+    epi.rank_geo = g.rank_geo;
+    epi.rank_co = g.rank_co;
+    uint32_t *chain = g.zero + geom_chain_off();
+    onesweep_sort<kItemsP, kEpiDepth>(keys, vals, a.P, nullptr, 32, g.zero + kZeroHist, g.zero + geom_look_off(a.P),
+                                      chain + 1, epi, s);
+    hipLaunchKernelGGL(area_scan_kernel, dim3((unsigned)nchunk_scan(a.P)), dim3(256), 0, s, g.area_rank, g.cand_off,
+                       g.first_rank, (uint32_t)max_emit_chunks(a.P, a.gx * a.gy), a.P, chain);
     return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------------------
-// K3: load-balanced emission.  Workgroup (chunk) j takes candidates [j*2048, +2048) of the
-// depth-ordered candidate sequence, tests each with tile_reached, and compacts the reached ones in
-// candidate order: keys[e] = tile, gid_by_e[e] = Gaussian.  Emission offsets are chained by
-// look-back; the last chunk stores L' = the number of emitted instances.  n_inst[g] (zeroed by the
-// depth sort) receives each Gaussian's count with integer atomics.  The first T threads of the grid
-// also zero the tile ranges.
-__global__ __launch_bounds__(256) void emit_instances_kernel(Args a, GeomState g, const int *__restrict__ radii,
-                                                             int L, uint32_t *__restrict__ keys,
+// K3: load-balanced emission.  Workgroup j takes candidates [j*2048, +2048) of the depth-ordered
+// candidate sequence; lane t owns 8 consecutive ones.  Their owning ranks come from a load-balancing
+// search in LDS: each rank starting inside the chunk marks its first slot, and a max-scan spreads the
+// marks.  Each candidate is tested with tile_reached; the reached ones are compacted in candidate
+// order: keys[e] = tile, gid_by_e[e] = Gaussian.  Emission offsets are chained by look-back; the last
+// chunk stores L'.  Also accumulated: n_inst[g] (integer atomics), the tile-sort digit histograms,
+// and (first T threads of the grid) zeroed tile ranges.
+__global__ __launch_bounds__(256) void emit_instances_kernel(Args a, GeomState g, int L, int npass,
+                                                             uint32_t *__restrict__ keys,
                                                              uint32_t *__restrict__ gid_by_e,
-                                                             uint32_t *__restrict__ counters,
-                                                             uint32_t *__restrict__ chain, uint2 *__restrict__ ranges) {
-    __shared__ uint32_t s_off[kEmitChunk + 1];
-    __shared__ uint32_t s_n[kEmitChunk];
-    __shared__ uint32_t s_cnt[kEmitItems][4];
-    __shared__ uint32_t s_bid, s_prefix;
+                                                             uint32_t *__restrict__ zero, uint2 *__restrict__ ranges) {
+    __shared__ uint32_t s_own[kEmitChunk];
+    __shared__ uint32_t s_off[kEmitChunk + 2];
+    __shared__ uint32_t s_n[kEmitChunk + 1];
+    __shared__ uint32_t s_hist[kMaxPasses][256];
+    __shared__ uint32_t s_w[4];
+    __shared__ uint32_t s_prefix;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     {
         const int gt = blockIdx.x * 256 + tid;
         if (gt < a.gx * a.gy) ranges[gt] = make_uint2(0u, 0u);
     }
-    if (tid == 0) s_bid = atomicAdd(chain, 1u);
-    __syncthreads();
-    const uint32_t b = s_bid;
+    const uint32_t b = blockIdx.x;
     const uint32_t c0 = b * kEmitChunk;
     if (c0 >= (uint32_t)L) return;  // grid padding for the range zeroing
     const uint32_t c1 = min((uint32_t)L, c0 + kEmitChunk);
-    const uint32_t *__restrict__ off = g.cand_off;
-    // ranks owning candidates c0 and c1-1: the last r with off[r] <= x (256-ary search, off[P] = L)
-    int lo0 = 0, hi0 = a.P, lo1 = 0, hi1 = a.P;
-    while (hi0 - lo0 > 1 || hi1 - lo1 > 1) {
-        const int st0 = (hi0 - lo0 + 255) / 256, st1 = (hi1 - lo1 + 255) / 256;
-        const int p0 = lo0 + tid * st0, p1 = lo1 + tid * st1;
-        const int n0 = __syncthreads_count(tid > 0 && p0 < hi0 && off[p0] <= c0);
-        const int n1 = __syncthreads_count(tid > 0 && p1 < hi1 && off[p1] <= c1 - 1);
-        lo0 += n0 * st0;
-        hi0 = min(hi0, lo0 + st0);
-        lo1 += n1 * st1;
-        hi1 = min(hi1, lo1 + st1);
-    }
-    // unbinned Gaussians (area 0) sort last, so every rank in [lo0, lo1] has area >= 1: nr <= 2048
-    const int rlo = lo0, nr = lo1 - lo0 + 1;
-    for (int i = tid; i <= nr; i += 256) s_off[i] = off[rlo + i];
-    for (int i = tid; i < nr; i += 256) s_n[i] = 0;
+    const int rlo = (int)g.first_rank[b];
+    const int nr = min(a.P - rlo, kEmitChunk + 1);  // ranks starting at or after c1 are ignored
+    for (int i = tid; i < kEmitChunk; i += 256) s_own[i] = 0;
+    for (int i = tid; i < kMaxPasses * 256; i += 256) (&s_hist[0][0])[i] = 0;
     __syncthreads();
-    uint32_t tile[kEmitItems], gid[kEmitItems];
-    uint64_t kept[kEmitItems];
+    for (int i = tid; i < nr; i += 256) {
+        const uint32_t st = g.cand_off[rlo + i];
+        s_off[i] = st;
+        s_n[i] = 0;
+        if (st > c0 && st < c1) s_own[st - c0] = (uint32_t)i;
+    }
+    if (tid == 0) s_off[nr] = g.cand_off[rlo + nr];
+    __syncthreads();
+    // inclusive max-scan of the marks over the lane's 8 slots, then across lanes
+    uint32_t own[kEmitPer];
+    uint32_t mx = 0;
 #pragma unroll
-    for (int it = 0; it < kEmitItems; it++) {
-        const uint32_t c = c0 + it * 256 + tid;
-        bool keep = false;
-        tile[it] = 0;
-        gid[it] = 0;
+    for (int k = 0; k < kEmitPer; k++) {
+        mx = max(mx, s_own[tid * kEmitPer + k]);
+        own[k] = mx;
+    }
+    {
+        uint32_t x = mx;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(x, off);
+            if (lane >= off) x = max(x, y);
+        }
+        if (lane == 63) s_w[w] = x;
+        __syncthreads();
+        uint32_t carry = __shfl_up(x, 1);
+        if (lane == 0) carry = 0;
+        for (int q = 0; q < w; q++) carry = max(carry, s_w[q]);
+#pragma unroll
+        for (int k = 0; k < kEmitPer; k++) own[k] = max(own[k], carry);
+    }
+    // test the candidates
+    uint32_t tile[kEmitPer];
+    uint32_t keep = 0;
+#pragma unroll
+    for (int k = 0; k < kEmitPer; k++) {
+        const uint32_t c = c0 + tid * kEmitPer + k;
+        tile[k] = 0;
         if (c < c1) {
-            int l = 0, h = nr - 1;  // last j with s_off[j] <= c
-            while (l < h) {
-                const int m = (l + h + 1) >> 1;
-                if (s_off[m] <= c) l = m; else h = m - 1;
-            }
-            const uint32_t id = g.dvals[0][rlo + l];
-            const float2 p = g.xy[id];
+            const int i = (int)own[k];
+            const float4 geo = g.rank_geo[rlo + i];
             int x0, y0, x1, y1;
-            getRect(p.x, p.y, radii[id], a.gx, a.gy, x0, y0, x1, y1);
-            const uint32_t local = c - s_off[l], wdt = (uint32_t)(x1 - x0);
+            getRect(geo.x, geo.y, __float_as_int(geo.z), a.gx, a.gy, x0, y0, x1, y1);
+            const uint32_t local = c - s_off[i], wdt = (uint32_t)(x1 - x0);
             const int ty = y0 + (int)(local / wdt), tx = x0 + (int)(local % wdt);
-            const uint32_t area = s_off[l + 1] - s_off[l];
-            keep = area > kTightMaxArea || tile_reached(p.x, p.y, g.conic_opacity[id], tx, ty, a.W, a.H);
-            tile[it] = (uint32_t)(ty * a.gx + tx);
-            gid[it] = id;
-            if (keep) atomicAdd(&s_n[l], 1u);
+            const uint32_t area = s_off[i + 1] - s_off[i];
+            if (area > kTightMaxArea || tile_reached(geo.x, geo.y, g.rank_co[rlo + i], tx, ty, a.W, a.H)) {
+                keep |= 1u << k;
+                tile[k] = (uint32_t)(ty * a.gx + tx);
+                atomicAdd(&s_n[i], 1u);
+                for (int p = 0; p < npass; p++) atomicAdd(&s_hist[p][(tile[k] >> (8 * p)) & 0xFFu], 1u);
+            }
         }
-        kept[it] = __ballot(keep);
-        if (lane == 0) s_cnt[it][w] = (uint32_t)__popcll(kept[it]);
+    }
+    // compaction offsets: exclusive scan of the per-lane counts, chunk total chained by look-back
+    const uint32_t cnt = __popc(keep);
+    uint32_t x = cnt;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off);
+        if (lane >= off) x += y;
     }
     __syncthreads();
-    if (tid == 0) {
-        uint32_t total = 0;
-        for (int it = 0; it < kEmitItems; it++)
-            for (int q = 0; q < 4; q++) total += s_cnt[it][q];
-        s_prefix = look_back(chain + 64, 1, b, total, chain + 1);
-        if (c1 == (uint32_t)L) counters[0] = s_prefix + total;
+    if (lane == 63) s_w[w] = x;
+    __syncthreads();
+    uint32_t before = 0, total = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        before += q < w ? s_w[q] : 0u;
+        total += s_w[q];
+    }
+    uint32_t *chain = zero + bin_chain_off();
+    if (w == 0) {
+        const uint32_t p = look_back_wave(chain + 64, b, total, chain + 1);
+        if (lane == 0) {
+            s_prefix = p;
+            if (c1 == (uint32_t)L) zero[0] = p + total;  // L'
+        }
     }
     __syncthreads();
-    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    uint32_t run = s_prefix;
+    uint32_t e = s_prefix + before + x - cnt;
 #pragma unroll
-    for (int it = 0; it < kEmitItems; it++) {
-        uint32_t before = 0, step = 0;
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            before += q < w ? s_cnt[it][q] : 0u;
-            step += s_cnt[it][q];
+    for (int k = 0; k < kEmitPer; k++) {
+        if ((keep >> k) & 1u) {
+            keys[e] = tile[k];
+            gid_by_e[e] = __float_as_uint(g.rank_geo[rlo + own[k]].w);
+            e++;
         }
-        if ((kept[it] >> lane) & 1ull) {
-            const uint32_t e = run + before + (uint32_t)__popcll(kept[it] & lt_mask);
-            keys[e] = tile[it];
-            gid_by_e[e] = gid[it];
-        }
-        run += step;
     }
     for (int i = tid; i < nr; i += 256)
-        if (s_n[i]) atomicAdd(&g.n_inst[g.dvals[0][rlo + i]], s_n[i]);
+        if (s_n[i]) atomicAdd(&g.n_inst[__float_as_uint(g.rank_geo[rlo + i].w)], s_n[i]);
+    uint32_t *hist = zero + kZeroHist + (b % kHistShards) * (kMaxPasses * 256);
+    for (int p = 0; p < npass; p++)
+        if (s_hist[p][tid]) atomicAdd(&hist[p * 256 + tid], s_hist[p][tid]);
 }
 
 // K5: tile ranges from the sorted tile keys (rasterizer_impl.cu:116-138); tiles without instances
@@ -452,22 +506,26 @@ __global__ void tile_ranges_kernel(const uint32_t *__restrict__ keys, const uint
 
 hipError_t launch_binning(const Args &a, GeomState g, const int *radii, BinningState b, int L, ImageState img,
                           hipStream_t s) {
+    (void)radii;
     const int T = a.gx * a.gy;
-    hipError_t e = hipMemsetAsync(b.scratch, 0, 4 * binning_scratch_words(L), s);
+    hipError_t e = hipMemsetAsync(b.scratch, 0, 4 * binning_zero_words(L), s);
     if (e != hipSuccess) return e;
     if (L == 0) return hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)T, s);
-    uint32_t *counters = b.scratch;
-    uint32_t *chain = counters + 64;
-    const int nchunk = (L + kEmitChunk - 1) / kEmitChunk;
-    const int nblk = max(nchunk, (T + 255) / 256);
-    hipLaunchKernelGGL(emit_instances_kernel, dim3(nblk), dim3(256), 0, s, a, g, radii, L, b.keys[0], b.gid_by_e,
-                       counters, chain, img.ranges);
-    const uint32_t *n_dev = counters;  // L' <= L reached instances
+    const int npass = (b.key_bits + 7) / 8;
+    const int nblk = std::max<int>((int)nchunk_emit(L), (T + 255) / 256);
+    hipLaunchKernelGGL(emit_instances_kernel, dim3(nblk), dim3(256), 0, s, a, g, L, npass, b.keys[0], b.gid_by_e,
+                       b.scratch, img.ranges);
+    const uint32_t *n_dev = b.scratch;  // L' <= L reached instances
     uint32_t *keys[2] = {b.keys[0], b.keys[1]};
     uint32_t *vals[2] = {b.vals[0], b.vals[1]};
-    const EpiPtrs epi = {b.point_list, b.gid_by_e, b.upos, nullptr};
-    const int buf = onesweep_sort<kItemsL, kEpiInstances>(keys, vals, L, n_dev, b.key_bits,
-                                                          chain + chain_words(nchunk), epi, s);
+    EpiPtrs epi = {};
+    epi.on = true;
+    epi.point_list = b.point_list;
+    epi.gid_by_e = b.gid_by_e;
+    epi.upos = b.upos;
+    const int buf = onesweep_sort<kItemsL, kEpiInstances>(keys, vals, L, n_dev, b.key_bits, b.scratch + kZeroHist,
+                                                          b.scratch + bin_look_off(L), b.scratch + bin_chain_off() + 1,
+                                                          epi, s);
     hipLaunchKernelGGL(tile_ranges_kernel, dim3((L + 255) / 256), dim3(256), 0, s, keys[buf], n_dev, img.ranges);
     return hipGetLastError();
 }

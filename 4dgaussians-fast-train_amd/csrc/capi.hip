@@ -3,6 +3,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -44,24 +45,24 @@ static void mark(const char *name, hipStream_t s) {
     if (!g_profiling) return;
     hipEvent_t ev;
     if (hipEventCreate(&ev) != hipSuccess) return;
-    hipEventRecord(ev, s);
+    (void)hipEventRecord(ev, s);
     g_marks.emplace_back(name, ev);
 }
 static void begin_marks(hipStream_t s) {
-    for (auto &m : g_marks) hipEventDestroy(m.second);
+    for (auto &m : g_marks) (void)hipEventDestroy(m.second);
     g_marks.clear();
     mark("begin", s);
 }
 static void end_marks() {
     if (!g_profiling || g_marks.empty()) return;
-    hipEventSynchronize(g_marks.back().second);
+    (void)hipEventSynchronize(g_marks.back().second);
     g_timings.clear();
     for (size_t i = 1; i < g_marks.size(); i++) {
         float ms = 0.f;
-        hipEventElapsedTime(&ms, g_marks[i - 1].second, g_marks[i].second);
+        (void)hipEventElapsedTime(&ms, g_marks[i - 1].second, g_marks[i].second);
         g_timings.emplace_back(g_marks[i].first, ms);
     }
-    for (auto &m : g_marks) hipEventDestroy(m.second);
+    for (auto &m : g_marks) (void)hipEventDestroy(m.second);
     g_marks.clear();
 }
 
@@ -72,10 +73,10 @@ static char *carve(char *&p, size_t bytes) {
 }
 
 // Sizes are computed by carving from a null base, so required() and carve() cannot disagree.
-size_t GeomState::required(int P) { return (size_t)carve(nullptr, P).sort_scratch + 4 * geom_scratch_words(P) + 512; }
-GeomState GeomState::carve(char *base, int P) {
+size_t GeomState::required(int P, int T) { return (size_t)carve(nullptr, P, T).zero + 4 * geom_zero_words(P) + 512; }
+GeomState GeomState::carve(char *base, int P, int T) {
     char *p = (char *)align_up((size_t)base, 256);
-    const size_t n = (size_t)P, nb = (n + kPreprocessBlock - 1) / kPreprocessBlock + 1;
+    const size_t n = (size_t)P;
     GeomState g;
     g.depths = (float *)gs4d::carve(p, 4 * n);
     g.radii = (int *)gs4d::carve(p, 4 * n);
@@ -86,14 +87,16 @@ GeomState GeomState::carve(char *base, int P) {
     g.clamped = (uint8_t *)gs4d::carve(p, n);
     g.tiles_touched = (uint32_t *)gs4d::carve(p, 4 * n);
     g.n_inst = (uint32_t *)gs4d::carve(p, 4 * n);
-    g.block_area = (uint32_t *)gs4d::carve(p, 4 * nb);
     g.dkeys[0] = (uint32_t *)gs4d::carve(p, 4 * n);
     g.dkeys[1] = (uint32_t *)gs4d::carve(p, 4 * n);
     g.dvals[0] = (uint32_t *)gs4d::carve(p, 4 * n);
     g.dvals[1] = (uint32_t *)gs4d::carve(p, 4 * n);
     g.area_rank = (uint32_t *)gs4d::carve(p, 4 * n);
     g.cand_off = (uint32_t *)gs4d::carve(p, 4 * n + 4);
-    g.sort_scratch = (uint32_t *)gs4d::carve(p, 4 * geom_scratch_words(P));
+    g.rank_geo = (float4 *)gs4d::carve(p, 16 * n);
+    g.rank_co = (float4 *)gs4d::carve(p, 16 * n);
+    g.first_rank = (uint32_t *)gs4d::carve(p, 4 * max_emit_chunks(P, T));
+    g.zero = (uint32_t *)gs4d::carve(p, 4 * geom_zero_words(P));
     return g;
 }
 
@@ -128,7 +131,7 @@ namespace gs4d {
 // instances are sorted by tile id only; tile ids need msb(T) bits (rasterizer_impl.cu:301)
 size_t BinningState::required(int L, int T) {
     BinningState b = carve(nullptr, L, T);
-    return (size_t)b.scratch + 4 * binning_scratch_words(L) + 512;
+    return (size_t)b.scratch + 4 * binning_zero_words(L) + 512;
 }
 BinningState BinningState::carve(char *base, int L, int T) {
     char *p = (char *)align_up((size_t)base, 256);
@@ -141,7 +144,7 @@ BinningState BinningState::carve(char *base, int L, int T) {
     b.gid_by_e = (uint32_t *)gs4d::carve(p, 4 * (size_t)L);
     b.point_list = (uint32_t *)gs4d::carve(p, 4 * (size_t)L);
     b.upos = (uint32_t *)gs4d::carve(p, 4 * (size_t)L);
-    b.scratch = (uint32_t *)gs4d::carve(p, 4 * binning_scratch_words(L));
+    b.scratch = (uint32_t *)gs4d::carve(p, 4 * binning_zero_words(L));
     return b;
 }
 
@@ -218,45 +221,41 @@ int gs4d_forward(gs4d_alloc_fn geometry_alloc, void *geometry_ctx, gs4d_alloc_fn
                        tan_fovy, prefiltered);
     begin_marks(stream);
 
-    char *gbuf = geometry_alloc(geometry_ctx, GeomState::required(P) + 16);
+    const int T = a.gx * a.gy;
+    char *gbuf = geometry_alloc(geometry_ctx, GeomState::required(P, T) + 16);
     if (!gbuf) return fail(GS4D_ERR_ALLOC, "forward: geometry buffer allocation failed");
-    GeomState g = GeomState::carve(gbuf, P);
+    GeomState g = GeomState::carve(gbuf, P, T);
     char *ibuf = image_alloc(image_ctx, ImageState::required(width, height));
     if (!ibuf) return fail(GS4D_ERR_ALLOC, "forward: image buffer allocation failed");
     ImageState img = ImageState::carve(ibuf, width, height);
     int *radii_ptr = radii ? radii : g.radii;
 
-    // the prefiltered error flag lives in the (zeroed) first word of ranges until binning starts
-    int *flag = (int *)img.ranges;
-    if (prefiltered) GS4D_HIP(hipMemsetAsync(flag, 0, sizeof(int), stream));
-
+    // one memset: prefiltered flag, num_rendered shards, depth-sort histograms and look-back words
+    GS4D_HIP(hipMemsetAsync(g.zero, 0, 4 * geom_zero_words(P), stream));
     GS4D_STAGE("preprocess", launch_preprocess(a, means3D, scales, rotations, opacities, shs, cov3D_precomp,
-                                               colors_precomp, radii_ptr, g, flag, stream));
-    GS4D_STAGE("scan", launch_scan_blocks(P, g, stream));
+                                               colors_precomp, radii_ptr, g, (int *)(g.zero + kZeroFlag), stream));
 
     // H1: the single device->host synchronisation of the forward (rasterizer_impl.cu:282).  The depth
     // ordering is enqueued before the host waits, so the GPU keeps working during the round trip.
     static thread_local uint32_t *pinned = nullptr;
     static thread_local hipEvent_t copied = nullptr;
-    if (!pinned) GS4D_HIP(hipHostMalloc((void **)&pinned, 16, hipHostMallocDefault));
+    if (!pinned) GS4D_HIP(hipHostMalloc((void **)&pinned, 128, hipHostMallocDefault));
     if (!copied) GS4D_HIP(hipEventCreateWithFlags(&copied, hipEventDisableTiming));
-    const int nblk = (P + kPreprocessBlock - 1) / kPreprocessBlock;
-    GS4D_HIP(hipMemcpyAsync(pinned, g.block_area + nblk, 4, hipMemcpyDeviceToHost, stream));
-    if (prefiltered) GS4D_HIP(hipMemcpyAsync(pinned + 1, flag, 4, hipMemcpyDeviceToHost, stream));
+    GS4D_HIP(hipMemcpyAsync(pinned, g.zero, 4 * (kZeroL + 16), hipMemcpyDeviceToHost, stream));
     GS4D_HIP(hipEventRecord(copied, stream));
-    GS4D_STAGE("depth_order", launch_depth_order(a, g, stream));
+    GS4D_STAGE("depth_order", launch_depth_order(a, g, radii_ptr, stream));
     GS4D_HIP(hipEventSynchronize(copied));
-    if (prefiltered && pinned[1] != 0)
+    if (prefiltered && pinned[kZeroFlag] != 0)
         return fail(GS4D_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
     // num_rendered keeps the reference's meaning (all 3-sigma rect instances, rasterizer_impl.cu:282)
     // and sizes the binning buffer; only the L' <= L instances that reach a pixel are materialised,
     // and L' stays on the device.
-    const uint32_t L32 = pinned[0];
-    if (L32 >= (1u << 30)) return fail(GS4D_ERR_ARG, "forward: more than 2^30 tile instances");
-    const int L = (int)L32;
+    uint64_t L64 = 0;
+    for (int i = 0; i < kHistShards; i++) L64 += reinterpret_cast<const uint64_t *>(pinned + kZeroL)[i];
+    if (L64 >= (1u << 30)) return fail(GS4D_ERR_ARG, "forward: more than 2^30 tile instances");
+    const int L = (int)L64;
     *num_rendered = L;
 
-    const int T = a.gx * a.gy;
     char *bbuf = binning_alloc(binning_ctx, BinningState::required(L, T));
     if (!bbuf) return fail(GS4D_ERR_ALLOC, "forward: binning buffer allocation failed");
     BinningState b = BinningState::carve(bbuf, L, T);
@@ -288,10 +287,10 @@ int gs4d_backward(int P, int D, int M, int R, const float *background, int width
     Args a = make_args(P, D, M, width, height, background, scale_modifier, viewmatrix, projmatrix, campos, tan_fovx,
                        tan_fovy, 0);
     begin_marks(stream);
-    GeomState g = GeomState::carve(geom_buffer, P);
+    const int T = a.gx * a.gy;
+    GeomState g = GeomState::carve(geom_buffer, P, T);
     ImageState img = ImageState::carve(image_buffer, width, height);
     const int *radii_ptr = radii ? radii : g.radii;
-    const int T = a.gx * a.gy;
     // backward scratch: per-instance gradient records (R x 48 B) | per-Gaussian conic gradients |
     // segmented-reduction partials
     const size_t rec_bytes = align_up((size_t)R * kContribStride * sizeof(float), 256);

@@ -28,15 +28,24 @@ struct GeomState {
     uint8_t *clamped;         // P   bit c set when channel c was clamped (forward.cu:67-69)
     uint32_t *tiles_touched;  // P   3-sigma rect area (the reference's tiles_touched, forward.cu:255)
     uint32_t *n_inst;         // P   tiles of the rect actually reached (tile_reached), <= tiles_touched
-    uint32_t *block_area;     // nblk_pre + 1: exclusive offsets of tiles_touched per id workgroup, [nblk] = L
     uint32_t *dkeys[2];       // P   depth-sort keys (ping-pong)
     uint32_t *dvals[2];       // P   depth-sort ids; dvals[0] = Gaussian id by depth rank after the sort
     uint32_t *area_rank;      // P   tiles_touched by depth rank
     uint32_t *cand_off;       // P+1 exclusive scan of area_rank: first candidate instance of each rank
-    uint32_t *sort_scratch;   // geom_scratch_words(P)
-    static size_t required(int P);
-    static GeomState carve(char *base, int P);
+    float4 *rank_geo;         // P   by depth rank: (x, y, radius bits, Gaussian id bits)
+    float4 *rank_co;          // P   by depth rank: conic_opacity
+    uint32_t *first_rank;     // nchunk_max: depth rank owning candidate j * kEmitChunk
+    uint32_t *zero;           // geom_zero_words(P): counters, histograms, look-back words (one memset)
+    static size_t required(int P, int T);
+    static GeomState carve(char *base, int P, int T);
 };
+// Zero regions (u32 words) of the geometry and binning states: [0..63] counters, then radix-sort
+// digit histograms [kHistShards][kMaxPasses][256] (producers add with atomics sharded by workgroup,
+// so no address takes more than 1/8 of the adds), then look-back words.
+// geometry: [0] prefiltered flag, [8..23] 8 u64 shards of num_rendered; binning: [0] = L'.
+constexpr int kZeroFlag = 0, kZeroL = 8, kZeroHist = 64;
+constexpr int kHistShards = 8, kMaxPasses = 4;
+constexpr int kHistWords = kHistShards * kMaxPasses * 256;
 
 struct ImageState {
     float *final_T;       // W*H
@@ -47,13 +56,16 @@ struct ImageState {
 };
 
 // Sized for L = num_rendered instances; only the L' <= L reached ones are used (L' lives on the device).
+constexpr int kEmitChunk = 2048;  // candidate instances per emission workgroup
+size_t max_emit_chunks(int P, int T);
+
 struct BinningState {
     uint32_t *keys[2];      // L each: tile id of each instance (ping-pong)
     uint32_t *vals[2];      // L each: emission slot of each instance (ping-pong)
     uint32_t *gid_by_e;     // L   Gaussian id of each emission slot
     uint32_t *point_list;   // L   Gaussian id of each sorted instance (render order)
     uint32_t *upos;         // L   emission slot of each sorted instance (where its gradient record goes)
-    uint32_t *scratch;      // binning_scratch_words(L); word 0 = L' (emitted instances)
+    uint32_t *scratch;      // binning_zero_words(L), zeroed by one memset; word 0 = L' (emitted instances)
     int key_bits;           // msb(T) (rasterizer_impl.cu:301)
     static size_t required(int L, int T);
     static BinningState carve(char *base, int L, int T);
@@ -75,8 +87,8 @@ __device__ __forceinline__ Mat4 load_mat4(const float *__restrict__ p) {
 }
 __device__ __forceinline__ V3 load_v3(const float *__restrict__ p) { return v3(p[0], p[1], p[2]); }
 
-size_t geom_scratch_words(int P);
-size_t binning_scratch_words(int L);
+size_t geom_zero_words(int P);
+size_t binning_zero_words(int L);
 
 // ---- exact tile culling ------------------------------------------------------------------------
 // The reference bins a splat into every tile of its 3-sigma rectangle (forward.cu:232-237), but a
@@ -117,8 +129,7 @@ hipError_t launch_preprocess(const Args &a, const float *means3D, const float *s
                              const float *opacities, const float *shs, const float *cov3D_precomp,
                              const float *colors_precomp, int *radii, GeomState g, int *err_flag, hipStream_t s);
 hipError_t launch_mark_visible(int P, const float *means3D, const float *viewmatrix, uint8_t *present, hipStream_t s);
-hipError_t launch_scan_blocks(int P, GeomState g, hipStream_t s);
-hipError_t launch_depth_order(const Args &a, GeomState g, hipStream_t s);
+hipError_t launch_depth_order(const Args &a, GeomState g, const int *radii, hipStream_t s);
 hipError_t launch_binning(const Args &a, GeomState g, const int *radii, BinningState b, int L, ImageState img,
                           hipStream_t s);
 hipError_t launch_render_forward(const Args &a, GeomState g, BinningState b, ImageState img, float *out_color,

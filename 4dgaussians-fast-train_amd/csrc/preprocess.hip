@@ -7,14 +7,18 @@
 
 namespace gs4d {
 
-// One thread per Gaussian.  Besides the reference's outputs it produces the per-workgroup sum of
-// tiles_touched (block_area), so that the prefix sum needs only one more single-workgroup pass, and
-// the depth-sort key of the Gaussian (binning.hip).
+// One thread per Gaussian.  Besides the reference's outputs it produces num_rendered (the sum of
+// tiles_touched, added per workgroup into 8 sharded u64 counters: only the total is ever needed) and
+// the depth-sort key of the Gaussian with its digit histograms for the radix sort (binning.hip).
 __global__ __launch_bounds__(kPreprocessBlock) void preprocess_kernel(
     Args a, const float *__restrict__ means3D, const float *__restrict__ scales, const float *__restrict__ rotations,
     const float *__restrict__ opacities, const float *__restrict__ shs, const float *__restrict__ cov3D_precomp,
     const float *__restrict__ colors_precomp, int *__restrict__ radii, GeomState g, int *__restrict__ err_flag) {
     __shared__ uint32_t s_wave[kPreprocessBlock / 64];
+    __shared__ uint32_t s_hist[4][256];
+#pragma unroll
+    for (int p = 0; p < 4; p++) s_hist[p][threadIdx.x] = 0;
+    __syncthreads();
     const int idx = blockIdx.x * kPreprocessBlock + threadIdx.x;
     const Mat4 view = load_mat4(a.viewmatrix), proj = load_mat4(a.projmatrix);
     uint32_t touched = 0;
@@ -85,7 +89,10 @@ __global__ __launch_bounds__(kPreprocessBlock) void preprocess_kernel(
         radii[idx] = my_r;
         g.tiles_touched[idx] = touched;
         // depth-sort key (binning.hip): positive depths order as their bits; unbinned sort last
-        g.dkeys[0][idx] = touched ? __float_as_uint(p_view.z) : 0xFFFFFFFFu;
+        const uint32_t key = touched ? __float_as_uint(p_view.z) : 0xFFFFFFFFu;
+        g.dkeys[0][idx] = key;
+#pragma unroll
+        for (int p = 0; p < 4; p++) atomicAdd(&s_hist[p][(key >> (8 * p)) & 0xFFu], 1u);
     }
     // workgroup sum of tiles_touched
     uint32_t v = touched;
@@ -93,12 +100,17 @@ __global__ __launch_bounds__(kPreprocessBlock) void preprocess_kernel(
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
     if ((threadIdx.x & 63) == 0) s_wave[threadIdx.x >> 6] = v;
     __syncthreads();
+    const int shard = blockIdx.x % kHistShards;
     if (threadIdx.x == 0) {
         uint32_t t = 0;
 #pragma unroll
         for (int w = 0; w < kPreprocessBlock / 64; w++) t += s_wave[w];
-        g.block_area[blockIdx.x] = t;
+        if (t) atomicAdd(reinterpret_cast<unsigned long long *>(g.zero + kZeroL) + shard, (unsigned long long)t);
     }
+    uint32_t *hist = g.zero + kZeroHist + shard * (kMaxPasses * 256);
+#pragma unroll
+    for (int p = 0; p < 4; p++)
+        if (s_hist[p][threadIdx.x]) atomicAdd(&hist[p * 256 + threadIdx.x], s_hist[p][threadIdx.x]);
 }
 
 hipError_t launch_preprocess(const Args &a, const float *means3D, const float *scales, const float *rotations,
@@ -110,46 +122,6 @@ hipError_t launch_preprocess(const Args &a, const float *means3D, const float *s
     return hipGetLastError();
 }
 
-// Exclusive scan of per-workgroup sums in place; sums[n] receives the total.
-// One workgroup of 1024 threads; each thread scans a contiguous chunk serially.
-__global__ __launch_bounds__(1024) void scan_blocks_kernel(uint32_t *__restrict__ sums, int n) {
-    __shared__ uint32_t s_tot[1024 / 64];
-    const int tid = threadIdx.x;
-    const int chunk = (n + 1023) / 1024;
-    const int b = tid * chunk, e = min(n, b + chunk);
-    uint32_t local = 0;
-    for (int i = b; i < e; i++) local += sums[i];
-    // inclusive wave scan
-    const int lane = tid & 63;
-    uint32_t x = local;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        uint32_t y = __shfl_up(x, off);
-        if (lane >= off) x += y;
-    }
-    if (lane == 63) s_tot[tid >> 6] = x;
-    __syncthreads();
-    uint32_t wave_base = 0;
-    for (int w = 0; w < (tid >> 6); w++) wave_base += s_tot[w];
-    uint32_t run = wave_base + x - local;  // exclusive prefix of this thread's chunk
-    for (int i = b; i < e; i++) {
-        uint32_t v = sums[i];
-        sums[i] = run;
-        run += v;
-    }
-    if (tid == 1023) {
-        uint32_t tot = 0;
-        for (int w = 0; w < 1024 / 64; w++) tot += s_tot[w];
-        sums[n] = tot;
-    }
-}
-
-// block_area -> offsets of the 3-sigma instances, [nblk] = num_rendered
-hipError_t launch_scan_blocks(int P, GeomState g, hipStream_t s) {
-    const int nblk = (P + kPreprocessBlock - 1) / kPreprocessBlock;
-    hipLaunchKernelGGL(scan_blocks_kernel, dim3(1), dim3(1024), 0, s, g.block_area, nblk);
-    return hipGetLastError();
-}
 // rasterizer_impl.cu:54-66 checkFrustum
 __global__ void mark_visible_kernel(int P, const float *__restrict__ means3D, const float *__restrict__ viewmatrix,
                                     uint8_t *__restrict__ present) {
