@@ -17,23 +17,24 @@
 //      reference's (tile, depth, id) order: ceil(msb(T)/8) passes over u32 keys (2 at the metric
 //      config instead of 6 over 12-byte pairs).
 // Every pass is one launch.  Digit histograms are accumulated by the kernel that produces the keys
-// (preprocess for depths, emission for tiles).  Scan, compaction and sort passes chain their
-// workgroups by decoupled look-back in launch order (workgroup i waits only on workgroups < i, which
-// the in-order dispatcher has already placed; waits are bounded): one 32-bit status+count word per
-// chunk (and digit), stored and polled with agent-scope relaxed atomics, so each word is its own flag.
+// (preprocess for depths, emission for tiles).  Scan, compaction and sort passes are single launches
+// whose workgroups publish their chunk counts (one 32-bit status+count word per chunk and digit,
+// agent-scope relaxed atomic stores and loads, so each word is its own flag) and sum the counts of
+// all lower chunks directly (sum_published).
 #include <algorithm>
 
 #include "gs4d_internal.h"
 
 namespace gs4d {
 
-constexpr int kSortThreads = 256;
-constexpr int kItemsL = 8;     // keys per lane for the instance sort (2048 per workgroup)
-constexpr int kItemsP = 4;     // keys per lane for the Gaussian depth sort (1024 per workgroup)
+constexpr int kSortThreads = 1024;  // radix-sort workgroup: 16 waves rank one chunk together
+constexpr int kItemsL = 8;     // keys per lane for the instance sort (8192 per workgroup)
+constexpr int kItemsP = 4;     // keys per lane for the Gaussian depth sort (4096 per workgroup)
 constexpr int kScanItems = 4;  // area scan: 1024 per workgroup
 constexpr int kEmitPer = kEmitChunk / 256;  // candidates per lane in the emission pass
-constexpr uint32_t kAgg = 1u << 30, kPrefix = 2u << 30, kValMask = (1u << 30) - 1;
+constexpr uint32_t kAgg = 1u << 30, kValMask = (1u << 30) - 1;
 constexpr uint32_t kSpinLimit = 1u << 20;
+constexpr int kLookBatch = 16;
 
 __device__ __forceinline__ void store_word(uint32_t *p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -46,93 +47,79 @@ __device__ __forceinline__ int count_of(int n_host, const uint32_t *n_dev) {
     return n_dev ? (int)__builtin_amdgcn_readfirstlane(*n_dev) : n_host;
 }
 
-// Decoupled look-back by one thread for one value (words look[p * stride]): publishes c and returns
-// the exclusive prefix over chunks 0..b-1.  Predecessor words are polled 4 at a time.
-__device__ __forceinline__ uint32_t look_back(uint32_t *look, size_t stride, uint32_t b, uint32_t c, uint32_t *err) {
-    uint32_t *mine = look + (size_t)b * stride;
-    if (b == 0) {
-        store_word(mine, kPrefix | c);
-        return 0;
-    }
-    store_word(mine, kAgg | c);
-    uint32_t excl = 0, spins = 0;
-    int p = (int)b - 1;
-    while (p >= 0) {
-        uint32_t v[4];
+// Chunk prefixes without a chain.  Every chunk publishes its count as soon as it is known (status
+// bit kAgg | count, agent-scope store); a chunk then sums the published counts of ALL lower chunks
+// directly, many loads in flight at once.  Chained look-back makes the last of N chunks wait
+// ~N/window round trips; this waits ~1, for O(N) loads per chunk (N is at most a few hundred here).
+// Lower chunks publish before they wait on anything, and the dispatcher starts them first, so the
+// waits terminate; they are bounded anyway (err).
+__device__ __forceinline__ uint32_t sum_published(const uint32_t *look, size_t stride, int b, int first, int step,
+                                                  uint32_t *err) {
+    constexpr int kBatch = 16;
+    uint32_t sum = 0;
+    for (int p0 = first; p0 < b; p0 += kBatch * step) {
+        uint32_t v[kBatch];
+        bool ready = true;
 #pragma unroll
-        for (int i = 0; i < 4; i++) v[i] = p - i >= 0 ? load_word(look + (size_t)(p - i) * stride) : kPrefix;
-        // consume the batch up to the first prefix or the first not-yet-published word
-        int used = 0;
-        bool done = false;
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            if (done || used != i) continue;
-            if ((v[i] & ~kValMask) == 0) continue;  // not published yet: poll again from here
-            excl += v[i] & kValMask;
-            used = i + 1;
-            if (v[i] & kPrefix) done = true;
+        for (int i = 0; i < kBatch; i++) {
+            const int p = p0 + i * step;
+            v[i] = p < b ? load_word(look + (size_t)p * stride) : kAgg;
         }
-        if (done) break;
-        p -= used;
-        if (used == 0) {
-            if (++spins > kSpinLimit) {
-                atomicOr(err, 1u);
-                break;
+#pragma unroll
+        for (int i = 0; i < kBatch; i++) ready &= (v[i] & kAgg) != 0;
+        if (!ready) {
+            // slow path: poll the words one by one (reloaded: v[] must not be indexed dynamically)
+#pragma nounroll
+            for (int i = 0; i < kBatch; i++) {
+                const int p = p0 + i * step;
+                if (p >= b) break;
+                uint32_t w = load_word(look + (size_t)p * stride), spins = 0;
+                while ((w & kAgg) == 0) {
+                    if (++spins > kSpinLimit) {
+                        atomicOr(err, 1u);
+                        w = kAgg;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    w = load_word(look + (size_t)p * stride);
+                }
+                sum += w & kValMask;
             }
-            __builtin_amdgcn_s_sleep(1);
+        } else {
+#pragma unroll
+            for (int i = 0; i < kBatch; i++) sum += v[i] & kValMask;
         }
     }
-    store_word(mine, kPrefix | (excl + c));
-    return excl;
+    return sum;
 }
 
-// Same, by one full wave: 64 predecessors polled per step (lane i <-> chunk b-1-i).  Wave-uniform.
-__device__ __forceinline__ uint32_t look_back_wave(uint32_t *look, uint32_t b, uint32_t c, uint32_t *err) {
-    const int lane = threadIdx.x & 63;
-    if (lane == 0) store_word(look + b, b == 0 ? (kPrefix | c) : (kAgg | c));
-    if (b == 0) return 0;
-    uint32_t excl = 0, spins = 0;
-    int p = (int)b - 1;
-    while (true) {
-        const int q = p - lane;
-        const uint32_t v = q >= 0 ? load_word(look + q) : kPrefix;  // before chunk 0: prefix 0
-        const uint64_t pref = __builtin_amdgcn_ballot_w64((v & kPrefix) != 0);
-        const uint64_t ready = __builtin_amdgcn_ballot_w64((v & ~kValMask) != 0);
-        // lanes needed: up to and including the nearest prefix (all 64 if none)
-        const int last = pref ? __builtin_ctzll(pref) : 63;
-        const uint64_t need = last == 63 ? ~0ull : ((2ull << last) - 1);
-        if ((ready & need) != need) {
-            if (++spins > kSpinLimit) {
-                if (lane == 0) atomicOr(err, 1u);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-            continue;
-        }
-        uint32_t x = lane <= last ? (v & kValMask) : 0u;
+// Exclusive prefix of chunk b's count c over a 256-thread workgroup (call from every thread).
+__device__ __forceinline__ uint32_t block_prefix(uint32_t *look, uint32_t b, uint32_t c, uint32_t *err,
+                                                 uint32_t *s_tmp /* 4 words of LDS */) {
+    const int tid = threadIdx.x;
+    if (tid == 0) store_word(look + b, kAgg | c);
+    uint32_t x = sum_published(look, 1, (int)b, tid, 256, err);
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
-        excl += x;
-        if (pref) break;
-        p -= 64;
-    }
-    if (lane == 0) store_word(look + b, kPrefix | (excl + c));
-    return excl;
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+    __syncthreads();
+    if ((tid & 63) == 0) s_tmp[tid >> 6] = x;
+    __syncthreads();
+    return s_tmp[0] + s_tmp[1] + s_tmp[2] + s_tmp[3];
 }
 
 // ---------------------------------------------------------------------------------------------
 // Zero-region layouts (u32 words).
-static int sort_nblk(int n, int items) { return (n + kSortThreads * items - 1) / (kSortThreads * items); }
+static int sort_nblk(int n, int chunk) { return (n + chunk - 1) / chunk; }
 static size_t nchunk_scan(int P) { return ((size_t)P + 256 * kScanItems - 1) / (256 * kScanItems); }
 static size_t nchunk_emit(int L) { return ((size_t)L + kEmitChunk - 1) / kEmitChunk; }
 // geometry: counters | depth histograms | area-scan chain (+ err) | depth-sort look-back
 __host__ __device__ static size_t geom_chain_off() { return kZeroHist + kHistWords; }
 static size_t geom_look_off(int P) { return geom_chain_off() + nchunk_scan(P) + 64; }
-size_t geom_zero_words(int P) { return geom_look_off(P) + (size_t)4 * 256 * sort_nblk(P, kItemsP) + 64; }
+size_t geom_zero_words(int P) { return geom_look_off(P) + (size_t)4 * 256 * sort_nblk(P, kSortThreads * kItemsP) + 64; }
 // binning: counters | tile histograms | emission chain (+ err) | instance-sort look-back
 __host__ __device__ static size_t bin_chain_off() { return kZeroHist + kHistWords; }
 static size_t bin_look_off(int L) { return bin_chain_off() + nchunk_emit(L) + 64; }
-size_t binning_zero_words(int L) { return bin_look_off(L) + (size_t)kMaxPasses * 256 * sort_nblk(L, kItemsL) + 64; }
+size_t binning_zero_words(int L) { return bin_look_off(L) + (size_t)kMaxPasses * 256 * sort_nblk(L, kSortThreads * kItemsL) + 64; }
 size_t max_emit_chunks(int P, int T) {
     // L < 2^30 is enforced by the caller
     const size_t bound = ((size_t)P * (size_t)T + kEmitChunk - 1) / kEmitChunk;
@@ -163,21 +150,26 @@ struct EpiPtrs {
 //                  n_inst[v] = 0
 //   kEpiInstances: point_list[pos] = gid_by_e[v] (Gaussian id, render order), upos[pos] = v (the
 //                  emission slot, where the backward stores the instance's gradient record)
-template <int ITEMS, int EPI>
-__global__ __launch_bounds__(kSortThreads) void onesweep_kernel(const uint32_t *__restrict__ kin,
-                                                                const uint32_t *__restrict__ vin,
-                                                                uint32_t *__restrict__ kout,
-                                                                uint32_t *__restrict__ vout, int n_host,
-                                                                const uint32_t *__restrict__ n_dev, int shift,
-                                                                const uint32_t *__restrict__ hist,
-                                                                uint32_t *__restrict__ look,
-                                                                uint32_t *__restrict__ err, EpiPtrs e) {
-    __shared__ uint32_t s_cnt[kSortThreads / 64][256];
-    __shared__ uint32_t s_wsum[kSortThreads / 64];
+// MODE: diagnostic knob for tools/bench/sortbench.hip only (0 in the library): 1 skips the chunk
+// prefix sums (wrong order, in-bounds positions: timing only).
+template <int THREADS, int ITEMS, int EPI, int MODE = 0>
+__global__ __launch_bounds__(THREADS) void onesweep_kernel(const uint32_t *__restrict__ kin,
+                                                           const uint32_t *__restrict__ vin,
+                                                           uint32_t *__restrict__ kout, uint32_t *__restrict__ vout,
+                                                           int n_host, const uint32_t *__restrict__ n_dev, int shift,
+                                                           const uint32_t *__restrict__ hist,
+                                                           uint32_t *__restrict__ look, uint32_t *__restrict__ err,
+                                                           EpiPtrs e) {
+    constexpr int NW = THREADS / 64;
+    __shared__ uint32_t s_cnt[NW][256];
+    __shared__ uint32_t s_wsum[4], s_lsum[4];
+    __shared__ uint32_t s_delta[256], s_lexc[256], s_c[256];
+    __shared__ uint32_t s_part[THREADS / 256][256];
+    __shared__ uint32_t s_key[THREADS * ITEMS], s_val[THREADS * ITEMS];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int n = count_of(n_host, n_dev);
     const uint32_t b = blockIdx.x;
-    const size_t wbase = (size_t)b * (kSortThreads * ITEMS) + (size_t)w * (64 * ITEMS);
+    const size_t wbase = (size_t)b * (THREADS * ITEMS) + (size_t)w * (64 * ITEMS);
     uint32_t key[ITEMS], val[ITEMS], lrank[ITEMS];
     // issue every load of the chunk first
 #pragma unroll
@@ -187,22 +179,24 @@ __global__ __launch_bounds__(kSortThreads) void onesweep_kernel(const uint32_t *
         key[r] = valid ? kin[i] : 0u;
         val[r] = valid ? (vin ? vin[i] : (uint32_t)i) : 0u;
     }
-    uint32_t gcount = 0;
+    // threads 0..255 <-> digits: global digit count and its exclusive scan
+    uint32_t gcount = 0, gx = 0;
+    if (tid < 256) {
 #pragma unroll
-    for (int s = 0; s < kHistShards; s++) gcount += hist[s * (kMaxPasses * 256) + tid];
+        for (int s = 0; s < kHistShards; s++) gcount += hist[s * (kMaxPasses * 256) + tid];
+        gx = gcount;
 #pragma unroll
-    for (int q = 0; q < kSortThreads / 64; q++) s_cnt[q][tid] = 0;
-    // exclusive scan of the global digit histogram (thread tid <-> digit tid)
-    uint32_t gx = gcount;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t y = __shfl_up(gx, off);
-        if (lane >= off) gx += y;
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(gx, off);
+            if (lane >= off) gx += y;
+        }
+        if (lane == 63) s_wsum[w] = gx;
     }
-    if (lane == 63) s_wsum[w] = gx;
+    for (int i = tid; i < NW * 256; i += THREADS) (&s_cnt[0][0])[i] = 0;
     __syncthreads();
     uint32_t gbase = gx - gcount;
-    for (int q = 0; q < w; q++) gbase += s_wsum[q];
+    if (tid < 256)
+        for (int q = 0; q < w; q++) gbase += s_wsum[q];
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
 #pragma unroll
     for (int r = 0; r < ITEMS; r++) {
@@ -221,42 +215,109 @@ __global__ __launch_bounds__(kSortThreads) void onesweep_kernel(const uint32_t *
         lrank[r] = old + below;
     }
     __syncthreads();
-    // thread tid <-> digit tid: chunk count, look-back, global offset
-    uint32_t c = 0;
+    // digit threads publish the chunk's digit counts; every thread then sums a strided share of the
+    // lower chunks' published counts of digit tid & 255
+    constexpr int PARTS = THREADS / 256;
+    if (tid < 256) {
+        uint32_t c = 0;
 #pragma unroll
-    for (int q = 0; q < kSortThreads / 64; q++) c += s_cnt[q][tid];
-    const uint32_t excl = look_back(look + tid, 256, b, c, err);
-    {
-        uint32_t run = gbase + excl;
+        for (int q = 0; q < NW; q++) c += s_cnt[q][tid];
+        s_c[tid] = c;
+        store_word(look + (size_t)b * 256 + tid, kAgg | c);
+    }
+    s_part[tid >> 8][tid & 255] = (MODE & 1) ? 0u : sum_published(look + (tid & 255), 256, (int)b, tid >> 8, PARTS, err);
+    __syncthreads();
+    // for every wave's run of the digit: its start in the chunk's locally sorted order; delta[d] maps a
+    // local position of digit d to its global one
+    if (tid < 256) {
+        const uint32_t c = s_c[tid];
+        uint32_t excl = 0;
 #pragma unroll
-        for (int q = 0; q < kSortThreads / 64; q++) {
+        for (int k = 0; k < PARTS; k++) excl += s_part[k][tid];
+        uint32_t x = c;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(x, off);
+            if (lane >= off) x += y;
+        }
+        s_lsum[w] = x;
+        s_delta[tid] = gbase + excl;  // global start of this chunk's run of digit tid
+        s_lexc[tid] = x - c;          // wave-local exclusive part
+    }
+    __syncthreads();
+    if (tid < 256) {
+        uint32_t lbase = s_lexc[tid];
+        for (int q = 0; q < w; q++) lbase += s_lsum[q];
+        s_delta[tid] -= lbase;
+        uint32_t run = lbase;
+#pragma unroll
+        for (int q = 0; q < NW; q++) {
             const uint32_t cq = s_cnt[q][tid];
             s_cnt[q][tid] = run;
             run += cq;
         }
     }
     __syncthreads();
+    // stage the chunk in digit order in LDS, then write it out with consecutive lanes on consecutive
+    // global positions (each digit's run is contiguous in the output)
 #pragma unroll
     for (int r = 0; r < ITEMS; r++) {
-        const size_t i = wbase + (size_t)r * 64 + lane;
-        if (i < (size_t)n) {
-            const uint32_t d = (key[r] >> shift) & 0xFFu;
-            const uint32_t pos = s_cnt[w][d] + lrank[r];
-            kout[pos] = key[r];
-            if (vout) vout[pos] = val[r];
-            if (EPI == kEpiDepth && e.on) {
-                const uint32_t g = val[r];
-                e.area_rank[pos] = e.tiles_touched[g];
-                e.n_inst[g] = 0u;
-                const float2 p = e.xy[g];
-                e.rank_geo[pos] = make_float4(p.x, p.y, __int_as_float(e.radii[g]), __uint_as_float(g));
-                e.rank_co[pos] = e.conic_opacity[g];
-            }
-            if (EPI == kEpiInstances && e.on) {
-                e.point_list[pos] = e.gid_by_e[val[r]];
-                e.upos[pos] = val[r];
-            }
+        if (wbase + (size_t)r * 64 + lane < (size_t)n) {
+            const uint32_t lp = s_cnt[w][(key[r] >> shift) & 0xFFu] + lrank[r];
+            s_key[lp] = key[r];
+            s_val[lp] = val[r];
         }
+    }
+    __syncthreads();
+    const int nvalid = (int)min((size_t)(THREADS * ITEMS), (size_t)n - min((size_t)n, (size_t)b * (THREADS * ITEMS)));
+    uint32_t pos[ITEMS];
+    bool ok[ITEMS];
+#pragma unroll
+    for (int r = 0; r < ITEMS; r++) {
+        const int lp = r * THREADS + tid;
+        ok[r] = lp < nvalid;
+        key[r] = ok[r] ? s_key[lp] : 0u;
+        val[r] = ok[r] ? s_val[lp] : 0u;
+        pos[r] = lp + s_delta[(key[r] >> shift) & 0xFFu];
+    }
+    if (EPI == kEpiDepth && e.on) {
+        uint32_t area[ITEMS];
+        int rad[ITEMS];
+        float2 p[ITEMS];
+        float4 co[ITEMS];
+#pragma unroll
+        for (int r = 0; r < ITEMS; r++) {
+            const uint32_t g = ok[r] ? val[r] : 0u;
+            area[r] = e.tiles_touched[g];
+            rad[r] = e.radii[g];
+            p[r] = e.xy[g];
+            co[r] = e.conic_opacity[g];
+        }
+#pragma unroll
+        for (int r = 0; r < ITEMS; r++) {
+            if (!ok[r]) continue;
+            e.area_rank[pos[r]] = area[r];
+            e.n_inst[val[r]] = 0u;
+            e.rank_geo[pos[r]] = make_float4(p[r].x, p[r].y, __int_as_float(rad[r]), __uint_as_float(val[r]));
+            e.rank_co[pos[r]] = co[r];
+        }
+    }
+    if (EPI == kEpiInstances && e.on) {
+        uint32_t gid[ITEMS];
+#pragma unroll
+        for (int r = 0; r < ITEMS; r++) gid[r] = e.gid_by_e[ok[r] ? val[r] : 0u];
+#pragma unroll
+        for (int r = 0; r < ITEMS; r++) {
+            if (!ok[r]) continue;
+            e.point_list[pos[r]] = gid[r];
+            e.upos[pos[r]] = val[r];
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < ITEMS; r++) {
+        if (!ok[r]) continue;
+        kout[pos[r]] = key[r];
+        if (vout) vout[pos[r]] = val[r];
     }
 }
 
@@ -264,11 +325,11 @@ __global__ __launch_bounds__(kSortThreads) void onesweep_kernel(const uint32_t *
 // launch per pass.  hist = the producer's sharded digit histograms, look = zeroed look-back words.
 // n = n_host, or *n_dev when n_dev != nullptr (then n_host is only the grid-sizing upper bound).
 // Returns the buffer index holding the sorted keys.
-template <int ITEMS, int EPI>
+template <int THREADS, int ITEMS, int EPI, int MODE = 0>
 static int onesweep_sort(uint32_t *keys[2], uint32_t *vals[2], int n_host, const uint32_t *n_dev, int nbits,
                          const uint32_t *hist, uint32_t *look, uint32_t *err, EpiPtrs epi, hipStream_t s) {
     const int npass = (nbits + 7) / 8;
-    const int nblk = sort_nblk(n_host, ITEMS);
+    const int nblk = sort_nblk(n_host, THREADS * ITEMS);
     int cur = 0;
     EpiPtrs none = epi;
     none.on = false;
@@ -276,7 +337,7 @@ static int onesweep_sort(uint32_t *keys[2], uint32_t *vals[2], int n_host, const
         const bool last = p == npass - 1;
         // the instance sort's last pass writes render-order ids instead of sorted values
         uint32_t *vout = (last && EPI == kEpiInstances) ? nullptr : vals[cur ^ 1];
-        hipLaunchKernelGGL((onesweep_kernel<ITEMS, EPI>), dim3(nblk), dim3(kSortThreads), 0, s, keys[cur],
+        hipLaunchKernelGGL((onesweep_kernel<THREADS, ITEMS, EPI, MODE>), dim3(nblk), dim3(THREADS), 0, s, keys[cur],
                            p == 0 ? nullptr : vals[cur], keys[cur ^ 1], vout, n_host, n_dev, 8 * p, hist + 256 * p,
                            look + (size_t)p * 256 * nblk, err, last ? epi : none);
         cur ^= 1;
@@ -290,8 +351,7 @@ static int onesweep_sort(uint32_t *keys[2], uint32_t *vals[2], int n_host, const
 __global__ __launch_bounds__(256) void area_scan_kernel(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
                                                         uint32_t *__restrict__ first_rank, uint32_t jmax,
                                                         int n, uint32_t *__restrict__ chain) {
-    __shared__ uint32_t s_w[4];
-    __shared__ uint32_t s_prefix;
+    __shared__ uint32_t s_w[4], s_tmp[4];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t b = blockIdx.x;
     const size_t base = (size_t)b * (256 * kScanItems) + (size_t)tid * kScanItems;
@@ -315,12 +375,8 @@ __global__ __launch_bounds__(256) void area_scan_kernel(const uint32_t *__restri
         before += q < w ? s_w[q] : 0u;
         total += s_w[q];
     }
-    if (w == 0) {
-        const uint32_t p = look_back_wave(chain + 64, b, total, chain + 1);
-        if (lane == 0) s_prefix = p;
-    }
-    __syncthreads();
-    uint32_t run = s_prefix + before + x - t;
+    const uint32_t prefix = block_prefix(chain + 64, b, total, chain + 1, s_tmp);
+    uint32_t run = prefix + before + x - t;
 #pragma unroll
     for (int i = 0; i < kScanItems; i++) {
         if (base + i < (size_t)n) {
@@ -349,7 +405,7 @@ hipError_t launch_depth_order(const Args &a, GeomState g, const int *radii, hipS
     epi.rank_geo = g.rank_geo;
     epi.rank_co = g.rank_co;
     uint32_t *chain = g.zero + geom_chain_off();
-    onesweep_sort<kItemsP, kEpiDepth>(keys, vals, a.P, nullptr, 32, g.zero + kZeroHist, g.zero + geom_look_off(a.P),
+    onesweep_sort<kSortThreads, kItemsP, kEpiDepth>(keys, vals, a.P, nullptr, 32, g.zero + kZeroHist, g.zero + geom_look_off(a.P),
                                       chain + 1, epi, s);
     hipLaunchKernelGGL(area_scan_kernel, dim3((unsigned)nchunk_scan(a.P)), dim3(256), 0, s, g.area_rank, g.cand_off,
                        g.first_rank, (uint32_t)max_emit_chunks(a.P, a.gx * a.gy), a.P, chain);
@@ -372,8 +428,7 @@ __global__ __launch_bounds__(256) void emit_instances_kernel(Args a, GeomState g
     __shared__ uint32_t s_off[kEmitChunk + 2];
     __shared__ uint32_t s_n[kEmitChunk + 1];
     __shared__ uint32_t s_hist[kMaxPasses][256];
-    __shared__ uint32_t s_w[4];
-    __shared__ uint32_t s_prefix;
+    __shared__ uint32_t s_w[4], s_tmp[4];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     {
         const int gt = blockIdx.x * 256 + tid;
@@ -419,7 +474,14 @@ __global__ __launch_bounds__(256) void emit_instances_kernel(Args a, GeomState g
 #pragma unroll
         for (int k = 0; k < kEmitPer; k++) own[k] = max(own[k], carry);
     }
-    // test the candidates
+    // test the candidates (every gather issued before the first test)
+    float4 geo[kEmitPer], co[kEmitPer];
+#pragma unroll
+    for (int k = 0; k < kEmitPer; k++) {
+        const int r = rlo + (int)own[k];
+        geo[k] = g.rank_geo[r];
+        co[k] = g.rank_co[r];
+    }
     uint32_t tile[kEmitPer];
     uint32_t keep = 0;
 #pragma unroll
@@ -428,13 +490,12 @@ __global__ __launch_bounds__(256) void emit_instances_kernel(Args a, GeomState g
         tile[k] = 0;
         if (c < c1) {
             const int i = (int)own[k];
-            const float4 geo = g.rank_geo[rlo + i];
             int x0, y0, x1, y1;
-            getRect(geo.x, geo.y, __float_as_int(geo.z), a.gx, a.gy, x0, y0, x1, y1);
+            getRect(geo[k].x, geo[k].y, __float_as_int(geo[k].z), a.gx, a.gy, x0, y0, x1, y1);
             const uint32_t local = c - s_off[i], wdt = (uint32_t)(x1 - x0);
             const int ty = y0 + (int)(local / wdt), tx = x0 + (int)(local % wdt);
             const uint32_t area = s_off[i + 1] - s_off[i];
-            if (area > kTightMaxArea || tile_reached(geo.x, geo.y, g.rank_co[rlo + i], tx, ty, a.W, a.H)) {
+            if (area > kTightMaxArea || tile_reached(geo[k].x, geo[k].y, co[k], tx, ty, a.W, a.H)) {
                 keep |= 1u << k;
                 tile[k] = (uint32_t)(ty * a.gx + tx);
                 atomicAdd(&s_n[i], 1u);
@@ -460,20 +521,14 @@ __global__ __launch_bounds__(256) void emit_instances_kernel(Args a, GeomState g
         total += s_w[q];
     }
     uint32_t *chain = zero + bin_chain_off();
-    if (w == 0) {
-        const uint32_t p = look_back_wave(chain + 64, b, total, chain + 1);
-        if (lane == 0) {
-            s_prefix = p;
-            if (c1 == (uint32_t)L) zero[0] = p + total;  // L'
-        }
-    }
-    __syncthreads();
-    uint32_t e = s_prefix + before + x - cnt;
+    const uint32_t prefix = block_prefix(chain + 64, b, total, chain + 1, s_tmp);
+    if (tid == 0 && c1 == (uint32_t)L) zero[0] = prefix + total;  // L'
+    uint32_t e = prefix + before + x - cnt;
 #pragma unroll
     for (int k = 0; k < kEmitPer; k++) {
         if ((keep >> k) & 1u) {
             keys[e] = tile[k];
-            gid_by_e[e] = __float_as_uint(g.rank_geo[rlo + own[k]].w);
+            gid_by_e[e] = __float_as_uint(geo[k].w);
             e++;
         }
     }
@@ -523,7 +578,7 @@ hipError_t launch_binning(const Args &a, GeomState g, const int *radii, BinningS
     epi.point_list = b.point_list;
     epi.gid_by_e = b.gid_by_e;
     epi.upos = b.upos;
-    const int buf = onesweep_sort<kItemsL, kEpiInstances>(keys, vals, L, n_dev, b.key_bits, b.scratch + kZeroHist,
+    const int buf = onesweep_sort<kSortThreads, kItemsL, kEpiInstances>(keys, vals, L, n_dev, b.key_bits, b.scratch + kZeroHist,
                                                           b.scratch + bin_look_off(L), b.scratch + bin_chain_off() + 1,
                                                           epi, s);
     hipLaunchKernelGGL(tile_ranges_kernel, dim3((L + 255) / 256), dim3(256), 0, s, keys[buf], n_dev, img.ranges);
