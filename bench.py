@@ -27,6 +27,9 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: 8.0 TB/s spec
+# VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 4 cycles per SIMD at 2.4 GHz
+# (MI355X_MICROARCH.md: v_fma_f32 issue cost 4 cycles)
+VALU_PEAK_GINST = 256 * 4 * 2.4 / 4
 
 
 def algorithmic_bytes(P, L, W, H, K=16):
@@ -132,13 +135,14 @@ def main():
         dom_bytes = ab["render_backward"] if dom == "bwd.render_backward" else (
             ab["render"] if dom == "fwd.render" else None)
         achieved = dom_bytes / (dom_ms * 1e-3) / 1e9 if dom_bytes else None
-        traffic = None
-        tr_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(tr_path):
+        def pmc(name):
+            path = os.path.join(ROOT, "profiles", name)
             try:
-                traffic = json.load(open(tr_path)).get(dom.split(".", 1)[1], None)
+                return json.load(open(path)).get(dom.split(".", 1)[1], None)
             except Exception:
-                traffic = None
+                return None
+        traffic = pmc("pmc_traffic.json")
+        valu = pmc("pmc_valu.json")
         out = {
             "metric": "rasterizer fwd+bwd MGaussians/s @100k pts, 1352x1014 (train-step ms in ms_per_step)",
             "value": round(value, 3), "unit": "MGaussians/s", "n_gpus": world, "steps": args.steps,
@@ -152,6 +156,12 @@ def main():
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None, "traffic": traffic,
                          "algorithmic_bytes": dom_bytes, "avg_ms": round(dom_ms, 4)},
+            # the blend kernels are VALU-issue bound, not HBM bound: instruction rate vs the issue peak
+            "valu_issue": {"kernel": dom, "insts_per_launch": valu,
+                           "achieved_Ginst_s": round(valu / (dom_ms * 1e-3) / 1e9, 1) if valu else None,
+                           "peak_Ginst_s": VALU_PEAK_GINST,
+                           "frac": round(valu / (dom_ms * 1e-3) / 1e9 / VALU_PEAK_GINST, 4) if valu else None,
+                           "source": "SQ_INSTS_VALU per launch, profiles/pmc_valu.json (rocprofv3 --pmc)"},
             "step_roofline": {"algorithmic_bytes": ab["step"],
                               "achieved_GBs": round(ab["step"] / (ms_per_step * 1e-3) / 1e9, 2),
                               "frac": round(ab["step"] / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)},
