@@ -30,7 +30,6 @@ namespace gs4d {
 constexpr int kSortThreads = 1024;  // radix-sort workgroup: 16 waves rank one chunk together
 constexpr int kItemsL = 8;     // keys per lane for the instance sort (8192 per workgroup)
 constexpr int kItemsP = 4;     // keys per lane for the Gaussian depth sort (4096 per workgroup)
-constexpr int kScanItems = 4;  // area scan: 1024 per workgroup
 constexpr int kEmitPer = kEmitChunk / 256;  // candidates per lane in the emission pass
 constexpr uint32_t kAgg = 1u << 30, kValMask = (1u << 30) - 1;
 constexpr uint32_t kSpinLimit = 1u << 20;
@@ -110,56 +109,36 @@ __device__ __forceinline__ uint32_t block_prefix(uint32_t *look, uint32_t b, uin
 // ---------------------------------------------------------------------------------------------
 // Zero-region layouts (u32 words).
 static int sort_nblk(int n, int chunk) { return (n + chunk - 1) / chunk; }
-static size_t nchunk_scan(int P) { return ((size_t)P + 256 * kScanItems - 1) / (256 * kScanItems); }
+static size_t nchunk_scan(int P) { return ((size_t)P + 255) / 256; }
 static size_t nchunk_emit(int L) { return ((size_t)L + kEmitChunk - 1) / kEmitChunk; }
 // geometry: counters | depth histograms | area-scan chain (+ err) | depth-sort look-back
 __host__ __device__ static size_t geom_chain_off() { return kZeroHist + kHistWords; }
 static size_t geom_look_off(int P) { return geom_chain_off() + nchunk_scan(P) + 64; }
-size_t geom_zero_words(int P) { return geom_look_off(P) + (size_t)4 * 256 * sort_nblk(P, kSortThreads * kItemsP) + 64; }
+// rounded to 256 B so that one fill kernel clears each region
+size_t geom_zero_words(int P) { return align_up(geom_look_off(P) + (size_t)4 * 256 * sort_nblk(P, kSortThreads * kItemsP), 64); }
 // binning: counters | tile histograms | emission chain (+ err) | instance-sort look-back
 __host__ __device__ static size_t bin_chain_off() { return kZeroHist + kHistWords; }
 static size_t bin_look_off(int L) { return bin_chain_off() + nchunk_emit(L) + 64; }
-size_t binning_zero_words(int L) { return bin_look_off(L) + (size_t)kMaxPasses * 256 * sort_nblk(L, kSortThreads * kItemsL) + 64; }
+size_t binning_zero_words(int L) {
+    return align_up(bin_look_off(L) + (size_t)kMaxPasses * 256 * sort_nblk(L, kSortThreads * kItemsL), 64);
+}
 size_t max_emit_chunks(int P, int T) {
     // L < 2^30 is enforced by the caller
     const size_t bound = ((size_t)P * (size_t)T + kEmitChunk - 1) / kEmitChunk;
     return std::min<size_t>(bound, ((size_t)1 << 30) / kEmitChunk) + 1;
 }
 
-enum Epilogue { kEpiDepth = 1, kEpiInstances = 2 };
-// Last-pass side outputs (see onesweep_kernel); `on` == false disables them.
-struct EpiPtrs {
-    bool on;
-    // kEpiInstances: point_list, gid_by_e, upos
-    uint32_t *point_list;
-    const uint32_t *gid_by_e;
-    uint32_t *upos;
-    // kEpiDepth
-    const uint32_t *tiles_touched;
-    uint32_t *area_rank, *n_inst;
-    const float2 *xy;
-    const int *radii;
-    const float4 *conic_opacity;
-    float4 *rank_geo, *rank_co;
-};
-
 // One LSD pass over 8 bits at `shift` (chunk = blockIdx.x).  Values: vin == nullptr -> identity (the
 // item's index).  hist: the 8 shards of the producer's digit histogram for this pass.
-// Epilogue on the last pass:
-//   kEpiDepth:     per depth rank pos of Gaussian v: area_rank[pos], rank_geo[pos], rank_co[pos];
-//                  n_inst[v] = 0
-//   kEpiInstances: point_list[pos] = gid_by_e[v] (Gaussian id, render order), upos[pos] = v (the
-//                  emission slot, where the backward stores the instance's gradient record)
 // MODE: diagnostic knob for tools/bench/sortbench.hip only (0 in the library): 1 skips the chunk
 // prefix sums (wrong order, in-bounds positions: timing only).
-template <int THREADS, int ITEMS, int EPI, int MODE = 0>
+template <int THREADS, int ITEMS, int MODE = 0>
 __global__ __launch_bounds__(THREADS) void onesweep_kernel(const uint32_t *__restrict__ kin,
                                                            const uint32_t *__restrict__ vin,
                                                            uint32_t *__restrict__ kout, uint32_t *__restrict__ vout,
                                                            int n_host, const uint32_t *__restrict__ n_dev, int shift,
                                                            const uint32_t *__restrict__ hist,
-                                                           uint32_t *__restrict__ look, uint32_t *__restrict__ err,
-                                                           EpiPtrs e) {
+                                                           uint32_t *__restrict__ look, uint32_t *__restrict__ err) {
     constexpr int NW = THREADS / 64;
     __shared__ uint32_t s_cnt[NW][256];
     __shared__ uint32_t s_wsum[4], s_lsum[4];
@@ -280,39 +259,6 @@ __global__ __launch_bounds__(THREADS) void onesweep_kernel(const uint32_t *__res
         val[r] = ok[r] ? s_val[lp] : 0u;
         pos[r] = lp + s_delta[(key[r] >> shift) & 0xFFu];
     }
-    if (EPI == kEpiDepth && e.on) {
-        uint32_t area[ITEMS];
-        int rad[ITEMS];
-        float2 p[ITEMS];
-        float4 co[ITEMS];
-#pragma unroll
-        for (int r = 0; r < ITEMS; r++) {
-            const uint32_t g = ok[r] ? val[r] : 0u;
-            area[r] = e.tiles_touched[g];
-            rad[r] = e.radii[g];
-            p[r] = e.xy[g];
-            co[r] = e.conic_opacity[g];
-        }
-#pragma unroll
-        for (int r = 0; r < ITEMS; r++) {
-            if (!ok[r]) continue;
-            e.area_rank[pos[r]] = area[r];
-            e.n_inst[val[r]] = 0u;
-            e.rank_geo[pos[r]] = make_float4(p[r].x, p[r].y, __int_as_float(rad[r]), __uint_as_float(val[r]));
-            e.rank_co[pos[r]] = co[r];
-        }
-    }
-    if (EPI == kEpiInstances && e.on) {
-        uint32_t gid[ITEMS];
-#pragma unroll
-        for (int r = 0; r < ITEMS; r++) gid[r] = e.gid_by_e[ok[r] ? val[r] : 0u];
-#pragma unroll
-        for (int r = 0; r < ITEMS; r++) {
-            if (!ok[r]) continue;
-            e.point_list[pos[r]] = gid[r];
-            e.upos[pos[r]] = val[r];
-        }
-    }
 #pragma unroll
     for (int r = 0; r < ITEMS; r++) {
         if (!ok[r]) continue;
@@ -325,21 +271,17 @@ __global__ __launch_bounds__(THREADS) void onesweep_kernel(const uint32_t *__res
 // launch per pass.  hist = the producer's sharded digit histograms, look = zeroed look-back words.
 // n = n_host, or *n_dev when n_dev != nullptr (then n_host is only the grid-sizing upper bound).
 // Returns the buffer index holding the sorted keys.
-template <int THREADS, int ITEMS, int EPI, int MODE = 0>
+template <int THREADS, int ITEMS, int MODE = 0>
 static int onesweep_sort(uint32_t *keys[2], uint32_t *vals[2], int n_host, const uint32_t *n_dev, int nbits,
-                         const uint32_t *hist, uint32_t *look, uint32_t *err, EpiPtrs epi, hipStream_t s) {
+                         const uint32_t *hist, uint32_t *look, uint32_t *err, hipStream_t s) {
     const int npass = (nbits + 7) / 8;
     const int nblk = sort_nblk(n_host, THREADS * ITEMS);
     int cur = 0;
-    EpiPtrs none = epi;
-    none.on = false;
     for (int p = 0; p < npass; p++) {
-        const bool last = p == npass - 1;
-        // the instance sort's last pass writes render-order ids instead of sorted values
-        uint32_t *vout = (last && EPI == kEpiInstances) ? nullptr : vals[cur ^ 1];
-        hipLaunchKernelGGL((onesweep_kernel<THREADS, ITEMS, EPI, MODE>), dim3(nblk), dim3(THREADS), 0, s, keys[cur],
+        uint32_t *vout = vals[cur ^ 1];
+        hipLaunchKernelGGL((onesweep_kernel<THREADS, ITEMS, MODE>), dim3(nblk), dim3(THREADS), 0, s, keys[cur],
                            p == 0 ? nullptr : vals[cur], keys[cur ^ 1], vout, n_host, n_dev, 8 * p, hist + 256 * p,
-                           look + (size_t)p * 256 * nblk, err, last ? epi : none);
+                           look + (size_t)p * 256 * nblk, err);
         cur ^= 1;
     }
     return cur;
@@ -348,20 +290,26 @@ static int onesweep_sort(uint32_t *keys[2], uint32_t *vals[2], int n_host, const
 // ---------------------------------------------------------------------------------------------
 // Exclusive scan of the rect areas in depth-rank order: cand_off[r] = first candidate of rank r,
 // cand_off[P] = num_rendered; and first_rank[j] = the rank owning candidate j * kEmitChunk.
-__global__ __launch_bounds__(256) void area_scan_kernel(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
-                                                        uint32_t *__restrict__ first_rank, uint32_t jmax,
-                                                        int n, uint32_t *__restrict__ chain) {
+// Rank-ordered splat records and the exclusive scan of the rect areas in depth-rank order:
+// rank_geo[r] / rank_co[r] = the record of the Gaussian of depth rank r (gathered here with the whole
+// chip's memory parallelism -- the sort's last pass runs on a few dozen workgroups only),
+// cand_off[r] = its first candidate, cand_off[P] = num_rendered, first_rank[j] = the rank owning
+// candidate j * kEmitChunk.  One rank per thread; chunk prefixes from the published counts.
+__global__ __launch_bounds__(256) void rank_records_kernel(GeomState g, const int *__restrict__ radii, int n,
+                                                           uint32_t jmax, uint32_t *__restrict__ chain) {
     __shared__ uint32_t s_w[4], s_tmp[4];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t b = blockIdx.x;
-    const size_t base = (size_t)b * (256 * kScanItems) + (size_t)tid * kScanItems;
-    uint32_t v[kScanItems], t = 0;
-#pragma unroll
-    for (int i = 0; i < kScanItems; i++) {
-        v[i] = base + i < (size_t)n ? in[base + i] : 0u;
-        t += v[i];
+    const int r = (int)b * 256 + tid;
+    uint32_t v = 0;
+    if (r < n) {
+        const uint32_t gid = g.dvals[0][r];
+        v = g.tiles_touched[gid];
+        const float2 p = g.xy[gid];
+        g.rank_geo[r] = make_float4(p.x, p.y, __int_as_float(radii[gid]), __uint_as_float(gid));
+        g.rank_co[r] = g.conic_opacity[gid];
     }
-    uint32_t x = t;
+    uint32_t x = v;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
         const uint32_t y = __shfl_up(x, off);
@@ -376,39 +324,25 @@ __global__ __launch_bounds__(256) void area_scan_kernel(const uint32_t *__restri
         total += s_w[q];
     }
     const uint32_t prefix = block_prefix(chain + 64, b, total, chain + 1, s_tmp);
-    uint32_t run = prefix + before + x - t;
-#pragma unroll
-    for (int i = 0; i < kScanItems; i++) {
-        if (base + i < (size_t)n) {
-            out[base + i] = run;
-            // chunk starts inside this rank's candidates
-            for (uint32_t j = (run + kEmitChunk - 1) / kEmitChunk; j * (uint32_t)kEmitChunk < run + v[i] && j < jmax;
-                 j++)
-                first_rank[j] = (uint32_t)(base + i);
-        }
-        run += v[i];
+    const uint32_t run = prefix + before + x - v;
+    if (r < n) {
+        g.cand_off[r] = run;
+        // chunk starts inside this rank's candidates
+        for (uint32_t j = (run + kEmitChunk - 1) / kEmitChunk; j * (uint32_t)kEmitChunk < run + v && j < jmax; j++)
+            g.first_rank[j] = (uint32_t)r;
+        if (r == n - 1) g.cand_off[n] = run + v;
     }
-    if (base < (size_t)n && base + kScanItems >= (size_t)n) out[n] = run;
 }
 
 hipError_t launch_depth_order(const Args &a, GeomState g, const int *radii, hipStream_t s) {
+    // dkeys[0] = depth bits (unbinned: ~0u, last); afterwards dvals[0] = Gaussian id by depth rank
     uint32_t *keys[2] = {g.dkeys[0], g.dkeys[1]};
     uint32_t *vals[2] = {g.dvals[0], g.dvals[1]};
-    EpiPtrs epi = {};
-    epi.on = true;
-    epi.tiles_touched = g.tiles_touched;
-    epi.area_rank = g.area_rank;
-    epi.n_inst = g.n_inst;
-    epi.xy = g.xy;
-    epi.radii = radii;
-    epi.conic_opacity = g.conic_opacity;
-    epi.rank_geo = g.rank_geo;
-    epi.rank_co = g.rank_co;
     uint32_t *chain = g.zero + geom_chain_off();
-    onesweep_sort<kSortThreads, kItemsP, kEpiDepth>(keys, vals, a.P, nullptr, 32, g.zero + kZeroHist, g.zero + geom_look_off(a.P),
-                                      chain + 1, epi, s);
-    hipLaunchKernelGGL(area_scan_kernel, dim3((unsigned)nchunk_scan(a.P)), dim3(256), 0, s, g.area_rank, g.cand_off,
-                       g.first_rank, (uint32_t)max_emit_chunks(a.P, a.gx * a.gy), a.P, chain);
+    onesweep_sort<kSortThreads, kItemsP>(keys, vals, a.P, nullptr, 32, g.zero + kZeroHist,
+                                      g.zero + geom_look_off(a.P), chain + 1, s);
+    hipLaunchKernelGGL(rank_records_kernel, dim3((unsigned)nchunk_scan(a.P)), dim3(256), 0, s, g, radii, a.P,
+                       (uint32_t)max_emit_chunks(a.P, a.gx * a.gy), chain);
     return hipGetLastError();
 }
 
@@ -573,15 +507,9 @@ hipError_t launch_binning(const Args &a, GeomState g, const int *radii, BinningS
     const uint32_t *n_dev = b.scratch;  // L' <= L reached instances
     uint32_t *keys[2] = {b.keys[0], b.keys[1]};
     uint32_t *vals[2] = {b.vals[0], b.vals[1]};
-    EpiPtrs epi = {};
-    epi.on = true;
-    epi.point_list = b.point_list;
-    epi.gid_by_e = b.gid_by_e;
-    epi.upos = b.upos;
-    const int buf = onesweep_sort<kSortThreads, kItemsL, kEpiInstances>(keys, vals, L, n_dev, b.key_bits, b.scratch + kZeroHist,
-                                                          b.scratch + bin_look_off(L), b.scratch + bin_chain_off() + 1,
-                                                          epi, s);
-    hipLaunchKernelGGL(tile_ranges_kernel, dim3((L + 255) / 256), dim3(256), 0, s, keys[buf], n_dev, img.ranges);
+    onesweep_sort<kSortThreads, kItemsL>(keys, vals, L, n_dev, b.key_bits, b.scratch + kZeroHist,
+                                         b.scratch + bin_look_off(L), b.scratch + bin_chain_off() + 1, s);
+    hipLaunchKernelGGL(tile_ranges_kernel, dim3((L + 255) / 256), dim3(256), 0, s, b.sorted_keys, n_dev, img.ranges);
     return hipGetLastError();
 }
 

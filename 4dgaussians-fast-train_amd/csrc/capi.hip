@@ -91,7 +91,6 @@ GeomState GeomState::carve(char *base, int P, int T) {
     g.dkeys[1] = (uint32_t *)gs4d::carve(p, 4 * n);
     g.dvals[0] = (uint32_t *)gs4d::carve(p, 4 * n);
     g.dvals[1] = (uint32_t *)gs4d::carve(p, 4 * n);
-    g.area_rank = (uint32_t *)gs4d::carve(p, 4 * n);
     g.cand_off = (uint32_t *)gs4d::carve(p, 4 * n + 4);
     g.rank_geo = (float4 *)gs4d::carve(p, 16 * n);
     g.rank_co = (float4 *)gs4d::carve(p, 16 * n);
@@ -142,8 +141,9 @@ BinningState BinningState::carve(char *base, int L, int T) {
         b.vals[i] = (uint32_t *)gs4d::carve(p, 4 * (size_t)L);
     }
     b.gid_by_e = (uint32_t *)gs4d::carve(p, 4 * (size_t)L);
-    b.point_list = (uint32_t *)gs4d::carve(p, 4 * (size_t)L);
-    b.upos = (uint32_t *)gs4d::carve(p, 4 * (size_t)L);
+    const int final_buf = ((b.key_bits + 7) / 8) & 1;  // each LSD pass swaps the ping-pong buffers
+    b.upos = b.vals[final_buf];
+    b.sorted_keys = b.keys[final_buf];
     b.scratch = (uint32_t *)gs4d::carve(p, 4 * binning_zero_words(L));
     return b;
 }
@@ -306,7 +306,7 @@ int gs4d_backward(int P, int D, int M, int R, const float *background, int width
         b = BinningState::carve(binning_buffer, R, T);
         const float *color_ptr = colors_precomp;  // NULL -> the forward's rgb (rasterizer_impl.cu:392)
         GS4D_STAGE("render_backward",
-                   launch_render_backward(a, g, b.point_list, b.upos, img, color_ptr, dL_dpix, contrib, stream));
+                   launch_render_backward(a, g, b.gid_by_e, b.upos, img, color_ptr, dL_dpix, contrib, stream));
     }
     GS4D_STAGE("contrib_reduce", launch_contrib_reduce(a, g, b, R, contrib, reduce_scratch, dL_dmean2D, dconic,
                                                        dL_dopacity, dL_dcolor, stream));

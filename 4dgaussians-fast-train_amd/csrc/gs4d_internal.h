@@ -30,8 +30,8 @@ struct GeomState {
     uint32_t *n_inst;         // P   tiles of the rect actually reached (tile_reached), <= tiles_touched
     uint32_t *dkeys[2];       // P   depth-sort keys (ping-pong)
     uint32_t *dvals[2];       // P   depth-sort ids; dvals[0] = Gaussian id by depth rank after the sort
-    uint32_t *area_rank;      // P   tiles_touched by depth rank
-    uint32_t *cand_off;       // P+1 exclusive scan of area_rank: first candidate instance of each rank
+    uint32_t *cand_off;       // P+1 exclusive scan of tiles_touched in depth-rank order: first candidate
+                              //     instance of each rank
     float4 *rank_geo;         // P   by depth rank: (x, y, radius bits, Gaussian id bits)
     float4 *rank_co;          // P   by depth rank: conic_opacity
     uint32_t *first_rank;     // nchunk_max: depth rank owning candidate j * kEmitChunk
@@ -63,8 +63,10 @@ struct BinningState {
     uint32_t *keys[2];      // L each: tile id of each instance (ping-pong)
     uint32_t *vals[2];      // L each: emission slot of each instance (ping-pong)
     uint32_t *gid_by_e;     // L   Gaussian id of each emission slot
-    uint32_t *point_list;   // L   Gaussian id of each sorted instance (render order)
-    uint32_t *upos;         // L   emission slot of each sorted instance (where its gradient record goes)
+    uint32_t *upos;         // = the vals buffer holding the sorted result: emission slot of each instance
+                            //     in render order (its Gaussian is gid_by_e[upos[i]]; its gradient
+                            //     record goes to slot upos[i])
+    uint32_t *sorted_keys;  // = the keys buffer holding the sorted tile ids
     uint32_t *scratch;      // binning_zero_words(L), zeroed by one memset; word 0 = L' (emitted instances)
     int key_bits;           // msb(T) (rasterizer_impl.cu:301)
     static size_t required(int L, int T);
@@ -134,7 +136,7 @@ hipError_t launch_binning(const Args &a, GeomState g, const int *radii, BinningS
                           hipStream_t s);
 hipError_t launch_render_forward(const Args &a, GeomState g, BinningState b, ImageState img, float *out_color,
                                  float *out_depth, hipStream_t s);
-hipError_t launch_render_backward(const Args &a, GeomState g, const uint32_t *point_list, const uint32_t *upos, ImageState img,
+hipError_t launch_render_backward(const Args &a, GeomState g, const uint32_t *gid_by_e, const uint32_t *upos, ImageState img,
                                   const float *colors, const float *dL_dpix, float *contrib, hipStream_t s);
 size_t contrib_scratch_bytes(int R);
 hipError_t launch_contrib_reduce(const Args &a, GeomState g, BinningState b, int R, const float *contrib,

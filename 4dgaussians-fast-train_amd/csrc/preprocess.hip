@@ -88,6 +88,7 @@ __global__ __launch_bounds__(kPreprocessBlock) void preprocess_kernel(
         }
         radii[idx] = my_r;
         g.tiles_touched[idx] = touched;
+        g.n_inst[idx] = 0;
         // depth-sort key (binning.hip): positive depths order as their bits; unbinned sort last
         const uint32_t key = touched ? __float_as_uint(p_view.z) : 0xFFFFFFFFu;
         g.dkeys[0][idx] = key;

@@ -82,7 +82,8 @@ __device__ __forceinline__ bool lane_bit(uint64_t m) { return __builtin_amdgcn_i
 
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void render_forward_kernel(Args a, const uint2 *__restrict__ ranges,
-                                                            const uint32_t *__restrict__ point_list,
+                                                            const uint32_t *__restrict__ upos,
+                                                            const uint32_t *__restrict__ gid_by_e,
                                                             const float2 *__restrict__ xy,
                                                             const float4 *__restrict__ conic_opacity,
                                                             const float4 *__restrict__ rgbd,
@@ -113,7 +114,7 @@ __global__ __launch_bounds__(64) void render_forward_kernel(Args a, const uint2 
     SplatRegs nxt;
     if (range.x < range.y) {
         const bool v = range.x + lane < range.y;
-        load_splat(nxt, v, v ? point_list[range.x + lane] : 0u, xy, conic_opacity, rgbd, nullptr);
+        load_splat(nxt, v, v ? gid_by_e[upos[range.x + lane]] : 0u, xy, conic_opacity, rgbd, nullptr);
     }
     for (uint32_t base = range.x; base < range.y; base += 64) {
         if ((alive[0] | alive[1] | alive[2] | alive[3]) == 0) break;  // forward.cu:312-314
@@ -126,7 +127,7 @@ __global__ __launch_bounds__(64) void render_forward_kernel(Args a, const uint2 
         {
             const uint32_t nb = base + 64;
             const bool v = nb + lane < range.y;
-            if (nb < range.y) load_splat(nxt, v, v ? point_list[nb + lane] : 0u, xy, conic_opacity, rgbd, nullptr);
+            if (nb < range.y) load_splat(nxt, v, v ? gid_by_e[upos[nb + lane]] : 0u, xy, conic_opacity, rgbd, nullptr);
         }
         const uint32_t pos0 = base - range.x;
         // software pipeline: splat j+1's constants are read from LDS while splat j is blended
@@ -203,7 +204,7 @@ __global__ __launch_bounds__(64) void render_forward_kernel(Args a, const uint2 
 hipError_t launch_render_forward(const Args &a, GeomState g, BinningState b, ImageState img, float *out_color,
                                  float *out_depth, hipStream_t s) {
     const int T = a.gx * a.gy;
-    hipLaunchKernelGGL(render_forward_kernel, dim3(T), dim3(64), 0, s, a, img.ranges, b.point_list, g.xy,
+    hipLaunchKernelGGL(render_forward_kernel, dim3(T), dim3(64), 0, s, a, img.ranges, b.upos, b.gid_by_e, g.xy,
                        g.conic_opacity, g.rgbd, img.final_T, img.n_contrib, out_color, out_depth);
     return hipGetLastError();
 }
@@ -254,7 +255,7 @@ __device__ __forceinline__ void wave_sum9_to_lds(const float v[9], float *dst, i
 }
 
 __global__ __launch_bounds__(64) void render_backward_kernel(Args a, const uint2 *__restrict__ ranges,
-                                                             const uint32_t *__restrict__ point_list,
+                                                             const uint32_t *__restrict__ gid_by_e,
                                                              const uint32_t *__restrict__ upos,
                                                              const float2 *__restrict__ xy,
                                                              const float4 *__restrict__ conic_opacity,
@@ -322,8 +323,8 @@ __global__ __launch_bounds__(64) void render_backward_kernel(Args a, const uint2
     auto fetch = [&](int end) {
         const int n = min(64, end);
         const bool v = lane < n;
-        const uint32_t gid = v ? point_list[range.x + end - 1 - lane] : 0u;
         unxt = v ? upos[range.x + end - 1 - lane] : 0u;
+        const uint32_t gid = v ? gid_by_e[unxt] : 0u;
         load_splat(nxt, v, gid, xy, conic_opacity, rgbd, colors);  // colour: colors_precomp or rgb
     };
     if (max_last > 0) fetch((int)max_last);
@@ -392,11 +393,11 @@ __global__ __launch_bounds__(64) void render_backward_kernel(Args a, const uint2
     }
 }
 
-hipError_t launch_render_backward(const Args &a, GeomState g, const uint32_t *point_list, const uint32_t *upos,
+hipError_t launch_render_backward(const Args &a, GeomState g, const uint32_t *gid_by_e, const uint32_t *upos,
                                   ImageState img, const float *colors, const float *dL_dpix, float *contrib,
                                   hipStream_t s) {
     const int T = a.gx * a.gy;
-    hipLaunchKernelGGL(render_backward_kernel, dim3(T), dim3(64), 0, s, a, img.ranges, point_list, upos, g.xy,
+    hipLaunchKernelGGL(render_backward_kernel, dim3(T), dim3(64), 0, s, a, img.ranges, gid_by_e, upos, g.xy,
                        g.conic_opacity, g.rgbd, colors, img.final_T, img.n_contrib, dL_dpix, contrib);
     return hipGetLastError();
 }

@@ -36,7 +36,6 @@ static void run(const char *name, int n, int bits, bool sorted_hi) {
     hipEvent_t a, b;
     CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
     const int npass = (bits + 7) / 8;
-    EpiPtrs none = {};
     float best = 1e9;
     for (int it = 0; it < 20; it++) {
         CK(hipMemcpy(k0, h.data(), 4 * n, hipMemcpyHostToDevice));
@@ -45,9 +44,9 @@ static void run(const char *name, int n, int bits, bool sorted_hi) {
         CK(hipDeviceSynchronize());
         uint32_t *keys[2] = {k0, k1}, *vals[2] = {v0, v1};
         CK(hipEventRecord(a, 0));
-        onesweep_sort<THREADS, ITEMS, kEpiInstances, MODE>(keys, vals, n, nullptr, bits, zero + kZeroHist,
+        onesweep_sort<THREADS, ITEMS, MODE>(keys, vals, n, nullptr, bits, zero + kZeroHist,
                                                      zero + kZeroHist + kHistWords + 64, zero + kZeroHist + kHistWords,
-                                                     none, 0);
+                                                     0);
         CK(hipEventRecord(b, 0));
         CK(hipEventSynchronize(b));
         float ms;
