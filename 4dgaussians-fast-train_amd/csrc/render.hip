@@ -107,7 +107,6 @@ __global__ __launch_bounds__(64) void render_forward_kernel(Args a, const uint2 
     f2 C0[2] = {bc2(0.f), bc2(0.f)}, C1[2] = {bc2(0.f), bc2(0.f)}, C2[2] = {bc2(0.f), bc2(0.f)},
        Dp[2] = {bc2(0.f), bc2(0.f)};
     uint32_t stop[4] = {0, 0, 0, 0};  // list position of the terminating splat (retired pixels)
-    uint32_t seen = 0;                // 1 + list position of the last splat that touched a pixel
     uint2 range = ranges[tile];
     range.x = __builtin_amdgcn_readfirstlane(range.x);
     range.y = __builtin_amdgcn_readfirstlane(range.y);
@@ -143,19 +142,17 @@ __global__ __launch_bounds__(64) void render_forward_kernel(Args a, const uint2 
             const float dx = geo.x - pfx;
             const float pa = geo.z * dx * dx, pb = geo.w * dx;
             f2 ae[2], tT[2];
-            uint64_t any = 0, term[4];
+            uint64_t term[4];
 #pragma unroll
             for (int h = 0; h < 2; h++) {
                 const Falloff f = falloff(geo, opc, pa, pb, pfy[h]);
                 const uint64_t m0 = blend_mask(f.pw.x, f.alpha.x) & alive[2 * h];
                 const uint64_t m1 = blend_mask(f.pw.y, f.alpha.y) & alive[2 * h + 1];
-                any |= m0 | m1;
                 ae[h] = f2{lane_bit(m0) ? f.alpha.x : 0.f, lane_bit(m1) ? f.alpha.y : 0.f};
                 tT[h] = T[h] * (bc2(1.f) - ae[h]);  // forward.cu:349
                 term[2 * h] = ballot(tT[h].x < 0.0001f);
                 term[2 * h + 1] = ballot(tT[h].y < 0.0001f);
             }
-            seen = any ? pos0 + j + 1 : seen;
             if ((term[0] | term[1] | term[2] | term[3]) != 0) {
                 // forward.cu:350-354: the splat that would drop T below 1e-4 is not blended; the pixel retires
 #pragma unroll
@@ -191,8 +188,9 @@ __global__ __launch_bounds__(64) void render_forward_kernel(Args a, const uint2 
             const float t = (k & 1) ? T[h].y : T[h].x;
             const size_t pix = (size_t)py * a.W + px;
             final_T[pix] = t;
-            // splats at positions >= n_contrib never blended into this pixel (the backward's bound)
-            n_contrib[pix] = lane_bit(alive[k]) ? seen : stop[k];
+            // splats at positions >= n_contrib never blended into this pixel (the backward's bound):
+            // the terminating splat's position, or the list length for pixels that never terminated
+            n_contrib[pix] = lane_bit(alive[k]) ? range.y - range.x : stop[k];
             out_color[pix] = ((k & 1) ? C0[h].y : C0[h].x) + t * bg.x;
             out_color[HW + pix] = ((k & 1) ? C1[h].y : C1[h].x) + t * bg.y;
             out_color[2 * HW + pix] = ((k & 1) ? C2[h].y : C2[h].x) + t * bg.z;
