@@ -11,7 +11,7 @@
 //      tie order as the reference's stable sort of instances emitted in id order);
 //   2. the candidate instances (each Gaussian's 3-sigma tile rectangle, row-major, Gaussians in depth
 //      order) are numbered by a prefix sum of the rectangle areas, and emitted -- only for tiles the
-//      splat actually reaches (tile_reached, gs4d_internal.h) -- in one load-balanced stream
+//      splat actually reaches (half_reach, gs4d_internal.h) -- in one load-balanced stream
 //      compaction pass: every workgroup takes a fixed number of candidates, whatever the splat sizes;
 //   3. the emitted sequence is already depth-ordered, so a STABLE sort by tile id alone yields the
 //      reference's (tile, depth, id) order: ceil(msb(T)/8) passes over u32 keys (2 at the metric
@@ -350,8 +350,8 @@ hipError_t launch_depth_order(const Args &a, GeomState g, const int *radii, hipS
 // K3: load-balanced emission.  Workgroup j takes candidates [j*2048, +2048) of the depth-ordered
 // candidate sequence; lane t owns 8 consecutive ones.  Their owning ranks come from a load-balancing
 // search in LDS: each rank starting inside the chunk marks its first slot, and a max-scan spreads the
-// marks.  Each candidate is tested with tile_reached; the reached ones are compacted in candidate
-// order: keys[e] = tile, gid_by_e[e] = Gaussian.  Emission offsets are chained by look-back; the last
+// marks.  Each candidate is tested with half_reach; the reached ones are compacted in candidate
+// order: keys[e] = tile, gid_by_e[e] = Gaussian | reach bits.  Emission offsets are chained by look-back; the last
 // chunk stores L'.  Also accumulated: n_inst[g] (integer atomics), the tile-sort digit histograms,
 // and (first T threads of the grid) zeroed tile ranges.
 __global__ __launch_bounds__(256) void emit_instances_kernel(Args a, GeomState g, int L, int npass,
@@ -416,20 +416,21 @@ __global__ __launch_bounds__(256) void emit_instances_kernel(Args a, GeomState g
         geo[k] = g.rank_geo[r];
         co[k] = g.rank_co[r];
     }
-    uint32_t tile[kEmitPer];
+    uint32_t tile[kEmitPer], reach[kEmitPer];
     uint32_t keep = 0;
 #pragma unroll
     for (int k = 0; k < kEmitPer; k++) {
         const uint32_t c = c0 + tid * kEmitPer + k;
         tile[k] = 0;
+        reach[k] = 0;
         if (c < c1) {
             const int i = (int)own[k];
             int x0, y0, x1, y1;
             getRect(geo[k].x, geo[k].y, __float_as_int(geo[k].z), a.gx, a.gy, x0, y0, x1, y1);
             const uint32_t local = c - s_off[i], wdt = (uint32_t)(x1 - x0);
             const int ty = y0 + (int)(local / wdt), tx = x0 + (int)(local % wdt);
-            const uint32_t area = s_off[i + 1] - s_off[i];
-            if (area > kTightMaxArea || tile_reached(geo[k].x, geo[k].y, co[k], tx, ty, a.W, a.H)) {
+            reach[k] = half_reach(geo[k].x, geo[k].y, co[k], tx, ty, a.W, a.H);
+            if (reach[k] != 0) {
                 keep |= 1u << k;
                 tile[k] = (uint32_t)(ty * a.gx + tx);
                 atomicAdd(&s_n[i], 1u);
@@ -462,7 +463,7 @@ __global__ __launch_bounds__(256) void emit_instances_kernel(Args a, GeomState g
     for (int k = 0; k < kEmitPer; k++) {
         if ((keep >> k) & 1u) {
             keys[e] = tile[k];
-            gid_by_e[e] = __float_as_uint(geo[k].w);
+            gid_by_e[e] = __float_as_uint(geo[k].w) | (reach[k] << kReachShift);
             e++;
         }
     }

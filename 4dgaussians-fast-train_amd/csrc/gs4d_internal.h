@@ -27,7 +27,7 @@ struct GeomState {
     float *cov3D;             // 6P  world covariance (forward.cu:211)
     uint8_t *clamped;         // P   bit c set when channel c was clamped (forward.cu:67-69)
     uint32_t *tiles_touched;  // P   3-sigma rect area (the reference's tiles_touched, forward.cu:255)
-    uint32_t *n_inst;         // P   tiles of the rect actually reached (tile_reached), <= tiles_touched
+    uint32_t *n_inst;         // P   tiles of the rect actually reached (half_reach), <= tiles_touched
     uint32_t *dkeys[2];       // P   depth-sort keys (ping-pong)
     uint32_t *dvals[2];       // P   depth-sort ids; dvals[0] = Gaussian id by depth rank after the sort
     uint32_t *cand_off;       // P+1 exclusive scan of tiles_touched in depth-rank order: first candidate
@@ -95,22 +95,20 @@ size_t binning_zero_words(int L);
 // ---- exact tile culling ------------------------------------------------------------------------
 // The reference bins a splat into every tile of its 3-sigma rectangle (forward.cu:232-237), but a
 // pixel only blends a splat when alpha = min(0.99, o * exp(power)) >= 1/255 (forward.cu:346-348).
-// tile_reached() is false only when NO pixel centre of the tile (clipped to the image) can reach that
+// rect_reached() is false only when NO pixel centre of the rectangle [x0,x1] x [y0,y1] can reach that
 // threshold: the minimum of the quadratic form q = a dx^2 + 2b dx dy + c dy^2 (power = -q/2) over
-// the tile's centre rectangle is taken in closed form (convex q: interior minimum or clamped
-// stationary point on an edge) and compared with a 0.1% margin.  Dropping such (tile, splat) pairs
-// changes no output bit: the reference skips every one of their pixel evaluations.  Splats with a
-// rectangle larger than kTightMaxArea tiles, or a conic that is not positive definite, are not culled.
-constexpr uint32_t kTightMaxArea = 64;
-
-__device__ __forceinline__ bool tile_reached(float mx, float my, float4 co, int tx, int ty, int W, int H) {
-    // evaluated identically wherever it is inlined (count and emit passes)
+// the rectangle is taken in closed form (convex q: interior minimum or clamped stationary point on
+// an edge) and compared with a 0.1% margin.  Dropping such (tile, splat) pairs -- or such half tiles
+// in the blend kernels -- changes no output bit: the reference skips every one of their pixel
+// evaluations.  A conic that is not positive definite is never culled.
+__device__ __forceinline__ bool rect_reached(float mx, float my, float4 co, int x0, int x1, int y0, int y1) {
+    // evaluated identically wherever it is inlined (emission and blend passes)
 #pragma clang fp contract(off)
     const float a = co.x, b = co.y, c = co.z, o = co.w;
     if (!(a > 0.f && c > 0.f && a * c - b * b > 0.f)) return true;
-    // d = mean - pixel centre, over the tile's pixel centres inside the image
-    const float X0 = mx - (float)min(tx * kBlockX + kBlockX - 1, W - 1), X1 = mx - (float)(tx * kBlockX);
-    const float Y0 = my - (float)min(ty * kBlockY + kBlockY - 1, H - 1), Y1 = my - (float)(ty * kBlockY);
+    // d = mean - pixel centre over the rectangle
+    const float X0 = mx - (float)x1, X1 = mx - (float)x0;
+    const float Y0 = my - (float)y1, Y1 = my - (float)y0;
     float q = 0.f;
     if (!(X0 <= 0.f && X1 >= 0.f && Y0 <= 0.f && Y1 >= 0.f)) {
         const float ia = 1.f / a, ic = 1.f / c;
@@ -126,6 +124,24 @@ __device__ __forceinline__ bool tile_reached(float mx, float my, float4 co, int 
     }
     return !(o * __expf(-0.5f * q) * 1.001f < 1.0f / 255.0f);
 }
+// Rows [8h, 8h+7] of a tile are blended by the pixel pair h of every lane (render.hip), so the
+// emission records, per instance, which half tiles the splat reaches (bit h; pixel centres inside the
+// image) and the blend kernels skip a half it cannot reach.  An instance reaching neither half is
+// not emitted.
+__device__ __forceinline__ uint32_t half_reach(float mx, float my, float4 co, int tx, int ty, int W, int H) {
+    const int x0 = tx * kBlockX, x1 = min(x0 + kBlockX - 1, W - 1);
+    uint32_t r = 0;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const int y0 = ty * kBlockY + 8 * h, y1 = min(y0 + 7, H - 1);
+        if (y0 <= y1 && rect_reached(mx, my, co, x0, x1, y0, y1)) r |= 1u << h;
+    }
+    return r;
+}
+// gid_by_e[e] = Gaussian id | half-reach bits << kReachShift (P < 2^30)
+constexpr int kReachShift = 30;
+constexpr uint32_t kGidMask = (1u << kReachShift) - 1u;
+
 // ---- launchers (each enqueues on `stream`, returns hipError_t of the launch) ------------------
 hipError_t launch_preprocess(const Args &a, const float *means3D, const float *scales, const float *rotations,
                              const float *opacities, const float *shs, const float *cov3D_precomp,

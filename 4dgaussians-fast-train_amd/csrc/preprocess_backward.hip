@@ -78,7 +78,7 @@ __global__ __launch_bounds__(256) void contrib_segments_kernel(const uint32_t *_
     if (w * 64 >= n) return;
     const int e = w * 64 + lane;
     const bool valid = e < n;
-    const uint32_t key = valid ? gid_by_e[e] : 0xFFFFFFFFu;
+    const uint32_t key = valid ? gid_by_e[e] & kGidMask : 0xFFFFFFFFu;
     float acc[9];
     {
         float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a, c = a;
@@ -92,8 +92,8 @@ __global__ __launch_bounds__(256) void contrib_segments_kernel(const uint32_t *_
         acc[8] = c.x;
     }
     uint32_t kp = __shfl_up(key, 1), kn = __shfl_down(key, 1);
-    if (lane == 0) kp = e > 0 ? gid_by_e[e - 1] : 0xFFFFFFFFu;
-    if (lane == 63) kn = e + 1 < n ? gid_by_e[e + 1] : 0xFFFFFFFFu;
+    if (lane == 0) kp = e > 0 ? gid_by_e[e - 1] & kGidMask : 0xFFFFFFFFu;
+    if (lane == 63) kn = e + 1 < n ? gid_by_e[e + 1] & kGidMask : 0xFFFFFFFFu;
     const bool head = valid && key != kp;  // first slot of its Gaussian
     const bool tail = valid && key != kn;  // last slot of its Gaussian
     bool f = head || lane == 0;
@@ -144,7 +144,7 @@ __global__ __launch_bounds__(256) void contrib_finish_kernel(int P, const uint32
             add9(acc, part + ((size_t)w * 2) * 3);
             if (flags[w] & 1u) break;
         }
-        write_grads(o, gid_by_e[(size_t)i * 64 + 63], acc);
+        write_grads(o, gid_by_e[(size_t)i * 64 + 63] & kGidMask, acc);
     }
     if (i < P && n_inst[i] == 0) write_zero_grads(o, (uint32_t)i);
 }

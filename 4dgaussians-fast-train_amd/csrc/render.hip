@@ -23,6 +23,8 @@
 // LDS, and stored once per (tile, splat) instance at its emission slot (coalesced 48-byte records,
 // no float atomics).  The per-Gaussian pass (preprocess_backward.hip) sums a Gaussian's records in
 // a fixed order and applies the moment -> gradient map once (bitwise reproducible).
+#include <type_traits>
+
 #include "gs4d_internal.h"
 
 namespace gs4d {
@@ -40,20 +42,25 @@ struct SplatLDS {
 };
 struct SplatRegs {
     float4 geo, opc, col;
+    uint32_t reach;  // bit h: the splat reaches some pixel centre of half tile h (rows 8h..8h+7)
 };
 
-__device__ __forceinline__ void load_splat(SplatRegs &r, bool valid, uint32_t gid, const float2 *__restrict__ xy,
+// ge = gid_by_e entry of the instance (Gaussian id | half-reach bits)
+__device__ __forceinline__ void load_splat(SplatRegs &r, bool valid, uint32_t ge, const float2 *__restrict__ xy,
                                            const float4 *__restrict__ conic_opacity, const float4 *__restrict__ rgbd,
                                            const float *__restrict__ colors) {
     if (valid) {
+        const uint32_t gid = ge & kGidMask;
         const float2 p = xy[gid];
         const float4 co = conic_opacity[gid];
         r.geo = make_float4(p.x, p.y, (-0.5f * co.x) * kLog2e, (-co.y) * kLog2e);
         r.opc = make_float4((-0.5f * co.z) * kLog2e, co.w, 0.f, 0.f);
         r.col = rgbd[gid];
         if (colors) r.col = make_float4(colors[3 * gid], colors[3 * gid + 1], colors[3 * gid + 2], r.col.w);
+        r.reach = ge >> kReachShift;
     } else {
         r.geo = r.opc = r.col = make_float4(0.f, 0.f, 0.f, 0.f);
+        r.reach = 0;
     }
 }
 
@@ -72,13 +79,16 @@ __device__ __forceinline__ Falloff falloff(const float4 &geo, const float4 &opc,
     return f;
 }
 __device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
-// lanes where the splat blends into the pixel: power <= 0 and alpha >= 1/255 (forward.cu:341-348);
-// two ballots of plain compares, combined on the scalar unit
-__device__ __forceinline__ uint64_t blend_mask(float pw, float alpha) {
-    return ballot(pw <= 0.0f) & ballot(alpha >= 1.0f / 255.0f);
-}
 // this lane's bit of a wave mask, used directly as the select condition (no VALU shift)
 __device__ __forceinline__ bool lane_bit(uint64_t m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
+
+// ---------------------------------------------------------------------------------------------
+// A splat whose conic is positive definite has power <= 0 at every pixel (up to rounding at its
+// centre), so the power test of forward.cu:341 is only evaluated in batches holding another splat.
+__device__ __forceinline__ bool conic_pd(const float4 &geo, const float4 &opc) {
+    // geo.z = -a/2 k, geo.w = -b k, opc.x = -c/2 k (k = log2 e > 0): a > 0 and ac - b^2 > 0
+    return geo.z < 0.f && 4.f * geo.z * opc.x - geo.w * geo.w > 0.f;
+}
 
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void render_forward_kernel(Args a, const uint2 *__restrict__ ranges,
@@ -118,6 +128,8 @@ __global__ __launch_bounds__(64) void render_forward_kernel(Args a, const uint2 
     for (uint32_t base = range.x; base < range.y; base += 64) {
         if ((alive[0] | alive[1] | alive[2] | alive[3]) == 0) break;  // forward.cu:312-314
         const uint32_t n = min(64u, range.y - base);
+        const uint64_t reach[2] = {ballot(nxt.reach & 1u), ballot(nxt.reach & 2u)};
+        const uint64_t nonpd = ballot(!conic_pd(nxt.geo, nxt.opc));
         __syncthreads();
         s_sp[lane].geo = nxt.geo;
         s_sp[lane].opc = nxt.opc;
@@ -129,52 +141,41 @@ __global__ __launch_bounds__(64) void render_forward_kernel(Args a, const uint2 
             if (nb < range.y) load_splat(nxt, v, v ? gid_by_e[upos[nb + lane]] : 0u, xy, conic_opacity, rgbd, nullptr);
         }
         const uint32_t pos0 = base - range.x;
-        // software pipeline: splat j+1's constants are read from LDS while splat j is blended
-        float4 geo_n = s_sp[0].geo, opc_n = s_sp[0].opc, col_n = s_sp[0].col;
-        for (uint32_t j = 0; j < n; j++) {
-            const float4 geo = geo_n, opc = opc_n, col = col_n;
-            {
-                const uint32_t jn = (j + 1) & 63;
-                geo_n = s_sp[jn].geo;
-                opc_n = s_sp[jn].opc;
-                col_n = s_sp[jn].col;
-            }
-            const float dx = geo.x - pfx;
-            const float pa = geo.z * dx * dx, pb = geo.w * dx;
-            f2 ae[2], tT[2];
-            uint64_t term[4];
+        // The two half tiles blend independently: each walks only the batch's splats that reach it.
 #pragma unroll
-            for (int h = 0; h < 2; h++) {
+        for (int h = 0; h < 2; h++) {
+            for (uint64_t todo = reach[h]; todo != 0; todo &= todo - 1) {
+                const uint32_t j = (uint32_t)__builtin_ctzll(todo);
+                const float4 geo = s_sp[j].geo, opc = s_sp[j].opc, col = s_sp[j].col;
+                const float dx = geo.x - pfx;
+                const float pa = geo.z * dx * dx, pb = geo.w * dx;
                 const Falloff f = falloff(geo, opc, pa, pb, pfy[h]);
-                const uint64_t m0 = blend_mask(f.pw.x, f.alpha.x) & alive[2 * h];
-                const uint64_t m1 = blend_mask(f.pw.y, f.alpha.y) & alive[2 * h + 1];
-                ae[h] = f2{lane_bit(m0) ? f.alpha.x : 0.f, lane_bit(m1) ? f.alpha.y : 0.f};
-                tT[h] = T[h] * (bc2(1.f) - ae[h]);  // forward.cu:349
-                term[2 * h] = ballot(tT[h].x < 0.0001f);
-                term[2 * h + 1] = ballot(tT[h].y < 0.0001f);
-            }
-            if ((term[0] | term[1] | term[2] | term[3]) != 0) {
-                // forward.cu:350-354: the splat that would drop T below 1e-4 is not blended; the pixel retires
-#pragma unroll
-                for (int h = 0; h < 2; h++) {
-                    const bool t0 = lane_bit(term[2 * h]), t1 = lane_bit(term[2 * h + 1]);
-                    ae[h] = f2{t0 ? 0.f : ae[h].x, t1 ? 0.f : ae[h].y};
-                    tT[h] = f2{t0 ? T[h].x : tT[h].x, t1 ? T[h].y : tT[h].y};
+                uint64_t m0 = ballot(f.alpha.x >= 1.0f / 255.0f) & alive[2 * h];
+                uint64_t m1 = ballot(f.alpha.y >= 1.0f / 255.0f) & alive[2 * h + 1];
+                if ((nonpd >> j) & 1) {  // forward.cu:341-342
+                    m0 &= ballot(f.pw.x <= 0.0f);
+                    m1 &= ballot(f.pw.y <= 0.0f);
+                }
+                f2 ae = f2{lane_bit(m0) ? f.alpha.x : 0.f, lane_bit(m1) ? f.alpha.y : 0.f};
+                f2 tT = T[h] * (bc2(1.f) - ae);  // forward.cu:349
+                const uint64_t t0m = ballot(tT.x < 0.0001f), t1m = ballot(tT.y < 0.0001f);
+                if ((t0m | t1m) != 0) {
+                    // forward.cu:350-354: the splat that would drop T below 1e-4 is not blended; the pixel retires
+                    const bool t0 = lane_bit(t0m), t1 = lane_bit(t1m);
+                    ae = f2{t0 ? 0.f : ae.x, t1 ? 0.f : ae.y};
+                    tT = f2{t0 ? T[h].x : tT.x, t1 ? T[h].y : tT.y};
                     stop[2 * h] = t0 ? pos0 + j : stop[2 * h];
                     stop[2 * h + 1] = t1 ? pos0 + j : stop[2 * h + 1];
+                    alive[2 * h] &= ~t0m;
+                    alive[2 * h + 1] &= ~t1m;
                 }
-#pragma unroll
-                for (int k = 0; k < 4; k++) alive[k] &= ~term[k];
-            }
-            // every live pixel takes the update; pixels the splat does not touch have ae = 0
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const f2 w = ae[h] * T[h];  // forward.cu:357-358
+                // every live pixel takes the update; pixels the splat does not touch have ae = 0
+                const f2 w = ae * T[h];  // forward.cu:357-358
                 C0[h] = fma2(bc2(col.x), w, C0[h]);
                 C1[h] = fma2(bc2(col.y), w, C1[h]);
                 C2[h] = fma2(bc2(col.z), w, C2[h]);
                 Dp[h] = fma2(bc2(col.w), w, Dp[h]);
-                T[h] = tT[h];
+                T[h] = tT;
             }
         }
     }
@@ -252,17 +253,82 @@ __device__ __forceinline__ void wave_sum9_to_lds(const float v[9], float *dst, i
     }
 }
 
-__global__ __launch_bounds__(64) void render_backward_kernel(Args a, const uint2 *__restrict__ ranges,
-                                                             const uint32_t *__restrict__ gid_by_e,
-                                                             const uint32_t *__restrict__ upos,
-                                                             const float2 *__restrict__ xy,
-                                                             const float4 *__restrict__ conic_opacity,
-                                                             const float4 *__restrict__ rgbd,
-                                                             const float *__restrict__ colors,
-                                                             const float *__restrict__ final_Ts,
-                                                             const uint32_t *__restrict__ n_contrib,
-                                                             const float *__restrict__ dL_dpixels,
-                                                             float *__restrict__ contrib) {
+// Wave64 totals of the 18 per-lane values of two splats (9 each), left in LDS:
+// dst0[q] = sum over lanes of v[q] (q < 9), dst1[q - 9] likewise (q >= 9).  v_permlane32_swap then
+// v_permlane16_swap halve pairs of values (reduce-scatter: after them row r of register i holds value
+// 4i + {0, 2, 1, 3}[r]); a 16-lane DPP tree finishes each register, and the first lane of each row
+// stores its value.
+__device__ __forceinline__ void wave_sum18_to_lds(const float v[18], float *dst0, float *dst1, int lane) {
+    float h[9];
+#pragma unroll
+    for (int m = 0; m < 9; m++) h[m] = swap32_add(v[2 * m], v[2 * m + 1]);
+    float q[5];
+#pragma unroll
+    for (int i = 0; i < 4; i++) q[i] = row_sum(swap16_add(h[2 * i], h[2 * i + 1]));
+    q[4] = row_sum(swap16_add(h[8], 0.f));
+    if ((lane & 15) == 0) {
+        const int r = lane >> 4;
+        const int slot = ((r & 1) << 1) | (r >> 1);  // row -> value offset {0, 2, 1, 3}
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int k = 4 * i + slot;
+            float *d = k < 9 ? dst0 + k : dst1 + (k - 9);
+            *d = q[i];
+        }
+        if (r == 0) dst1[7] = q[4];  // value 16
+        if (r == 2) dst1[8] = q[4];  // value 17
+    }
+}
+
+// Per-pixel state of the reverse walk (pairs): T (recovered backwards), A = accum_rec . dL/dpix,
+// dL/dpix and the background term -T_final (bg . dL/dpix) (backward.cu:534).
+struct BwdPixels {
+    f2 T[2], A[2], dp0[2], dp1[2], dp2[2], nTb[2];
+};
+
+// One half tile of one splat of the reverse walk: updates the half's pixel state and adds its
+// per-lane partial sums (moments of u = G dL/dalpha, and the colour sums) to U0..U2 / W0..W2.
+__device__ __forceinline__ void walk_half(f2 &T, f2 &A, const f2 dp0, const f2 dp1, const f2 dp2, const f2 nTb,
+                                          const float4 &geo, const float4 &opc, const float4 &col, float pa, float pb,
+                                          f2 pfy, bool check_pw, uint64_t act0, uint64_t act1, f2 &U0, f2 &U1,
+                                          f2 &U2, f2 &W0, f2 &W1, f2 &W2) {
+    const Falloff f = falloff(geo, opc, pa, pb, pfy);
+    // backward.cu:486-497: contributor test, alpha < 1/255 and (for a conic that is not positive
+    // definite) power > 0 skips -- the same decisions as the forward
+    uint64_t m0 = ballot(f.alpha.x >= 1.0f / 255.0f) & act0;
+    uint64_t m1 = ballot(f.alpha.y >= 1.0f / 255.0f) & act1;
+    if (check_pw) {
+        m0 &= ballot(f.pw.x <= 0.0f);
+        m1 &= ballot(f.pw.y <= 0.0f);
+    }
+    const bool b0 = lane_bit(m0), b1 = lane_bit(m1);
+    const f2 ae = f2{b0 ? f.alpha.x : 0.f, b1 ? f.alpha.y : 0.f};
+    const f2 Ge = f2{b0 ? f.G.x : 0.f, b1 ? f.G.y : 0.f};
+    const f2 om = bc2(1.f) - ae;
+    const f2 inv = f2{__builtin_amdgcn_rcpf(om.x), __builtin_amdgcn_rcpf(om.y)};
+    const f2 Tn = T * inv;  // backward.cu:503
+    T = Tn;
+    const f2 CD = fma2(bc2(col.z), dp2, fma2(bc2(col.y), dp1, bc2(col.x) * dp0));
+    const f2 diff = CD - A;
+    const f2 dLda = fma2(diff, Tn, nTb * inv);  // backward.cu:519-534
+    A = fma2(ae, diff, A);                      // accum_rec for the next splat in front
+    const f2 u = Ge * dLda;
+    const f2 w = ae * Tn;                       // dchannel_dcolor (backward.cu:521)
+    const f2 ud = u * f.dy;
+    U0 += u;
+    U1 += ud;
+    U2 = fma2(ud, f.dy, U2);
+    W0 = fma2(w, dp0, W0);
+    W1 = fma2(w, dp1, W1);
+    W2 = fma2(w, dp2, W2);
+}
+
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void render_backward_kernel(Args a, const uint2 *__restrict__ ranges, const uint32_t *__restrict__ gid_by_e,
+                            const uint32_t *__restrict__ upos, const float2 *__restrict__ xy,
+                            const float4 *__restrict__ conic_opacity, const float4 *__restrict__ rgbd,
+                            const float *__restrict__ colors, const float *__restrict__ final_Ts,
+                            const uint32_t *__restrict__ n_contrib, const float *__restrict__ dL_dpixels,
+                            float *__restrict__ contrib) {
     __shared__ SplatLDS s_sp[64];
     __shared__ float4 s_rec[64][3];  // reduced moments of the batch's splats
     const int tile = blockIdx.x;
@@ -279,11 +345,10 @@ __global__ __launch_bounds__(64) void render_backward_kernel(Args a, const uint2
     const V3 bg = load_v3(a.bg);
     const f2 pfy[2] = {f2{(float)py0, (float)(py0 + 4)}, f2{(float)(py0 + 8), (float)(py0 + 12)}};
 
-    // per-pixel state (pairs): T (recovered backwards), A = accum_rec . dL/dpix, dL/dpix, and the
-    // background term -T_final (bg . dL/dpix) (backward.cu:534)
-    f2 T[2], A[2], dp0[2], dp1[2], dp2[2], nTb[2];
+    BwdPixels st;
     uint32_t lastc[4];
-    uint32_t max_last = 0;
+    uint64_t inside_m[4];
+    uint32_t max_last = 0, min_last = 0xffffffffu;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const int py = py0 + 4 * k;
@@ -294,19 +359,26 @@ __global__ __launch_bounds__(64) void render_backward_kernel(Args a, const uint2
         const float d1 = inside ? dL_dpixels[HW + pix] : 0.f;
         const float d2 = inside ? dL_dpixels[2 * HW + pix] : 0.f;
         lastc[k] = inside ? n_contrib[pix] : 0u;
+        inside_m[k] = ballot(inside);
         const float nb = -tf * (bg.x * d0 + bg.y * d1 + bg.z * d2);
         const int h = k >> 1;
         if (k & 1) {
-            T[h].y = tf; dp0[h].y = d0; dp1[h].y = d1; dp2[h].y = d2; nTb[h].y = nb; A[h].y = 0.f;
+            st.T[h].y = tf; st.dp0[h].y = d0; st.dp1[h].y = d1; st.dp2[h].y = d2; st.nTb[h].y = nb; st.A[h].y = 0.f;
         } else {
-            T[h].x = tf; dp0[h].x = d0; dp1[h].x = d1; dp2[h].x = d2; nTb[h].x = nb; A[h].x = 0.f;
+            st.T[h].x = tf; st.dp0[h].x = d0; st.dp1[h].x = d1; st.dp2[h].x = d2; st.nTb[h].x = nb; st.A[h].x = 0.f;
         }
         max_last = max(max_last, lastc[k]);
+        if (inside) min_last = min(min_last, lastc[k]);
     }
-    // splats at list position >= every pixel's n_contrib never contribute: the walk starts there
+    // splats at list position >= every pixel's n_contrib never contribute: the walk starts there;
+    // below every inside pixel's n_contrib the contributor test (backward.cu:486-488) always passes
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) max_last = max(max_last, (uint32_t)__shfl_xor((int)max_last, off));
+    for (int off = 32; off > 0; off >>= 1) {
+        max_last = max(max_last, (uint32_t)__shfl_xor((int)max_last, off));
+        min_last = min(min_last, (uint32_t)__shfl_xor((int)min_last, off));
+    }
     max_last = __builtin_amdgcn_readfirstlane(max_last);
+    min_last = __builtin_amdgcn_readfirstlane(min_last);
 
     const uint32_t len = range.y - range.x;
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -329,52 +401,30 @@ __global__ __launch_bounds__(64) void render_backward_kernel(Args a, const uint2
     for (int end = (int)max_last; end > 0; end -= 64) {
         const int n = min(64, end);
         const uint32_t ucur = unxt;
+        const uint64_t reach[2] = {ballot(nxt.reach & 1u), ballot(nxt.reach & 2u)};
+        const uint64_t nonpd = ballot(!conic_pd(nxt.geo, nxt.opc));
         __syncthreads();
         s_sp[lane].geo = nxt.geo;
         s_sp[lane].opc = nxt.opc;
         s_sp[lane].col = nxt.col;
         __syncthreads();
         if (end - 64 > 0) fetch(end - 64);
-        float4 geo_n = s_sp[0].geo, opc_n = s_sp[0].opc, col_n = s_sp[0].col;
         for (int j = 0; j < n; j++) {
+            const float4 geo = s_sp[j].geo, opc = s_sp[j].opc, col = s_sp[j].col;
             const uint32_t contributor = (uint32_t)(end - 1 - j);
-            const float4 geo = geo_n, opc = opc_n, col = col_n;
-            {
-                const int jn = (j + 1) & 63;
-                geo_n = s_sp[jn].geo;
-                opc_n = s_sp[jn].opc;
-                col_n = s_sp[jn].col;
-            }
             const float dx = geo.x - pfx;
             const float pa = geo.z * dx * dx, pb = geo.w * dx;
             f2 U0 = bc2(0.f), U1 = bc2(0.f), U2 = bc2(0.f), W0 = bc2(0.f), W1 = bc2(0.f), W2 = bc2(0.f);
-            // every pixel takes the update; pixels the splat does not touch have alpha = G = 0, which
-            // leaves T and A unchanged and adds nothing
+            // a half tile the splat does not reach has alpha = G = 0 at all its pixels: T and A stay,
+            // nothing is added
 #pragma unroll
             for (int h = 0; h < 2; h++) {
-                const Falloff f = falloff(geo, opc, pa, pb, pfy[h]);
-                const uint64_t m0 = blend_mask(f.pw.x, f.alpha.x) & ballot(contributor < lastc[2 * h]);
-                const uint64_t m1 = blend_mask(f.pw.y, f.alpha.y) & ballot(contributor < lastc[2 * h + 1]);
-                const bool b0 = lane_bit(m0), b1 = lane_bit(m1);
-                const f2 ae = f2{b0 ? f.alpha.x : 0.f, b1 ? f.alpha.y : 0.f};
-                const f2 Ge = f2{b0 ? f.G.x : 0.f, b1 ? f.G.y : 0.f};
-                const f2 om = bc2(1.f) - ae;
-                const f2 inv = f2{__builtin_amdgcn_rcpf(om.x), __builtin_amdgcn_rcpf(om.y)};
-                const f2 Tn = T[h] * inv;  // backward.cu:503
-                T[h] = Tn;
-                const f2 CD = fma2(bc2(col.z), dp2[h], fma2(bc2(col.y), dp1[h], bc2(col.x) * dp0[h]));
-                const f2 diff = CD - A[h];
-                const f2 dLda = fma2(diff, Tn, nTb[h] * inv);  // backward.cu:519-534
-                A[h] = fma2(ae, diff, A[h]);                   // accum_rec for the next splat in front
-                const f2 u = Ge * dLda;
-                const f2 w = ae * Tn;                          // dchannel_dcolor (backward.cu:521)
-                const f2 ud = u * f.dy;
-                U0 += u;
-                U1 += ud;
-                U2 = fma2(ud, f.dy, U2);
-                W0 = fma2(w, dp0[h], W0);
-                W1 = fma2(w, dp1[h], W1);
-                W2 = fma2(w, dp2[h], W2);
+                if ((reach[h] >> j) & 1) {
+                    const uint64_t act0 = ballot(contributor < lastc[2 * h]);
+                    const uint64_t act1 = ballot(contributor < lastc[2 * h + 1]);
+                    walk_half(st.T[h], st.A[h], st.dp0[h], st.dp1[h], st.dp2[h], st.nTb[h], geo, opc, col, pa, pb,
+                              pfy[h], (nonpd >> j) & 1, act0, act1, U0, U1, U2, W0, W1, W2);
+                }
             }
             const float u0 = U0.x + U0.y, u1 = U1.x + U1.y;
             const float v[9] = {u0, dx * u0, u1, dx * dx * u0, dx * u1, U2.x + U2.y, W0.x + W0.y, W1.x + W1.y,

@@ -45,6 +45,8 @@ def main():
     tmax = nc.reshape(-1, 16, gx, 16).max(axis=(1, 3)).reshape(-1)
     print("walk length/tile (max n_contrib)", q(tmax), "mean", float(tmax.mean()), "sum", int(tmax.sum()))
     print("sum over tiles of instances", int(cnt.sum()), "frac walked", float(tmax.sum() / max(1, cnt.sum())))
+    os.makedirs("gpurun_out", exist_ok=True)
+    np.savez_compressed("gpurun_out/tile_stats.npz", cnt=cnt, tmax=tmax, gx=gx)
 
 
 if __name__ == "__main__":
