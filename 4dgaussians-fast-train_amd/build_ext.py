@@ -1,10 +1,11 @@
-"""In-tree build of the MI355X rasterizer.
+"""In-tree build of the MI355X rasterizer and kNN initialiser.
 
-  libgs4d.so  -- HIP kernels + C ABI (include/gs4d.h), hipcc --offload-arch=gfx950
-  _C.*.so     -- the PyTorch-ROCm binding (csrc/torch_glue.cpp), linked against libgs4d.so
+  diff_gaussian_rasterization/libgs4d.so -- HIP kernels + C ABI (include/gs4d.h), hipcc --offload-arch=gfx950
+  diff_gaussian_rasterization/_C.*.so    -- PyTorch-ROCm binding of the rasterizer (csrc/torch_glue.cpp)
+  simple_knn/_C.*.so                     -- PyTorch-ROCm binding of distCUDA2 (csrc/knn_glue.cpp)
 
-Both land in diff_gaussian_rasterization/ so `import diff_gaussian_rasterization` loads them from the
-tree (never from site-packages or a JIT cache).  Usage: python build_ext.py [--force] [-v]
+The modules link libgs4d.so by rpath, so both packages load from the tree (never from site-packages
+or a JIT cache).  Usage: python build_ext.py [--force] [-v]
 """
 import concurrent.futures as cf
 import os
@@ -18,11 +19,13 @@ OUT = os.path.join(HERE, "diff_gaussian_rasterization")
 OBJ = os.path.join(HERE, "build", "obj")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 ARCH = os.environ.get("GS4D_ARCH", "gfx950")
-HIP_SOURCES = ["preprocess.hip", "binning.hip", "render.hip", "preprocess_backward.hip", "capi.hip"]
+HIP_SOURCES = ["preprocess.hip", "binning.hip", "render.hip", "preprocess_backward.hip", "knn.hip", "capi.hip"]
 # Per-Gaussian math (K1, K8/K9) is compiled without FMA contraction: it costs nothing measurable
 # (those kernels are tiny) and keeps radii / tile rects -- discrete decisions -- bit-identical to the
 # oracle.  The per-pixel blend kernels keep contraction for throughput.
-NO_CONTRACT = {"preprocess.hip", "preprocess_backward.hip", "binning.hip"}
+# (package, pybind glue) pairs: each package gets an in-tree `_C` module over libgs4d
+BINDINGS = [("diff_gaussian_rasterization", "torch_glue.cpp"), ("simple_knn", "knn_glue.cpp")]
+NO_CONTRACT = {"preprocess.hip", "preprocess_backward.hip", "binning.hip", "knn.hip"}
 HIPCC_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics", "-Wall",
                "-Wno-unused-result", "-I" + INCLUDE]
 
@@ -51,13 +54,13 @@ def lib_path():
     return os.path.join(OUT, "libgs4d.so")
 
 
-def module_path():
-    return os.path.join(OUT, "_C" + ext_suffix())
+def module_path(pkg="diff_gaussian_rasterization"):
+    return os.path.join(HERE, pkg, "_C" + ext_suffix())
 
 
 def build(force=False, verbose=False):
     os.makedirs(OBJ, exist_ok=True)
-    headers = [os.path.join(CSRC, h) for h in ("gs4d_math.h", "gs4d_internal.h")] + [os.path.join(INCLUDE, "gs4d.h")]
+    headers = [os.path.join(CSRC, h) for h in ("gs4d_math.h", "gs4d_internal.h", "radix_sort.h")] + [os.path.join(INCLUDE, "gs4d.h")]
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
     def compile_one(src):
@@ -74,27 +77,32 @@ def build(force=False, verbose=False):
     if force or _newer(lib, objs):
         _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", lib], verbose)
 
-    # torch binding
+    # torch bindings: (package dir, glue source); each links libgs4d from diff_gaussian_rasterization/
     import torch
     from torch.utils import cpp_extension as ce
-    mod = module_path()
-    glue = os.path.join(CSRC, "torch_glue.cpp")
-    if force or _newer(mod, [glue, lib, os.path.join(INCLUDE, "gs4d.h")]):
-        tdir = os.path.dirname(torch.__file__)
-        incs = ce.include_paths(device_type="cuda") if "device_type" in ce.include_paths.__code__.co_varnames \
-            else ce.include_paths(cuda=True)
-        abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
-        cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", glue, "-o", mod,
-               f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",
-               "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-DHIPBLAS_V2",
-               "-I" + sysconfig.get_paths()["include"]] + ["-I" + p for p in incs] + [
-            "-L" + os.path.join(tdir, "lib"), "-L/opt/rocm/lib", "-L" + OUT,
-            "-lgs4d", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python", "-lamdhip64",
-            "-Wl,-rpath,$ORIGIN", "-Wl,-rpath," + os.path.join(tdir, "lib"), "-Wl,-rpath,/opt/rocm/lib"]
-        _run(cmd, verbose)
-    return lib, mod
+    tdir = os.path.dirname(torch.__file__)
+    incs = ce.include_paths(device_type="cuda") if "device_type" in ce.include_paths.__code__.co_varnames \
+        else ce.include_paths(cuda=True)
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    mods = []
+    for pkg, glue_src in BINDINGS:
+        mod = module_path(pkg)
+        glue = os.path.join(CSRC, glue_src)
+        rel = os.path.relpath(OUT, os.path.join(HERE, pkg))
+        if force or _newer(mod, [glue, lib, os.path.join(INCLUDE, "gs4d.h")]):
+            cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", glue, "-o", mod,
+                   f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",
+                   "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-DHIPBLAS_V2",
+                   "-I" + sysconfig.get_paths()["include"]] + ["-I" + p for p in incs] + [
+                "-L" + os.path.join(tdir, "lib"), "-L/opt/rocm/lib", "-L" + OUT,
+                "-lgs4d", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python", "-lamdhip64",
+                "-Wl,-rpath,$ORIGIN" + ("" if rel == "." else "/" + rel), "-Wl,-rpath," + os.path.join(tdir, "lib"),
+                "-Wl,-rpath,/opt/rocm/lib"]
+            _run(cmd, verbose)
+        mods.append(mod)
+    return lib, mods
 
 
 if __name__ == "__main__":
     build(force="--force" in sys.argv, verbose="-v" in sys.argv)
-    print("built", lib_path(), module_path())
+    print("built", lib_path(), *[module_path(p) for p, _ in BINDINGS])

@@ -320,4 +320,16 @@ int gs4d_backward(int P, int D, int M, int R, const float *background, int width
     return GS4D_OK;
 }
 
+int gs4d_knn_mean_dist(int P, const float *points, float *mean_dists, gs4d_alloc_fn scratch_alloc, void *scratch_ctx,
+                       void *stream_) {
+    hipStream_t stream = (hipStream_t)stream_;
+    if (P < 0 || P >= (1 << 30)) return fail(GS4D_ERR_ARG, "knn: P must be in [0, 2^30)");
+    if (P == 0) return GS4D_OK;
+    if (!points || !mean_dists || !scratch_alloc) return fail(GS4D_ERR_ARG, "knn: missing buffers");
+    char *scratch = scratch_alloc(scratch_ctx, knn_scratch_bytes(P));
+    if (!scratch) return fail(GS4D_ERR_ALLOC, "knn: scratch allocation failed");
+    GS4D_HIP(launch_knn(P, points, mean_dists, scratch, stream));
+    return GS4D_OK;
+}
+
 }  // extern "C"

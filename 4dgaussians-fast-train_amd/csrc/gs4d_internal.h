@@ -164,6 +164,9 @@ hipError_t launch_gaussian_backward(const Args &a, GeomState g, const int *radii
                                     float *dL_dmean3D, float *dL_dcov3D, float *dL_dsh, float *dL_dscale,
                                     float *dL_drot, hipStream_t s);
 
+size_t knn_scratch_bytes(int P);
+hipError_t launch_knn(int P, const float *pts, float *mean_dists, char *scratch, hipStream_t s);
+
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 }  // namespace gs4d

@@ -76,6 +76,16 @@ int gs4d_backward(int P, int D, int M, int R, const float *background, int width
                   float *dL_dcov3D, float *dL_dsh, float *dL_dscale, float *dL_drot, gs4d_alloc_fn scratch_alloc,
                   void *scratch_ctx, int debug, void *stream);
 
+/* Replaces SimpleKNN::knn (submodules/simple-knn/simple_knn.h:14-20, simple_knn.cu:187-223), the
+ * native layer behind simple_knn._C.distCUDA2 (spatial.cu:15-25, ext.cpp:15-16), which
+ * scene/gaussian_model.py:148-149 uses to initialise the Gaussian scales.
+ * points: P x 3 fp32 (device, contiguous).  mean_dists[i] = mean of the squared distances from point i
+ * to its 3 nearest other points (the reference's Morton-box search, which prunes but never changes the
+ * result).  The scratch buffer comes from scratch_alloc and must stay valid until the stream has run
+ * the launches.  P == 0 is a no-op. */
+int gs4d_knn_mean_dist(int P, const float *points, float *mean_dists, gs4d_alloc_fn scratch_alloc, void *scratch_ctx,
+                       void *stream);
+
 /* Human-readable message for the last error on this thread (never NULL). */
 const char *gs4d_last_error(void);
 

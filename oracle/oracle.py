@@ -56,6 +56,7 @@ def _load():
                                              _u32p, _u32p, _f32p, _u32p, _f32p]
     lib.gs4d_oracle_mark_visible.argtypes = [ctypes.c_int, _f32p, _f32p, _f32p, _u8p]
     lib.gs4d_oracle_sh_forward.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _f32p, _f32p, _f32p, _f32p, _u8p]
+    lib.gs4d_oracle_knn.argtypes = [ctypes.c_int, _f32p, _f32p]
     lib.gs4d_oracle_set_threads.argtypes = [ctypes.c_int]
     lib.gs4d_oracle_get_threads.restype = ctypes.c_int
     _lib = lib
@@ -204,3 +205,14 @@ def mark_visible(means3D, viewmatrix, projmatrix):
         pm, pp = _arr(projmatrix)
         lib.gs4d_oracle_mark_visible(P, means3D.ctypes.data_as(_f32p), vp, pp, out.ctypes.data_as(_u8p))
     return out.astype(bool)
+
+
+def knn_mean_dist(points):
+    """Mirror of simple_knn._C.distCUDA2 (submodules/simple-knn/spatial.cu:15-25) -- knn_oracle.c."""
+    lib = _load()
+    pts = np.ascontiguousarray(np.asarray(points, np.float32))
+    if pts.ndim != 2 or pts.shape[1] != 3:
+        raise RuntimeError("points must have dimensions (num_points, 3)")
+    out = np.zeros(pts.shape[0], np.float32)
+    lib.gs4d_oracle_knn(pts.shape[0], pts.ctypes.data_as(_f32p), out.ctypes.data_as(_f32p))
+    return out
