@@ -3,6 +3,7 @@
   diff_gaussian_rasterization/libgs4d.so -- HIP kernels + C ABI (include/gs4d.h), hipcc --offload-arch=gfx950
   diff_gaussian_rasterization/_C.*.so    -- PyTorch-ROCm binding of the rasterizer (csrc/torch_glue.cpp)
   simple_knn/_C.*.so                     -- PyTorch-ROCm binding of distCUDA2 (csrc/knn_glue.cpp)
+  gs4d_train/_C.*.so                     -- PyTorch-ROCm binding of the train-step kernels (csrc/train_glue.cpp)
 
 The modules link libgs4d.so by rpath, so both packages load from the tree (never from site-packages
 or a JIT cache).  Usage: python build_ext.py [--force] [-v]
@@ -19,13 +20,13 @@ OUT = os.path.join(HERE, "diff_gaussian_rasterization")
 OBJ = os.path.join(HERE, "build", "obj")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 ARCH = os.environ.get("GS4D_ARCH", "gfx950")
-HIP_SOURCES = ["preprocess.hip", "binning.hip", "render.hip", "preprocess_backward.hip", "knn.hip", "capi.hip"]
+HIP_SOURCES = ["preprocess.hip", "binning.hip", "render.hip", "preprocess_backward.hip", "knn.hip", "train_tail.hip", "hexplane.hip", "capi.hip"]
 # Per-Gaussian math (K1, K8/K9) is compiled without FMA contraction: it costs nothing measurable
 # (those kernels are tiny) and keeps radii / tile rects -- discrete decisions -- bit-identical to the
 # oracle.  The per-pixel blend kernels keep contraction for throughput.
 # (package, pybind glue) pairs: each package gets an in-tree `_C` module over libgs4d
-BINDINGS = [("diff_gaussian_rasterization", "torch_glue.cpp"), ("simple_knn", "knn_glue.cpp")]
-NO_CONTRACT = {"preprocess.hip", "preprocess_backward.hip", "binning.hip", "knn.hip"}
+BINDINGS = [("diff_gaussian_rasterization", "torch_glue.cpp"), ("simple_knn", "knn_glue.cpp"), ("gs4d_train", "train_glue.cpp")]
+NO_CONTRACT = {"preprocess.hip", "preprocess_backward.hip", "binning.hip", "knn.hip", "train_tail.hip", "hexplane.hip"}
 HIPCC_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics", "-Wall",
                "-Wno-unused-result", "-I" + INCLUDE]
 
@@ -60,7 +61,7 @@ def module_path(pkg="diff_gaussian_rasterization"):
 
 def build(force=False, verbose=False):
     os.makedirs(OBJ, exist_ok=True)
-    headers = [os.path.join(CSRC, h) for h in ("gs4d_math.h", "gs4d_internal.h", "radix_sort.h")] + [os.path.join(INCLUDE, "gs4d.h")]
+    headers = [os.path.join(CSRC, h) for h in ("gs4d_math.h", "gs4d_internal.h", "radix_sort.h")] + [os.path.join(INCLUDE, h) for h in ("gs4d.h", "gs4d_train.h")]
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
     def compile_one(src):
@@ -89,7 +90,7 @@ def build(force=False, verbose=False):
         mod = module_path(pkg)
         glue = os.path.join(CSRC, glue_src)
         rel = os.path.relpath(OUT, os.path.join(HERE, pkg))
-        if force or _newer(mod, [glue, lib, os.path.join(INCLUDE, "gs4d.h")]):
+        if force or _newer(mod, [glue, lib, os.path.join(INCLUDE, "gs4d.h"), os.path.join(INCLUDE, "gs4d_train.h")]):
             cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", glue, "-o", mod,
                    f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",
                    "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-DHIPBLAS_V2",

@@ -1,0 +1,287 @@
+// hexplane.hip -- the HexPlane field of the deformation network, fused.
+//
+// Reference: scene/hexplane.py:75-110 (interpolate_ms_features, concat_features=True) over the
+// grids of init_grid_param (:50-72): for every point (x, y, z, t) in normalised coordinates and every
+// resolution level, the product over the 6 coordinate pairs (0,1) (0,2) (0,3) (1,2) (1,3) (2,3) of a
+// bilinear F.grid_sample (align_corners=True, padding_mode="border", :22-48) of the pair's plane
+// (1, F, reso[c1], reso[c0]); the levels are concatenated.  The backward is the one torch's autograd
+// derives from that graph: grid_sampler_2d_backward's tap weights and coordinate gradients
+// (border-clipped coordinates, borders included, get zero coordinate gradient) chained through the
+// left-to-right product.
+//
+// The reference runs 2 x 6 grid_sample launches + gathers + 10 products forward and the same again
+// backward (~10 ms of the 100k-Gaussian train step, dominated by grid_sampler_2d_backward's atomics
+// and the gather backward).  Here: one forward and one backward launch.  MI355X mapping:
+//   - planes are repacked channels-last, (H, W, F) per plane, in one buffer: a bilinear tap is F
+//     contiguous floats, so a thread serving 4 features reads one float4 per tap;
+//   - a point is served by F/4 consecutive lanes; plane values stay in registers, so the backward
+//     recomputes them instead of storing the 6 x levels intermediate tensors the reference keeps;
+//   - coordinate gradients are reduced over the point's lanes with shuffles (no atomics);
+//   - grid gradients are hardware float atomics (no-return) into the channels-last buffer, repacked to
+//     the (1, F, H, W) parameter layout by one launch.
+#include "../../include/gs4d_train.h"
+#include "gs4d_internal.h"
+
+namespace gs4d {
+
+constexpr int kHexThreads = 256;
+__constant__ int kPairC0[6] = {0, 0, 0, 1, 1, 2};
+__constant__ int kPairC1[6] = {1, 2, 3, 2, 3, 3};
+
+struct Tap {
+    int i00, i10, i01, i11;  // cell indices (row-major H x W) of nw, ne, sw, se; -1 when outside
+    float w00, w10, w01, w11;
+    float ix, iy, gxm, gym;  // unnormalised coordinates and their chain factors (0 when clipped)
+    int x0, y0;
+};
+
+// grid_sampler_unnormalize (align_corners) + clip_coordinates(_set_grad) for border padding
+__device__ __forceinline__ float unnorm_clip(float c, int size, float &gmul) {
+    float v = ((c + 1.f) / 2.f) * (float)(size - 1);
+    const float lim = (float)(size - 1);
+    if (v <= 0.f) {
+        gmul = 0.f;
+        return 0.f;
+    }
+    if (v >= lim) {
+        gmul = 0.f;
+        return lim;
+    }
+    gmul = (float)(size - 1) / 2.f;
+    return v;
+}
+
+__device__ __forceinline__ Tap make_tap(float x, float y, int W, int H) {
+    Tap t;
+    t.ix = unnorm_clip(x, W, t.gxm);
+    t.iy = unnorm_clip(y, H, t.gym);
+    t.x0 = (int)floorf(t.ix);
+    t.y0 = (int)floorf(t.iy);
+    const int x1 = t.x0 + 1, y1 = t.y0 + 1;
+    t.w00 = ((float)x1 - t.ix) * ((float)y1 - t.iy);
+    t.w10 = (t.ix - (float)t.x0) * ((float)y1 - t.iy);
+    t.w01 = ((float)x1 - t.ix) * (t.iy - (float)t.y0);
+    t.w11 = (t.ix - (float)t.x0) * (t.iy - (float)t.y0);
+    const bool in_x0 = t.x0 >= 0 && t.x0 < W, in_x1 = x1 >= 0 && x1 < W;
+    const bool in_y0 = t.y0 >= 0 && t.y0 < H, in_y1 = y1 >= 0 && y1 < H;
+    t.i00 = (in_x0 && in_y0) ? t.y0 * W + t.x0 : -1;
+    t.i10 = (in_x1 && in_y0) ? t.y0 * W + x1 : -1;
+    t.i01 = (in_x0 && in_y1) ? y1 * W + t.x0 : -1;
+    t.i11 = (in_x1 && in_y1) ? y1 * W + x1 : -1;
+    return t;
+}
+
+__device__ __forceinline__ float4 ld4(const float *base, int cell, int F, int q) {
+    return cell >= 0 ? *reinterpret_cast<const float4 *>(base + (size_t)cell * F + 4 * q)
+                     : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+__device__ __forceinline__ float sel(const float4 &v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
+
+// the 4 taps of one plane for features [4q, 4q+4): value (grid_sampler_2d accumulation order)
+struct TapVals {
+    float4 v00, v10, v01, v11;
+};
+__device__ __forceinline__ TapVals load_taps(const float *plane, const Tap &t, int F, int q) {
+    TapVals r;
+    r.v00 = ld4(plane, t.i00, F, q);
+    r.v10 = ld4(plane, t.i10, F, q);
+    r.v01 = ld4(plane, t.i01, F, q);
+    r.v11 = ld4(plane, t.i11, F, q);
+    return r;
+}
+__device__ __forceinline__ float interp(const TapVals &r, const Tap &t, int k) {
+    float v = 0.f;
+    v = fmaf(sel(r.v00, k), t.w00, v);
+    v = fmaf(sel(r.v10, k), t.w10, v);
+    v = fmaf(sel(r.v01, k), t.w01, v);
+    v = fmaf(sel(r.v11, k), t.w11, v);
+    return v;
+}
+
+__global__ __launch_bounds__(kHexThreads) void hexplane_forward_kernel(int N, const float *__restrict__ pts,
+                                                                       gs4d_hexplane_layout lay,
+                                                                       const float *__restrict__ packed,
+                                                                       float *__restrict__ feat) {
+    const int G = lay.F / 4;
+    const int64_t tid = (int64_t)blockIdx.x * kHexThreads + threadIdx.x;
+    const int n = (int)(tid / G), q = (int)(tid % G);
+    if (n >= N) return;
+    const float4 p4 = reinterpret_cast<const float4 *>(pts)[n];
+    const float pc[4] = {p4.x, p4.y, p4.z, p4.w};
+    for (int l = 0; l < lay.levels; l++) {
+        float prod[4] = {1.f, 1.f, 1.f, 1.f};
+        for (int p = 0; p < 6; p++) {
+            const gs4d_hexplane_plane pl = lay.plane[6 * l + p];
+            const Tap t = make_tap(pc[kPairC0[p]], pc[kPairC1[p]], pl.W, pl.H);
+            const TapVals r = load_taps(packed + pl.offset, t, lay.F, q);
+#pragma unroll
+            for (int k = 0; k < 4; k++) prod[k] = prod[k] * interp(r, t, k);  // interp_space * interp
+        }
+        *reinterpret_cast<float4 *>(feat + (size_t)n * lay.levels * lay.F + l * lay.F + 4 * q) =
+            make_float4(prod[0], prod[1], prod[2], prod[3]);
+    }
+}
+
+__global__ __launch_bounds__(kHexThreads) void hexplane_backward_kernel(int N, const float *__restrict__ pts,
+                                                                        gs4d_hexplane_layout lay,
+                                                                        const float *__restrict__ packed,
+                                                                        const float *__restrict__ dfeat,
+                                                                        float *__restrict__ dpacked,
+                                                                        float *__restrict__ dpts) {
+    const int G = lay.F / 4;
+    const int64_t tid = (int64_t)blockIdx.x * kHexThreads + threadIdx.x;
+    const int n = (int)(tid / G), q = (int)(tid % G);
+    const bool live = n < N;
+    float pc[4] = {0.f, 0.f, 0.f, 0.f};
+    if (live) {
+        const float4 p4 = reinterpret_cast<const float4 *>(pts)[n];
+        pc[0] = p4.x; pc[1] = p4.y; pc[2] = p4.z; pc[3] = p4.w;
+    }
+    float gpt[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int l = 0; l < lay.levels && live; l++) {
+        float v[6][4], pre[6][4];
+        for (int p = 0; p < 6; p++) {
+            const gs4d_hexplane_plane pl = lay.plane[6 * l + p];
+            const Tap t = make_tap(pc[kPairC0[p]], pc[kPairC1[p]], pl.W, pl.H);
+            const TapVals r = load_taps(packed + pl.offset, t, lay.F, q);
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                v[p][k] = interp(r, t, k);
+                pre[p][k] = (p == 0 ? 1.f : pre[p - 1][k]) * v[p][k];  // left-to-right product
+            }
+        }
+        const float4 d4 = *reinterpret_cast<const float4 *>(dfeat + (size_t)n * lay.levels * lay.F + l * lay.F + 4 * q);
+        float g[4] = {d4.x, d4.y, d4.z, d4.w};
+        for (int p = 5; p >= 0; p--) {
+            // autograd of prod_p = prod_{p-1} * v_p: dv_p = g * prod_{p-1}, g <- g * v_p
+            float dv[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                dv[k] = g[k] * (p == 0 ? 1.f : pre[p - 1][k]);
+                g[k] = g[k] * v[p][k];
+            }
+            const gs4d_hexplane_plane pl = lay.plane[6 * l + p];
+            const Tap t = make_tap(pc[kPairC0[p]], pc[kPairC1[p]], pl.W, pl.H);
+            const TapVals r = load_taps(packed + pl.offset, t, lay.F, q);
+            float gix = 0.f, giy = 0.f;
+            const float x1 = (float)(t.x0 + 1), y1 = (float)(t.y0 + 1), x0 = (float)t.x0, y0 = (float)t.y0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const float go = dv[k];
+                // grid_sampler_2d_backward (bilinear): input gradient and coordinate gradient
+                gix -= sel(r.v00, k) * (y1 - t.iy) * go;
+                giy -= sel(r.v00, k) * (x1 - t.ix) * go;
+                gix += sel(r.v10, k) * (y1 - t.iy) * go;
+                giy -= sel(r.v10, k) * (t.ix - x0) * go;
+                gix -= sel(r.v01, k) * (t.iy - y0) * go;
+                giy += sel(r.v01, k) * (x1 - t.ix) * go;
+                gix += sel(r.v11, k) * (t.iy - y0) * go;
+                giy += sel(r.v11, k) * (t.ix - x0) * go;
+            }
+            float *dpl = dpacked + pl.offset + 4 * q;
+            const int cells[4] = {t.i00, t.i10, t.i01, t.i11};
+            const float ws[4] = {t.w00, t.w10, t.w01, t.w11};
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                if (cells[c] < 0) continue;
+                float *dst = dpl + (size_t)cells[c] * lay.F;
+#pragma unroll
+                for (int k = 0; k < 4; k++) unsafeAtomicAdd(dst + k, ws[c] * dv[k]);
+            }
+            gpt[kPairC0[p]] += t.gxm * gix;
+            gpt[kPairC1[p]] += t.gym * giy;
+        }
+    }
+    // sum the coordinate gradient over the point's F/4 lanes (consecutive lanes)
+#pragma unroll
+    for (int c = 0; c < 4; c++)
+        for (int off = 1; off < G; off <<= 1) gpt[c] += __shfl_xor(gpt[c], off);
+    if (live && q == 0)
+        reinterpret_cast<float4 *>(dpts)[n] = make_float4(gpt[0], gpt[1], gpt[2], gpt[3]);
+}
+
+// (1, F, H, W) planes <-> the packed channels-last buffer.  One thread per packed element.
+template <bool PACK>
+__global__ __launch_bounds__(kHexThreads) void hexplane_repack_kernel(gs4d_hexplane_layout lay,
+                                                                      float *__restrict__ packed) {
+    const int64_t i = (int64_t)blockIdx.x * kHexThreads + threadIdx.x;
+    if (i >= lay.total) return;
+    int p = 0;
+    while (p + 1 < 6 * lay.levels && lay.plane[p + 1].offset <= i) p++;
+    const gs4d_hexplane_plane pl = lay.plane[p];
+    const int64_t local = i - pl.offset;  // = cell * F + f
+    const int f = (int)(local % lay.F);
+    const int64_t cell = local / lay.F;
+    const int64_t planar = (int64_t)f * pl.H * pl.W + cell;  // (F, H, W) index
+    if (PACK) packed[i] = pl.param[planar];
+    else pl.grad[planar] = packed[i];
+}
+
+}  // namespace gs4d
+
+using namespace gs4d;
+
+extern "C" {
+
+int gs4d_hexplane_layout_init(gs4d_hexplane_layout *lay, int levels, int F, const int *W, const int *H) {
+    if (!lay || levels < 1 || levels > GS4D_HEXPLANE_MAX_LEVELS || F < 4 || F % 4 != 0 || F > 256) return 1;
+    if (((F / 4) & (F / 4 - 1)) != 0) return 1;  // the lanes of a point form an aligned power-of-two group
+    lay->levels = levels;
+    lay->F = F;
+    int64_t off = 0;
+    for (int i = 0; i < 6 * levels; i++) {
+        if (W[i] < 1 || H[i] < 1) return 1;
+        lay->plane[i].W = W[i];
+        lay->plane[i].H = H[i];
+        lay->plane[i].offset = off;
+        lay->plane[i].param = nullptr;
+        lay->plane[i].grad = nullptr;
+        off += (int64_t)W[i] * H[i] * F;
+    }
+    lay->total = off;
+    return 0;
+}
+
+int gs4d_hexplane_pack(const gs4d_hexplane_layout *lay, float *packed, void *stream) {
+    if (!lay || !packed) return 1;
+    for (int p = 0; p < 6 * lay->levels; p++)
+        if (!lay->plane[p].param) return 1;
+    const int64_t nb = (lay->total + kHexThreads - 1) / kHexThreads;
+    hipLaunchKernelGGL(hexplane_repack_kernel<true>, dim3((unsigned)nb), dim3(kHexThreads), 0, (hipStream_t)stream,
+                       *lay, packed);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+int gs4d_hexplane_unpack(const gs4d_hexplane_layout *lay, const float *packed, void *stream) {
+    if (!lay || !packed) return 1;
+    for (int p = 0; p < 6 * lay->levels; p++)
+        if (!lay->plane[p].grad) return 1;
+    const int64_t nb = (lay->total + kHexThreads - 1) / kHexThreads;
+    hipLaunchKernelGGL(hexplane_repack_kernel<false>, dim3((unsigned)nb), dim3(kHexThreads), 0, (hipStream_t)stream,
+                       *lay, (float *)packed);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+int gs4d_hexplane_forward(int N, const float *pts, const gs4d_hexplane_layout *lay, const float *packed, float *feat,
+                          void *stream) {
+    if (N < 0 || !lay || (N > 0 && (!pts || !packed || !feat))) return 1;
+    if (((size_t)pts & 15) || ((size_t)packed & 15) || ((size_t)feat & 15)) return 1;
+    if (N == 0) return 0;
+    const int64_t threads = (int64_t)N * (lay->F / 4);
+    hipLaunchKernelGGL(hexplane_forward_kernel, dim3((unsigned)((threads + kHexThreads - 1) / kHexThreads)),
+                       dim3(kHexThreads), 0, (hipStream_t)stream, N, pts, *lay, packed, feat);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+int gs4d_hexplane_backward(int N, const float *pts, const gs4d_hexplane_layout *lay, const float *packed,
+                           const float *dfeat, float *dpacked, float *dpts, void *stream) {
+    if (N < 0 || !lay || (N > 0 && (!pts || !packed || !dfeat || !dpacked || !dpts))) return 1;
+    if (((size_t)pts & 15) || ((size_t)packed & 15) || ((size_t)dfeat & 15) || ((size_t)dpts & 15)) return 1;
+    if (N == 0) return 0;
+    const int64_t threads = (int64_t)N * (lay->F / 4);
+    hipLaunchKernelGGL(hexplane_backward_kernel, dim3((unsigned)((threads + kHexThreads - 1) / kHexThreads)),
+                       dim3(kHexThreads), 0, (hipStream_t)stream, N, pts, *lay, packed, dfeat, dpacked, dpts);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+}  // extern "C"

@@ -1,0 +1,195 @@
+// train_glue.cpp -- the `gs4d_train._C` extension: PyTorch-ROCm tensors -> the train-step C ABI
+// (include/gs4d_train.h).  Launches go to the current HIP stream; CPU tensors raise.
+#include <ATen/ATen.h>
+#include <c10/hip/HIPGuard.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/extension.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/gs4d.h"
+#include "../../include/gs4d_train.h"
+
+namespace {
+void need(bool ok, const std::string &msg) {
+    if (!ok) throw std::runtime_error(msg);
+}
+void check(int st, const char *what) {
+    if (st != 0) throw std::runtime_error(std::string(what) + " failed (status " + std::to_string(st) + ")");
+}
+void gpu_f32(const torch::Tensor &t, const char *name) {
+    need(t.is_cuda(), std::string(name) + " must be a HIP (GPU) tensor");
+    need(t.scalar_type() == torch::kFloat32, std::string(name) + " must be float32");
+    need(t.is_contiguous(), std::string(name) + " must be contiguous");
+}
+hipStream_t stream_of(const torch::Tensor &t) { return c10::hip::getCurrentHIPStream(t.device().index()).stream(); }
+}  // namespace
+
+// l1_loss forward: returns (loss (0-dim), sign (int8, x's shape))
+std::tuple<torch::Tensor, torch::Tensor> l1_forward(const torch::Tensor &x_, const torch::Tensor &y_) {
+    need(x_.sizes() == y_.sizes(), "l1_loss: shapes differ");
+    need(x_.is_cuda() && y_.is_cuda(), "l1_loss: inputs must be HIP (GPU) tensors");
+    c10::hip::HIPGuard guard(x_.device().index());
+    torch::Tensor x = x_.to(torch::kFloat32).contiguous(), y = y_.to(torch::kFloat32).contiguous();
+    const int64_t n = x.numel();
+    torch::Tensor sign = torch::empty(x.sizes(), x.options().dtype(torch::kInt8));
+    torch::Tensor loss = torch::empty({}, x.options());
+    torch::Tensor scratch = torch::empty({(int64_t)gs4d_l1_scratch_bytes(n)}, x.options().dtype(torch::kUInt8));
+    check(gs4d_l1_loss_forward(n, x.data_ptr<float>(), y.data_ptr<float>(), sign.data_ptr<int8_t>(),
+                               loss.data_ptr<float>(), scratch.data_ptr(), stream_of(x)),
+          "l1_loss forward");
+    return {loss, sign};
+}
+
+torch::Tensor l1_backward(const torch::Tensor &sign, const torch::Tensor &dloss_) {
+    c10::hip::HIPGuard guard(sign.device().index());
+    torch::Tensor dloss = dloss_.to(torch::kFloat32).contiguous();
+    torch::Tensor grad = torch::empty(sign.sizes(), sign.options().dtype(torch::kFloat32));
+    check(gs4d_l1_loss_backward(sign.numel(), sign.data_ptr<int8_t>(), dloss.data_ptr<float>(), grad.data_ptr<float>(),
+                                stream_of(sign)),
+          "l1_loss backward");
+    return grad;
+}
+
+void densify_stats(const torch::Tensor &vs_grad, const torch::Tensor &visible, const torch::Tensor &radii,
+                   torch::Tensor &grad_accum, torch::Tensor &denom, torch::Tensor &max_radii) {
+    gpu_f32(vs_grad, "viewspace grad");
+    gpu_f32(grad_accum, "xyz_gradient_accum");
+    gpu_f32(denom, "denom");
+    const int P = (int)vs_grad.size(0);
+    need(vs_grad.dim() == 2 && vs_grad.size(1) == 3, "viewspace grad must be (P, 3)");
+    need(visible.scalar_type() == torch::kBool && visible.numel() == P && visible.is_cuda(), "visibility must be bool (P)");
+    need(grad_accum.numel() == P && denom.numel() == P, "accumulators must have P elements");
+    c10::hip::HIPGuard guard(vs_grad.device().index());
+    torch::Tensor vis = visible.contiguous();
+    torch::Tensor r;
+    if (radii.numel()) {
+        need(radii.numel() == P && radii.is_cuda(), "radii must have P elements");
+        gpu_f32(max_radii, "max_radii2D");
+        r = radii.to(torch::kInt32).contiguous();
+    }
+    check(gs4d_densify_stats(P, vs_grad.data_ptr<float>(), reinterpret_cast<const uint8_t *>(vis.data_ptr<bool>()),
+                             r.defined() ? r.data_ptr<int>() : nullptr, grad_accum.data_ptr<float>(),
+                             denom.data_ptr<float>(), r.defined() ? max_radii.data_ptr<float>() : nullptr,
+                             stream_of(vs_grad)),
+          "densify_stats");
+}
+
+// One multi-tensor Adam step over lists of equally long (param, grad, exp_avg, exp_avg_sq) tensors;
+// neg_step_sizes / bc2_sqrts hold the per-tensor scalars (torch computes them in double).
+void adam_step(std::vector<torch::Tensor> params, std::vector<torch::Tensor> grads, std::vector<torch::Tensor> exp_avgs,
+               std::vector<torch::Tensor> exp_avg_sqs, std::vector<double> neg_step_sizes, std::vector<double> bc2_sqrts,
+               double beta1, double beta2, double eps) {
+    const size_t n = params.size();
+    need(grads.size() == n && exp_avgs.size() == n && exp_avg_sqs.size() == n && neg_step_sizes.size() == n &&
+             bc2_sqrts.size() == n,
+         "adam_step: list lengths differ");
+    if (n == 0) return;
+    c10::hip::HIPGuard guard(params[0].device().index());
+    hipStream_t s = stream_of(params[0]);
+    gs4d_adam_batch b;
+    auto reset = [&]() {
+        b.count = 0;
+        b.beta1 = (float)beta1;
+        b.one_minus_beta1 = (float)(1.0 - beta1);
+        b.beta2 = (float)beta2;
+        b.one_minus_beta2 = (float)(1.0 - beta2);
+        b.eps = (float)eps;
+    };
+    reset();
+    int64_t chunks = 0;
+    for (size_t i = 0; i < n; i++) {
+        for (auto *t : {&params[i], &grads[i], &exp_avgs[i], &exp_avg_sqs[i]}) gpu_f32(*t, "adam tensor");
+        need(params[i].device() == params[0].device(), "adam_step: tensors on several devices");
+        need(grads[i].numel() == params[i].numel() && exp_avgs[i].numel() == params[i].numel() &&
+                 exp_avg_sqs[i].numel() == params[i].numel(),
+             "adam_step: tensor sizes differ");
+        if (b.count == GS4D_ADAM_MAX_TENSORS) {
+            check(gs4d_adam_step(&b, (void *)s), "adam_step");
+            reset();
+            chunks = 0;
+        }
+        gs4d_adam_tensor &d = b.t[b.count++];
+        d.param = params[i].data_ptr<float>();
+        d.grad = grads[i].data_ptr<float>();
+        d.exp_avg = exp_avgs[i].data_ptr<float>();
+        d.exp_avg_sq = exp_avg_sqs[i].data_ptr<float>();
+        d.n = params[i].numel();
+        d.first_chunk = chunks;
+        d.neg_step_size = (float)neg_step_sizes[i];
+        d.bias_correction2_sqrt = (float)bc2_sqrts[i];
+        chunks += gs4d_adam_chunks(d.n);
+    }
+    check(gs4d_adam_step(&b, (void *)s), "adam_step");
+}
+
+// ---- HexPlane field -------------------------------------------------------------------------------
+static gs4d_hexplane_layout hex_layout(const std::vector<torch::Tensor> &planes) {
+    need(!planes.empty() && planes.size() % 6 == 0, "hexplane: expected 6 planes per level");
+    const int levels = (int)(planes.size() / 6);
+    const int F = (int)planes[0].size(1);
+    std::vector<int> W, H;
+    for (auto &p : planes) {
+        gpu_f32(p, "hexplane plane");
+        need(p.dim() == 4 && p.size(0) == 1 && p.size(1) == F, "hexplane planes must be (1, F, H, W) with one F");
+        W.push_back((int)p.size(3));
+        H.push_back((int)p.size(2));
+    }
+    gs4d_hexplane_layout lay;
+    check(gs4d_hexplane_layout_init(&lay, levels, F, W.data(), H.data()), "hexplane layout");
+    for (size_t i = 0; i < planes.size(); i++) lay.plane[i].param = planes[i].data_ptr<float>();
+    return lay;
+}
+
+// returns (feat (N, levels*F), packed channels-last planes for the backward)
+std::tuple<torch::Tensor, torch::Tensor> hexplane_forward(const torch::Tensor &pts_, std::vector<torch::Tensor> planes) {
+    need(pts_.dim() == 2 && pts_.size(1) == 4 && pts_.is_cuda(), "hexplane: pts must be (N, 4) on the GPU");
+    c10::hip::HIPGuard guard(pts_.device().index());
+    torch::Tensor pts = pts_.to(torch::kFloat32).contiguous();
+    gs4d_hexplane_layout lay = hex_layout(planes);
+    const int N = (int)pts.size(0);
+    torch::Tensor packed = torch::empty({lay.total}, pts.options());
+    torch::Tensor feat = torch::empty({N, (int64_t)lay.levels * lay.F}, pts.options());
+    hipStream_t s = stream_of(pts);
+    check(gs4d_hexplane_pack(&lay, packed.data_ptr<float>(), (void *)s), "hexplane pack");
+    check(gs4d_hexplane_forward(N, pts.data_ptr<float>(), &lay, packed.data_ptr<float>(), feat.data_ptr<float>(), (void *)s),
+          "hexplane forward");
+    return {feat, packed};
+}
+
+// returns (dpts (N, 4), plane gradients (1, F, H, W) each)
+std::tuple<torch::Tensor, std::vector<torch::Tensor>> hexplane_backward(const torch::Tensor &pts_,
+                                                                         std::vector<torch::Tensor> planes,
+                                                                         const torch::Tensor &packed,
+                                                                         const torch::Tensor &dfeat_) {
+    c10::hip::HIPGuard guard(pts_.device().index());
+    torch::Tensor pts = pts_.to(torch::kFloat32).contiguous(), dfeat = dfeat_.to(torch::kFloat32).contiguous();
+    gs4d_hexplane_layout lay = hex_layout(planes);
+    const int N = (int)pts.size(0);
+    need(packed.numel() == lay.total, "hexplane backward: packed buffer size");
+    need(dfeat.dim() == 2 && dfeat.size(0) == N && dfeat.size(1) == (int64_t)lay.levels * lay.F, "hexplane backward: dfeat shape");
+    torch::Tensor dpacked = torch::zeros({lay.total}, pts.options());
+    torch::Tensor dpts = torch::empty({N, 4}, pts.options());
+    std::vector<torch::Tensor> grads;
+    for (size_t i = 0; i < planes.size(); i++) {
+        grads.push_back(torch::empty_like(planes[i]));
+        lay.plane[i].grad = grads.back().data_ptr<float>();
+    }
+    hipStream_t s = stream_of(pts);
+    check(gs4d_hexplane_backward(N, pts.data_ptr<float>(), &lay, packed.data_ptr<float>(), dfeat.data_ptr<float>(),
+                                 dpacked.data_ptr<float>(), dpts.data_ptr<float>(), (void *)s),
+          "hexplane backward");
+    check(gs4d_hexplane_unpack(&lay, dpacked.data_ptr<float>(), (void *)s), "hexplane unpack");
+    return {dpts, grads};
+}
+
+PYBIND11_MODULE(_C, m) {
+    m.def("hexplane_forward", &hexplane_forward);
+    m.def("hexplane_backward", &hexplane_backward);
+    m.def("l1_forward", &l1_forward);
+    m.def("l1_backward", &l1_backward);
+    m.def("densify_stats", &densify_stats);
+    m.def("adam_step", &adam_step);
+    m.def("version", []() { return std::string(gs4d_version()); });
+}

@@ -1,0 +1,179 @@
+"""The HexPlane deformation field that runs before the rasterizer in the fine stage.
+
+Restates scene/hexplane.py and scene/deformation.py of the reference in
+PyTorch, module for module, so that a trained reference `deformation.pth` state dict loads into it
+unchanged (same parameter names and shapes: `deformation_net.grid.grids.{level}.{plane}`,
+`deformation_net.feature_out.*`, `deformation_net.{pos,scales,rotations,opacity,shs}_deform.*`,
+`timenet.*`).  The grid interpolation (the field's cost centre) can run either through
+`F.grid_sample` exactly as the reference does, or through the fused HIP kernel of libgs4d
+(`gs4d_train.kernels.hexplane`), selected by `HexPlaneField.fused`.
+"""
+import itertools
+from typing import Sequence
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+def normalize_aabb(pts, aabb):
+    """scene/hexplane.py:20-21.  aabb[0] is the MAX corner, aabb[1] the min (set_aabb order)."""
+    return (pts - aabb[0]) * (2.0 / (aabb[1] - aabb[0])) - 1.0
+
+
+def grid_sample_wrapper(grid, coords, align_corners=True):
+    """scene/hexplane.py:22-48: bilinear, border padding, (1, F, H, W) grid at (n, 2) coords -> (n, F)."""
+    grid_dim = coords.shape[-1]
+    if grid.dim() == grid_dim + 1:
+        grid = grid.unsqueeze(0)
+    if coords.dim() == 2:
+        coords = coords.unsqueeze(0)
+    coords = coords.view([coords.shape[0]] + [1] * (grid_dim - 1) + list(coords.shape[1:]))
+    B, feature_dim = grid.shape[:2]
+    n = coords.shape[-2]
+    interp = F.grid_sample(grid, coords, align_corners=align_corners, mode="bilinear", padding_mode="border")
+    interp = interp.view(B, feature_dim, n).transpose(-1, -2)
+    return interp.squeeze()
+
+
+def init_grid_param(grid_nd, in_dim, out_dim, reso: Sequence[int], a=0.1, b=0.5):
+    """scene/hexplane.py:50-72: one (1, out_dim, reso[c1], reso[c0]) plane per coordinate pair;
+    planes that involve time (coordinate 3) start at 1, the others uniform in [a, b]."""
+    assert in_dim == len(reso)
+    has_time_planes = in_dim == 4
+    grid_coefs = nn.ParameterList()
+    for coo_comb in itertools.combinations(range(in_dim), grid_nd):
+        p = nn.Parameter(torch.empty([1, out_dim] + [reso[cc] for cc in coo_comb[::-1]]))
+        if has_time_planes and 3 in coo_comb:
+            nn.init.ones_(p)
+        else:
+            nn.init.uniform_(p, a=a, b=b)
+        grid_coefs.append(p)
+    return grid_coefs
+
+
+class HexPlaneField(nn.Module):
+    """scene/hexplane.py:113-190 (concat_features=True)."""
+
+    def __init__(self, bounds, planeconfig, multires):
+        super().__init__()
+        aabb = torch.tensor([[bounds, bounds, bounds], [-bounds, -bounds, -bounds]])
+        self.aabb = nn.Parameter(aabb, requires_grad=False)
+        self.grid_config = [planeconfig]
+        self.multiscale_res_multipliers = multires
+        self.concat_features = True
+        self.grids = nn.ModuleList()
+        self.feat_dim = 0
+        for res in multires:
+            config = dict(self.grid_config[0])
+            config["resolution"] = [r * res for r in config["resolution"][:3]] + config["resolution"][3:]
+            gp = init_grid_param(config["grid_dimensions"], config["input_coordinate_dim"],
+                                 config["output_coordinate_dim"], config["resolution"])
+            self.feat_dim += gp[-1].shape[1]
+            self.grids.append(gp)
+        self.fused = False  # True: the HIP kernel (kernels.hexplane) instead of F.grid_sample
+
+    @property
+    def get_aabb(self):
+        return self.aabb[0], self.aabb[1]
+
+    def set_aabb(self, xyz_max, xyz_min):
+        self.aabb = nn.Parameter(torch.tensor([xyz_max, xyz_min], dtype=torch.float32, device=self.aabb.device),
+                                 requires_grad=False)
+
+    def forward(self, pts, timestamps=None):
+        """get_density (scene/hexplane.py:160-177): normalised (x, y, z, t) -> per-level plane products."""
+        pts = normalize_aabb(pts, self.aabb)
+        pts = torch.cat((pts, timestamps), dim=-1).reshape(-1, 4)
+        if self.fused:
+            from .kernels import hexplane
+            return hexplane(pts, [list(g) for g in self.grids])
+        return interpolate_ms_features(pts, self.grids)
+
+
+def interpolate_ms_features(pts, ms_grids):
+    """scene/hexplane.py:75-110 with concat_features=True, grid_dimensions=2."""
+    coo_combs = list(itertools.combinations(range(pts.shape[-1]), 2))
+    out = []
+    for grid in ms_grids:
+        interp_space = 1.0
+        for ci, coo_comb in enumerate(coo_combs):
+            feature_dim = grid[ci].shape[1]
+            interp_space = interp_space * grid_sample_wrapper(grid[ci], pts[..., coo_comb]).view(-1, feature_dim)
+        out.append(interp_space)
+    return torch.cat(out, dim=-1)
+
+
+class Deformation(nn.Module):
+    """scene/deformation.py:16-172 (no_grid=False, grid_pe=0, empty_voxel=False, static_mlp=False)."""
+
+    def __init__(self, D=8, W=256, args=None):
+        super().__init__()
+        self.D, self.W, self.args = D, W, args
+        self.grid = HexPlaneField(args.bounds, args.kplanes_config, args.multires)
+        self.feature_out = [nn.Linear(self.grid.feat_dim, W)]
+        for _ in range(D - 1):
+            self.feature_out += [nn.ReLU(), nn.Linear(W, W)]
+        self.feature_out = nn.Sequential(*self.feature_out)
+        head = lambda n: nn.Sequential(nn.ReLU(), nn.Linear(W, W), nn.ReLU(), nn.Linear(W, n))
+        self.pos_deform, self.scales_deform, self.rotations_deform = head(3), head(3), head(4)
+        self.opacity_deform, self.shs_deform = head(1), head(16 * 3)
+
+    def forward(self, xyz, scales, rotations, opacity, shs, time):
+        """forward_dynamic (scene/deformation.py:97-146); mask = 1 (no static_mlp / empty_voxel)."""
+        hidden = self.feature_out(self.grid(xyz[:, :3], time[:, :1]))
+        a = self.args
+        pts = xyz[:, :3] if a.no_dx else xyz[:, :3] + self.pos_deform(hidden)
+        sc = scales[:, :3] if a.no_ds else scales[:, :3] + self.scales_deform(hidden)
+        if a.no_dr:
+            rot = rotations[:, :4]
+        elif a.apply_rotation:
+            raise NotImplementedError("apply_rotation (documented as unused in arguments/__init__.py:104)")
+        else:
+            rot = rotations[:, :4] + self.rotations_deform(hidden)
+        op = opacity[:, :1] if a.no_do else opacity[:, :1] + self.opacity_deform(hidden)
+        sh = shs if a.no_dshs else shs + self.shs_deform(hidden).reshape([shs.shape[0], 16, 3])
+        return pts, sc, rot, op, sh
+
+    def get_mlp_parameters(self):
+        return [p for n, p in self.named_parameters() if "grid" not in n]
+
+    def get_grid_parameters(self):
+        return [p for n, p in self.named_parameters() if "grid" in n]
+
+
+class DeformNetwork(nn.Module):
+    """deform_network (scene/deformation.py:173-234).  The reference computes positional encodings of
+    the inputs (poc_fre) but its Deformation only reads their raw leading columns, so they are not
+    materialised here; the (unused) timenet is kept so state dicts match."""
+
+    def __init__(self, args):
+        super().__init__()
+        times_ch = 2 * args.timebase_pe + 1
+        self.timenet = nn.Sequential(nn.Linear(times_ch, args.timenet_width), nn.ReLU(),
+                                     nn.Linear(args.timenet_width, args.timenet_output))
+        self.deformation_net = Deformation(W=args.net_width, D=args.defor_depth, args=args)
+        self.register_buffer("time_poc", torch.FloatTensor([(2 ** i) for i in range(args.timebase_pe)]))
+        self.register_buffer("pos_poc", torch.FloatTensor([(2 ** i) for i in range(args.posebase_pe)]))
+        self.register_buffer("rotation_scaling_poc", torch.FloatTensor([(2 ** i) for i in range(args.scale_rotation_pe)]))
+        self.register_buffer("opacity_poc", torch.FloatTensor([(2 ** i) for i in range(args.opacity_pe)]))
+        self.apply(initialize_weights)
+
+    @property
+    def get_aabb(self):
+        return self.deformation_net.grid.get_aabb
+
+    def forward(self, point, scales=None, rotations=None, opacity=None, shs=None, times_sel=None):
+        return self.deformation_net(point, scales, rotations, opacity, shs, times_sel)
+
+    def get_mlp_parameters(self):
+        return self.deformation_net.get_mlp_parameters() + list(self.timenet.parameters())
+
+    def get_grid_parameters(self):
+        return self.deformation_net.get_grid_parameters()
+
+
+def initialize_weights(m):
+    """scene/deformation.py:236-242: xavier-uniform weights (the bias keeps nn.Linear's default)."""
+    if isinstance(m, nn.Linear):
+        nn.init.xavier_uniform_(m.weight, gain=1)

@@ -1,0 +1,114 @@
+"""Torch-facing wrappers of libgs4d's train-step kernels (include/gs4d_train.h, csrc/train_tail.hip).
+
+Importing this module loads the in-tree `gs4d_train._C` extension and fails loudly when it is not
+built: there is no silent torch fallback here.  (The reference's torch formulations live in the
+callers -- GaussianModel(fused=False), losses.l1_loss_torch -- and serve the parity tests.)
+"""
+import math
+
+import torch
+
+from . import _C
+
+__all__ = ["l1_loss", "densify_stats", "FusedAdam", "hexplane"]
+
+
+class _L1Loss(torch.autograd.Function):
+    """utils/loss_utils.py:20-21 |x - y|.mean() in one pass; backward = sign(x - y) / N * dL/dloss."""
+
+    @staticmethod
+    def forward(ctx, x, y):
+        loss, sign = _C.l1_forward(x, y)
+        ctx.save_for_backward(sign)
+        ctx.x_dtype = x.dtype
+        return loss
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        (sign,) = ctx.saved_tensors
+        return _C.l1_backward(sign, grad_out.reshape(1)).to(ctx.x_dtype), None
+
+
+def l1_loss(network_output, gt):
+    """Drop-in for utils/loss_utils.l1_loss; the ground truth receives no gradient (as in training)."""
+    return _L1Loss.apply(network_output, gt.detach())
+
+
+@torch.no_grad()
+def densify_stats(viewspace_grad, visibility, radii, grad_accum, denom, max_radii2D):
+    """train.py:346-349 + gaussian_model.py:521-523 in one launch, in place."""
+    r = radii if radii is not None else torch.empty(0, dtype=torch.int32, device=viewspace_grad.device)
+    _C.densify_stats(viewspace_grad.contiguous(), visibility, r, grad_accum, denom, max_radii2D)
+
+
+class FusedAdam(torch.optim.Optimizer):
+    """torch.optim.Adam (no weight decay / amsgrad / maximize) with the whole update in ONE launch.
+
+    Keeps torch.optim.Adam's param_groups and per-parameter state layout ({"step", "exp_avg",
+    "exp_avg_sq"}), so scene/gaussian_model.py's optimizer-state surgery (replace / prune / cat of
+    exp_avg and exp_avg_sq, :316-388) works on it unchanged.  The per-tensor scalars are formed in
+    double precision exactly as torch's multi-tensor path does (torch/optim/adam.py
+    _multi_tensor_adam): step_size = -lr / (1 - beta1^step), sqrt(1 - beta2^step).
+    """
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps))
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        by_hyper = {}
+        for group in self.param_groups:
+            beta1, beta2 = group["betas"]
+            key = (beta1, beta2, group["eps"])
+            lists = by_hyper.setdefault(key, ([], [], [], [], [], []))
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                if p.grad.is_sparse:
+                    raise RuntimeError("FusedAdam does not support sparse gradients")
+                st = self.state[p]
+                if len(st) == 0:
+                    st["step"] = torch.tensor(0.0, dtype=torch.float32)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["step"] += 1
+                step = st["step"].item()
+                bc1 = 1 - beta1 ** step
+                bc2 = 1 - beta2 ** step
+                g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
+                lists[0].append(p)
+                lists[1].append(g)
+                lists[2].append(st["exp_avg"])
+                lists[3].append(st["exp_avg_sq"])
+                lists[4].append((group["lr"] / bc1) * -1)
+                lists[5].append(bc2 ** 0.5)
+        for (beta1, beta2, eps), (ps, gs, ms, vs, ss, bs) in by_hyper.items():
+            if ps:
+                _C.adam_step(ps, gs, ms, vs, ss, bs, beta1, beta2, eps)
+        return loss
+
+
+class _HexPlane(torch.autograd.Function):
+    """scene/hexplane.py:75-110 interpolate_ms_features over all levels in one launch each way."""
+
+    @staticmethod
+    def forward(ctx, pts, *planes):
+        feat, packed = _C.hexplane_forward(pts, list(planes))
+        ctx.save_for_backward(pts, packed, *planes)
+        return feat
+
+    @staticmethod
+    def backward(ctx, dfeat):
+        pts, packed, *planes = ctx.saved_tensors
+        dpts, dplanes = _C.hexplane_backward(pts, planes, packed, dfeat)
+        return (dpts, *dplanes)
+
+
+def hexplane(pts, ms_grids):
+    """pts (N, 4) normalised (x, y, z, t); ms_grids: per level the 6 (1, F, H, W) planes."""
+    planes = [p for level in ms_grids for p in level]
+    return _HexPlane.apply(pts.contiguous(), *planes)

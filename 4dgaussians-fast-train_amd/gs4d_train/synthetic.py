@@ -61,3 +61,35 @@ def make_upstream_grad(color, seed=1):
     C, H, W = color.shape
     gt = np.random.default_rng(seed).uniform(0, 1, (C, H, W)).astype(np.float32)
     return (np.sign(color - gt) / (C * H * W)).astype(np.float32), gt
+
+
+def make_training_views(n_views, W, H, seed=0, time_range=(0.0, 1.0), radius=4.0, device="cuda"):
+    """Cameras on an arc looking at the origin, one timestamp per view, with uniform-random ground
+    truth images (3, H, W) -- synthetic data of the metric's shape (no dataset is available here)."""
+    import torch
+    rng = np.random.default_rng(seed)
+    views = []
+    for v in range(n_views):
+        a = 2 * math.pi * v / max(1, n_views) * 0.25
+        # world->camera rotation looking at the origin from (r sin a, 0, -r cos a)
+        c = np.array([radius * math.sin(a), 0.0, -radius * math.cos(a)])
+        fwd = -c / np.linalg.norm(c)
+        right = np.cross(np.array([0.0, 1.0, 0.0]), fwd)
+        right /= np.linalg.norm(right)
+        up = np.cross(fwd, right)
+        Rw2c = np.stack([right, up, fwd], 0)       # rows: camera axes in world
+        R = Rw2c.T                                 # the reference stores R transposed (getWorld2View2)
+        T = -Rw2c @ c
+        t = time_range[0] + (time_range[1] - time_range[0]) * (v / max(1, n_views - 1) if n_views > 1 else 0.0)
+        cam = make_camera(W, H, R=R, T=T, time=t)
+        gt = torch.tensor(rng.uniform(0, 1, (3, H, W)).astype(np.float32), device=device)
+        views.append((cam, gt))
+    return views
+
+
+def make_point_cloud(P, seed=0, extent=1.2):
+    """Random initial point cloud inside the deformation field's bounds, with random colours."""
+    rng = np.random.default_rng(seed)
+    pts = rng.uniform(-extent, extent, (P, 3)).astype(np.float32)
+    cols = rng.uniform(0, 1, (P, 3)).astype(np.float32)
+    return pts, cols

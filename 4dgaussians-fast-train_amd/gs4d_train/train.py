@@ -1,0 +1,104 @@
+"""One training iteration of the reference's train.py (scene_reconstruction, :144-387), restated.
+
+train_step() renders a batch of views through the deformation field and the rasterizer, takes the
+L1 loss (+ HexPlane regularisers in the fine stage, + D-SSIM when lambda_dssim != 0), back-propagates,
+sums the viewspace gradients over the views, updates the densification statistics, densifies /
+prunes / resets opacity on the reference's schedule, and steps the optimizer.  What it leaves out
+is logging and I/O: the reference's per-step host syncs for the progress bar (loss.item(), psnr)
+and the NaN check that re-execs the program (:255-257) are not part of a training step's work.
+
+With `data_parallel=True` the views of the batch are sharded over the torch.distributed ranks
+(gs4d_train.dp): each rank renders its share, and the parameter gradients, viewspace gradients,
+radii and visibility are reduced so every replica takes the single-process step.
+"""
+import torch
+
+from . import dp
+from .render import render
+
+
+def l1_loss_torch(network_output, gt):
+    """utils/loss_utils.py:20-21"""
+    return torch.abs((network_output - gt)).mean()
+
+
+def train_step(gaussians, views, opt, hyper, iteration, background, stage="fine", fused_loss=None,
+               data_parallel=False):
+    """views: list of (camera, gt_image (3, H, W)).  Returns the (detached) batch loss tensor."""
+    fused = gaussians.fused if fused_loss is None else fused_loss
+    gaussians.update_learning_rate(iteration)
+    if iteration % 1000 == 0:
+        gaussians.oneupSHdegree()
+    mine = dp.shard_views(len(views)) if data_parallel else list(range(len(views)))
+    images, gts, radii_list, vis_list, vs_list = [], [], [], [], []
+    for v in mine:
+        cam, gt = views[v]
+        pkg = render(cam, gaussians, False, background, stage=stage)
+        images.append(pkg["render"].unsqueeze(0))
+        gts.append(gt.unsqueeze(0))
+        radii_list.append(pkg["radii"].unsqueeze(0))
+        vis_list.append(pkg["visibility_filter"].unsqueeze(0))
+        vs_list.append(pkg["viewspace_points"])
+    P = gaussians.get_xyz.shape[0]
+    dev = gaussians.get_xyz.device
+    radii = torch.cat(radii_list, 0).max(dim=0).values if radii_list else torch.zeros(P, dtype=torch.int32, device=dev)
+    visibility_filter = torch.cat(vis_list).any(dim=0) if vis_list else torch.zeros(P, dtype=torch.bool, device=dev)
+    if images:
+        image_tensor = torch.cat(images, 0)
+        gt_image_tensor = torch.cat(gts, 0)
+        if fused:
+            from .kernels import l1_loss
+            Ll1 = l1_loss(image_tensor, gt_image_tensor[:, :3, :, :])
+        else:
+            Ll1 = l1_loss_torch(image_tensor, gt_image_tensor[:, :3, :, :])
+        # the batch mean over all views: each rank holds len(mine) of len(views)
+        loss = Ll1 * (len(mine) / len(views)) if data_parallel else Ll1
+    else:
+        loss = torch.zeros((), device=dev)
+    if stage == "fine" and hyper.time_smoothness_weight != 0:
+        reg = gaussians.compute_regulation(hyper.time_smoothness_weight, hyper.l1_time_planes, hyper.plane_tv_weight)
+        loss = loss + (reg / dp.world() if data_parallel else reg)
+    if opt.lambda_dssim != 0 and images:
+        from .losses import ssim
+        loss = loss + opt.lambda_dssim * (1.0 - ssim(image_tensor, gt_image_tensor)) * (
+            len(mine) / len(views) if data_parallel else 1.0)
+    loss.backward()
+    viewspace_grad = torch.zeros_like(gaussians.get_xyz)
+    for t in vs_list:
+        viewspace_grad = viewspace_grad + t.grad
+    loss_out = loss.detach().reshape(1).clone()
+    if data_parallel and dp.world() > 1:
+        params = [p for g in gaussians.optimizer.param_groups for p in g["params"]]
+        for p in params:
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+        vis_i = visibility_filter.to(torch.int32)
+        dp.allreduce_sum_([p.grad for p in params] + [viewspace_grad, loss_out])
+        torch.distributed.all_reduce(radii, op=torch.distributed.ReduceOp.MAX)
+        torch.distributed.all_reduce(vis_i, op=torch.distributed.ReduceOp.MAX)
+        visibility_filter = vis_i.bool()
+    with torch.no_grad():
+        if iteration < opt.densify_until_iter:
+            gaussians.add_densification_stats(viewspace_grad, visibility_filter, radii)
+            if stage == "coarse":
+                opacity_threshold = opt.opacity_threshold_coarse
+                densify_threshold = opt.densify_grad_threshold_coarse
+            else:
+                opacity_threshold = opt.opacity_threshold_fine_init - iteration * (
+                    opt.opacity_threshold_fine_init - opt.opacity_threshold_fine_after) / opt.densify_until_iter
+                densify_threshold = opt.densify_grad_threshold_fine_init - iteration * (
+                    opt.densify_grad_threshold_fine_init - opt.densify_grad_threshold_after) / opt.densify_until_iter
+            extent = getattr(gaussians, "cameras_extent", 1.0)
+            if iteration > opt.densify_from_iter and iteration % opt.densification_interval == 0 and P < 360000:
+                size_threshold = 20 if iteration > opt.opacity_reset_interval else None
+                gaussians.densify(densify_threshold, opacity_threshold, extent, size_threshold)
+            if iteration > opt.pruning_from_iter and iteration % opt.pruning_interval == 0 and \
+                    gaussians.get_xyz.shape[0] > 200000:
+                size_threshold = 20 if iteration > opt.opacity_reset_interval else None
+                gaussians.prune(densify_threshold, opacity_threshold, extent, size_threshold)
+            if iteration % opt.opacity_reset_interval == 0:
+                gaussians.reset_opacity()
+        if iteration < opt.iterations:
+            gaussians.optimizer.step()
+            gaussians.optimizer.zero_grad(set_to_none=True)
+    return loss_out[0]

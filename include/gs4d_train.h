@@ -1,0 +1,92 @@
+/*
+ * gs4d_train.h -- C ABI of libgs4d's train-step kernels: the rows SURVEY.md §8f lists on either side
+ * of the rasterizer (the HexPlane deformation field before it, the loss / densification statistics /
+ * optimizer after it).  Each entry point replaces a PyTorch formulation of the reference; the
+ * reference file:line it restates is given with it.  Same conventions as gs4d.h: device pointers,
+ * fp32, C-contiguous, launches enqueued on `stream`, status 0 = OK, 1 = bad argument, 3 = HIP error.
+ */
+#ifndef GS4D_TRAIN_H_INCLUDED
+#define GS4D_TRAIN_H_INCLUDED
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- L1 loss: utils/loss_utils.py:20-21 l1_loss(x, y) = |x - y|.mean(), and its autograd gradient.
+ * forward: *loss = mean |x - y| (fp64 partial sums in a fixed order), sign[i] = sign(x[i] - y[i]);
+ * scratch must hold gs4d_l1_scratch_bytes(n) bytes.  backward: grad[i] = sign[i] * (*dloss) / n. */
+size_t gs4d_l1_scratch_bytes(int64_t n);
+int gs4d_l1_loss_forward(int64_t n, const float *x, const float *y, int8_t *sign, float *loss, void *scratch,
+                         void *stream);
+int gs4d_l1_loss_backward(int64_t n, const int8_t *sign, const float *dloss, float *grad, void *stream);
+
+/* ---- densification statistics: train.py:346-349 and scene/gaussian_model.py:521-523.
+ * For every i with visible[i]: max_radii[i] = max(max_radii[i], radii[i]) (skipped when radii is
+ * NULL), grad_accum[i] += |viewspace_grad[i, 0:2]|, denom[i] += 1.  viewspace_grad is (P, 3). */
+int gs4d_densify_stats(int P, const float *viewspace_grad, const uint8_t *visible, const int *radii, float *grad_accum,
+                       float *denom, float *max_radii, void *stream);
+
+/* ---- Adam: torch.optim.Adam(params, lr, betas=(0.9, 0.999), eps=1e-15) as built by
+ * scene/gaussian_model.py:165-184, one launch for up to GS4D_ADAM_MAX_TENSORS tensors.  Per element:
+ *   m = m + (1 - beta1) (g - m);  v = beta2 v + (1 - beta2) g^2;
+ *   p = p + neg_step_size * m / (sqrt(v) / bias_correction2_sqrt + eps)
+ * with neg_step_size = -lr / (1 - beta1^step) and bias_correction2_sqrt = sqrt(1 - beta2^step)
+ * computed by the caller in double precision (as torch does).  first_chunk of tensor i must be the
+ * sum of gs4d_adam_chunks(n) over tensors 0..i-1. */
+#define GS4D_ADAM_MAX_TENSORS 48
+typedef struct {
+    float *param;
+    const float *grad;
+    float *exp_avg;
+    float *exp_avg_sq;
+    int64_t n;
+    int64_t first_chunk;
+    float neg_step_size;
+    float bias_correction2_sqrt;
+} gs4d_adam_tensor;
+typedef struct {
+    int count;
+    float beta1, one_minus_beta1, beta2, one_minus_beta2, eps;
+    gs4d_adam_tensor t[GS4D_ADAM_MAX_TENSORS];
+} gs4d_adam_batch;
+int64_t gs4d_adam_chunks(int64_t n);
+int gs4d_adam_step(const gs4d_adam_batch *batch, void *stream);
+
+/* ---- HexPlane field: scene/hexplane.py:75-110 interpolate_ms_features (concat_features=True) over the
+ * planes of init_grid_param (:50-72), each sampled with F.grid_sample(align_corners=True, bilinear,
+ * padding_mode="border") (:22-48).  pts: (N, 4) normalised (x, y, z, t), 16-byte aligned.
+ * feat: (N, levels * F) = for each level the product over the 6 coordinate pairs (0,1) (0,2) (0,3)
+ * (1,2) (1,3) (2,3) of the pair's bilinear sample.  Plane 6*l + p of level l is a (1, F, H, W)
+ * parameter tensor with W = reso[c0], H = reso[c1]; the kernels read a packed channels-last copy
+ * of all planes (gs4d_hexplane_pack) and accumulate plane gradients into a zeroed packed buffer
+ * that gs4d_hexplane_unpack writes back to (1, F, H, W) gradient tensors.  dpts receives the
+ * gradient w.r.t. pts (all 4 columns). */
+#define GS4D_HEXPLANE_MAX_LEVELS 4
+typedef struct {
+    int W, H;
+    int64_t offset; /* first float of the plane in the packed buffer: (H, W, F) */
+    const float *param; /* (1, F, H, W) parameter (pack source) */
+    float *grad;        /* (1, F, H, W) gradient (unpack destination) */
+} gs4d_hexplane_plane;
+typedef struct {
+    int levels, F; /* F: features per plane, a multiple of 4 with F / 4 a power of two */
+    int64_t total; /* floats in the packed buffer */
+    gs4d_hexplane_plane plane[6 * GS4D_HEXPLANE_MAX_LEVELS];
+} gs4d_hexplane_layout;
+/* Fills offsets/total from the per-plane sizes W[6*levels], H[6*levels]; param/grad pointers are set by the caller. */
+int gs4d_hexplane_layout_init(gs4d_hexplane_layout *lay, int levels, int F, const int *W, const int *H);
+int gs4d_hexplane_pack(const gs4d_hexplane_layout *lay, float *packed, void *stream);
+int gs4d_hexplane_unpack(const gs4d_hexplane_layout *lay, const float *packed, void *stream);
+int gs4d_hexplane_forward(int N, const float *pts, const gs4d_hexplane_layout *lay, const float *packed, float *feat,
+                          void *stream);
+int gs4d_hexplane_backward(int N, const float *pts, const gs4d_hexplane_layout *lay, const float *packed,
+                           const float *dfeat, float *dpacked, float *dpts, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GS4D_TRAIN_H_INCLUDED */
