@@ -19,6 +19,8 @@
 //   - coordinate gradients are reduced over the point's lanes with shuffles (no atomics);
 //   - grid gradients are hardware float atomics (no-return) into the channels-last buffer, repacked to
 //     the (1, F, H, W) parameter layout by one launch.
+#include <algorithm>
+
 #include "../../include/gs4d_train.h"
 #include "gs4d_internal.h"
 
@@ -122,82 +124,148 @@ __global__ __launch_bounds__(kHexThreads) void hexplane_forward_kernel(int N, co
     }
 }
 
+// Time planes: within one render call every point has the same t, so all points touch the same two
+// rows of the three (c, t) planes of a level.  Their gradients are first summed in LDS per workgroup
+// (a workgroup serves several point chunks) and added to HBM once per workgroup; the spatial planes
+// (spread over the whole plane) take direct atomics.  Workgroups whose points do not share the time
+// row (or levels whose rows do not fit kHexLdsFloats) use direct atomics throughout.
+constexpr int kHexLdsFloats = 16384;  // 64 KiB
+__device__ __forceinline__ bool is_time_plane(int p) { return kPairC1[p] == 3; }
+__device__ __forceinline__ int time_slot(int p) { return p == 2 ? 0 : (p == 4 ? 1 : 2); }
+
 __global__ __launch_bounds__(kHexThreads) void hexplane_backward_kernel(int N, const float *__restrict__ pts,
                                                                         gs4d_hexplane_layout lay,
                                                                         const float *__restrict__ packed,
                                                                         const float *__restrict__ dfeat,
                                                                         float *__restrict__ dpacked,
-                                                                        float *__restrict__ dpts) {
-    const int G = lay.F / 4;
-    const int64_t tid = (int64_t)blockIdx.x * kHexThreads + threadIdx.x;
-    const int n = (int)(tid / G), q = (int)(tid % G);
-    const bool live = n < N;
-    float pc[4] = {0.f, 0.f, 0.f, 0.f};
-    if (live) {
-        const float4 p4 = reinterpret_cast<const float4 *>(pts)[n];
-        pc[0] = p4.x; pc[1] = p4.y; pc[2] = p4.z; pc[3] = p4.w;
-    }
-    float gpt[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int l = 0; l < lay.levels && live; l++) {
-        float v[6][4], pre[6][4];
-        for (int p = 0; p < 6; p++) {
-            const gs4d_hexplane_plane pl = lay.plane[6 * l + p];
-            const Tap t = make_tap(pc[kPairC0[p]], pc[kPairC1[p]], pl.W, pl.H);
-            const TapVals r = load_taps(packed + pl.offset, t, lay.F, q);
+                                                                        float *__restrict__ dpts, int chunks_per_wg) {
+    extern __shared__ float s_rows[];  // [3 time planes][2 rows][W][F] of the current level
+    __shared__ int s_y0, s_uniform;
+    const int G = lay.F / 4, ppc = kHexThreads / G;  // lanes per point, points per chunk
+    const int q = threadIdx.x % G, slot = threadIdx.x / G;
+    const int64_t first = (int64_t)blockIdx.x * chunks_per_wg * ppc;
+    for (int l = 0; l < lay.levels; l++) {
+        const gs4d_hexplane_plane *tp[3] = {&lay.plane[6 * l + 2], &lay.plane[6 * l + 4], &lay.plane[6 * l + 5]};
+        int roff[3], nrows = 0;
+        for (int i = 0; i < 3; i++) {
+            roff[i] = nrows;
+            nrows += 2 * tp[i]->W * lay.F;
+        }
+        const int Ht = tp[0]->H;
+        bool use_lds = nrows <= kHexLdsFloats;
+        if (use_lds) {
+            // does every point of this workgroup share the time row?
+            if (threadIdx.x == 0) {
+                s_uniform = 1;
+                float gm;
+                s_y0 = first < N ? (int)floorf(unnorm_clip(pts[4 * first + 3], Ht, gm)) : 0;
+            }
+            __syncthreads();
+            for (int c = 0; c < chunks_per_wg; c++) {
+                const int64_t n = first + (int64_t)c * ppc + slot;
+                float gm;
+                if (q == 0 && n < N && (int)floorf(unnorm_clip(pts[4 * n + 3], Ht, gm)) != s_y0) s_uniform = 0;
+            }
+            for (int i = threadIdx.x; i < nrows; i += kHexThreads) s_rows[i] = 0.f;
+            __syncthreads();
+            use_lds = s_uniform != 0;
+        }
+        const int y0w = s_y0;
+        for (int c = 0; c < chunks_per_wg; c++) {
+            const int64_t n = first + (int64_t)c * ppc + slot;
+            if (n >= N) break;
+            const float4 p4 = reinterpret_cast<const float4 *>(pts)[n];
+            const float pc[4] = {p4.x, p4.y, p4.z, p4.w};
+            float gpt[4] = {0.f, 0.f, 0.f, 0.f};
+            float v[6][4], pre[6][4];
+            for (int p = 0; p < 6; p++) {
+                const gs4d_hexplane_plane pl = lay.plane[6 * l + p];
+                const Tap t = make_tap(pc[kPairC0[p]], pc[kPairC1[p]], pl.W, pl.H);
+                const TapVals r = load_taps(packed + pl.offset, t, lay.F, q);
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
-                v[p][k] = interp(r, t, k);
-                pre[p][k] = (p == 0 ? 1.f : pre[p - 1][k]) * v[p][k];  // left-to-right product
+                for (int k = 0; k < 4; k++) {
+                    v[p][k] = interp(r, t, k);
+                    pre[p][k] = (p == 0 ? 1.f : pre[p - 1][k]) * v[p][k];  // left-to-right product
+                }
+            }
+            const float4 d4 = *reinterpret_cast<const float4 *>(dfeat + (size_t)n * lay.levels * lay.F + l * lay.F + 4 * q);
+            float g[4] = {d4.x, d4.y, d4.z, d4.w};
+            for (int p = 5; p >= 0; p--) {
+                // autograd of prod_p = prod_{p-1} * v_p: dv_p = g * prod_{p-1}, g <- g * v_p
+                float dv[4];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    dv[k] = g[k] * (p == 0 ? 1.f : pre[p - 1][k]);
+                    g[k] = g[k] * v[p][k];
+                }
+                const gs4d_hexplane_plane pl = lay.plane[6 * l + p];
+                const Tap t = make_tap(pc[kPairC0[p]], pc[kPairC1[p]], pl.W, pl.H);
+                const TapVals r = load_taps(packed + pl.offset, t, lay.F, q);
+                float gix = 0.f, giy = 0.f;
+                const float x1 = (float)(t.x0 + 1), y1 = (float)(t.y0 + 1), x0 = (float)t.x0, y0 = (float)t.y0;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const float go = dv[k];
+                    // grid_sampler_2d_backward (bilinear): input gradient and coordinate gradient
+                    gix -= sel(r.v00, k) * (y1 - t.iy) * go;
+                    giy -= sel(r.v00, k) * (x1 - t.ix) * go;
+                    gix += sel(r.v10, k) * (y1 - t.iy) * go;
+                    giy -= sel(r.v10, k) * (t.ix - x0) * go;
+                    gix -= sel(r.v01, k) * (t.iy - y0) * go;
+                    giy += sel(r.v01, k) * (x1 - t.ix) * go;
+                    gix += sel(r.v11, k) * (t.iy - y0) * go;
+                    giy += sel(r.v11, k) * (t.ix - x0) * go;
+                }
+                const int cells[4] = {t.i00, t.i10, t.i01, t.i11};
+                const float ws[4] = {t.w00, t.w10, t.w01, t.w11};
+                if (use_lds && is_time_plane(p)) {
+                    // rows y0w, y0w + 1 of the plane -> LDS rows 0, 1
+                    float *dst0 = s_rows + roff[time_slot(p)] + 4 * q;
+#pragma unroll
+                    for (int cc = 0; cc < 4; cc++) {
+                        if (cells[cc] < 0) continue;
+                        const int row = cells[cc] / pl.W - y0w, x = cells[cc] % pl.W;
+                        float *dst = dst0 + (row * pl.W + x) * lay.F;
+#pragma unroll
+                        for (int k = 0; k < 4; k++) atomicAdd(dst + k, ws[cc] * dv[k]);
+                    }
+                } else {
+                    float *dpl = dpacked + pl.offset + 4 * q;
+#pragma unroll
+                    for (int cc = 0; cc < 4; cc++) {
+                        if (cells[cc] < 0) continue;
+                        float *dst = dpl + (size_t)cells[cc] * lay.F;
+#pragma unroll
+                        for (int k = 0; k < 4; k++) unsafeAtomicAdd(dst + k, ws[cc] * dv[k]);
+                    }
+                }
+                gpt[kPairC0[p]] += t.gxm * gix;
+                gpt[kPairC1[p]] += t.gym * giy;
+            }
+            // sum the coordinate gradient over the point's lanes; levels accumulate in dpts
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                for (int off = 1; off < G; off <<= 1) gpt[k] += __shfl_xor(gpt[k], off, G);
+            if (q == 0) {
+                float4 *o = reinterpret_cast<float4 *>(dpts) + n;
+                float4 acc = l == 0 ? make_float4(0.f, 0.f, 0.f, 0.f) : *o;
+                acc.x += gpt[0]; acc.y += gpt[1]; acc.z += gpt[2]; acc.w += gpt[3];
+                *o = acc;
             }
         }
-        const float4 d4 = *reinterpret_cast<const float4 *>(dfeat + (size_t)n * lay.levels * lay.F + l * lay.F + 4 * q);
-        float g[4] = {d4.x, d4.y, d4.z, d4.w};
-        for (int p = 5; p >= 0; p--) {
-            // autograd of prod_p = prod_{p-1} * v_p: dv_p = g * prod_{p-1}, g <- g * v_p
-            float dv[4];
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                dv[k] = g[k] * (p == 0 ? 1.f : pre[p - 1][k]);
-                g[k] = g[k] * v[p][k];
+        if (use_lds) {
+            __syncthreads();
+            for (int i = 0; i < 3; i++) {
+                const int W = tp[i]->W, cnt = 2 * W * lay.F;
+                for (int e = threadIdx.x; e < cnt; e += kHexThreads) {
+                    const float val = s_rows[roff[i] + e];
+                    const int row = y0w + e / (W * lay.F);
+                    if (val != 0.f && row < Ht) unsafeAtomicAdd(dpacked + tp[i]->offset + (size_t)row * W * lay.F + e % (W * lay.F), val);
+                }
             }
-            const gs4d_hexplane_plane pl = lay.plane[6 * l + p];
-            const Tap t = make_tap(pc[kPairC0[p]], pc[kPairC1[p]], pl.W, pl.H);
-            const TapVals r = load_taps(packed + pl.offset, t, lay.F, q);
-            float gix = 0.f, giy = 0.f;
-            const float x1 = (float)(t.x0 + 1), y1 = (float)(t.y0 + 1), x0 = (float)t.x0, y0 = (float)t.y0;
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const float go = dv[k];
-                // grid_sampler_2d_backward (bilinear): input gradient and coordinate gradient
-                gix -= sel(r.v00, k) * (y1 - t.iy) * go;
-                giy -= sel(r.v00, k) * (x1 - t.ix) * go;
-                gix += sel(r.v10, k) * (y1 - t.iy) * go;
-                giy -= sel(r.v10, k) * (t.ix - x0) * go;
-                gix -= sel(r.v01, k) * (t.iy - y0) * go;
-                giy += sel(r.v01, k) * (x1 - t.ix) * go;
-                gix += sel(r.v11, k) * (t.iy - y0) * go;
-                giy += sel(r.v11, k) * (t.ix - x0) * go;
-            }
-            float *dpl = dpacked + pl.offset + 4 * q;
-            const int cells[4] = {t.i00, t.i10, t.i01, t.i11};
-            const float ws[4] = {t.w00, t.w10, t.w01, t.w11};
-#pragma unroll
-            for (int c = 0; c < 4; c++) {
-                if (cells[c] < 0) continue;
-                float *dst = dpl + (size_t)cells[c] * lay.F;
-#pragma unroll
-                for (int k = 0; k < 4; k++) unsafeAtomicAdd(dst + k, ws[c] * dv[k]);
-            }
-            gpt[kPairC0[p]] += t.gxm * gix;
-            gpt[kPairC1[p]] += t.gym * giy;
         }
+        __syncthreads();
     }
-    // sum the coordinate gradient over the point's F/4 lanes (consecutive lanes)
-#pragma unroll
-    for (int c = 0; c < 4; c++)
-        for (int off = 1; off < G; off <<= 1) gpt[c] += __shfl_xor(gpt[c], off);
-    if (live && q == 0)
-        reinterpret_cast<float4 *>(dpts)[n] = make_float4(gpt[0], gpt[1], gpt[2], gpt[3]);
 }
 
 // (1, F, H, W) planes <-> the packed channels-last buffer.  One thread per packed element.
@@ -278,9 +346,17 @@ int gs4d_hexplane_backward(int N, const float *pts, const gs4d_hexplane_layout *
     if (N < 0 || !lay || (N > 0 && (!pts || !packed || !dfeat || !dpacked || !dpts))) return 1;
     if (((size_t)pts & 15) || ((size_t)packed & 15) || ((size_t)dfeat & 15) || ((size_t)dpts & 15)) return 1;
     if (N == 0) return 0;
-    const int64_t threads = (int64_t)N * (lay->F / 4);
-    hipLaunchKernelGGL(hexplane_backward_kernel, dim3((unsigned)((threads + kHexThreads - 1) / kHexThreads)),
-                       dim3(kHexThreads), 0, (hipStream_t)stream, N, pts, *lay, packed, dfeat, dpacked, dpts);
+    const int ppc = kHexThreads / (lay->F / 4);
+    const int64_t chunks = ((int64_t)N + ppc - 1) / ppc;
+    const int cpw = (int)std::max<int64_t>(1, (chunks + 511) / 512);  // ~512 workgroups
+    const int nwg = (int)((chunks + cpw - 1) / cpw);
+    size_t lds = 0;
+    for (int l = 0; l < lay->levels; l++) {
+        const size_t f = 2 * (size_t)lay->F * (lay->plane[6 * l + 2].W + lay->plane[6 * l + 4].W + lay->plane[6 * l + 5].W);
+        if (f <= (size_t)kHexLdsFloats) lds = std::max(lds, f);
+    }
+    hipLaunchKernelGGL(hexplane_backward_kernel, dim3(nwg), dim3(kHexThreads), 4 * lds, (hipStream_t)stream, N, pts,
+                       *lay, packed, dfeat, dpacked, dpts, cpw);
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 

@@ -10,15 +10,15 @@ import pytest
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADER = os.path.join(ROOT, "include", "gs4d.h")
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("gs4d.h", "gs4d_train.h")]
 PKG = os.path.join(ROOT, "4dgaussians-fast-train_amd", "diff_gaussian_rasterization")
 LIB = os.path.join(PKG, "libgs4d.so")
 
 
 def declared():
-    text = open(HEADER).read()
+    text = "".join(open(h).read() for h in HEADERS)
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(gs4d_[a-z_]+)\s*\(", text)))
+    return sorted(set(re.findall(r"\b(gs4d_[a-z0-9_]+)\s*\(", text)))
 
 
 @pytest.fixture(scope="module")
@@ -33,7 +33,9 @@ def lib():
 
 def test_header_declares_the_reference_entry_points():
     names = declared()
-    for n in ("gs4d_forward", "gs4d_backward", "gs4d_mark_visible", "gs4d_last_error", "gs4d_version"):
+    for n in ("gs4d_forward", "gs4d_backward", "gs4d_mark_visible", "gs4d_last_error", "gs4d_version",
+              "gs4d_knn_mean_dist", "gs4d_l1_loss_forward", "gs4d_adam_step", "gs4d_densify_stats",
+              "gs4d_hexplane_forward", "gs4d_hexplane_backward"):
         assert n in names
 
 
@@ -113,3 +115,34 @@ def test_product_package_has_no_oracle_or_cpu_fallback():
                 src = open(os.path.join(dirpath, f)).read()
                 assert not re.search(r"^\s*(from|import)\s+oracle", src, flags=re.M), f
                 assert "gs4d_oracle" not in src, f
+
+
+def test_knn_and_train_bindings_load_and_refuse_cpu():
+    from simple_knn._C import distCUDA2
+    import gs4d_train.kernels as K
+    with pytest.raises(RuntimeError):
+        distCUDA2(torch.zeros(5, 3))
+    with pytest.raises(RuntimeError):
+        K._C.l1_forward(torch.zeros(4), torch.zeros(4))
+    with pytest.raises(RuntimeError):
+        K._C.hexplane_forward(torch.zeros(4, 4), [torch.zeros(1, 4, 2, 2)] * 6)
+
+
+def test_adam_batch_argument_errors(lib):
+    # a descriptor table whose chunk offsets do not chain is refused before any launch
+    class T(ctypes.Structure):
+        _fields_ = [("param", ctypes.c_void_p), ("grad", ctypes.c_void_p), ("m", ctypes.c_void_p),
+                    ("v", ctypes.c_void_p), ("n", ctypes.c_int64), ("first_chunk", ctypes.c_int64),
+                    ("s", ctypes.c_float), ("b", ctypes.c_float)]
+
+    class B(ctypes.Structure):
+        _fields_ = [("count", ctypes.c_int), ("b1", ctypes.c_float), ("omb1", ctypes.c_float),
+                    ("b2", ctypes.c_float), ("omb2", ctypes.c_float), ("eps", ctypes.c_float), ("t", T * 48)]
+
+    b = B()
+    b.count = 1
+    b.t[0].n = 10
+    b.t[0].first_chunk = 3
+    assert lib.gs4d_adam_step(ctypes.byref(b), None) == 1
+    b.count = 49
+    assert lib.gs4d_adam_step(ctypes.byref(b), None) == 1

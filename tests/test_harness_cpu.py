@@ -1,0 +1,198 @@
+"""CPU tests of the train-step harness around the rasterizer, no GPU calls:
+
+* the HexPlane field's torch graph (gs4d_train.deformation, the parity reference of the fused HIP
+  kernel) against an independent numpy restatement of grid_sample(bilinear, align_corners=True,
+  border) and the per-level plane product of scene/hexplane.py:75-110;
+* state-dict names and shapes of the deformation network as scene/deformation.py builds them, so a
+  reference deformation.pth loads;
+* the PLY layout of scene/gaussian_model.py:214-314 (header, attribute order, round trip);
+* the optimizer-state surgery of densify / prune / reset_opacity with torch.optim.Adam;
+* the learning-rate schedule of utils/general_utils.get_expon_lr_func.
+"""
+import itertools
+import math
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from gs4d_train import config
+from gs4d_train.deformation import DeformNetwork, HexPlaneField, interpolate_ms_features
+from gs4d_train.gaussians import GaussianModel, get_expon_lr_func
+from gs4d_train import ply
+
+
+def np_grid_sample_border(plane, x, y):
+    """plane (F, H, W); x, y in [-1, 1] (clipped): bilinear, align_corners=True, border padding."""
+    F, H, W = plane.shape
+    ix = np.clip((x + 1) / 2 * (W - 1), 0, W - 1)
+    iy = np.clip((y + 1) / 2 * (H - 1), 0, H - 1)
+    x0, y0 = np.floor(ix).astype(int), np.floor(iy).astype(int)
+    x1, y1 = x0 + 1, y0 + 1
+    out = np.zeros((len(x), F))
+    for xx, yy, w in ((x0, y0, (x1 - ix) * (y1 - iy)), (x1, y0, (ix - x0) * (y1 - iy)),
+                      (x0, y1, (x1 - ix) * (iy - y0)), (x1, y1, (ix - x0) * (iy - y0))):
+        ok = (xx >= 0) & (xx < W) & (yy >= 0) & (yy < H)
+        out[ok] += plane[:, yy[ok], xx[ok]].T * w[ok, None]
+    return out
+
+
+def test_hexplane_torch_graph_matches_numpy():
+    torch.manual_seed(0)
+    f = HexPlaneField(1.6, {"grid_dimensions": 2, "input_coordinate_dim": 4, "output_coordinate_dim": 8,
+                            "resolution": [16, 12, 10, 7]}, [1, 2])
+    with torch.no_grad():
+        for level in f.grids:
+            for p in level:
+                p.uniform_(0.2, 1.1)
+    rng = np.random.default_rng(1)
+    pts = rng.uniform(-1.2, 1.2, (500, 4)).astype(np.float32)
+    out = interpolate_ms_features(torch.tensor(pts), f.grids).detach().numpy()
+    ref = []
+    for level in f.grids:
+        prod = np.ones((500, 8))
+        for ci, (a, b) in enumerate(itertools.combinations(range(4), 2)):
+            prod = prod * np_grid_sample_border(level[ci].detach().numpy()[0].astype(np.float64), pts[:, a], pts[:, b])
+        ref.append(prod)
+    np.testing.assert_allclose(out, np.concatenate(ref, 1), rtol=2e-5, atol=1e-6)
+    # plane shapes: (1, F, reso[c1], reso[c0]) with the spatial resolution scaled per level
+    assert tuple(f.grids[0][0].shape) == (1, 8, 12, 16) and tuple(f.grids[1][2].shape) == (1, 8, 7, 32)
+    # time planes start at 1 only when initialised fresh
+    g = HexPlaneField(1.6, {"grid_dimensions": 2, "input_coordinate_dim": 4, "output_coordinate_dim": 4,
+                            "resolution": [8, 8, 8, 5]}, [1])
+    assert torch.all(g.grids[0][2] == 1) and not torch.all(g.grids[0][0] == 1)
+
+
+def test_deformation_state_dict_matches_reference_names():
+    hyper, _ = config.dynerf()
+    sd = DeformNetwork(hyper).state_dict()
+    expect = {
+        "deformation_net.grid.aabb": (2, 3),
+        "deformation_net.grid.grids.0.0": (1, 16, 64, 64),
+        "deformation_net.grid.grids.0.2": (1, 16, 150, 64),
+        "deformation_net.grid.grids.1.5": (1, 16, 150, 128),
+        "deformation_net.feature_out.0.weight": (128, 32),
+        "deformation_net.pos_deform.1.weight": (128, 128),
+        "deformation_net.pos_deform.3.weight": (3, 128),
+        "deformation_net.rotations_deform.3.weight": (4, 128),
+        "deformation_net.shs_deform.3.bias": (48,),
+        "timenet.0.weight": (64, 9),
+        "time_poc": (4,),
+        "pos_poc": (10,),
+    }
+    for k, shape in expect.items():
+        assert k in sd, k
+        assert tuple(sd[k].shape) == shape, (k, tuple(sd[k].shape))
+    assert sum(v.numel() for k, v in sd.items() if "grid" in k and "aabb" not in k) == \
+        16 * (3 * 64 * 64 + 3 * 64 * 150 + 3 * 128 * 128 + 3 * 128 * 150)
+
+
+def _cpu_model(P=300, seed=0):
+    hyper, opt = config.dnerf()
+    torch.manual_seed(seed)
+    g = GaussianModel(3, hyper, fused=False)
+    rng = np.random.default_rng(seed)
+    g._xyz = torch.nn.Parameter(torch.tensor(rng.normal(size=(P, 3)), dtype=torch.float32))
+    g._features_dc = torch.nn.Parameter(torch.tensor(rng.normal(size=(P, 1, 3)), dtype=torch.float32))
+    g._features_rest = torch.nn.Parameter(torch.tensor(rng.normal(size=(P, 15, 3)), dtype=torch.float32))
+    g._scaling = torch.nn.Parameter(torch.tensor(rng.normal(-3, 0.5, size=(P, 3)), dtype=torch.float32))
+    g._rotation = torch.nn.Parameter(torch.tensor(rng.normal(size=(P, 4)), dtype=torch.float32))
+    g._opacity = torch.nn.Parameter(torch.tensor(rng.normal(size=(P, 1)), dtype=torch.float32))
+    g.max_radii2D = torch.zeros(P)
+    g._deformation_table = torch.ones(P, dtype=torch.bool)
+    g.spatial_lr_scale = 1.0
+    return g, opt
+
+
+def test_ply_round_trip_and_layout(tmp_path):
+    g, _ = _cpu_model()
+    path = os.path.join(tmp_path, "point_cloud", "iteration_7", "point_cloud.ply")
+    g.save_ply(path)
+    head = open(path, "rb").read(4096).split(b"end_header\n")[0].decode()
+    names = [l.split()[-1] for l in head.splitlines() if l.startswith("property")]
+    assert names == ply.attribute_names(3, 45)
+    assert "format binary_little_endian 1.0" in head and "element vertex 300" in head
+    assert all(l.startswith("property float ") for l in head.splitlines() if l.startswith("property"))
+    el = ply.read_ply(path)
+    # f_rest is channel-major: f_rest_{c*15 + k} = features_rest[:, k, c]
+    np.testing.assert_array_equal(el["f_rest_16"], g._features_rest.detach().numpy()[:, 1, 1])
+    np.testing.assert_array_equal(el["nx"], 0)
+    h, _ = _cpu_model(seed=1)
+    h.load_ply(path, device="cpu")
+    for k in ("_xyz", "_features_dc", "_features_rest", "_scaling", "_rotation", "_opacity"):
+        torch.testing.assert_close(getattr(h, k), getattr(g, k), rtol=0, atol=0)
+    assert h.active_sh_degree == 3
+
+
+def test_ply_reader_handles_ascii_and_shuffled_suffixes(tmp_path):
+    p = os.path.join(tmp_path, "a.ply")
+    with open(p, "w") as f:
+        f.write("ply\nformat ascii 1.0\ncomment x\nelement vertex 2\nproperty float x\nproperty double y\n"
+                "property uchar z\nend_header\n1.5 2.5 3\n-1 0.25 7\n")
+    el = ply.read_ply(p)
+    np.testing.assert_allclose(el["x"], [1.5, -1.0])
+    np.testing.assert_allclose(el["y"], [2.5, 0.25])
+    np.testing.assert_array_equal(el["z"], [3, 7])
+
+
+def test_deformation_checkpoint_round_trip(tmp_path):
+    g, _ = _cpu_model()
+    g._deformation_accum = torch.rand(300, 3)
+    ply.save_model(str(tmp_path), 100, g)
+    h, _ = _cpu_model(seed=2)
+    ply.load_model(str(tmp_path), 100, h, device="cpu")
+    for (ka, a), (kb, b) in zip(g._deformation.state_dict().items(), h._deformation.state_dict().items()):
+        assert ka == kb
+        torch.testing.assert_close(a, b, rtol=0, atol=0)
+    torch.testing.assert_close(h._deformation_accum, g._deformation_accum)
+
+
+def test_densify_prune_keep_optimizer_state_aligned():
+    g, opt = _cpu_model(P=400)
+    g.training_setup(opt)
+    P0 = g.get_xyz.shape[0]
+    # give every parameter a gradient and take one Adam step so the state exists
+    loss = sum((p ** 2).sum() for grp in g.optimizer.param_groups for p in grp["params"])
+    loss.backward()
+    g.optimizer.step()
+    g.xyz_gradient_accum = torch.rand(P0, 1) * 1e-3
+    g.denom = torch.ones(P0, 1)
+    g.percent_dense = 0.05
+    torch.manual_seed(3)
+    g.densify(5e-4, 0.005, 1.0, None)
+    P1 = g.get_xyz.shape[0]
+    assert P1 != P0
+    for grp in g.optimizer.param_groups:
+        if len(grp["params"]) > 1 or grp["name"] in ("deformation", "grid"):
+            continue
+        p = grp["params"][0]
+        st = g.optimizer.state[p]
+        assert p.shape[0] == P1 and st["exp_avg"].shape == p.shape and st["exp_avg_sq"].shape == p.shape
+    assert g.max_radii2D.shape[0] == P1 and g.denom.shape[0] == P1 and g._deformation_table.shape[0] == P1
+    g.prune(5e-4, 0.4, 1.0, None)
+    P2 = g.get_xyz.shape[0]
+    assert P2 < P1 and bool((g.get_opacity >= 0.4).all())
+    g.reset_opacity()
+    assert float(g.get_opacity.detach().max()) <= 0.01 + 1e-6
+    st = g.optimizer.state[g._opacity]
+    assert float(st["exp_avg"].abs().sum()) == 0.0
+
+
+def test_expon_lr_schedule():
+    f = get_expon_lr_func(1.6e-4, 1.6e-6, lr_delay_mult=0.01, max_steps=20000)
+    assert math.isclose(f(0), 1.6e-4)
+    assert math.isclose(f(20000), 1.6e-6, rel_tol=1e-9)
+    assert math.isclose(f(10000), math.sqrt(1.6e-4 * 1.6e-6), rel_tol=1e-9)
+    d = get_expon_lr_func(1.0, 1.0, lr_delay_steps=100, lr_delay_mult=0.1)
+    assert math.isclose(d(0), 0.1) and math.isclose(d(100), 1.0)
+    assert f(-1) == 0.0
+
+
+def test_regularisers_run_and_are_zero_at_init():
+    hyper, _ = config.dynerf()
+    g = GaussianModel(3, hyper, fused=False)
+    # time planes initialise to 1: second differences and |1 - plane| vanish on them
+    assert float(g.compute_regulation(0.0, 1.0, 0.0)) == 0.0
+    assert float(g.compute_regulation(1.0, 0.0, 0.0)) == 0.0
+    assert float(g.compute_regulation(0.0, 0.0, 1.0)) > 0.0
