@@ -104,6 +104,49 @@ def interpolate_ms_features(pts, ms_grids):
     return torch.cat(out, dim=-1)
 
 
+class _LinearSplitK(torch.autograd.Function):
+    """F.linear whose weight gradient dW = dY^T X (a (out x in) result reduced over P ~ 1e5 rows) is
+    computed as a split-K batched GEMM: the library's default kernel for that tall-skinny reduction
+    tiles only the tiny output and runs at ~4-12 TF/s on MI355X (tools/gemm_probe.py); splitting the P
+    rows into chunks of kChunk restores ~25-50 TF/s.  Forward, dX and db are unchanged."""
+
+    kChunk = 1024
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.has_bias = b is not None
+        return F.linear(x, w, b)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx = dy @ w if ctx.needs_input_grad[0] else None
+        dw = db = None
+        if ctx.needs_input_grad[1]:
+            P, c = x.shape[0], _LinearSplitK.kChunk
+            S = P // c
+            if S >= 2:
+                dw = torch.bmm(dy[:S * c].view(S, c, -1).transpose(1, 2), x[:S * c].view(S, c, -1)).sum(0)
+                if P > S * c:
+                    dw = dw + dy[S * c:].t() @ x[S * c:]
+            else:
+                dw = dy.t() @ x
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = dy.sum(0)
+        return dx, dw, db
+
+
+class Linear(nn.Linear):
+    """nn.Linear (same parameters and state-dict entries) with the split-K weight gradient on GPU."""
+
+    def forward(self, x):
+        if x.is_cuda and x.dim() == 2 and torch.is_grad_enabled():
+            return _LinearSplitK.apply(x.contiguous(), self.weight, self.bias)
+        return F.linear(x, self.weight, self.bias)
+
+
 class Deformation(nn.Module):
     """scene/deformation.py:16-172 (no_grid=False, grid_pe=0, empty_voxel=False, static_mlp=False)."""
 
@@ -111,11 +154,11 @@ class Deformation(nn.Module):
         super().__init__()
         self.D, self.W, self.args = D, W, args
         self.grid = HexPlaneField(args.bounds, args.kplanes_config, args.multires)
-        self.feature_out = [nn.Linear(self.grid.feat_dim, W)]
+        self.feature_out = [Linear(self.grid.feat_dim, W)]
         for _ in range(D - 1):
-            self.feature_out += [nn.ReLU(), nn.Linear(W, W)]
+            self.feature_out += [nn.ReLU(), Linear(W, W)]
         self.feature_out = nn.Sequential(*self.feature_out)
-        head = lambda n: nn.Sequential(nn.ReLU(), nn.Linear(W, W), nn.ReLU(), nn.Linear(W, n))
+        head = lambda n: nn.Sequential(nn.ReLU(), Linear(W, W), nn.ReLU(), Linear(W, n))
         self.pos_deform, self.scales_deform, self.rotations_deform = head(3), head(3), head(4)
         self.opacity_deform, self.shs_deform = head(1), head(16 * 3)
 

@@ -26,6 +26,8 @@ sys.path.insert(0, os.path.join(ROOT, "4dgaussians-fast-train_amd"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
+# BASELINE.json's metric; value = the rasterizer fwd+bwd MGaussians/s, train_step.ms = the train-step ms
+BASELINE_METRIC = "train-step ms + rasterizer fwd+bwd MGaussians/s @100k pts, 1352\u00d71014"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: 8.0 TB/s spec
 # VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 4 cycles per SIMD at 2.4 GHz
 # (MI355X_MICROARCH.md: v_fma_f32 issue cost 4 cycles)
@@ -51,6 +53,8 @@ def main():
     ap.add_argument("--config", default="metric")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-train-step", action="store_true", help="skip the full train-step timing")
+    ap.add_argument("--train-steps", type=int, default=20)
     args = ap.parse_args()
 
     from gs4d_train.synthetic import CONFIGS, make_scene, make_upstream_grad
@@ -74,15 +78,17 @@ def main():
     means3D, opac, scales, rots, shs = (t(s[k]) for k in ("means3D", "opacities", "scales", "rotations", "shs"))
     e = torch.empty(0, device=dev)
     C = dgr._C
+    from gs4d_train import _C as TC
+    one = torch.ones(1, device=dev)
     gt = t(np.random.default_rng(rank + 1).uniform(0, 1, (3, H, W)).astype(np.float32))
 
     def step():
         fwd = C.rasterize_gaussians(bg, means3D, e, opac, scales, rots, 1.0, e, vm, pm, s["tanfovx"], s["tanfovy"],
                                     H, W, shs, 3, cp, False, False)
         nr, color, depth, radii, gb, bb, ib = fwd
-        diff = color - gt
-        loss = diff.abs().mean()                      # train.py:244 L1
-        grad = torch.sign(diff) / diff.numel()
+        # train.py:244 L1 loss and its gradient sign(color - gt) / N (fused kernels, csrc/train_tail.hip)
+        loss, sgn = TC.l1_forward(color, gt)
+        grad = TC.l1_backward(sgn, one)
         grads = C.rasterize_gaussians_backward(bg, means3D, radii, e, scales, rots, 1.0, e, vm, pm, s["tanfovx"],
                                                s["tanfovy"], grad, shs, 3, cp, gb, nr, bb, ib, False)
         if dist:
@@ -127,6 +133,10 @@ def main():
     C.set_profiling(False)
     stage_avg = {k: float(np.mean(v)) for k, v in stage_ms.items()}
 
+    # ---- the full fine-stage train step (the metric's "train-step ms") ----
+    train = None if args.no_train_step else train_step_timing(P, W, H, dev, world, rank, args.train_steps,
+                                                              args.warmup, dist)
+
     if rank == 0:
         L = int(nr)
         ab = algorithmic_bytes(P, L, W, H)
@@ -142,9 +152,10 @@ def main():
             except Exception:
                 return None
         traffic = pmc("pmc_traffic.json")
+        traffic_raw = pmc("pmc_traffic_raw.json")
         valu = pmc("pmc_valu.json")
         out = {
-            "metric": "rasterizer fwd+bwd MGaussians/s @100k pts, 1352x1014 (train-step ms in ms_per_step)",
+            "metric": BASELINE_METRIC,
             "value": round(value, 3), "unit": "MGaussians/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic (seeded, SURVEY §8d)",
@@ -155,6 +166,10 @@ def main():
             "roofline": {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 2) if achieved else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None, "traffic": traffic,
+                         "traffic_raw": traffic_raw,
+                         "traffic_note": "PMC bytes per launch (profiles/r01_pmc.json): traffic = 2 x FETCH_SIZE + "
+                                         "WRITE_SIZE (gfx950 wide-read correction), traffic_raw = FETCH_SIZE + "
+                                         "WRITE_SIZE; the kernel's reads are mostly gathers, so the truth lies between",
                          "algorithmic_bytes": dom_bytes, "avg_ms": round(dom_ms, 4)},
             # the blend kernels are VALU-issue bound, not HBM bound: instruction rate vs the issue peak
             "valu_issue": {"kernel": dom, "insts_per_launch": valu,
@@ -166,11 +181,69 @@ def main():
                               "achieved_GBs": round(ab["step"] / (ms_per_step * 1e-3) / 1e9, 2),
                               "frac": round(ab["step"] / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)},
         }
+        if train is not None:
+            out["train_step"] = train
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(s, args.cpu_seconds)
         print(json.dumps(out), flush=True)
     if dist:
         tdist.destroy_process_group()
+
+
+def train_step_timing(P, W, H, dev, world, rank, steps, warmup, dist, unfused=True):
+    """One fine-stage training iteration of train.py (gs4d_train.train.train_step): HexPlane deformation
+    + rasterizer fwd/bwd + L1 + HexPlane regularisers + backward + densification statistics + Adam, for
+    one synthetic view per GPU (global batch = world; views shard across ranks, gradients all-reduced
+    over RCCL).  Timed like the rasterizer steps: barrier + synchronize around K steps, max over ranks.
+    With unfused=True (rank 0, single GPU) the reference's PyTorch tail (grid_sample HexPlane, torch
+    L1 / Adam / statistics) is timed the same way for comparison."""
+    import torch.distributed as tdist
+    from gs4d_train import config
+    from gs4d_train.gaussians import GaussianModel
+    from gs4d_train.synthetic import make_point_cloud, make_training_views
+    from gs4d_train.train import train_step
+
+    def run(fused, n_steps, n_warm):
+        hyper, opt = config.dynerf()
+        torch.manual_seed(0)
+        g = GaussianModel(3, hyper, fused=fused)
+        pts, cols = make_point_cloud(P, seed=0)
+        g.create_from_pcd(pts, cols, spatial_lr_scale=1.0, device=dev)
+        g._deformation.deformation_net.grid.fused = fused
+        g.training_setup(opt)
+        g.active_sh_degree = 3
+        views = make_training_views(world, W, H, seed=1, device=dev)
+        bg = torch.ones(3, device=dev)
+        it0 = 3001  # fine stage, densification statistics on, no densify/prune/reset iteration in range
+        for i in range(n_warm):
+            train_step(g, views, opt, hyper, it0 + i, bg, data_parallel=dist)
+        torch.cuda.synchronize()
+        if dist:
+            tdist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(n_steps):
+            loss = train_step(g, views, opt, hyper, it0 + n_warm + i, bg, data_parallel=dist)
+        torch.cuda.synchronize()
+        if dist:
+            tdist.barrier()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        if dist:
+            et = torch.tensor([el], device=dev, dtype=torch.float64)
+            tdist.all_reduce(et, op=tdist.ReduceOp.MAX)
+            el = float(et.item())
+        return el / n_steps * 1e3, float(loss)
+
+    ms, loss = run(True, steps, warmup)
+    res = {"ms": round(ms, 3), "views_per_gpu": 1, "global_batch": world, "gaussians": P,
+           "image": f"{W}x{H}", "loss": round(loss, 6),
+           "config": "arguments/dynerf/default.py (HexPlane 16 x [64,64,64,150], multires [1,2], MLP width 128, "
+                     "opacity+SH deform), fused libgs4d HexPlane / L1 / densification stats / Adam kernels"}
+    if unfused and world == 1:
+        ums, _ = run(False, max(3, steps // 4), 2)
+        res["reference_torch_tail_ms"] = round(ums, 3)
+    return res
 
 
 def cpu_baseline(s, budget_s):

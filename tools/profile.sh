@@ -5,7 +5,7 @@
 # Usage: tools/profile.sh <tag> [bench args...]
 set -o pipefail
 TAG=${1:-r01}; shift
-ARGS=${@:---steps 10 --warmup 3 --no-cpu-baseline}
+ARGS=${@:---steps 10 --warmup 3 --no-cpu-baseline --no-train-step}
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
