@@ -1,50 +1,56 @@
-// binning.hip -- depth order, culled (tile, Gaussian) instance emission (K3), radix sort (K4) and tile
-// ranges (K5).
+// binning.hip -- instance emission (K3), tile binning and the per-tile depth sort (K4), tile ranges (K5).
 //
 // Reference: cuda_rasterizer/rasterizer_impl.cu:70-111 (duplicateWithKeys), :116-138
 // (identifyTileRanges), :301-318 (cub::DeviceRadixSort::SortPairs of (tile<<32 | depth_bits, id)
-// on bits [0, 32+msb(T)), stable).
+// on bits [0, 32+msb(T)), stable over instances emitted in Gaussian-id order).
 //
 // MI355X design (this library's own).  The reference sorts L ~ 1.4M 64-bit (tile, depth) keys over
-// 45 bits.  Here:
-//   1. the P Gaussians are sorted by depth bits (32-bit stable radix sort, ties by id -> the same
-//      tie order as the reference's stable sort of instances emitted in id order);
-//   2. the candidate instances (each Gaussian's 3-sigma tile rectangle, row-major, Gaussians in depth
-//      order) are numbered by a prefix sum of the rectangle areas, and emitted -- only for tiles the
-//      splat actually reaches (half_reach, gs4d_internal.h) -- in one load-balanced stream
-//      compaction pass: every workgroup takes a fixed number of candidates, whatever the splat sizes;
-//   3. the emitted sequence is already depth-ordered, so a STABLE sort by tile id alone yields the
-//      reference's (tile, depth, id) order: ceil(msb(T)/8) passes over u32 keys (2 at the metric
-//      config instead of 6 over 12-byte pairs).
-// Every pass is one launch.  Digit histograms are accumulated by the kernel that produces the keys
-// (preprocess for depths, emission for tiles).  Scan, compaction and sort passes are single launches
-// whose workgroups publish their chunk counts (one 32-bit status+count word per chunk and digit,
-// agent-scope relaxed atomic stores and loads, so each word is its own flag) and sum the counts of
-// all lower chunks directly (sum_published).
+// 45 bits (6 radix passes over 12-byte pairs).  Its order is: by tile, then by depth bits, ties by
+// Gaussian id.  Here:
+//   1. visible_scan: one pass over the Gaussians in id order compacts the visible ones (tiles_touched
+//      > 0) and numbers their candidate instances (the 3-sigma tile rectangles, row-major) by a prefix
+//      sum of the rectangle areas -- two chunk-prefix chains in one launch;
+//   2. emission: one load-balanced pass over the L candidates (a fixed number per workgroup, whatever
+//      the splat sizes) keeps only the (tile, splat) pairs the splat reaches (half_reach,
+//      gs4d_internal.h) and compacts them in candidate order (so a Gaussian's instances are
+//      consecutive: the backward reduces its gradient records by segment);
+//   3. a STABLE LSD radix sort of the emitted instances by tile id alone (ceil(msb(T)/8) passes over
+//      u32 keys; digit histograms built by the emission, no atomics on contended counters): each
+//      tile's run is left in Gaussian-id order; tile ranges follow from the sorted keys;
+//   4. tile_sort: each tile's run is sorted by the 64-bit key (depth bits, Gaussian id) -- exactly the
+//      reference's within-tile order: runs of up to 256 by one wave in registers (bitonic network
+//      over lane shuffles), up to 4096 by one workgroup in LDS, longer ones as LDS-sorted 4096-runs
+//      merged by the same network's global steps.  The key is unique inside a tile.
+// The P Gaussians are never sorted by depth globally (the reference's 45-bit key needs 6 passes; a
+// global depth sort needs 4 more over the Gaussians).  Prefix sums publish per-chunk counts (one
+// 32-bit status+count word per chunk, agent-scope relaxed atomics) and sum the lower chunks' words
+// directly (radix_sort.h).
 #include <algorithm>
 
 #include "radix_sort.h"
 
 namespace gs4d {
 
-constexpr int kSortThreads = 1024;  // radix-sort workgroup: 16 waves rank one chunk together
-constexpr int kItemsL = 8;     // keys per lane for the instance sort (8192 per workgroup)
-constexpr int kItemsP = 4;     // keys per lane for the Gaussian depth sort (4096 per workgroup)
 constexpr int kEmitPer = kEmitChunk / 256;  // candidates per lane in the emission pass
+constexpr int kSortThreads = 1024;          // radix-sort workgroup: 16 waves rank one chunk together
+constexpr int kItemsL = 8;                  // keys per lane for the instance sort (8192 per workgroup)
+constexpr int kWaveSortMax = 256;           // tile runs sorted by one wave in registers
+constexpr int kSortCap = 4096;              // tile runs sorted in LDS by one workgroup (48 KiB)
 
 // ---------------------------------------------------------------------------------------------
 // Zero-region layouts (u32 words).
-static size_t nchunk_scan(int P) { return ((size_t)P + 255) / 256; }
-static size_t nchunk_emit(int L) { return ((size_t)L + kEmitChunk - 1) / kEmitChunk; }
-// geometry: counters | depth histograms | area-scan chain (+ err) | depth-sort look-back
-__host__ __device__ static size_t geom_chain_off() { return kZeroHist + kHistWords; }
-static size_t geom_look_off(int P) { return geom_chain_off() + nchunk_scan(P) + 64; }
-// rounded to 256 B so that one fill kernel clears each region
-size_t geom_zero_words(int P) { return align_up(geom_look_off(P) + (size_t)4 * 256 * sort_nblk(P, kSortThreads * kItemsP), 64); }
-// binning: counters | tile histograms | emission chain (+ err) | instance-sort look-back
+__host__ __device__ static size_t nchunk_scan(int P) { return ((size_t)P + 255) / 256; }
+__host__ __device__ static size_t nchunk_emit(int L) { return ((size_t)L + kEmitChunk - 1) / kEmitChunk; }
+// geometry: counters | visible-count chain (+ err) | area chain (+ err)
+__host__ __device__ static size_t geom_vis_chain_off() { return 64; }
+__host__ __device__ static size_t geom_area_chain_off(int P) { return 64 + nchunk_scan(P) + 64; }
+// rounded to 256 B so that one fill clears each region
+size_t geom_zero_words(int P) { return align_up(geom_area_chain_off(P) + nchunk_scan(P) + 64, 64); }
+// binning: counters ([0] = L') | tile-sort digit histograms | emission chain (+ err) | sort look-back
 __host__ __device__ static size_t bin_chain_off() { return kZeroHist + kHistWords; }
 static size_t bin_look_off(int L) { return bin_chain_off() + nchunk_emit(L) + 64; }
-size_t binning_zero_words(int L) {
+size_t binning_zero_words(int L, int T) {
+    (void)T;
     return align_up(bin_look_off(L) + (size_t)kMaxPasses * 256 * sort_nblk(L, kSortThreads * kItemsL), 64);
 }
 size_t max_emit_chunks(int P, int T) {
@@ -53,93 +59,88 @@ size_t max_emit_chunks(int P, int T) {
     return std::min<size_t>(bound, ((size_t)1 << 30) / kEmitChunk) + 1;
 }
 
-// ---------------------------------------------------------------------------------------------
-// Exclusive scan of the rect areas in depth-rank order: cand_off[r] = first candidate of rank r,
-// cand_off[P] = num_rendered; and first_rank[j] = the rank owning candidate j * kEmitChunk.
-// Rank-ordered splat records and the exclusive scan of the rect areas in depth-rank order:
-// rank_geo[r] / rank_co[r] = the record of the Gaussian of depth rank r (gathered here with the whole
-// chip's memory parallelism -- the sort's last pass runs on a few dozen workgroups only),
-// cand_off[r] = its first candidate, cand_off[P] = num_rendered, first_rank[j] = the rank owning
-// candidate j * kEmitChunk.  One rank per thread; chunk prefixes from the published counts.
-__global__ __launch_bounds__(256) void rank_records_kernel(GeomState g, const int *__restrict__ radii, int n,
-                                                           uint32_t jmax, uint32_t *__restrict__ chain) {
-    __shared__ uint32_t s_w[4], s_tmp[4];
+// Exclusive 256-thread workgroup scan: returns this thread's exclusive prefix inside the workgroup
+// and (in *total) the workgroup sum.
+__device__ __forceinline__ uint32_t wg_exclusive(uint32_t v, uint32_t *s_w, uint32_t *total) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const uint32_t b = blockIdx.x;
-    const int r = (int)b * 256 + tid;
-    uint32_t v = 0;
-    if (r < n) {
-        const uint32_t gid = g.dvals[0][r];
-        v = g.tiles_touched[gid];
-        const float2 p = g.xy[gid];
-        g.rank_geo[r] = make_float4(p.x, p.y, __int_as_float(radii[gid]), __uint_as_float(gid));
-        g.rank_co[r] = g.conic_opacity[gid];
-    }
     uint32_t x = v;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
         const uint32_t y = __shfl_up(x, off);
         if (lane >= off) x += y;
     }
+    __syncthreads();
     if (lane == 63) s_w[w] = x;
     __syncthreads();
-    uint32_t before = 0, total = 0;
+    uint32_t before = 0, t = 0;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         before += q < w ? s_w[q] : 0u;
-        total += s_w[q];
+        t += s_w[q];
     }
-    const uint32_t prefix = block_prefix(chain + 64, b, total, chain + 1, s_tmp);
-    const uint32_t run = prefix + before + x - v;
-    if (r < n) {
-        g.cand_off[r] = run;
-        // chunk starts inside this rank's candidates
-        for (uint32_t j = (run + kEmitChunk - 1) / kEmitChunk; j * (uint32_t)kEmitChunk < run + v && j < jmax; j++)
-            g.first_rank[j] = (uint32_t)r;
-        if (r == n - 1) g.cand_off[n] = run + v;
+    *total = t;
+    return before + x - v;
+}
+
+// K2 replacement: visible Gaussians in id order and their candidate numbering.
+// vis_gid[v] = id of the v-th visible Gaussian; cand_off[v] = its first candidate (cand_off[V] = L);
+// first_vis[j] = the visible index owning candidate j * kEmitChunk.
+__global__ __launch_bounds__(256) void visible_scan_kernel(GeomState g, int P, uint32_t jmax) {
+    __shared__ uint32_t s_w[4], s_tmp[4];
+    const uint32_t b = blockIdx.x;
+    const int idx = (int)b * 256 + threadIdx.x;
+    const uint32_t t = idx < P ? g.tiles_touched[idx] : 0u;
+    const uint32_t vis = t > 0;
+    uint32_t vtot, atot;
+    const uint32_t vx = wg_exclusive(vis, s_w, &vtot);
+    const uint32_t ax = wg_exclusive(t, s_w, &atot);
+    uint32_t *vchain = g.zero + geom_vis_chain_off(), *achain = g.zero + geom_area_chain_off(P);
+    const uint32_t vpre = block_prefix(vchain + 64, b, vtot, vchain + 1, s_tmp);
+    const uint32_t apre = block_prefix(achain + 64, b, atot, achain + 1, s_tmp);
+    const uint32_t v = vpre + vx, run = apre + ax;
+    if (vis) {
+        g.vis_gid[v] = (uint32_t)idx;
+        g.cand_off[v] = run;
+        // emission chunks starting inside this Gaussian's candidates
+        for (uint32_t j = (run + kEmitChunk - 1) / kEmitChunk; j * (uint32_t)kEmitChunk < run + t && j < jmax; j++)
+            g.first_vis[j] = v;
+    }
+    if (idx == P - 1) {
+        g.cand_off[v + vis] = run + t;  // cand_off[V] = num_rendered
+        g.zero[kZeroV] = v + vis;       // V
     }
 }
 
-hipError_t launch_depth_order(const Args &a, GeomState g, const int *radii, hipStream_t s) {
-    // dkeys[0] = depth bits (unbinned: ~0u, last); afterwards dvals[0] = Gaussian id by depth rank
-    uint32_t *keys[2] = {g.dkeys[0], g.dkeys[1]};
-    uint32_t *vals[2] = {g.dvals[0], g.dvals[1]};
-    uint32_t *chain = g.zero + geom_chain_off();
-    onesweep_sort<kSortThreads, kItemsP>(keys, vals, a.P, nullptr, 32, g.zero + kZeroHist,
-                                      g.zero + geom_look_off(a.P), chain + 1, s);
-    hipLaunchKernelGGL(rank_records_kernel, dim3((unsigned)nchunk_scan(a.P)), dim3(256), 0, s, g, radii, a.P,
-                       (uint32_t)max_emit_chunks(a.P, a.gx * a.gy), chain);
+hipError_t launch_visible_scan(const Args &a, GeomState g, hipStream_t s) {
+    hipLaunchKernelGGL(visible_scan_kernel, dim3((unsigned)nchunk_scan(a.P)), dim3(256), 0, s, g, a.P,
+                       (uint32_t)max_emit_chunks(a.P, a.gx * a.gy));
     return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------------------
-// K3: load-balanced emission.  Workgroup j takes candidates [j*2048, +2048) of the depth-ordered
-// candidate sequence; lane t owns 8 consecutive ones.  Their owning ranks come from a load-balancing
-// search in LDS: each rank starting inside the chunk marks its first slot, and a max-scan spreads the
-// marks.  Each candidate is tested with half_reach; the reached ones are compacted in candidate
-// order: keys[e] = tile, gid_by_e[e] = Gaussian | reach bits.  Emission offsets are chained by look-back; the last
-// chunk stores L'.  Also accumulated: n_inst[g] (integer atomics), the tile-sort digit histograms,
-// and (first T threads of the grid) zeroed tile ranges.
-__global__ __launch_bounds__(256) void emit_instances_kernel(Args a, GeomState g, int L, int npass,
-                                                             uint32_t *__restrict__ keys,
+// K3: load-balanced emission.  Workgroup j takes candidates [j*2048, +2048) of the candidate sequence
+// (visible Gaussians in id order, each its rectangle row-major); lane t owns 8 consecutive ones.
+// Their owning Gaussians come from a load-balancing search in LDS: each Gaussian starting inside the
+// chunk marks its first slot, and a max-scan spreads the marks.  Each candidate is tested with
+// half_reach; the reached ones are compacted in candidate order: keys[e] = tile, gid_by_e[e] =
+// Gaussian | reach bits.  Emission offsets are chained by look-back; the last chunk stores L'.  Also
+// accumulated: n_inst[g] and the per-tile instance counts (integer atomics).
+__global__ __launch_bounds__(256) void emit_instances_kernel(Args a, GeomState g, const int *__restrict__ radii,
+                                                             int L, int npass, uint32_t *__restrict__ keys,
                                                              uint32_t *__restrict__ gid_by_e,
-                                                             uint32_t *__restrict__ zero, uint2 *__restrict__ ranges) {
+                                                             uint32_t *__restrict__ zero) {
     __shared__ uint32_t s_own[kEmitChunk];
     __shared__ uint32_t s_off[kEmitChunk + 2];
     __shared__ uint32_t s_n[kEmitChunk + 1];
     __shared__ uint32_t s_hist[kMaxPasses][256];
     __shared__ uint32_t s_w[4], s_tmp[4];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    {
-        const int gt = blockIdx.x * 256 + tid;
-        if (gt < a.gx * a.gy) ranges[gt] = make_uint2(0u, 0u);
-    }
     const uint32_t b = blockIdx.x;
     const uint32_t c0 = b * kEmitChunk;
-    if (c0 >= (uint32_t)L) return;  // grid padding for the range zeroing
     const uint32_t c1 = min((uint32_t)L, c0 + kEmitChunk);
-    const int rlo = (int)g.first_rank[b];
-    const int nr = min(a.P - rlo, kEmitChunk + 1);  // ranks starting at or after c1 are ignored
+    const int V = (int)(g.zero[kZeroV]);
+    const int rlo = (int)g.first_vis[b];
+    const int nr = min(V - rlo, kEmitChunk + 1);  // visible Gaussians starting at or after c1 are ignored
     for (int i = tid; i < kEmitChunk; i += 256) s_own[i] = 0;
     for (int i = tid; i < kMaxPasses * 256; i += 256) (&s_hist[0][0])[i] = 0;
     __syncthreads();
@@ -175,12 +176,16 @@ __global__ __launch_bounds__(256) void emit_instances_kernel(Args a, GeomState g
         for (int k = 0; k < kEmitPer; k++) own[k] = max(own[k], carry);
     }
     // test the candidates (every gather issued before the first test)
-    float4 geo[kEmitPer], co[kEmitPer];
+    float2 xy[kEmitPer];
+    float4 co[kEmitPer];
+    int rad[kEmitPer];
+    uint32_t gid[kEmitPer];
 #pragma unroll
     for (int k = 0; k < kEmitPer; k++) {
-        const int r = rlo + (int)own[k];
-        geo[k] = g.rank_geo[r];
-        co[k] = g.rank_co[r];
+        gid[k] = g.vis_gid[min(rlo + (int)own[k], V - 1)];
+        xy[k] = g.xy[gid[k]];
+        co[k] = g.conic_opacity[gid[k]];
+        rad[k] = radii[gid[k]];
     }
     uint32_t tile[kEmitPer], reach[kEmitPer];
     uint32_t keep = 0;
@@ -192,10 +197,10 @@ __global__ __launch_bounds__(256) void emit_instances_kernel(Args a, GeomState g
         if (c < c1) {
             const int i = (int)own[k];
             int x0, y0, x1, y1;
-            getRect(geo[k].x, geo[k].y, __float_as_int(geo[k].z), a.gx, a.gy, x0, y0, x1, y1);
+            getRect(xy[k].x, xy[k].y, rad[k], a.gx, a.gy, x0, y0, x1, y1);
             const uint32_t local = c - s_off[i], wdt = (uint32_t)(x1 - x0);
             const int ty = y0 + (int)(local / wdt), tx = x0 + (int)(local % wdt);
-            reach[k] = half_reach(geo[k].x, geo[k].y, co[k], tx, ty, a.W, a.H);
+            reach[k] = half_reach(xy[k].x, xy[k].y, co[k], tx, ty, a.W, a.H);
             if (reach[k] != 0) {
                 keep |= 1u << k;
                 tile[k] = (uint32_t)(ty * a.gx + tx);
@@ -229,19 +234,19 @@ __global__ __launch_bounds__(256) void emit_instances_kernel(Args a, GeomState g
     for (int k = 0; k < kEmitPer; k++) {
         if ((keep >> k) & 1u) {
             keys[e] = tile[k];
-            gid_by_e[e] = __float_as_uint(geo[k].w) | (reach[k] << kReachShift);
+            gid_by_e[e] = gid[k] | (reach[k] << kReachShift);
             e++;
         }
     }
     for (int i = tid; i < nr; i += 256)
-        if (s_n[i]) atomicAdd(&g.n_inst[__float_as_uint(g.rank_geo[rlo + i].w)], s_n[i]);
+        if (s_n[i]) atomicAdd(&g.n_inst[g.vis_gid[rlo + i]], s_n[i]);
     uint32_t *hist = zero + kZeroHist + (b % kHistShards) * (kMaxPasses * 256);
     for (int p = 0; p < npass; p++)
         if (s_hist[p][tid]) atomicAdd(&hist[p * 256 + tid], s_hist[p][tid]);
 }
 
-// K5: tile ranges from the sorted tile keys (rasterizer_impl.cu:116-138); tiles without instances
-// keep the emission pass's (0, 0).
+// K5: tile ranges from the sorted tile keys (rasterizer_impl.cu:116-138); tiles without instances keep
+// the (0, 0) of the memset.
 __global__ void tile_ranges_kernel(const uint32_t *__restrict__ keys, const uint32_t *__restrict__ n_dev,
                                    uint2 *__restrict__ ranges) {
     const int L = (int)*n_dev;
@@ -260,23 +265,216 @@ __global__ void tile_ranges_kernel(const uint32_t *__restrict__ keys, const uint
     if (idx == L - 1) ranges[cur].y = L;
 }
 
+// ---- K4: per-tile sort by (depth bits, Gaussian id) -------------------------------------------------
+// Bitonic network in its all-ascending ("flip") form: for k = 2, 4, ..: compare i with i ^ (k-1)
+// (flip), then for j = k/4 .. 1 with i ^ j.  Every comparison sends the smaller key to the lower
+// index, so a length n that is not a power of two is padded virtually with +inf: a pair whose
+// partner lies at or beyond n is left alone.
+struct TileSortLds {
+    uint64_t key[kSortCap];
+    uint32_t val[kSortCap];
+};
+
+__device__ __forceinline__ uint64_t inst_key(uint32_t e, const uint32_t *__restrict__ gid_by_e,
+                                             const float *__restrict__ depths) {
+    const uint32_t gid = gid_by_e[e] & kGidMask;
+    return ((uint64_t)__float_as_uint(depths[gid]) << 32) | gid;  // positive depths order as their bits
+}
+
+// Steps (k, j) for k = k_lo .. k_hi (j from j_top for the first k, from k/2 otherwise) over an
+// LDS-resident index space of `space` (a power of two) holding n valid elements.
+__device__ void lds_network(TileSortLds &s, int n, int space, int k_lo, int k_hi, int j_top) {
+    for (int k = k_lo; k <= k_hi; k <<= 1) {
+        for (int j = (k == k_lo ? j_top : k >> 1); j >= 1; j >>= 1) {
+            const bool flip = j == (k >> 1);
+            for (int p = threadIdx.x; p < (space >> 1); p += blockDim.x) {
+                const int i = (p / j) * 2 * j + (p % j);  // bit j of i clear
+                const int q = flip ? (i ^ (k - 1)) : (i + j);
+                if (q >= n) continue;
+                const uint64_t a = s.key[i], b = s.key[q];
+                if (b < a) {
+                    s.key[i] = b;
+                    s.key[q] = a;
+                    const uint32_t t = s.val[i];
+                    s.val[i] = s.val[q];
+                    s.val[q] = t;
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// Runs of up to 64*R instances: one wave, lane l holding positions l, 64 + l, ..  (R registers).  The
+// network is unrolled, so every partner is a compile-time (register, lane-xor) pair: cross-lane steps
+// are shuffles, cross-register steps plain selects; no LDS, no barriers.
+template <int R>
+__device__ __forceinline__ void wave_sort(uint32_t *seg, int n, const uint32_t *__restrict__ gid_by_e,
+                                          const float *__restrict__ depths) {
+    const int lane = threadIdx.x & 63;
+    uint64_t key[R];
+    uint32_t val[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const int i = r * 64 + lane;
+        const uint32_t e = i < n ? seg[i] : 0u;
+        key[r] = i < n ? inst_key(e, gid_by_e, depths) : ~0ull;  // +inf padding
+        val[r] = e;
+    }
+#pragma unroll
+    for (int k = 2; k <= 64 * R; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j >= 1; j >>= 1) {
+            const int mask = j == (k >> 1) ? k - 1 : j;  // flip, then half-cleaners
+            const int hb = j;                            // highest bit of mask
+            const int lx = mask & 63, rx = mask >> 6;
+            uint64_t pk[R];
+            uint32_t pv[R];
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                const int rq = r ^ rx;
+                if (lx == 0) {
+                    pk[r] = key[rq];
+                    pv[r] = val[rq];
+                } else {
+                    const uint32_t hi = __shfl_xor((uint32_t)(key[rq] >> 32), lx);
+                    const uint32_t lo = __shfl_xor((uint32_t)key[rq], lx);
+                    pk[r] = ((uint64_t)hi << 32) | lo;
+                    pv[r] = __shfl_xor(val[rq], lx);
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                const bool lower = ((r * 64 + lane) & hb) == 0;
+                const bool take = lower ? pk[r] < key[r] : pk[r] > key[r];
+                if (take) {
+                    key[r] = pk[r];
+                    val[r] = pv[r];
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const int i = r * 64 + lane;
+        if (i < n) seg[i] = val[r];
+    }
+}
+
+// Tiles with at most kWaveSortMax instances: one wave each, four tiles per workgroup.
+__global__ __launch_bounds__(256) void tile_sort_small_kernel(int T, const uint2 *__restrict__ ranges,
+                                                              const uint32_t *__restrict__ gid_by_e,
+                                                              const float *__restrict__ depths,
+                                                              uint32_t *__restrict__ upos) {
+    const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (tile >= T) return;
+    const uint2 r = ranges[tile];
+    const int n = (int)(r.y - r.x);
+    if (n <= 1 || n > kWaveSortMax) return;
+    uint32_t *seg = upos + r.x;
+    if (n <= 64) wave_sort<1>(seg, n, gid_by_e, depths);
+    else if (n <= 128) wave_sort<2>(seg, n, gid_by_e, depths);
+    else wave_sort<4>(seg, n, gid_by_e, depths);
+}
+
+// Tiles with more than kWaveSortMax instances: one workgroup each.
+__global__ __launch_bounds__(256) void tile_sort_kernel(const uint2 *__restrict__ ranges,
+                                                        const uint32_t *__restrict__ gid_by_e,
+                                                        const float *__restrict__ depths, uint32_t *__restrict__ upos,
+                                                        uint32_t *__restrict__ tkey_hi, uint32_t *__restrict__ tkey_lo) {
+    __shared__ TileSortLds s;
+    const uint2 r = ranges[blockIdx.x];
+    const int n = (int)(r.y - r.x);
+    if (n <= kWaveSortMax) return;
+    uint32_t *seg = upos + r.x;
+    if (n <= kSortCap) {
+        int m = 1;
+        while (m < n) m <<= 1;
+        for (int i = threadIdx.x; i < n; i += blockDim.x) {
+            const uint32_t e = seg[i];
+            s.key[i] = inst_key(e, gid_by_e, depths);
+            s.val[i] = e;
+        }
+        __syncthreads();
+        lds_network(s, n, m, 2, m, 2 >> 1);
+        for (int i = threadIdx.x; i < n; i += blockDim.x) seg[i] = s.val[i];
+        return;
+    }
+    // long tile: sort runs of kSortCap in LDS, then continue the network with its global steps
+    // (stride >= kSortCap) on the segment's keys in tkey_hi/lo (free binning buffers) and its LDS
+    // steps (stride < kSortCap) run by run.
+    uint32_t *khi = tkey_hi + r.x, *klo = tkey_lo + r.x;
+    int m = 1;
+    while (m < n) m <<= 1;
+    auto load_run = [&](int base, bool from_keys) {
+        const int cnt = min(kSortCap, n - base);
+        for (int i = threadIdx.x; i < cnt; i += blockDim.x) {
+            const uint32_t e = seg[base + i];
+            s.key[i] = from_keys ? (((uint64_t)khi[base + i] << 32) | klo[base + i]) : inst_key(e, gid_by_e, depths);
+            s.val[i] = e;
+        }
+        __syncthreads();
+        return cnt;
+    };
+    auto store_run = [&](int base, int cnt) {
+        for (int i = threadIdx.x; i < cnt; i += blockDim.x) {
+            seg[base + i] = s.val[i];
+            khi[base + i] = (uint32_t)(s.key[i] >> 32);
+            klo[base + i] = (uint32_t)s.key[i];
+        }
+        __syncthreads();
+    };
+    for (int base = 0; base < n; base += kSortCap) {
+        const int cnt = load_run(base, false);
+        lds_network(s, cnt, kSortCap, 2, kSortCap, 1);
+        store_run(base, cnt);
+    }
+    for (int k = 2 * kSortCap; k <= m; k <<= 1) {
+        for (int j = k >> 1; j >= kSortCap; j >>= 1) {
+            const bool flip = j == (k >> 1);
+            for (int p = threadIdx.x; p < (m >> 1); p += blockDim.x) {
+                const int i = (p / j) * 2 * j + (p % j);
+                const int q = flip ? (i ^ (k - 1)) : (i + j);
+                if (i >= n || q >= n) continue;
+                const uint64_t a = ((uint64_t)khi[i] << 32) | klo[i], b = ((uint64_t)khi[q] << 32) | klo[q];
+                if (b < a) {
+                    khi[i] = (uint32_t)(b >> 32); klo[i] = (uint32_t)b;
+                    khi[q] = (uint32_t)(a >> 32); klo[q] = (uint32_t)a;
+                    const uint32_t t = seg[i];
+                    seg[i] = seg[q];
+                    seg[q] = t;
+                }
+            }
+            __syncthreads();
+        }
+        for (int base = 0; base < n; base += kSortCap) {
+            const int cnt = load_run(base, true);
+            lds_network(s, cnt, kSortCap, k, k, kSortCap >> 1);
+            store_run(base, cnt);
+        }
+    }
+}
+
 hipError_t launch_binning(const Args &a, GeomState g, const int *radii, BinningState b, int L, ImageState img,
                           hipStream_t s) {
-    (void)radii;
     const int T = a.gx * a.gy;
-    hipError_t e = hipMemsetAsync(b.scratch, 0, 4 * binning_zero_words(L), s);
+    hipError_t e = hipMemsetAsync(b.scratch, 0, 4 * binning_zero_words(L, T), s);
     if (e != hipSuccess) return e;
-    if (L == 0) return hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)T, s);
+    e = hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)T, s);
+    if (e != hipSuccess || L == 0) return e;
     const int npass = (b.key_bits + 7) / 8;
-    const int nblk = std::max<int>((int)nchunk_emit(L), (T + 255) / 256);
-    hipLaunchKernelGGL(emit_instances_kernel, dim3(nblk), dim3(256), 0, s, a, g, L, npass, b.keys[0], b.gid_by_e,
-                       b.scratch, img.ranges);
+    hipLaunchKernelGGL(emit_instances_kernel, dim3((unsigned)nchunk_emit(L)), dim3(256), 0, s, a, g, radii, L, npass,
+                       b.keys[0], b.gid_by_e, b.scratch);
     const uint32_t *n_dev = b.scratch;  // L' <= L reached instances
     uint32_t *keys[2] = {b.keys[0], b.keys[1]};
     uint32_t *vals[2] = {b.vals[0], b.vals[1]};
     onesweep_sort<kSortThreads, kItemsL>(keys, vals, L, n_dev, b.key_bits, b.scratch + kZeroHist,
                                          b.scratch + bin_look_off(L), b.scratch + bin_chain_off() + 1, s);
     hipLaunchKernelGGL(tile_ranges_kernel, dim3((L + 255) / 256), dim3(256), 0, s, b.sorted_keys, n_dev, img.ranges);
+    hipLaunchKernelGGL(tile_sort_small_kernel, dim3((T + 3) / 4), dim3(256), 0, s, T, img.ranges, b.gid_by_e,
+                       g.depths, b.upos);
+    hipLaunchKernelGGL(tile_sort_kernel, dim3(T), dim3(256), 0, s, img.ranges, b.gid_by_e, g.depths, b.upos,
+                       b.tmp_hi, b.tmp_lo);
     return hipGetLastError();
 }
 

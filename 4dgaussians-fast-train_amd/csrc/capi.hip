@@ -87,14 +87,9 @@ GeomState GeomState::carve(char *base, int P, int T) {
     g.clamped = (uint8_t *)gs4d::carve(p, n);
     g.tiles_touched = (uint32_t *)gs4d::carve(p, 4 * n);
     g.n_inst = (uint32_t *)gs4d::carve(p, 4 * n);
-    g.dkeys[0] = (uint32_t *)gs4d::carve(p, 4 * n);
-    g.dkeys[1] = (uint32_t *)gs4d::carve(p, 4 * n);
-    g.dvals[0] = (uint32_t *)gs4d::carve(p, 4 * n);
-    g.dvals[1] = (uint32_t *)gs4d::carve(p, 4 * n);
+    g.vis_gid = (uint32_t *)gs4d::carve(p, 4 * n);
     g.cand_off = (uint32_t *)gs4d::carve(p, 4 * n + 4);
-    g.rank_geo = (float4 *)gs4d::carve(p, 16 * n);
-    g.rank_co = (float4 *)gs4d::carve(p, 16 * n);
-    g.first_rank = (uint32_t *)gs4d::carve(p, 4 * max_emit_chunks(P, T));
+    g.first_vis = (uint32_t *)gs4d::carve(p, 4 * max_emit_chunks(P, T));
     g.zero = (uint32_t *)gs4d::carve(p, 4 * geom_zero_words(P));
     return g;
 }
@@ -130,7 +125,7 @@ namespace gs4d {
 // instances are sorted by tile id only; tile ids need msb(T) bits (rasterizer_impl.cu:301)
 size_t BinningState::required(int L, int T) {
     BinningState b = carve(nullptr, L, T);
-    return (size_t)b.scratch + 4 * binning_zero_words(L) + 512;
+    return (size_t)b.scratch + 4 * binning_zero_words(L, T) + 512;
 }
 BinningState BinningState::carve(char *base, int L, int T) {
     char *p = (char *)align_up((size_t)base, 256);
@@ -144,7 +139,9 @@ BinningState BinningState::carve(char *base, int L, int T) {
     const int final_buf = ((b.key_bits + 7) / 8) & 1;  // each LSD pass swaps the ping-pong buffers
     b.upos = b.vals[final_buf];
     b.sorted_keys = b.keys[final_buf];
-    b.scratch = (uint32_t *)gs4d::carve(p, 4 * binning_zero_words(L));
+    b.tmp_hi = b.keys[final_buf ^ 1];
+    b.tmp_lo = b.vals[final_buf ^ 1];
+    b.scratch = (uint32_t *)gs4d::carve(p, 4 * binning_zero_words(L, T));
     return b;
 }
 
@@ -235,15 +232,16 @@ int gs4d_forward(gs4d_alloc_fn geometry_alloc, void *geometry_ctx, gs4d_alloc_fn
     GS4D_STAGE("preprocess", launch_preprocess(a, means3D, scales, rotations, opacities, shs, cov3D_precomp,
                                                colors_precomp, radii_ptr, g, (int *)(g.zero + kZeroFlag), stream));
 
-    // H1: the single device->host synchronisation of the forward (rasterizer_impl.cu:282).  The depth
-    // ordering is enqueued before the host waits, so the GPU keeps working during the round trip.
+    // H1: the single device->host synchronisation of the forward (rasterizer_impl.cu:282).  The scan of
+    // the visible Gaussians is enqueued before the host waits, so the GPU keeps working during the
+    // round trip.
     static thread_local uint32_t *pinned = nullptr;
     static thread_local hipEvent_t copied = nullptr;
     if (!pinned) GS4D_HIP(hipHostMalloc((void **)&pinned, 128, hipHostMallocDefault));
     if (!copied) GS4D_HIP(hipEventCreateWithFlags(&copied, hipEventDisableTiming));
     GS4D_HIP(hipMemcpyAsync(pinned, g.zero, 4 * (kZeroL + 16), hipMemcpyDeviceToHost, stream));
     GS4D_HIP(hipEventRecord(copied, stream));
-    GS4D_STAGE("depth_order", launch_depth_order(a, g, radii_ptr, stream));
+    GS4D_STAGE("visible_scan", launch_visible_scan(a, g, stream));
     GS4D_HIP(hipEventSynchronize(copied));
     if (prefiltered && pinned[kZeroFlag] != 0)
         return fail(GS4D_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");

@@ -28,22 +28,20 @@ struct GeomState {
     uint8_t *clamped;         // P   bit c set when channel c was clamped (forward.cu:67-69)
     uint32_t *tiles_touched;  // P   3-sigma rect area (the reference's tiles_touched, forward.cu:255)
     uint32_t *n_inst;         // P   tiles of the rect actually reached (half_reach), <= tiles_touched
-    uint32_t *dkeys[2];       // P   depth-sort keys (ping-pong)
-    uint32_t *dvals[2];       // P   depth-sort ids; dvals[0] = Gaussian id by depth rank after the sort
-    uint32_t *cand_off;       // P+1 exclusive scan of tiles_touched in depth-rank order: first candidate
-                              //     instance of each rank
-    float4 *rank_geo;         // P   by depth rank: (x, y, radius bits, Gaussian id bits)
-    float4 *rank_co;          // P   by depth rank: conic_opacity
-    uint32_t *first_rank;     // nchunk_max: depth rank owning candidate j * kEmitChunk
+    uint32_t *vis_gid;        // P   id of the v-th visible Gaussian (tiles_touched > 0), id order
+    uint32_t *cand_off;       // P+1 exclusive scan of tiles_touched over the visible Gaussians: first
+                              //     candidate instance of each (cand_off[V] = num_rendered)
+    uint32_t *first_vis;      // nchunk_max: visible index owning candidate j * kEmitChunk
     uint32_t *zero;           // geom_zero_words(P): counters, histograms, look-back words (one memset)
     static size_t required(int P, int T);
     static GeomState carve(char *base, int P, int T);
 };
-// Zero regions (u32 words) of the geometry and binning states: [0..63] counters, then radix-sort
-// digit histograms [kHistShards][kMaxPasses][256] (producers add with atomics sharded by workgroup,
-// so no address takes more than 1/8 of the adds), then look-back words.
-// geometry: [0] prefiltered flag, [8..23] 8 u64 shards of num_rendered; binning: [0] = L'.
-constexpr int kZeroFlag = 0, kZeroL = 8, kZeroHist = 64;
+// Zero regions (u32 words) of the geometry and binning states: [0..63] counters, then the per-state
+// regions of binning.hip (chunk-prefix chains, tile counts).
+// geometry: [0] prefiltered flag, [8..23] 8 u64 shards of num_rendered, [24] V (visible Gaussians);
+// binning: [0] = L'.  Radix-sort users (knn.hip) keep digit histograms [kHistShards][kMaxPasses][256]
+// of their own: producers add with atomics sharded by workgroup.
+constexpr int kZeroFlag = 0, kZeroL = 8, kZeroV = 24, kZeroHist = 64;
 constexpr int kHistShards = 8, kMaxPasses = 4;
 constexpr int kHistWords = kHistShards * kMaxPasses * 256;
 
@@ -60,14 +58,15 @@ constexpr int kEmitChunk = 2048;  // candidate instances per emission workgroup
 size_t max_emit_chunks(int P, int T);
 
 struct BinningState {
-    uint32_t *keys[2];      // L each: tile id of each instance (ping-pong)
+    uint32_t *keys[2];      // L each: tile id of each instance (ping-pong radix sort)
     uint32_t *vals[2];      // L each: emission slot of each instance (ping-pong)
-    uint32_t *gid_by_e;     // L   Gaussian id of each emission slot
-    uint32_t *upos;         // = the vals buffer holding the sorted result: emission slot of each instance
-                            //     in render order (its Gaussian is gid_by_e[upos[i]]; its gradient
-                            //     record goes to slot upos[i])
+    uint32_t *gid_by_e;     // L   Gaussian id | half-reach bits of each emission slot
+    uint32_t *upos;         // = the vals buffer holding the sorted result: emission slot of each instance in
+                            //     render order (tile, depth, id); its Gaussian is gid_by_e[upos[i]], its
+                            //     gradient record goes to slot upos[i]
     uint32_t *sorted_keys;  // = the keys buffer holding the sorted tile ids
-    uint32_t *scratch;      // binning_zero_words(L), zeroed by one memset; word 0 = L' (emitted instances)
+    uint32_t *tmp_hi, *tmp_lo;  // = the other ping-pong pair: long-tile sort keys
+    uint32_t *scratch;      // binning_zero_words(L, T), zeroed by one memset; word 0 = L' (emitted instances)
     int key_bits;           // msb(T) (rasterizer_impl.cu:301)
     static size_t required(int L, int T);
     static BinningState carve(char *base, int L, int T);
@@ -90,7 +89,7 @@ __device__ __forceinline__ Mat4 load_mat4(const float *__restrict__ p) {
 __device__ __forceinline__ V3 load_v3(const float *__restrict__ p) { return v3(p[0], p[1], p[2]); }
 
 size_t geom_zero_words(int P);
-size_t binning_zero_words(int L);
+size_t binning_zero_words(int L, int T);
 
 // ---- exact tile culling ------------------------------------------------------------------------
 // The reference bins a splat into every tile of its 3-sigma rectangle (forward.cu:232-237), but a
@@ -147,7 +146,7 @@ hipError_t launch_preprocess(const Args &a, const float *means3D, const float *s
                              const float *opacities, const float *shs, const float *cov3D_precomp,
                              const float *colors_precomp, int *radii, GeomState g, int *err_flag, hipStream_t s);
 hipError_t launch_mark_visible(int P, const float *means3D, const float *viewmatrix, uint8_t *present, hipStream_t s);
-hipError_t launch_depth_order(const Args &a, GeomState g, const int *radii, hipStream_t s);
+hipError_t launch_visible_scan(const Args &a, GeomState g, hipStream_t s);
 hipError_t launch_binning(const Args &a, GeomState g, const int *radii, BinningState b, int L, ImageState img,
                           hipStream_t s);
 hipError_t launch_render_forward(const Args &a, GeomState g, BinningState b, ImageState img, float *out_color,

@@ -8,17 +8,12 @@
 namespace gs4d {
 
 // One thread per Gaussian.  Besides the reference's outputs it produces num_rendered (the sum of
-// tiles_touched, added per workgroup into 8 sharded u64 counters: only the total is ever needed) and
-// the depth-sort key of the Gaussian with its digit histograms for the radix sort (binning.hip).
+// tiles_touched, added per workgroup into 8 sharded u64 counters: only the total is ever needed).
 __global__ __launch_bounds__(kPreprocessBlock) void preprocess_kernel(
     Args a, const float *__restrict__ means3D, const float *__restrict__ scales, const float *__restrict__ rotations,
     const float *__restrict__ opacities, const float *__restrict__ shs, const float *__restrict__ cov3D_precomp,
     const float *__restrict__ colors_precomp, int *__restrict__ radii, GeomState g, int *__restrict__ err_flag) {
     __shared__ uint32_t s_wave[kPreprocessBlock / 64];
-    __shared__ uint32_t s_hist[4][256];
-#pragma unroll
-    for (int p = 0; p < 4; p++) s_hist[p][threadIdx.x] = 0;
-    __syncthreads();
     const int idx = blockIdx.x * kPreprocessBlock + threadIdx.x;
     const Mat4 view = load_mat4(a.viewmatrix), proj = load_mat4(a.projmatrix);
     uint32_t touched = 0;
@@ -89,11 +84,6 @@ __global__ __launch_bounds__(kPreprocessBlock) void preprocess_kernel(
         radii[idx] = my_r;
         g.tiles_touched[idx] = touched;
         g.n_inst[idx] = 0;
-        // depth-sort key (binning.hip): positive depths order as their bits; unbinned sort last
-        const uint32_t key = touched ? __float_as_uint(p_view.z) : 0xFFFFFFFFu;
-        g.dkeys[0][idx] = key;
-#pragma unroll
-        for (int p = 0; p < 4; p++) atomicAdd(&s_hist[p][(key >> (8 * p)) & 0xFFu], 1u);
     }
     // workgroup sum of tiles_touched
     uint32_t v = touched;
@@ -108,10 +98,6 @@ __global__ __launch_bounds__(kPreprocessBlock) void preprocess_kernel(
         for (int w = 0; w < kPreprocessBlock / 64; w++) t += s_wave[w];
         if (t) atomicAdd(reinterpret_cast<unsigned long long *>(g.zero + kZeroL) + shard, (unsigned long long)t);
     }
-    uint32_t *hist = g.zero + kZeroHist + shard * (kMaxPasses * 256);
-#pragma unroll
-    for (int p = 0; p < 4; p++)
-        if (s_hist[p][threadIdx.x]) atomicAdd(&hist[p * 256 + threadIdx.x], s_hist[p][threadIdx.x]);
 }
 
 hipError_t launch_preprocess(const Args &a, const float *means3D, const float *scales, const float *rotations,

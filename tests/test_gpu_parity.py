@@ -125,6 +125,22 @@ def test_parity_opaque_stack_termination(C, oracle, dev):
     _check(C, oracle, s, dev)
 
 
+def test_parity_long_tiles(C, oracle, dev):
+    """Tiles holding more instances than one workgroup sorts in LDS (4096): 30k large, faint splats
+    over a 12-tile image (9k-16k instances per tile) exercise the per-tile sort's global merge steps."""
+    s = make_scene(30000, 64, 48, seed=19, log_scale=math.log(0.3))
+    s["opacities"] = np.full_like(s["opacities"], 0.03)
+    fwd, _ = _check(C, oracle, s, dev)
+    assert fwd[0] > 12 * 4096
+
+
+def test_parity_depth_ties(C, oracle, dev):
+    """Groups of Gaussians at exactly the same depth: within a tile the reference orders ties by id."""
+    s = make_scene(4000, 160, 96, seed=20)
+    s["means3D"][:, 2] = np.round(s["means3D"][:, 2] * 4) / 4  # a handful of distinct depths
+    _check(C, oracle, s, dev)
+
+
 def test_empty_and_all_culled(C, oracle, dev):
     s = make_scene(100, 64, 48, seed=14)
     d = to_dev(s, dev)
