@@ -127,7 +127,6 @@ __global__ __launch_bounds__(64) void render_forward_kernel(Args a, const uint2 
     }
     for (uint32_t base = range.x; base < range.y; base += 64) {
         if ((alive[0] | alive[1] | alive[2] | alive[3]) == 0) break;  // forward.cu:312-314
-        const uint32_t n = min(64u, range.y - base);
         const uint64_t reach[2] = {ballot(nxt.reach & 1u), ballot(nxt.reach & 2u)};
         const uint64_t nonpd = ballot(!conic_pd(nxt.geo, nxt.opc));
         __syncthreads();
@@ -286,57 +285,77 @@ struct BwdPixels {
     f2 T[2], A[2], dp0[2], dp1[2], dp2[2], nTb[2];
 };
 
+// Backward splat constants in LDS, every value stored twice so that a broadcast ds_read_b128 yields
+// the (x, x) operand pairs of the packed-f32 pixel math directly:
+// q0 = (mx, mx, my, my), q1 = (A, A, B, B), q2 = (Cc, Cc, o, o), q3 = (r, r, g, g), q4 = (b, b)
+// with A = -a/2 log2e, B = -b log2e, Cc = -c/2 log2e.
+struct SplatPairsLDS {
+    float4 q[4];
+    float2 q4;
+    float2 pad;
+};
+__device__ __forceinline__ f2 lo2(const float4 &v) { return f2{v.x, v.y}; }
+__device__ __forceinline__ f2 hi2(const float4 &v) { return f2{v.z, v.w}; }
+
 // One half tile of one splat of the reverse walk: updates the half's pixel state and adds its
 // per-lane partial sums (moments of u = G dL/dalpha, and the colour sums) to U0..U2 / W0..W2.
+// The falloff is the forward's sequence (falloff()) on operand pairs: identical blend decisions.
 __device__ __forceinline__ void walk_half(f2 &T, f2 &A, const f2 dp0, const f2 dp1, const f2 dp2, const f2 nTb,
-                                          const float4 &geo, const float4 &opc, const float4 &col, float pa, float pb,
-                                          f2 pfy, bool check_pw, uint64_t act0, uint64_t act1, f2 &U0, f2 &U1,
-                                          f2 &U2, f2 &W0, f2 &W1, f2 &W2) {
-    const Falloff f = falloff(geo, opc, pa, pb, pfy);
+                                          const f2 Y2, const f2 C2, const f2 O2, const f2 R2, const f2 G2,
+                                          const f2 B2, const f2 pa2, const f2 pb2, f2 pfy, bool check_pw,
+                                          uint64_t act0, uint64_t act1, f2 &U0, f2 &U1, f2 &U2, f2 &W0, f2 &W1,
+                                          f2 &W2) {
+    const f2 dy = Y2 - pfy;
+    const f2 pw = fma2(dy, fma2(C2, dy, pb2), pa2);
+    const f2 G = f2{__builtin_amdgcn_exp2f(pw.x), __builtin_amdgcn_exp2f(pw.y)};
+    const f2 al = O2 * G;
+    const f2 alpha = f2{fminf(0.99f, al.x), fminf(0.99f, al.y)};
     // backward.cu:486-497: contributor test, alpha < 1/255 and (for a conic that is not positive
     // definite) power > 0 skips -- the same decisions as the forward
-    uint64_t m0 = ballot(f.alpha.x >= 1.0f / 255.0f) & act0;
-    uint64_t m1 = ballot(f.alpha.y >= 1.0f / 255.0f) & act1;
+    uint64_t m0 = ballot(alpha.x >= 1.0f / 255.0f) & act0;
+    uint64_t m1 = ballot(alpha.y >= 1.0f / 255.0f) & act1;
     if (check_pw) {
-        m0 &= ballot(f.pw.x <= 0.0f);
-        m1 &= ballot(f.pw.y <= 0.0f);
+        m0 &= ballot(pw.x <= 0.0f);
+        m1 &= ballot(pw.y <= 0.0f);
     }
     const bool b0 = lane_bit(m0), b1 = lane_bit(m1);
-    const f2 ae = f2{b0 ? f.alpha.x : 0.f, b1 ? f.alpha.y : 0.f};
-    const f2 Ge = f2{b0 ? f.G.x : 0.f, b1 ? f.G.y : 0.f};
+    const f2 ae = f2{b0 ? alpha.x : 0.f, b1 ? alpha.y : 0.f};
+    const f2 Ge = f2{b0 ? G.x : 0.f, b1 ? G.y : 0.f};
     const f2 om = bc2(1.f) - ae;
     const f2 inv = f2{__builtin_amdgcn_rcpf(om.x), __builtin_amdgcn_rcpf(om.y)};
     const f2 Tn = T * inv;  // backward.cu:503
     T = Tn;
-    const f2 CD = fma2(bc2(col.z), dp2, fma2(bc2(col.y), dp1, bc2(col.x) * dp0));
+    const f2 CD = fma2(B2, dp2, fma2(G2, dp1, R2 * dp0));
     const f2 diff = CD - A;
     const f2 dLda = fma2(diff, Tn, nTb * inv);  // backward.cu:519-534
     A = fma2(ae, diff, A);                      // accum_rec for the next splat in front
     const f2 u = Ge * dLda;
     const f2 w = ae * Tn;                       // dchannel_dcolor (backward.cu:521)
-    const f2 ud = u * f.dy;
+    const f2 ud = u * dy;
     U0 += u;
     U1 += ud;
-    U2 = fma2(ud, f.dy, U2);
+    U2 = fma2(ud, dy, U2);
     W0 = fma2(w, dp0, W0);
     W1 = fma2(w, dp1, W1);
     W2 = fma2(w, dp2, W2);
 }
 
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void render_backward_kernel(Args a, const uint2 *__restrict__ ranges, const uint32_t *__restrict__ gid_by_e,
+// No occupancy attribute: 98 VGPRs (4 waves/SIMD, every tile's wave resident within two rounds) ran
+// as fast as a spilling 80-VGPR build at 6 waves/SIMD.
+__global__ __launch_bounds__(64) void render_backward_kernel(Args a, const uint2 *__restrict__ ranges, const uint32_t *__restrict__ gid_by_e,
                             const uint32_t *__restrict__ upos, const float2 *__restrict__ xy,
                             const float4 *__restrict__ conic_opacity, const float4 *__restrict__ rgbd,
                             const float *__restrict__ colors, const float *__restrict__ final_Ts,
                             const uint32_t *__restrict__ n_contrib, const float *__restrict__ dL_dpixels,
                             float *__restrict__ contrib) {
-    __shared__ SplatLDS s_sp[64];
+    __shared__ SplatPairsLDS s_sp[64];
     __shared__ float4 s_rec[64][3];  // reduced moments of the batch's splats
     const int tile = blockIdx.x;
     const int tx = tile % a.gx, ty = tile / a.gx;
     const int lane = threadIdx.x;
     const int px = tx * kBlockX + (lane & 15);
     const int py0 = ty * kBlockY + (lane >> 4);
-    const float pfx = (float)px;
+    const f2 pfx2 = bc2((float)px);
     const size_t HW = (size_t)a.W * a.H;
     uint2 range = ranges[tile];
     range.x = __builtin_amdgcn_readfirstlane(range.x);
@@ -404,16 +423,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void re
         const uint64_t reach[2] = {ballot(nxt.reach & 1u), ballot(nxt.reach & 2u)};
         const uint64_t nonpd = ballot(!conic_pd(nxt.geo, nxt.opc));
         __syncthreads();
-        s_sp[lane].geo = nxt.geo;
-        s_sp[lane].opc = nxt.opc;
-        s_sp[lane].col = nxt.col;
+        s_sp[lane].q[0] = make_float4(nxt.geo.x, nxt.geo.x, nxt.geo.y, nxt.geo.y);
+        s_sp[lane].q[1] = make_float4(nxt.geo.z, nxt.geo.z, nxt.geo.w, nxt.geo.w);
+        s_sp[lane].q[2] = make_float4(nxt.opc.x, nxt.opc.x, nxt.opc.y, nxt.opc.y);
+        s_sp[lane].q[3] = make_float4(nxt.col.x, nxt.col.x, nxt.col.y, nxt.col.y);
+        s_sp[lane].q4 = make_float2(nxt.col.z, nxt.col.z);
         __syncthreads();
         if (end - 64 > 0) fetch(end - 64);
         for (int j = 0; j < n; j++) {
-            const float4 geo = s_sp[j].geo, opc = s_sp[j].opc, col = s_sp[j].col;
+            const float4 q0 = s_sp[j].q[0], q1 = s_sp[j].q[1], q2 = s_sp[j].q[2], q3 = s_sp[j].q[3];
+            const float2 q4 = s_sp[j].q4;
             const uint32_t contributor = (uint32_t)(end - 1 - j);
-            const float dx = geo.x - pfx;
-            const float pa = geo.z * dx * dx, pb = geo.w * dx;
+            const f2 dx2 = lo2(q0) - pfx2;
+            const f2 pa2 = lo2(q1) * dx2 * dx2, pb2 = hi2(q1) * dx2;  // forward: geo.z * dx * dx, geo.w * dx
+            const float dx = dx2.x;
             f2 U0 = bc2(0.f), U1 = bc2(0.f), U2 = bc2(0.f), W0 = bc2(0.f), W1 = bc2(0.f), W2 = bc2(0.f);
             // a half tile the splat does not reach has alpha = G = 0 at all its pixels: T and A stay,
             // nothing is added
@@ -422,8 +445,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void re
                 if ((reach[h] >> j) & 1) {
                     const uint64_t act0 = ballot(contributor < lastc[2 * h]);
                     const uint64_t act1 = ballot(contributor < lastc[2 * h + 1]);
-                    walk_half(st.T[h], st.A[h], st.dp0[h], st.dp1[h], st.dp2[h], st.nTb[h], geo, opc, col, pa, pb,
-                              pfy[h], (nonpd >> j) & 1, act0, act1, U0, U1, U2, W0, W1, W2);
+                    walk_half(st.T[h], st.A[h], st.dp0[h], st.dp1[h], st.dp2[h], st.nTb[h], hi2(q0), lo2(q2),
+                              hi2(q2), lo2(q3), hi2(q3), f2{q4.x, q4.y}, pa2, pb2, pfy[h], (nonpd >> j) & 1, act0, act1,
+                              U0, U1, U2, W0, W1, W2);
                 }
             }
             const float u0 = U0.x + U0.y, u1 = U1.x + U1.y;
