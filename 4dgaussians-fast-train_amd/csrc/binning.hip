@@ -18,9 +18,10 @@
 //      u32 keys; digit histograms built by the emission, no atomics on contended counters): each
 //      tile's run is left in Gaussian-id order; tile ranges follow from the sorted keys;
 //   4. tile_sort: each tile's run is sorted by the 64-bit key (depth bits, Gaussian id) -- exactly the
-//      reference's within-tile order: runs of up to 256 by one wave in registers (bitonic network
-//      over lane shuffles), up to 4096 by one workgroup in LDS, longer ones as LDS-sorted 4096-runs
-//      merged by the same network's global steps.  The key is unique inside a tile.
+//      reference's within-tile order (the key is unique inside a tile).  Runs of up to kWaveSortMax
+//      (256) are sorted by the render forward itself, in registers, before it blends them
+//      (render.hip); here runs of up to 4096 by one workgroup in LDS, longer ones as LDS-sorted
+//      4096-runs merged by the same network's global steps.
 // The P Gaussians are never sorted by depth globally (the reference's 45-bit key needs 6 passes; a
 // global depth sort needs 4 more over the Gaussians).  Prefix sums publish per-chunk counts (one
 // 32-bit status+count word per chunk, agent-scope relaxed atomics) and sum the lower chunks' words
@@ -34,7 +35,6 @@ namespace gs4d {
 constexpr int kEmitPer = kEmitChunk / 256;  // candidates per lane in the emission pass
 constexpr int kSortThreads = 1024;          // radix-sort workgroup: 16 waves rank one chunk together
 constexpr int kItemsL = 8;                  // keys per lane for the instance sort (8192 per workgroup)
-constexpr int kWaveSortMax = 256;           // tile runs sorted by one wave in registers
 constexpr int kSortCap = 4096;              // tile runs sorted in LDS by one workgroup (48 KiB)
 
 // ---------------------------------------------------------------------------------------------
@@ -305,78 +305,6 @@ __device__ void lds_network(TileSortLds &s, int n, int space, int k_lo, int k_hi
     }
 }
 
-// Runs of up to 64*R instances: one wave, lane l holding positions l, 64 + l, ..  (R registers).  The
-// network is unrolled, so every partner is a compile-time (register, lane-xor) pair: cross-lane steps
-// are shuffles, cross-register steps plain selects; no LDS, no barriers.
-template <int R>
-__device__ __forceinline__ void wave_sort(uint32_t *seg, int n, const uint32_t *__restrict__ gid_by_e,
-                                          const float *__restrict__ depths) {
-    const int lane = threadIdx.x & 63;
-    uint64_t key[R];
-    uint32_t val[R];
-#pragma unroll
-    for (int r = 0; r < R; r++) {
-        const int i = r * 64 + lane;
-        const uint32_t e = i < n ? seg[i] : 0u;
-        key[r] = i < n ? inst_key(e, gid_by_e, depths) : ~0ull;  // +inf padding
-        val[r] = e;
-    }
-#pragma unroll
-    for (int k = 2; k <= 64 * R; k <<= 1) {
-#pragma unroll
-        for (int j = k >> 1; j >= 1; j >>= 1) {
-            const int mask = j == (k >> 1) ? k - 1 : j;  // flip, then half-cleaners
-            const int hb = j;                            // highest bit of mask
-            const int lx = mask & 63, rx = mask >> 6;
-            uint64_t pk[R];
-            uint32_t pv[R];
-#pragma unroll
-            for (int r = 0; r < R; r++) {
-                const int rq = r ^ rx;
-                if (lx == 0) {
-                    pk[r] = key[rq];
-                    pv[r] = val[rq];
-                } else {
-                    const uint32_t hi = __shfl_xor((uint32_t)(key[rq] >> 32), lx);
-                    const uint32_t lo = __shfl_xor((uint32_t)key[rq], lx);
-                    pk[r] = ((uint64_t)hi << 32) | lo;
-                    pv[r] = __shfl_xor(val[rq], lx);
-                }
-            }
-#pragma unroll
-            for (int r = 0; r < R; r++) {
-                const bool lower = ((r * 64 + lane) & hb) == 0;
-                const bool take = lower ? pk[r] < key[r] : pk[r] > key[r];
-                if (take) {
-                    key[r] = pk[r];
-                    val[r] = pv[r];
-                }
-            }
-        }
-    }
-#pragma unroll
-    for (int r = 0; r < R; r++) {
-        const int i = r * 64 + lane;
-        if (i < n) seg[i] = val[r];
-    }
-}
-
-// Tiles with at most kWaveSortMax instances: one wave each, four tiles per workgroup.
-__global__ __launch_bounds__(256) void tile_sort_small_kernel(int T, const uint2 *__restrict__ ranges,
-                                                              const uint32_t *__restrict__ gid_by_e,
-                                                              const float *__restrict__ depths,
-                                                              uint32_t *__restrict__ upos) {
-    const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (tile >= T) return;
-    const uint2 r = ranges[tile];
-    const int n = (int)(r.y - r.x);
-    if (n <= 1 || n > kWaveSortMax) return;
-    uint32_t *seg = upos + r.x;
-    if (n <= 64) wave_sort<1>(seg, n, gid_by_e, depths);
-    else if (n <= 128) wave_sort<2>(seg, n, gid_by_e, depths);
-    else wave_sort<4>(seg, n, gid_by_e, depths);
-}
-
 // Tiles with more than kWaveSortMax instances: one workgroup each.
 __global__ __launch_bounds__(256) void tile_sort_kernel(const uint2 *__restrict__ ranges,
                                                         const uint32_t *__restrict__ gid_by_e,
@@ -471,8 +399,6 @@ hipError_t launch_binning(const Args &a, GeomState g, const int *radii, BinningS
     onesweep_sort<kSortThreads, kItemsL>(keys, vals, L, n_dev, b.key_bits, b.scratch + kZeroHist,
                                          b.scratch + bin_look_off(L), b.scratch + bin_chain_off() + 1, s);
     hipLaunchKernelGGL(tile_ranges_kernel, dim3((L + 255) / 256), dim3(256), 0, s, b.sorted_keys, n_dev, img.ranges);
-    hipLaunchKernelGGL(tile_sort_small_kernel, dim3((T + 3) / 4), dim3(256), 0, s, T, img.ranges, b.gid_by_e,
-                       g.depths, b.upos);
     hipLaunchKernelGGL(tile_sort_kernel, dim3(T), dim3(256), 0, s, img.ranges, b.gid_by_e, g.depths, b.upos,
                        b.tmp_hi, b.tmp_lo);
     return hipGetLastError();

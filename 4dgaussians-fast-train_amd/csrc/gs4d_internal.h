@@ -137,6 +137,9 @@ __device__ __forceinline__ uint32_t half_reach(float mx, float my, float4 co, in
     }
     return r;
 }
+// Tile runs of up to kWaveSortMax instances are depth-sorted by the render forward (render.hip), longer
+// ones by tile_sort_kernel (binning.hip) before it.
+constexpr int kWaveSortMax = 256;
 // gid_by_e[e] = Gaussian id | half-reach bits << kReachShift (P < 2^30)
 constexpr int kReachShift = 30;
 constexpr uint32_t kGidMask = (1u << kReachShift) - 1u;
@@ -150,7 +153,7 @@ hipError_t launch_visible_scan(const Args &a, GeomState g, hipStream_t s);
 hipError_t launch_binning(const Args &a, GeomState g, const int *radii, BinningState b, int L, ImageState img,
                           hipStream_t s);
 hipError_t launch_render_forward(const Args &a, GeomState g, BinningState b, ImageState img, float *out_color,
-                                 float *out_depth, hipStream_t s);
+                                 float *out_depth, hipStream_t s);  // also sorts runs <= kWaveSortMax
 hipError_t launch_render_backward(const Args &a, GeomState g, const uint32_t *gid_by_e, const uint32_t *upos, ImageState img,
                                   const float *colors, const float *dL_dpix, float *contrib, hipStream_t s);
 size_t contrib_scratch_bytes(int R);

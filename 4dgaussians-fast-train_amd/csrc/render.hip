@@ -91,8 +91,62 @@ __device__ __forceinline__ bool conic_pd(const float4 &geo, const float4 &opc) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// K4 for short tiles, fused into the forward: a run of up to 64*R instances is sorted by the key
+// (depth bits << 32 | emission slot) by one wave in registers, lane l holding positions l, 64 + l, ..
+// Inside a tile the emission slot increases with the Gaussian id (emission follows the visible
+// Gaussians in id order), so this is the reference's (depth, id) order (rasterizer_impl.cu:94-105,
+// 304-309) and the key carries its own value.  Bitonic network in its all-ascending ("flip") form,
+// unrolled: every partner is a compile-time (register, lane-xor) pair, so cross-lane steps are
+// shuffles and cross-register steps plain selects; a length that is not a power of two is padded
+// with +inf keys.  The sorted slots are written back for the backward and returned in ev[].
+template <int R>
+__device__ __forceinline__ void sort_run(uint32_t *__restrict__ seg, int n, const uint32_t *__restrict__ gid_by_e,
+                                         const float *__restrict__ depths, int lane, uint32_t ev[4]) {
+    uint64_t key[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const int i = r * 64 + lane;
+        const uint32_t e = i < n ? seg[i] : 0u;
+        const uint32_t gid = i < n ? gid_by_e[e] & kGidMask : 0u;
+        key[r] = i < n ? ((uint64_t)__float_as_uint(depths[gid]) << 32) | e : ~0ull;  // depths > 0.2
+    }
+#pragma unroll
+    for (int k = 2; k <= 64 * R; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j >= 1; j >>= 1) {
+            const int mask = j == (k >> 1) ? k - 1 : j;  // flip, then half-cleaners
+            const int lx = mask & 63, rx = mask >> 6;
+            uint64_t pk[R];
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                const int rq = r ^ rx;
+                if (lx == 0) {
+                    pk[r] = key[rq];
+                } else {
+                    const uint32_t hi = __shfl_xor((uint32_t)(key[rq] >> 32), lx);
+                    const uint32_t lo = __shfl_xor((uint32_t)key[rq], lx);
+                    pk[r] = ((uint64_t)hi << 32) | lo;
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                const bool lower = ((r * 64 + lane) & j) == 0;
+                const uint64_t kr = key[r];
+                key[r] = lower ? (pk[r] < kr ? pk[r] : kr) : (pk[r] > kr ? pk[r] : kr);
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int i = r * 64 + lane;
+        ev[r] = r < R ? (uint32_t)key[r < R ? r : 0] : 0u;
+        if (r < R && i < n) seg[i] = ev[r];
+    }
+}
+
 __global__ __launch_bounds__(64) void render_forward_kernel(Args a, const uint2 *__restrict__ ranges,
-                                                            const uint32_t *__restrict__ upos,
+                                                            uint32_t *__restrict__ upos,
+                                                            const float *__restrict__ depths,
                                                             const uint32_t *__restrict__ gid_by_e,
                                                             const float2 *__restrict__ xy,
                                                             const float4 *__restrict__ conic_opacity,
@@ -120,10 +174,23 @@ __global__ __launch_bounds__(64) void render_forward_kernel(Args a, const uint2 
     uint2 range = ranges[tile];
     range.x = __builtin_amdgcn_readfirstlane(range.x);
     range.y = __builtin_amdgcn_readfirstlane(range.y);
+    // short runs: sorted here, their emission slots kept in registers (batch b in ev[0] after b shifts)
+    const int n_run = (int)(range.y - range.x);
+    const bool in_regs = n_run <= kWaveSortMax;
+    uint32_t ev[4] = {0u, 0u, 0u, 0u};
+    if (n_run > 1 && in_regs) {
+        uint32_t *seg = upos + range.x;
+        if (n_run <= 64) sort_run<1>(seg, n_run, gid_by_e, depths, lane, ev);
+        else if (n_run <= 128) sort_run<2>(seg, n_run, gid_by_e, depths, lane, ev);
+        else sort_run<4>(seg, n_run, gid_by_e, depths, lane, ev);
+    } else if (n_run == 1 && lane == 0) {
+        ev[0] = upos[range.x];
+    }
     SplatRegs nxt;
     if (range.x < range.y) {
         const bool v = range.x + lane < range.y;
-        load_splat(nxt, v, v ? gid_by_e[upos[range.x + lane]] : 0u, xy, conic_opacity, rgbd, nullptr);
+        const uint32_t e = in_regs ? ev[0] : (v ? upos[range.x + lane] : 0u);
+        load_splat(nxt, v, v ? gid_by_e[e] : 0u, xy, conic_opacity, rgbd, nullptr);
     }
     for (uint32_t base = range.x; base < range.y; base += 64) {
         if ((alive[0] | alive[1] | alive[2] | alive[3]) == 0) break;  // forward.cu:312-314
@@ -137,7 +204,13 @@ __global__ __launch_bounds__(64) void render_forward_kernel(Args a, const uint2 
         {
             const uint32_t nb = base + 64;
             const bool v = nb + lane < range.y;
-            if (nb < range.y) load_splat(nxt, v, v ? gid_by_e[upos[nb + lane]] : 0u, xy, conic_opacity, rgbd, nullptr);
+            ev[0] = ev[1];
+            ev[1] = ev[2];
+            ev[2] = ev[3];
+            if (nb < range.y) {
+                const uint32_t e = in_regs ? ev[0] : (v ? upos[nb + lane] : 0u);
+                load_splat(nxt, v, v ? gid_by_e[e] : 0u, xy, conic_opacity, rgbd, nullptr);
+            }
         }
         const uint32_t pos0 = base - range.x;
         // The two half tiles blend independently: each walks only the batch's splats that reach it.
@@ -202,7 +275,7 @@ __global__ __launch_bounds__(64) void render_forward_kernel(Args a, const uint2 
 hipError_t launch_render_forward(const Args &a, GeomState g, BinningState b, ImageState img, float *out_color,
                                  float *out_depth, hipStream_t s) {
     const int T = a.gx * a.gy;
-    hipLaunchKernelGGL(render_forward_kernel, dim3(T), dim3(64), 0, s, a, img.ranges, b.upos, b.gid_by_e, g.xy,
+    hipLaunchKernelGGL(render_forward_kernel, dim3(T), dim3(64), 0, s, a, img.ranges, b.upos, g.depths, b.gid_by_e, g.xy,
                        g.conic_opacity, g.rgbd, img.final_T, img.n_contrib, out_color, out_depth);
     return hipGetLastError();
 }

@@ -1,0 +1,44 @@
+"""Train-step timing probe (diagnostic, GPU): N fine-stage steps of gs4d_train.train.train_step at a
+bench config, wall time per step and (under rocprofv3 --kernel-trace) the kernels it launches."""
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "4dgaussians-fast-train_amd")]
+from gs4d_train import config  # noqa: E402
+from gs4d_train.gaussians import GaussianModel  # noqa: E402
+from gs4d_train.synthetic import CONFIGS, make_point_cloud, make_training_views  # noqa: E402
+from gs4d_train.train import train_step  # noqa: E402
+
+
+def main(cfg="metric", steps=20, fused=True):
+    P, W, H = CONFIGS[cfg]
+    dev = torch.device("cuda:0")
+    hyper, opt = config.dynerf()
+    torch.manual_seed(0)
+    g = GaussianModel(3, hyper, fused=fused)
+    pts, cols = make_point_cloud(P, seed=0)
+    g.create_from_pcd(pts, cols, spatial_lr_scale=1.0, device=dev)
+    g._deformation.deformation_net.grid.fused = fused
+    g.training_setup(opt)
+    g.active_sh_degree = 3
+    views = make_training_views(1, W, H, seed=1, device=dev)
+    bg = torch.ones(3, device=dev)
+    for i in range(5):
+        train_step(g, views, opt, hyper, 3001 + i, bg)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        train_step(g, views, opt, hyper, 3006 + i, bg)
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) / steps * 1e3
+    # host-side cost: the same steps with the GPU work queued but not waited on is not separable; report
+    # the wall time and let the kernel trace give the device time
+    print(f"train_step {cfg} fused={fused}: {el:.3f} ms/step")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "metric")
