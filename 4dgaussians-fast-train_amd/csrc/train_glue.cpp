@@ -184,7 +184,57 @@ std::tuple<torch::Tensor, std::vector<torch::Tensor>> hexplane_backward(const to
     return {dpts, grads};
 }
 
+// ---- HexPlane regularisers ------------------------------------------------------------------------
+static gs4d_reg_batch reg_batch(const std::vector<torch::Tensor> &planes, const std::vector<double> &w_smooth,
+                                const std::vector<double> &w_l1, const std::vector<torch::Tensor> *grads) {
+    need(!planes.empty() && planes.size() <= GS4D_REG_MAX_PLANES, "hexplane_reg: 1..24 planes");
+    need(w_smooth.size() == planes.size() && w_l1.size() == planes.size(), "hexplane_reg: one weight pair per plane");
+    gs4d_reg_batch b;
+    b.count = (int)planes.size();
+    int64_t blocks = 0;
+    for (size_t i = 0; i < planes.size(); i++) {
+        const torch::Tensor &p = planes[i];
+        gpu_f32(p, "hexplane_reg plane");
+        need(p.dim() == 4 && p.size(0) == 1 && p.size(2) >= 3, "hexplane_reg planes must be (1, C, H >= 3, W)");
+        gs4d_reg_plane &d = b.p[i];
+        d.data = p.data_ptr<float>();
+        d.grad = grads ? (*grads)[i].data_ptr<float>() : nullptr;
+        d.C = (int)p.size(1);
+        d.H = (int)p.size(2);
+        d.W = (int)p.size(3);
+        d.w_smooth = (float)w_smooth[i];
+        d.w_l1 = (float)w_l1[i];
+        d.first_block = blocks;
+        blocks += gs4d_reg_blocks(d.C, d.H, d.W);
+    }
+    return b;
+}
+
+torch::Tensor hexplane_reg_forward(std::vector<torch::Tensor> planes, std::vector<double> w_smooth,
+                                   std::vector<double> w_l1) {
+    gs4d_reg_batch b = reg_batch(planes, w_smooth, w_l1, nullptr);
+    c10::hip::HIPGuard guard(planes[0].device().index());
+    hipStream_t s = stream_of(planes[0]);
+    auto loss = torch::empty({}, planes[0].options());
+    auto scratch = torch::empty({(int64_t)gs4d_reg_scratch_bytes(&b)}, planes[0].options().dtype(torch::kUInt8));
+    check(gs4d_hexplane_reg_forward(&b, loss.data_ptr<float>(), scratch.data_ptr(), (void *)s), "hexplane_reg forward");
+    return loss;
+}
+
+std::vector<torch::Tensor> hexplane_reg_backward(std::vector<torch::Tensor> planes, std::vector<double> w_smooth,
+                                                 std::vector<double> w_l1, const torch::Tensor &dloss_) {
+    std::vector<torch::Tensor> grads;
+    for (auto &p : planes) grads.push_back(torch::empty_like(p));
+    gs4d_reg_batch b = reg_batch(planes, w_smooth, w_l1, &grads);
+    c10::hip::HIPGuard guard(planes[0].device().index());
+    auto dloss = dloss_.to(planes[0].device(), torch::kFloat32).contiguous();
+    check(gs4d_hexplane_reg_backward(&b, dloss.data_ptr<float>(), (void *)stream_of(planes[0])), "hexplane_reg backward");
+    return grads;
+}
+
 PYBIND11_MODULE(_C, m) {
+    m.def("hexplane_reg_forward", &hexplane_reg_forward);
+    m.def("hexplane_reg_backward", &hexplane_reg_backward);
     m.def("hexplane_forward", &hexplane_forward);
     m.def("hexplane_backward", &hexplane_backward);
     m.def("l1_forward", &l1_forward);

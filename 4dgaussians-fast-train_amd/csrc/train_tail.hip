@@ -1,5 +1,5 @@
 // train_tail.hip -- the train step after the rasterizer: fused L1 loss, the
-// densification statistics and a multi-tensor Adam.
+// densification statistics, a multi-tensor Adam and the HexPlane regularisers.
 //
 // Reference: utils/loss_utils.py:20-21 (l1_loss) with the L1 gradient torch's autograd derives
 // (sign(x - y) / N), train.py:346-349 + scene/gaussian_model.py:521-523 (densification statistics),
@@ -13,7 +13,10 @@
 //   adam:   per element reads p, g, m, v and writes p, m, v (28 bytes) for EVERY parameter tensor of
 //           the model in one launch (tensor descriptors passed by value, chunk -> tensor lookup);
 //   stats:  per Gaussian reads the viewspace gradient, visibility and radius and updates the three
-//           accumulators in place.
+//           accumulators in place;
+//   reg:    the 12 planes' smoothness + L1 terms (scene/gaussian_model.py:538-577), which torch runs as
+//           ~100 slice / sub / square / mean kernels forward and their slice-backward zero-fills
+//           backward: one launch per direction over every plane (plus one fixed-order final sum).
 #include <math.h>
 
 #include "../../include/gs4d_train.h"
@@ -124,11 +127,138 @@ __global__ __launch_bounds__(kTailThreads) void adam_kernel(gs4d_adam_batch batc
     }
 }
 
+// ---- HexPlane regularisers ------------------------------------------------------------------------
+constexpr int kRegPerThread = 8;
+constexpr int kRegBlock = kTailThreads * kRegPerThread;  // plane elements per workgroup
+
+__device__ __forceinline__ int reg_plane_of(const gs4d_reg_batch &b, int64_t blk) {
+    int t = 0;
+    while (t + 1 < b.count && b.p[t + 1].first_block <= blk) t++;
+    return t;
+}
+
+// second difference along H at row y (0 <= y <= H-3), in the reference's operation order
+// (regulation.py:25-26): first[j] = t[j+1] - t[j], second[y] = first[y+1] - first[y]
+__device__ __forceinline__ float second_diff(const float *__restrict__ col, int y, int W) {
+    const float t0 = col[(size_t)y * W], t1 = col[(size_t)(y + 1) * W], t2 = col[(size_t)(y + 2) * W];
+    return (t2 - t1) - (t1 - t0);
+}
+
+__global__ __launch_bounds__(kTailThreads) void reg_forward_kernel(gs4d_reg_batch b, double *__restrict__ part) {
+    const int64_t blk = blockIdx.x;
+    const gs4d_reg_plane d = b.p[reg_plane_of(b, blk)];
+    const int64_t n = (int64_t)d.C * d.H * d.W, hw = (int64_t)d.H * d.W;
+    const double cs = (double)d.w_smooth / ((double)d.C * (d.H - 2) * d.W), cl = (double)d.w_l1 / (double)n;
+    double acc = 0.0;
+#pragma unroll
+    for (int k = 0; k < kRegPerThread; k++) {
+        const int64_t i = (blk - d.first_block) * kRegBlock + (int64_t)k * kTailThreads + threadIdx.x;
+        if (i >= n) break;
+        const float t = d.data[i];
+        const int y = (int)((i % hw) / d.W);
+        if (y <= d.H - 3) {
+            const float s2 = second_diff(d.data + (i - (int64_t)y * d.W), y, d.W);
+            acc += cs * (double)(s2 * s2);
+        }
+        acc += cl * (double)fabsf(1.f - t);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+    __shared__ double s_w[kTailThreads / 64];
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) part[blk] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+}
+
+__global__ __launch_bounds__(kTailThreads) void reg_final_kernel(int nblk, const double *__restrict__ part,
+                                                                 float *__restrict__ loss) {
+    double s = 0.0;
+    for (int i = threadIdx.x; i < nblk; i += kTailThreads) s += part[i];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+    __shared__ double s_w[kTailThreads / 64];
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) *loss = (float)(s_w[0] + s_w[1] + s_w[2] + s_w[3]);
+}
+
+// d/dt of the batch loss, as autograd derives it from the reference's graph: mean -> g / N, square
+// -> 2 s g, second[y] = first[y+1] - first[y] -> dfirst[j] = ds[j-1] - ds[j], first[j] = t[j+1] - t[j]
+// -> dt[y] = dfirst[y-1] - dfirst[y] (out-of-range terms are 0); abs(1 - t) -> -sign(1 - t) g / N.
+__global__ __launch_bounds__(kTailThreads) void reg_backward_kernel(gs4d_reg_batch b, const float *__restrict__ dloss) {
+    const int64_t blk = blockIdx.x;
+    const gs4d_reg_plane d = b.p[reg_plane_of(b, blk)];
+    const int64_t n = (int64_t)d.C * d.H * d.W, hw = (int64_t)d.H * d.W;
+    const float g = *dloss;
+    const float gs = (g * d.w_smooth) / (float)((int64_t)d.C * (d.H - 2) * d.W);
+    const float gl = (g * d.w_l1) / (float)n;
+#pragma unroll
+    for (int k = 0; k < kRegPerThread; k++) {
+        const int64_t i = (blk - d.first_block) * kRegBlock + (int64_t)k * kTailThreads + threadIdx.x;
+        if (i >= n) break;
+        const int y = (int)((i % hw) / d.W);
+        const float *col = d.data + (i - (int64_t)y * d.W);
+        float ds[3];  // ds[y-2], ds[y-1], ds[y]
+#pragma unroll
+        for (int q = 0; q < 3; q++) {
+            const int yy = y - 2 + q;
+            ds[q] = (yy >= 0 && yy <= d.H - 3) ? 2.f * second_diff(col, yy, d.W) * gs : 0.f;
+        }
+        const float df_prev = (y >= 1) ? ds[0] - ds[1] : 0.f;      // dfirst[y-1] = ds[y-2] - ds[y-1]
+        const float df_cur = (y <= d.H - 2) ? ds[1] - ds[2] : 0.f;  // dfirst[y] = ds[y-1] - ds[y]
+        const float t = d.data[i];
+        const float one_m = 1.f - t;
+        const float sg = (float)((one_m > 0.f) - (one_m < 0.f));
+        d.grad[i] = (df_prev - df_cur) + (-sg) * gl;
+    }
+}
+
 }  // namespace gs4d
 
 using namespace gs4d;
 
 extern "C" {
+
+int64_t gs4d_reg_blocks(int C, int H, int W) { return ((int64_t)C * H * W + kRegBlock - 1) / kRegBlock; }
+
+static int reg_check(const gs4d_reg_batch *b, int64_t *nblk) {
+    if (!b || b->count < 1 || b->count > GS4D_REG_MAX_PLANES) return 1;
+    int64_t blocks = 0;
+    for (int i = 0; i < b->count; i++) {
+        const gs4d_reg_plane &p = b->p[i];
+        if (!p.data || p.C < 1 || p.H < 3 || p.W < 1 || p.first_block != blocks) return 1;
+        blocks += gs4d_reg_blocks(p.C, p.H, p.W);
+    }
+    *nblk = blocks;
+    return 0;
+}
+
+size_t gs4d_reg_scratch_bytes(const gs4d_reg_batch *batch) {
+    int64_t nblk = 0;
+    if (reg_check(batch, &nblk)) return 0;
+    return 8 * (size_t)nblk + 256;
+}
+
+int gs4d_hexplane_reg_forward(const gs4d_reg_batch *batch, float *loss, void *scratch, void *stream) {
+    int64_t nblk = 0;
+    if (reg_check(batch, &nblk) || !loss || !scratch) return 1;
+    double *part = (double *)align_up((size_t)scratch, 8);
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(reg_forward_kernel, dim3((unsigned)nblk), dim3(kTailThreads), 0, s, *batch, part);
+    hipLaunchKernelGGL(reg_final_kernel, dim3(1), dim3(kTailThreads), 0, s, (int)nblk, part, loss);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+int gs4d_hexplane_reg_backward(const gs4d_reg_batch *batch, const float *dloss, void *stream) {
+    int64_t nblk = 0;
+    if (reg_check(batch, &nblk) || !dloss) return 1;
+    for (int i = 0; i < batch->count; i++)
+        if (!batch->p[i].grad) return 1;
+    hipLaunchKernelGGL(reg_backward_kernel, dim3((unsigned)nblk), dim3(kTailThreads), 0, (hipStream_t)stream, *batch,
+                       dloss);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
 
 size_t gs4d_l1_scratch_bytes(int64_t n) { return 8 * (size_t)((n + kL1Chunk - 1) / kL1Chunk) + 256; }
 

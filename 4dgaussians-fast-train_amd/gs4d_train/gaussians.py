@@ -6,9 +6,9 @@ groups and learning-rate schedules (:165-212), the densification statistics (:52
 clone / split / prune tensor surgery on the optimizer state (:316-505), opacity reset (:269-272),
 the HexPlane regularisers (:538-566) and the PLY layout (:214-226, 250-314; see gs4d_train/ply.py).
 
-Two places run libgs4d HIP kernels when `fused=True` (the default on a GPU): the optimizer step
-(one multi-tensor Adam launch, kernels.FusedAdam) and the densification statistics
-(kernels.densify_stats).  `fused=False` keeps the reference's torch formulation, which the parity
+Three places run libgs4d HIP kernels when `fused=True` (the default on a GPU): the optimizer step
+(one multi-tensor Adam launch, kernels.FusedAdam), the densification statistics
+(kernels.densify_stats) and the HexPlane regularisers (kernels.hexplane_regulation).  `fused=False` keeps the reference's torch formulation, which the parity
 tests compare against.
 """
 import math
@@ -335,6 +335,10 @@ class GaussianModel:
     # ---- HexPlane regularisers (gaussian_model.py:538-566)
     def compute_regulation(self, time_smoothness_weight, l1_time_planes_weight, plane_tv_weight):
         grids = self._deformation.deformation_net.grid.grids
+        if self.fused:
+            from .kernels import hexplane_regulation
+            return hexplane_regulation([list(g) for g in grids], time_smoothness_weight, l1_time_planes_weight,
+                                       plane_tv_weight)
         plane = sum(compute_plane_smoothness(g[i]) for g in grids for i in ([] if len(g) == 3 else [0, 1, 3]))
         time = sum(compute_plane_smoothness(g[i]) for g in grids for i in ([] if len(g) == 3 else [2, 4, 5]))
         l1 = sum(torch.abs(1 - g[i]).mean() for g in grids if len(g) != 3 for i in [2, 4, 5])

@@ -10,7 +10,7 @@ import torch
 
 from . import _C
 
-__all__ = ["l1_loss", "densify_stats", "FusedAdam", "hexplane"]
+__all__ = ["l1_loss", "densify_stats", "FusedAdam", "hexplane", "hexplane_regulation"]
 
 
 class _L1Loss(torch.autograd.Function):
@@ -112,3 +112,37 @@ def hexplane(pts, ms_grids):
     """pts (N, 4) normalised (x, y, z, t); ms_grids: per level the 6 (1, F, H, W) planes."""
     planes = [p for level in ms_grids for p in level]
     return _HexPlane.apply(pts.contiguous(), *planes)
+
+
+class _HexPlaneReg(torch.autograd.Function):
+    """scene/gaussian_model.py:538-577 compute_regulation over the planes in one launch each way."""
+
+    @staticmethod
+    def forward(ctx, w_smooth, w_l1, *planes):
+        ctx.w = (w_smooth, w_l1)
+        ctx.save_for_backward(*planes)
+        return _C.hexplane_reg_forward(list(planes), w_smooth, w_l1)
+
+    @staticmethod
+    def backward(ctx, dloss):
+        planes = ctx.saved_tensors
+        grads = _C.hexplane_reg_backward(list(planes), ctx.w[0], ctx.w[1], dloss.reshape(1))
+        return (None, None, *grads)
+
+
+def hexplane_regulation(ms_grids, time_smoothness_weight, l1_time_planes_weight, plane_tv_weight):
+    """plane_tv_weight * sum smoothness(spatial planes 0, 1, 3) + time_smoothness_weight * sum
+    smoothness(time planes 2, 4, 5) + l1_time_planes_weight * sum mean|1 - time plane| over the levels
+    (levels with 3 planes contribute nothing, as in the reference)."""
+    planes, ws, wl = [], [], []
+    for g in ms_grids:
+        if len(g) == 3:
+            continue
+        for i in range(6):
+            planes.append(g[i].contiguous())
+            time = i in (2, 4, 5)
+            ws.append(float(time_smoothness_weight if time else plane_tv_weight))
+            wl.append(float(l1_time_planes_weight if time else 0.0))
+    if not planes:
+        return torch.zeros((), device=ms_grids[0][0].device)
+    return _HexPlaneReg.apply(ws, wl, *planes)

@@ -85,6 +85,33 @@ int gs4d_hexplane_forward(int N, const float *pts, const gs4d_hexplane_layout *l
 int gs4d_hexplane_backward(int N, const float *pts, const gs4d_hexplane_layout *lay, const float *packed,
                            const float *dfeat, float *dpacked, float *dpts, void *stream);
 
+/* ---- HexPlane regularisers: scene/gaussian_model.py:538-577 (compute_regulation = plane_tv_weight *
+ * _plane_regulation + time_smoothness_weight * _time_regulation + l1_time_planes * _l1_regulation) with
+ * scene/regulation.py:22-28 compute_plane_smoothness.  For every plane t (1, C, H, W) of the batch:
+ *   w_smooth * mean over (C, H-2, W) of ((t[y+2] - t[y+1]) - (t[y+1] - t[y]))^2  +  w_l1 * mean |1 - t|
+ * (w_smooth: plane_tv_weight for the spatial planes, time_smoothness_weight for the time planes; w_l1:
+ * l1_time_planes for the time planes, 0 otherwise).  H >= 3.  forward: *loss = the sum over the
+ * batch (fp64 partials summed in a fixed order; scratch of gs4d_reg_scratch_bytes).  backward: grad
+ * (1, C, H, W) of each plane = dloss * d(loss)/d(t), the gradient autograd derives from the
+ * reference's graph (assigned, not accumulated).  first_block of plane i = the sum of
+ * gs4d_reg_blocks over planes 0..i-1. */
+#define GS4D_REG_MAX_PLANES 24
+typedef struct {
+    const float *data;
+    float *grad;
+    int C, H, W;
+    float w_smooth, w_l1;
+    int64_t first_block;
+} gs4d_reg_plane;
+typedef struct {
+    int count;
+    gs4d_reg_plane p[GS4D_REG_MAX_PLANES];
+} gs4d_reg_batch;
+int64_t gs4d_reg_blocks(int C, int H, int W);
+size_t gs4d_reg_scratch_bytes(const gs4d_reg_batch *batch);
+int gs4d_hexplane_reg_forward(const gs4d_reg_batch *batch, float *loss, void *scratch, void *stream);
+int gs4d_hexplane_reg_backward(const gs4d_reg_batch *batch, const float *dloss, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -110,6 +110,43 @@ def test_hexplane_fused_matches_grid_sample(F):
         torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-5 * max(a.abs().max().item(), 1e-6))
 
 
+def test_hexplane_regulation_fused_matches_torch():
+    """kernels.hexplane_regulation vs the reference's compute_regulation graph (scene/regulation.py:22-28,
+    scene/gaussian_model.py:538-577): loss to 1e-5 relative (fp64 partials vs torch's fp32 means),
+    every plane gradient to 1e-5 of its tensor's maximum; levels of DyNeRF's shape, random values
+    (time planes around their init of 1, with exact ones for the |1 - t| subgradient)."""
+    from types import SimpleNamespace
+
+    from gs4d_train.gaussians import GaussianModel
+    from gs4d_train.kernels import hexplane_regulation
+    torch.manual_seed(3)
+    F = 16
+    grids_t, grids_f = [], []
+    for reso in ([64, 64, 64, 150], [128, 128, 128, 150]):
+        pairs = [(0, 1), (0, 2), (0, 3), (1, 2), (1, 3), (2, 3)]
+        lvl = []
+        for c0, c1 in pairs:
+            t = torch.rand(1, F, reso[c1], reso[c0], device="cuda")
+            if c1 == 3:
+                t = 1.0 + 0.05 * (t - 0.5)
+                t.view(-1)[:100] = 1.0
+            lvl.append(t)
+        grids_t.append([t.clone().requires_grad_(True) for t in lvl])
+        grids_f.append([t.clone().requires_grad_(True) for t in lvl])
+    w = (1.0, 1e-4, 2e-4)  # time_smoothness_weight, l1_time_planes, plane_tv_weight (dynerf default)
+    g = GaussianModel.__new__(GaussianModel)
+    g.fused = False
+    g._deformation = SimpleNamespace(deformation_net=SimpleNamespace(grid=SimpleNamespace(grids=grids_t)))
+    lt = g.compute_regulation(*w)
+    lf = hexplane_regulation(grids_f, *w)
+    (2.5 * lt).backward()
+    (2.5 * lf).backward()
+    assert abs(lf.item() - lt.item()) <= 1e-5 * abs(lt.item())
+    for a, b in zip([p for l in grids_f for p in l], [p for l in grids_t for p in l]):
+        scale = max(float(b.grad.abs().max()), 1e-30)
+        assert float((a.grad - b.grad).abs().max()) <= 1e-5 * scale
+
+
 def test_train_step_fused_matches_torch_tail():
     """One fine-stage step through deformation + rasterizer + loss + densification statistics, fused
     (HexPlane kernel, L1 kernel, stats kernel) vs the reference's torch formulation.  The optimizer is

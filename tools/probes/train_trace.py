@@ -40,5 +40,33 @@ def main(cfg="metric", steps=20, fused=True):
     print(f"train_step {cfg} fused={fused}: {el:.3f} ms/step")
 
 
+def op_profile(cfg="metric", steps=5):
+    """torch.profiler op table (device time) of a few train steps."""
+    from torch.profiler import ProfilerActivity, profile
+    P, W, H = CONFIGS[cfg]
+    dev = torch.device("cuda:0")
+    hyper, opt = config.dynerf()
+    torch.manual_seed(0)
+    g = GaussianModel(3, hyper, fused=True)
+    pts, cols = make_point_cloud(P, seed=0)
+    g.create_from_pcd(pts, cols, spatial_lr_scale=1.0, device=dev)
+    g._deformation.deformation_net.grid.fused = True
+    g.training_setup(opt)
+    g.active_sh_degree = 3
+    views = make_training_views(1, W, H, seed=1, device=dev)
+    bg = torch.ones(3, device=dev)
+    for i in range(5):
+        train_step(g, views, opt, hyper, 3001 + i, bg)
+    torch.cuda.synchronize()
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+        for i in range(steps):
+            train_step(g, views, opt, hyper, 3006 + i, bg)
+        torch.cuda.synchronize()
+    print(prof.key_averages().table(sort_by="cuda_time_total", row_limit=45, max_name_column_width=60))
+
+
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "metric")
+    if "--ops" in sys.argv:
+        op_profile()
+    else:
+        main(sys.argv[1] if len(sys.argv) > 1 else "metric")
