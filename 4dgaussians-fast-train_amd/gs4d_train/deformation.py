@@ -147,6 +147,66 @@ class Linear(nn.Linear):
         return F.linear(x, self.weight, self.bias)
 
 
+def _splitk_dw(dy, x):
+    """dW = dy^T x reduced over the P rows as a split-K batched GEMM (see _LinearSplitK); x may be a
+    column slice of a wider row-major tensor (its rows are then strided)."""
+    P, c = x.shape[0], _LinearSplitK.kChunk
+    S = P // c
+    if S < 2:
+        return dy.t() @ x
+    xs = x[:S * c].unflatten(0, (S, c))
+    dw = torch.bmm(dy[:S * c].unflatten(0, (S, c)).transpose(1, 2), xs).sum(0)
+    if P > S * c:
+        dw = dw + dy[S * c:].t() @ x[S * c:]
+    return dw
+
+
+class _DeformHeads(torch.autograd.Function):
+    """The deformation heads (scene/deformation.py:73-78, each nn.Sequential(ReLU, Linear(W, W), ReLU,
+    Linear(W, n)) applied to the same hidden features) evaluated together: one ReLU of the shared
+    input, ONE (P x W) @ (W x kW) GEMM for the k first layers (weights concatenated), one ReLU, then
+    the k small second layers on column slices.  The backward mirrors it: the k (P x n) @ (n x W)
+    products land in column slices of one (P x kW) gradient, then one ReLU mask, one GEMM with K = kW
+    for the input gradient and one split-K GEMM for the concatenated first-layer weight gradient.
+    Same function as the k separate heads (and the same parameters, concatenated per call); the
+    GEMMs sum in a different order, so results agree to fp32 rounding."""
+
+    @staticmethod
+    def forward(ctx, hidden, w1, b1, *second):
+        k = len(second) // 2
+        W = hidden.shape[1]
+        h = torch.relu(hidden)
+        a = torch.addmm(b1, h, w1.t())
+        a.relu_()
+        outs = [torch.addmm(second[2 * i + 1], a[:, i * W:(i + 1) * W], second[2 * i].t()) for i in range(k)]
+        ctx.save_for_backward(h, a, w1, *second[0::2])
+        ctx.W = W
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *douts):
+        h, a, w1, *w2 = ctx.saved_tensors
+        W, k = ctx.W, len(w2)
+        da = torch.empty_like(a)
+        dw2, db2 = [], []
+        for i in range(k):
+            do = douts[i] if douts[i] is not None else torch.zeros(a.shape[0], w2[i].shape[0], device=a.device)
+            do = do.contiguous()
+            sl = a[:, i * W:(i + 1) * W]
+            torch.mm(do, w2[i], out=da[:, i * W:(i + 1) * W])
+            dw2.append(_splitk_dw(do, sl))
+            db2.append(do.sum(0))
+        da.masked_fill_(a <= 0, 0.0)               # ReLU backward (a = relu(z): a > 0 <=> z > 0)
+        dw1 = _splitk_dw(da, h)
+        db1 = da.sum(0)
+        dh = da @ w1
+        dh.masked_fill_(h <= 0, 0.0)               # the heads' first ReLU
+        grads = [dh, dw1, db1]
+        for i in range(k):
+            grads += [dw2[i], db2[i]]
+        return tuple(grads)
+
+
 class Deformation(nn.Module):
     """scene/deformation.py:16-172 (no_grid=False, grid_pe=0, empty_voxel=False, static_mlp=False)."""
 
@@ -161,21 +221,35 @@ class Deformation(nn.Module):
         head = lambda n: nn.Sequential(nn.ReLU(), Linear(W, W), nn.ReLU(), Linear(W, n))
         self.pos_deform, self.scales_deform, self.rotations_deform = head(3), head(3), head(4)
         self.opacity_deform, self.shs_deform = head(1), head(16 * 3)
+        self.fused_heads = False  # True: the heads as one _DeformHeads block (GPU training)
 
     def forward(self, xyz, scales, rotations, opacity, shs, time):
         """forward_dynamic (scene/deformation.py:97-146); mask = 1 (no static_mlp / empty_voxel)."""
-        hidden = self.feature_out(self.grid(xyz[:, :3], time[:, :1]))
         a = self.args
-        pts = xyz[:, :3] if a.no_dx else xyz[:, :3] + self.pos_deform(hidden)
-        sc = scales[:, :3] if a.no_ds else scales[:, :3] + self.scales_deform(hidden)
-        if a.no_dr:
-            rot = rotations[:, :4]
-        elif a.apply_rotation:
+        if a.apply_rotation and not a.no_dr:
             raise NotImplementedError("apply_rotation (documented as unused in arguments/__init__.py:104)")
+        # the inputs' leading columns (xyz[:, :3], ...) are the whole tensors here: no slicing, so
+        # autograd records no slice nodes
+        xyz, scales, rotations, opacity = (t if t.shape[1] == n else t[:, :n] for t, n in
+                                           ((xyz, 3), (scales, 3), (rotations, 4), (opacity, 1)))
+        time = time if time.shape[1] == 1 else time[:, :1]
+        hidden = self.feature_out(self.grid(xyz, time))
+        active = [(name, flag) for name, flag in (("pos_deform", a.no_dx), ("scales_deform", a.no_ds),
+                                                  ("rotations_deform", a.no_dr), ("opacity_deform", a.no_do),
+                                                  ("shs_deform", a.no_dshs)) if not flag]
+        if self.fused_heads and hidden.is_cuda and torch.is_grad_enabled() and active:
+            heads = [getattr(self, name) for name, _ in active]
+            w1 = torch.cat([hd[1].weight for hd in heads], 0)
+            b1 = torch.cat([hd[1].bias for hd in heads], 0)
+            second = [t for hd in heads for t in (hd[3].weight, hd[3].bias)]
+            outs = dict(zip([name for name, _ in active], _DeformHeads.apply(hidden, w1, b1, *second)))
         else:
-            rot = rotations[:, :4] + self.rotations_deform(hidden)
-        op = opacity[:, :1] if a.no_do else opacity[:, :1] + self.opacity_deform(hidden)
-        sh = shs if a.no_dshs else shs + self.shs_deform(hidden).reshape([shs.shape[0], 16, 3])
+            outs = {name: getattr(self, name)(hidden) for name, _ in active}
+        pts = xyz if a.no_dx else xyz + outs["pos_deform"]
+        sc = scales if a.no_ds else scales + outs["scales_deform"]
+        rot = rotations if a.no_dr else rotations + outs["rotations_deform"]
+        op = opacity if a.no_do else opacity + outs["opacity_deform"]
+        sh = shs if a.no_dshs else shs + outs["shs_deform"].reshape([shs.shape[0], 16, 3])
         return pts, sc, rot, op, sh
 
     def get_mlp_parameters(self):

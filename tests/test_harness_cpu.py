@@ -196,3 +196,29 @@ def test_regularisers_run_and_are_zero_at_init():
     assert float(g.compute_regulation(0.0, 1.0, 0.0)) == 0.0
     assert float(g.compute_regulation(1.0, 0.0, 0.0)) == 0.0
     assert float(g.compute_regulation(0.0, 0.0, 1.0)) > 0.0
+
+
+def test_deform_heads_block_matches_separate_heads():
+    """gs4d_train.deformation._DeformHeads (the 5 heads as one block: concatenated first layers, column
+    slices for the second) against the reference's separate nn.Sequential heads
+    (scene/deformation.py:73-78), float64 on CPU: outputs and every gradient to 1e-10."""
+    import torch
+    from gs4d_train.deformation import _DeformHeads
+    torch.manual_seed(0)
+    P, W, ns = 2500, 16, [3, 3, 4, 1, 48]   # P > 2 * 1024: exercises the split-K weight gradients
+    hid = torch.randn(P, W, dtype=torch.float64, requires_grad=True)
+    w1 = [torch.randn(W, W, dtype=torch.float64, requires_grad=True) for _ in ns]
+    b1 = [torch.randn(W, dtype=torch.float64, requires_grad=True) for _ in ns]
+    w2 = [torch.randn(n, W, dtype=torch.float64, requires_grad=True) for n in ns]
+    b2 = [torch.randn(n, dtype=torch.float64, requires_grad=True) for n in ns]
+    ups = [torch.randn(P, n, dtype=torch.float64) for n in ns]
+    leaves = [hid] + w1 + b1 + w2 + b2
+    outs = _DeformHeads.apply(hid, torch.cat(w1), torch.cat(b1), *[t for i in range(5) for t in (w2[i], b2[i])])
+    ga = torch.autograd.grad(sum((o * u).sum() for o, u in zip(outs, ups)), leaves)
+    F = torch.nn.functional
+    ref = [F.linear(torch.relu(F.linear(torch.relu(hid), w1[i], b1[i])), w2[i], b2[i]) for i in range(5)]
+    gb = torch.autograd.grad(sum((o * u).sum() for o, u in zip(ref, ups)), leaves)
+    for a, b in zip(outs, ref):
+        torch.testing.assert_close(a, b, rtol=1e-10, atol=1e-10)
+    for a, b in zip(ga, gb):
+        torch.testing.assert_close(a, b, rtol=1e-10, atol=1e-10)

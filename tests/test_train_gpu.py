@@ -167,6 +167,7 @@ def test_train_step_fused_matches_torch_tail():
         g = GaussianModel(3, hyper, fused=fused)
         g.create_from_pcd(pts, cols, 1.0)
         g._deformation.deformation_net.grid.fused = fused
+        g._deformation.deformation_net.fused_heads = fused
         g.training_setup(opt)
         g.active_sh_degree = 3
         loss = float(train_step(g, views, opt, hyper, 3001, bg))

@@ -23,6 +23,7 @@ def main(cfg="metric", steps=20, fused=True):
     pts, cols = make_point_cloud(P, seed=0)
     g.create_from_pcd(pts, cols, spatial_lr_scale=1.0, device=dev)
     g._deformation.deformation_net.grid.fused = fused
+    g._deformation.deformation_net.fused_heads = fused
     g.training_setup(opt)
     g.active_sh_degree = 3
     views = make_training_views(1, W, H, seed=1, device=dev)
@@ -51,6 +52,7 @@ def op_profile(cfg="metric", steps=5):
     pts, cols = make_point_cloud(P, seed=0)
     g.create_from_pcd(pts, cols, spatial_lr_scale=1.0, device=dev)
     g._deformation.deformation_net.grid.fused = True
+    g._deformation.deformation_net.fused_heads = True
     g.training_setup(opt)
     g.active_sh_degree = 3
     views = make_training_views(1, W, H, seed=1, device=dev)
