@@ -17,12 +17,19 @@
 //   - a point is served by F/4 consecutive lanes; plane values stay in registers, so the backward
 //     recomputes them instead of storing the 6 x levels intermediate tensors the reference keeps;
 //   - coordinate gradients are reduced over the point's lanes with shuffles (no atomics);
-//   - grid gradients are hardware float atomics (no-return) into the channels-last buffer, repacked to
-//     the (1, F, H, W) parameter layout by one launch.
+//   - points are visited in a 3-D Morton order (gs4d_hexplane_order: 24-bit codes of the normalised
+//     coordinates, the library's onesweep sort), so the ~128 points of a backward workgroup cover a
+//     small box of the field and each plane sees only a small window of cells;
+//   - grid gradients are summed in LDS over those windows (one window per plane and level, bounding
+//     box of the workgroup's taps) and added to HBM once per workgroup with hardware float atomics
+//     (no-return); a window that does not fit the LDS budget falls back to direct atomics.  The
+//     channels-last gradient buffer is repacked to the (1, F, H, W) parameter layout by one launch.
 #include <algorithm>
+#include <climits>
 
 #include "../../include/gs4d_train.h"
 #include "gs4d_internal.h"
+#include "radix_sort.h"
 
 namespace gs4d {
 
@@ -101,13 +108,15 @@ __device__ __forceinline__ float interp(const TapVals &r, const Tap &t, int k) {
 }
 
 __global__ __launch_bounds__(kHexThreads) void hexplane_forward_kernel(int N, const float *__restrict__ pts,
+                                                                       const uint32_t *__restrict__ order,
                                                                        gs4d_hexplane_layout lay,
                                                                        const float *__restrict__ packed,
                                                                        float *__restrict__ feat) {
     const int G = lay.F / 4;
     const int64_t tid = (int64_t)blockIdx.x * kHexThreads + threadIdx.x;
-    const int n = (int)(tid / G), q = (int)(tid % G);
-    if (n >= N) return;
+    const int i = (int)(tid / G), q = (int)(tid % G);
+    if (i >= N) return;
+    const int n = order ? (int)order[i] : i;
     const float4 p4 = reinterpret_cast<const float4 *>(pts)[n];
     const float pc[4] = {p4.x, p4.y, p4.z, p4.w};
     for (int l = 0; l < lay.levels; l++) {
@@ -124,56 +133,90 @@ __global__ __launch_bounds__(kHexThreads) void hexplane_forward_kernel(int N, co
     }
 }
 
-// Time planes: within one render call every point has the same t, so all points touch the same two
-// rows of the three (c, t) planes of a level.  Their gradients are first summed in LDS per workgroup
-// (a workgroup serves several point chunks) and added to HBM once per workgroup; the spatial planes
-// (spread over the whole plane) take direct atomics.  Workgroups whose points do not share the time
-// row (or levels whose rows do not fit kHexLdsFloats) use direct atomics throughout.
-constexpr int kHexLdsFloats = 16384;  // 64 KiB
-__device__ __forceinline__ bool is_time_plane(int p) { return kPairC1[p] == 3; }
-__device__ __forceinline__ int time_slot(int p) { return p == 2 ? 0 : (p == 4 ? 1 : 2); }
+// Backward.  A workgroup serves kHexPointsPerWG consecutive points of the Morton order.  Per level it
+// first takes, for each of the 6 planes, the bounding box of the cells its points' bilinear taps
+// touch, lays the boxes out in LDS (kHexLdsFloats budget, planes in order; a box that does not fit
+// keeps direct atomics), accumulates the plane gradients there with LDS atomics, then adds each box
+// to the packed gradient buffer with one no-return float atomic per non-zero element.  Time planes
+// get tiny boxes: within one render call every point has the same t, so their taps span two rows.
+constexpr int kHexPointsPerWG = 128;
+constexpr int kHexLdsFloats = 12288;  // 48 KiB: three workgroups per CU
 
 __global__ __launch_bounds__(kHexThreads) void hexplane_backward_kernel(int N, const float *__restrict__ pts,
+                                                                        const uint32_t *__restrict__ order,
                                                                         gs4d_hexplane_layout lay,
                                                                         const float *__restrict__ packed,
                                                                         const float *__restrict__ dfeat,
                                                                         float *__restrict__ dpacked,
-                                                                        float *__restrict__ dpts, int chunks_per_wg) {
-    extern __shared__ float s_rows[];  // [3 time planes][2 rows][W][F] of the current level
-    __shared__ int s_y0, s_uniform;
-    const int G = lay.F / 4, ppc = kHexThreads / G;  // lanes per point, points per chunk
+                                                                        float *__restrict__ dpts) {
+    __shared__ float s_win[kHexLdsFloats];
+    __shared__ int s_box[6][4];  // x0, x1, y0, y1 (inclusive) of the plane's touched cells
+    __shared__ int s_off[6];     // LDS offset of the plane's box, -1: direct atomics
+    __shared__ int s_used;
+    const int F = lay.F, G = F / 4, ppc = kHexThreads / G;  // lanes per point, points per chunk
+    const int cpw = max(1, kHexPointsPerWG / ppc);
     const int q = threadIdx.x % G, slot = threadIdx.x / G;
-    const int64_t first = (int64_t)blockIdx.x * chunks_per_wg * ppc;
+    const int64_t first = (int64_t)blockIdx.x * cpw * ppc;
+    auto point_of = [&](int c) -> int {
+        const int64_t i = first + (int64_t)c * ppc + slot;
+        return i < N ? (order ? (int)order[i] : (int)i) : -1;
+    };
     for (int l = 0; l < lay.levels; l++) {
-        const gs4d_hexplane_plane *tp[3] = {&lay.plane[6 * l + 2], &lay.plane[6 * l + 4], &lay.plane[6 * l + 5]};
-        int roff[3], nrows = 0;
-        for (int i = 0; i < 3; i++) {
-            roff[i] = nrows;
-            nrows += 2 * tp[i]->W * lay.F;
+        // 1. the planes' touched-cell boxes
+        if (threadIdx.x < 6) {
+            s_box[threadIdx.x][0] = INT_MAX; s_box[threadIdx.x][1] = INT_MIN;
+            s_box[threadIdx.x][2] = INT_MAX; s_box[threadIdx.x][3] = INT_MIN;
         }
-        const int Ht = tp[0]->H;
-        bool use_lds = nrows <= kHexLdsFloats;
-        if (use_lds) {
-            // does every point of this workgroup share the time row?
-            if (threadIdx.x == 0) {
-                s_uniform = 1;
-                float gm;
-                s_y0 = first < N ? (int)floorf(unnorm_clip(pts[4 * first + 3], Ht, gm)) : 0;
+        __syncthreads();
+        if (q == 0) {
+            int bx[6][4];
+#pragma unroll
+            for (int p = 0; p < 6; p++) { bx[p][0] = INT_MAX; bx[p][1] = INT_MIN; bx[p][2] = INT_MAX; bx[p][3] = INT_MIN; }
+            for (int c = 0; c < cpw; c++) {
+                const int n = point_of(c);
+                if (n < 0) break;
+                const float4 p4 = reinterpret_cast<const float4 *>(pts)[n];
+                const float pc[4] = {p4.x, p4.y, p4.z, p4.w};
+#pragma unroll
+                for (int p = 0; p < 6; p++) {
+                    const gs4d_hexplane_plane pl = lay.plane[6 * l + p];
+                    const Tap t = make_tap(pc[kPairC0[p]], pc[kPairC1[p]], pl.W, pl.H);
+                    // taps x0, x0 + 1 (y likewise) clipped to the plane: the cells make_tap keeps
+                    bx[p][0] = min(bx[p][0], max(t.x0, 0));
+                    bx[p][1] = max(bx[p][1], min(t.x0 + 1, pl.W - 1));
+                    bx[p][2] = min(bx[p][2], max(t.y0, 0));
+                    bx[p][3] = max(bx[p][3], min(t.y0 + 1, pl.H - 1));
+                }
             }
-            __syncthreads();
-            for (int c = 0; c < chunks_per_wg; c++) {
-                const int64_t n = first + (int64_t)c * ppc + slot;
-                float gm;
-                if (q == 0 && n < N && (int)floorf(unnorm_clip(pts[4 * n + 3], Ht, gm)) != s_y0) s_uniform = 0;
+#pragma unroll
+            for (int p = 0; p < 6; p++) {
+                atomicMin(&s_box[p][0], bx[p][0]); atomicMax(&s_box[p][1], bx[p][1]);
+                atomicMin(&s_box[p][2], bx[p][2]); atomicMax(&s_box[p][3], bx[p][3]);
             }
-            for (int i = threadIdx.x; i < nrows; i += kHexThreads) s_rows[i] = 0.f;
-            __syncthreads();
-            use_lds = s_uniform != 0;
         }
-        const int y0w = s_y0;
-        for (int c = 0; c < chunks_per_wg; c++) {
-            const int64_t n = first + (int64_t)c * ppc + slot;
-            if (n >= N) break;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int used = 0;
+            for (int p = 0; p < 6; p++) {
+                const int w = s_box[p][1] - s_box[p][0] + 1, h = s_box[p][3] - s_box[p][2] + 1;
+                const int need = (w > 0 && h > 0) ? w * h * F : 0;
+                if (need > 0 && used + need <= kHexLdsFloats) {
+                    s_off[p] = used;
+                    used += need;
+                } else {
+                    s_off[p] = -1;
+                }
+            }
+            s_used = used;
+        }
+        __syncthreads();
+        const int used = s_used;
+        for (int e = threadIdx.x; e < used; e += kHexThreads) s_win[e] = 0.f;
+        __syncthreads();
+        // 2. gradients
+        for (int c = 0; c < cpw; c++) {
+            const int n = point_of(c);
+            if (n < 0) break;
             const float4 p4 = reinterpret_cast<const float4 *>(pts)[n];
             const float pc[4] = {p4.x, p4.y, p4.z, p4.w};
             float gpt[4] = {0.f, 0.f, 0.f, 0.f};
@@ -181,14 +224,14 @@ __global__ __launch_bounds__(kHexThreads) void hexplane_backward_kernel(int N, c
             for (int p = 0; p < 6; p++) {
                 const gs4d_hexplane_plane pl = lay.plane[6 * l + p];
                 const Tap t = make_tap(pc[kPairC0[p]], pc[kPairC1[p]], pl.W, pl.H);
-                const TapVals r = load_taps(packed + pl.offset, t, lay.F, q);
+                const TapVals r = load_taps(packed + pl.offset, t, F, q);
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
                     v[p][k] = interp(r, t, k);
                     pre[p][k] = (p == 0 ? 1.f : pre[p - 1][k]) * v[p][k];  // left-to-right product
                 }
             }
-            const float4 d4 = *reinterpret_cast<const float4 *>(dfeat + (size_t)n * lay.levels * lay.F + l * lay.F + 4 * q);
+            const float4 d4 = *reinterpret_cast<const float4 *>(dfeat + (size_t)n * lay.levels * F + l * F + 4 * q);
             float g[4] = {d4.x, d4.y, d4.z, d4.w};
             for (int p = 5; p >= 0; p--) {
                 // autograd of prod_p = prod_{p-1} * v_p: dv_p = g * prod_{p-1}, g <- g * v_p
@@ -200,7 +243,7 @@ __global__ __launch_bounds__(kHexThreads) void hexplane_backward_kernel(int N, c
                 }
                 const gs4d_hexplane_plane pl = lay.plane[6 * l + p];
                 const Tap t = make_tap(pc[kPairC0[p]], pc[kPairC1[p]], pl.W, pl.H);
-                const TapVals r = load_taps(packed + pl.offset, t, lay.F, q);
+                const TapVals r = load_taps(packed + pl.offset, t, F, q);
                 float gix = 0.f, giy = 0.f;
                 const float x1 = (float)(t.x0 + 1), y1 = (float)(t.y0 + 1), x0 = (float)t.x0, y0 = (float)t.y0;
 #pragma unroll
@@ -218,14 +261,14 @@ __global__ __launch_bounds__(kHexThreads) void hexplane_backward_kernel(int N, c
                 }
                 const int cells[4] = {t.i00, t.i10, t.i01, t.i11};
                 const float ws[4] = {t.w00, t.w10, t.w01, t.w11};
-                if (use_lds && is_time_plane(p)) {
-                    // rows y0w, y0w + 1 of the plane -> LDS rows 0, 1
-                    float *dst0 = s_rows + roff[time_slot(p)] + 4 * q;
+                const int off = s_off[p];
+                if (off >= 0) {
+                    const int bx0 = s_box[p][0], by0 = s_box[p][2], bw = s_box[p][1] - bx0 + 1;
 #pragma unroll
                     for (int cc = 0; cc < 4; cc++) {
                         if (cells[cc] < 0) continue;
-                        const int row = cells[cc] / pl.W - y0w, x = cells[cc] % pl.W;
-                        float *dst = dst0 + (row * pl.W + x) * lay.F;
+                        const int cy = cells[cc] / pl.W, cx = cells[cc] - cy * pl.W;
+                        float *dst = s_win + off + ((cy - by0) * bw + (cx - bx0)) * F + 4 * q;
 #pragma unroll
                         for (int k = 0; k < 4; k++) atomicAdd(dst + k, ws[cc] * dv[k]);
                     }
@@ -234,7 +277,7 @@ __global__ __launch_bounds__(kHexThreads) void hexplane_backward_kernel(int N, c
 #pragma unroll
                     for (int cc = 0; cc < 4; cc++) {
                         if (cells[cc] < 0) continue;
-                        float *dst = dpl + (size_t)cells[cc] * lay.F;
+                        float *dst = dpl + (size_t)cells[cc] * F;
 #pragma unroll
                         for (int k = 0; k < 4; k++) unsafeAtomicAdd(dst + k, ws[cc] * dv[k]);
                     }
@@ -253,19 +296,61 @@ __global__ __launch_bounds__(kHexThreads) void hexplane_backward_kernel(int N, c
                 *o = acc;
             }
         }
-        if (use_lds) {
-            __syncthreads();
-            for (int i = 0; i < 3; i++) {
-                const int W = tp[i]->W, cnt = 2 * W * lay.F;
-                for (int e = threadIdx.x; e < cnt; e += kHexThreads) {
-                    const float val = s_rows[roff[i] + e];
-                    const int row = y0w + e / (W * lay.F);
-                    if (val != 0.f && row < Ht) unsafeAtomicAdd(dpacked + tp[i]->offset + (size_t)row * W * lay.F + e % (W * lay.F), val);
-                }
+        __syncthreads();
+        // 3. the boxes to HBM (rows of the box are contiguous cells x F floats in the packed layout)
+        for (int p = 0; p < 6; p++) {
+            const int off = s_off[p];
+            if (off < 0) continue;
+            const gs4d_hexplane_plane pl = lay.plane[6 * l + p];
+            const int bx0 = s_box[p][0], by0 = s_box[p][2], bw = s_box[p][1] - bx0 + 1;
+            const int row = bw * F, cnt = row * (s_box[p][3] - by0 + 1);
+            for (int e = threadIdx.x; e < cnt; e += kHexThreads) {
+                const float val = s_win[off + e];
+                if (val == 0.f) continue;
+                const int ry = e / row, rx = e - ry * row;
+                unsafeAtomicAdd(dpacked + pl.offset + ((size_t)(by0 + ry) * pl.W + bx0) * F + rx, val);
             }
         }
         __syncthreads();
     }
+}
+
+// Morton order of the points (normalised x, y, z in [-1, 1], 8 bits per axis): 24-bit codes and the
+// sharded digit histograms of the onesweep sort (radix_sort.h).
+__device__ __forceinline__ uint32_t spread3(uint32_t x) {  // bit i -> bit 3i (x < 1024)
+    x = (x | (x << 16)) & 0x030000FF;
+    x = (x | (x << 8)) & 0x0300F00F;
+    x = (x | (x << 4)) & 0x030C30C3;
+    x = (x | (x << 2)) & 0x09249249;
+    return x;
+}
+__device__ __forceinline__ uint32_t quant8(float c) {
+    const float v = (c + 1.f) * 128.f;
+    return v >= 255.f ? 255u : (v > 0.f ? (uint32_t)v : 0u);  // NaN -> 0
+}
+__global__ __launch_bounds__(kHexThreads) void hex_morton_kernel(int N, const float4 *__restrict__ pts,
+                                                                 uint32_t *__restrict__ codes,
+                                                                 uint32_t *__restrict__ hist) {
+    __shared__ uint32_t s_hist[3][256];
+    for (int p = 0; p < 3; p++) s_hist[p][threadIdx.x] = 0;
+    __syncthreads();
+    const int i = blockIdx.x * kHexThreads + threadIdx.x;
+    if (i < N) {
+        const float4 p4 = pts[i];
+        const uint32_t code = spread3(quant8(p4.x)) | (spread3(quant8(p4.y)) << 1) | (spread3(quant8(p4.z)) << 2);
+        codes[i] = code;
+#pragma unroll
+        for (int p = 0; p < 3; p++) atomicAdd(&s_hist[p][(code >> (8 * p)) & 0xFFu], 1u);
+    }
+    __syncthreads();
+    uint32_t *h = hist + (blockIdx.x % kHistShards) * (kMaxPasses * 256);
+#pragma unroll
+    for (int p = 0; p < 3; p++)
+        if (s_hist[p][threadIdx.x]) atomicAdd(&h[p * 256 + threadIdx.x], s_hist[p][threadIdx.x]);
+}
+constexpr int kHexSortThreads = 1024, kHexSortItems = 4;
+static size_t hex_order_zero_words(int N) {
+    return 64 + (size_t)kHistWords + 4 * 256 * (size_t)sort_nblk(N, kHexSortThreads * kHexSortItems);
 }
 
 // (1, F, H, W) planes <-> the packed channels-last buffer.  One thread per packed element.
@@ -330,33 +415,58 @@ int gs4d_hexplane_unpack(const gs4d_hexplane_layout *lay, const float *packed, v
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
-int gs4d_hexplane_forward(int N, const float *pts, const gs4d_hexplane_layout *lay, const float *packed, float *feat,
-                          void *stream) {
+size_t gs4d_hexplane_order_scratch_bytes(int N) {
+    if (N <= 0) return 256;
+    return 4 * hex_order_zero_words(N) + 3 * align_up(4 * (size_t)N, 256) + 1024;
+}
+
+int gs4d_hexplane_order(int N, const float *pts, uint32_t *order, void *scratch, void *stream) {
+    if (N < 0 || (N > 0 && (!pts || !order || !scratch))) return 1;
+    if ((size_t)pts & 15) return 1;
+    if (N == 0) return 0;
+    hipStream_t s = (hipStream_t)stream;
+    char *q = (char *)align_up((size_t)scratch, 256);
+    auto take = [&](size_t bytes) {
+        char *r = q;
+        q += align_up(bytes, 256);
+        return r;
+    };
+    const size_t zw = hex_order_zero_words(N);
+    uint32_t *zero = (uint32_t *)take(4 * zw);
+    uint32_t *codes[2] = {(uint32_t *)take(4 * (size_t)N), (uint32_t *)take(4 * (size_t)N)};
+    uint32_t *spare = (uint32_t *)take(4 * (size_t)N);
+    // 3 passes: the sorted values end in vals[1]
+    uint32_t *vals[2] = {spare, order};
+    uint32_t *err = zero + 8, *hist = zero + 64, *look = zero + 64 + kHistWords;
+    if (hipMemsetAsync(zero, 0, 4 * zw, s) != hipSuccess) return 3;
+    hipLaunchKernelGGL(hex_morton_kernel, dim3((N + kHexThreads - 1) / kHexThreads), dim3(kHexThreads), 0, s, N,
+                       (const float4 *)pts, codes[0], hist);
+    const int cur = onesweep_sort<kHexSortThreads, kHexSortItems>(codes, vals, N, nullptr, 24, hist, look, err, s);
+    if (cur != 1) return 3;
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+int gs4d_hexplane_forward(int N, const float *pts, const uint32_t *order, const gs4d_hexplane_layout *lay,
+                          const float *packed, float *feat, void *stream) {
     if (N < 0 || !lay || (N > 0 && (!pts || !packed || !feat))) return 1;
     if (((size_t)pts & 15) || ((size_t)packed & 15) || ((size_t)feat & 15)) return 1;
     if (N == 0) return 0;
     const int64_t threads = (int64_t)N * (lay->F / 4);
     hipLaunchKernelGGL(hexplane_forward_kernel, dim3((unsigned)((threads + kHexThreads - 1) / kHexThreads)),
-                       dim3(kHexThreads), 0, (hipStream_t)stream, N, pts, *lay, packed, feat);
+                       dim3(kHexThreads), 0, (hipStream_t)stream, N, pts, order, *lay, packed, feat);
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
-int gs4d_hexplane_backward(int N, const float *pts, const gs4d_hexplane_layout *lay, const float *packed,
-                           const float *dfeat, float *dpacked, float *dpts, void *stream) {
+int gs4d_hexplane_backward(int N, const float *pts, const uint32_t *order, const gs4d_hexplane_layout *lay,
+                           const float *packed, const float *dfeat, float *dpacked, float *dpts, void *stream) {
     if (N < 0 || !lay || (N > 0 && (!pts || !packed || !dfeat || !dpacked || !dpts))) return 1;
     if (((size_t)pts & 15) || ((size_t)packed & 15) || ((size_t)dfeat & 15) || ((size_t)dpts & 15)) return 1;
     if (N == 0) return 0;
     const int ppc = kHexThreads / (lay->F / 4);
-    const int64_t chunks = ((int64_t)N + ppc - 1) / ppc;
-    const int cpw = (int)std::max<int64_t>(1, (chunks + 511) / 512);  // ~512 workgroups
-    const int nwg = (int)((chunks + cpw - 1) / cpw);
-    size_t lds = 0;
-    for (int l = 0; l < lay->levels; l++) {
-        const size_t f = 2 * (size_t)lay->F * (lay->plane[6 * l + 2].W + lay->plane[6 * l + 4].W + lay->plane[6 * l + 5].W);
-        if (f <= (size_t)kHexLdsFloats) lds = std::max(lds, f);
-    }
-    hipLaunchKernelGGL(hexplane_backward_kernel, dim3(nwg), dim3(kHexThreads), 4 * lds, (hipStream_t)stream, N, pts,
-                       *lay, packed, dfeat, dpacked, dpts, cpw);
+    const int64_t per_wg = (int64_t)std::max(1, kHexPointsPerWG / ppc) * ppc;
+    const int64_t nwg = ((int64_t)N + per_wg - 1) / per_wg;
+    hipLaunchKernelGGL(hexplane_backward_kernel, dim3((unsigned)nwg), dim3(kHexThreads), 0, (hipStream_t)stream, N, pts,
+                       order, *lay, packed, dfeat, dpacked, dpts);
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 

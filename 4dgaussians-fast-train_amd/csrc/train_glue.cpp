@@ -142,8 +142,9 @@ static gs4d_hexplane_layout hex_layout(const std::vector<torch::Tensor> &planes)
     return lay;
 }
 
-// returns (feat (N, levels*F), packed channels-last planes for the backward)
-std::tuple<torch::Tensor, torch::Tensor> hexplane_forward(const torch::Tensor &pts_, std::vector<torch::Tensor> planes) {
+// returns (feat (N, levels*F), packed channels-last planes and the point order for the backward)
+std::tuple<torch::Tensor, torch::Tensor, torch::Tensor> hexplane_forward(const torch::Tensor &pts_,
+                                                                         std::vector<torch::Tensor> planes) {
     need(pts_.dim() == 2 && pts_.size(1) == 4 && pts_.is_cuda(), "hexplane: pts must be (N, 4) on the GPU");
     c10::hip::HIPGuard guard(pts_.device().index());
     torch::Tensor pts = pts_.to(torch::kFloat32).contiguous();
@@ -151,18 +152,24 @@ std::tuple<torch::Tensor, torch::Tensor> hexplane_forward(const torch::Tensor &p
     const int N = (int)pts.size(0);
     torch::Tensor packed = torch::empty({lay.total}, pts.options());
     torch::Tensor feat = torch::empty({N, (int64_t)lay.levels * lay.F}, pts.options());
+    torch::Tensor order = torch::empty({N}, pts.options().dtype(torch::kInt32));
+    torch::Tensor scratch = torch::empty({(int64_t)gs4d_hexplane_order_scratch_bytes(N)}, pts.options().dtype(torch::kUInt8));
     hipStream_t s = stream_of(pts);
     check(gs4d_hexplane_pack(&lay, packed.data_ptr<float>(), (void *)s), "hexplane pack");
-    check(gs4d_hexplane_forward(N, pts.data_ptr<float>(), &lay, packed.data_ptr<float>(), feat.data_ptr<float>(), (void *)s),
+    check(gs4d_hexplane_order(N, pts.data_ptr<float>(), (uint32_t *)order.data_ptr<int>(), scratch.data_ptr(), (void *)s),
+          "hexplane order");
+    check(gs4d_hexplane_forward(N, pts.data_ptr<float>(), (const uint32_t *)order.data_ptr<int>(), &lay,
+                                packed.data_ptr<float>(), feat.data_ptr<float>(), (void *)s),
           "hexplane forward");
-    return {feat, packed};
+    return {feat, packed, order};
 }
 
 // returns (dpts (N, 4), plane gradients (1, F, H, W) each)
 std::tuple<torch::Tensor, std::vector<torch::Tensor>> hexplane_backward(const torch::Tensor &pts_,
                                                                          std::vector<torch::Tensor> planes,
                                                                          const torch::Tensor &packed,
-                                                                         const torch::Tensor &dfeat_) {
+                                                                         const torch::Tensor &dfeat_,
+                                                                         const torch::Tensor &order) {
     c10::hip::HIPGuard guard(pts_.device().index());
     torch::Tensor pts = pts_.to(torch::kFloat32).contiguous(), dfeat = dfeat_.to(torch::kFloat32).contiguous();
     gs4d_hexplane_layout lay = hex_layout(planes);
@@ -177,8 +184,10 @@ std::tuple<torch::Tensor, std::vector<torch::Tensor>> hexplane_backward(const to
         lay.plane[i].grad = grads.back().data_ptr<float>();
     }
     hipStream_t s = stream_of(pts);
-    check(gs4d_hexplane_backward(N, pts.data_ptr<float>(), &lay, packed.data_ptr<float>(), dfeat.data_ptr<float>(),
-                                 dpacked.data_ptr<float>(), dpts.data_ptr<float>(), (void *)s),
+    need(order.numel() == N && order.scalar_type() == torch::kInt32 && order.is_contiguous(), "hexplane backward: order");
+    check(gs4d_hexplane_backward(N, pts.data_ptr<float>(), (const uint32_t *)order.data_ptr<int>(), &lay,
+                                 packed.data_ptr<float>(), dfeat.data_ptr<float>(), dpacked.data_ptr<float>(),
+                                 dpts.data_ptr<float>(), (void *)s),
           "hexplane backward");
     check(gs4d_hexplane_unpack(&lay, dpacked.data_ptr<float>(), (void *)s), "hexplane unpack");
     return {dpts, grads};

@@ -176,8 +176,7 @@ class _DeformHeads(torch.autograd.Function):
         k = len(second) // 2
         W = hidden.shape[1]
         h = torch.relu(hidden)
-        a = torch.addmm(b1, h, w1.t())
-        a.relu_()
+        a = torch._addmm_activation(b1, h, w1.t())  # bias + ReLU in the GEMM epilogue where supported
         outs = [torch.addmm(second[2 * i + 1], a[:, i * W:(i + 1) * W], second[2 * i].t()) for i in range(k)]
         ctx.save_for_backward(h, a, w1, *second[0::2])
         ctx.W = W
@@ -196,11 +195,10 @@ class _DeformHeads(torch.autograd.Function):
             torch.mm(do, w2[i], out=da[:, i * W:(i + 1) * W])
             dw2.append(_splitk_dw(do, sl))
             db2.append(do.sum(0))
-        da.masked_fill_(a <= 0, 0.0)               # ReLU backward (a = relu(z): a > 0 <=> z > 0)
+        da = torch.ops.aten.threshold_backward(da, a, 0)  # ReLU backward (a = relu(z): a > 0 <=> z > 0)
         dw1 = _splitk_dw(da, h)
         db1 = da.sum(0)
-        dh = da @ w1
-        dh.masked_fill_(h <= 0, 0.0)               # the heads' first ReLU
+        dh = torch.ops.aten.threshold_backward(da @ w1, h, 0)  # the heads' first ReLU
         grads = [dh, dw1, db1]
         for i in range(k):
             grads += [dw2[i], db2[i]]

@@ -97,14 +97,14 @@ class _HexPlane(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, pts, *planes):
-        feat, packed = _C.hexplane_forward(pts, list(planes))
-        ctx.save_for_backward(pts, packed, *planes)
+        feat, packed, order = _C.hexplane_forward(pts, list(planes))
+        ctx.save_for_backward(pts, packed, order, *planes)
         return feat
 
     @staticmethod
     def backward(ctx, dfeat):
-        pts, packed, *planes = ctx.saved_tensors
-        dpts, dplanes = _C.hexplane_backward(pts, planes, packed, dfeat)
+        pts, packed, order, *planes = ctx.saved_tensors
+        dpts, dplanes = _C.hexplane_backward(pts, planes, packed, dfeat, order)
         return (dpts, *dplanes)
 
 

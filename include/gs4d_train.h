@@ -80,10 +80,15 @@ typedef struct {
 int gs4d_hexplane_layout_init(gs4d_hexplane_layout *lay, int levels, int F, const int *W, const int *H);
 int gs4d_hexplane_pack(const gs4d_hexplane_layout *lay, float *packed, void *stream);
 int gs4d_hexplane_unpack(const gs4d_hexplane_layout *lay, const float *packed, void *stream);
-int gs4d_hexplane_forward(int N, const float *pts, const gs4d_hexplane_layout *lay, const float *packed, float *feat,
-                          void *stream);
-int gs4d_hexplane_backward(int N, const float *pts, const gs4d_hexplane_layout *lay, const float *packed,
-                           const float *dfeat, float *dpacked, float *dpts, void *stream);
+/* Visiting order of the points (a 3-D Morton order of the normalised x, y, z; any permutation of 0..N-1
+ * gives the same results up to float summation order, NULL = identity).  The backward sums plane
+ * gradients in LDS over the small windows of cells that Morton-consecutive points touch. */
+size_t gs4d_hexplane_order_scratch_bytes(int N);
+int gs4d_hexplane_order(int N, const float *pts, uint32_t *order, void *scratch, void *stream);
+int gs4d_hexplane_forward(int N, const float *pts, const uint32_t *order, const gs4d_hexplane_layout *lay,
+                          const float *packed, float *feat, void *stream);
+int gs4d_hexplane_backward(int N, const float *pts, const uint32_t *order, const gs4d_hexplane_layout *lay,
+                           const float *packed, const float *dfeat, float *dpacked, float *dpts, void *stream);
 
 /* ---- HexPlane regularisers: scene/gaussian_model.py:538-577 (compute_regulation = plane_tv_weight *
  * _plane_regulation + time_smoothness_weight * _time_regulation + l1_time_planes * _l1_regulation) with
