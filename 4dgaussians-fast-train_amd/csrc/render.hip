@@ -382,18 +382,18 @@ __device__ __forceinline__ void walk_half(f2 &T, f2 &A, const f2 dp0, const f2 d
     const f2 pw = fma2(dy, fma2(C2, dy, pb2), pa2);
     const f2 G = f2{__builtin_amdgcn_exp2f(pw.x), __builtin_amdgcn_exp2f(pw.y)};
     const f2 al = O2 * G;
-    const f2 alpha = f2{fminf(0.99f, al.x), fminf(0.99f, al.y)};
     // backward.cu:486-497: contributor test, alpha < 1/255 and (for a conic that is not positive
-    // definite) power > 0 skips -- the same decisions as the forward
-    uint64_t m0 = ballot(alpha.x >= 1.0f / 255.0f) & act0;
-    uint64_t m1 = ballot(alpha.y >= 1.0f / 255.0f) & act1;
+    // definite) power > 0 skips -- the same decisions as the forward (min(0.99, x) >= 1/255 <=> x >= 1/255)
+    uint64_t m0 = ballot(al.x >= 1.0f / 255.0f) & act0;
+    uint64_t m1 = ballot(al.y >= 1.0f / 255.0f) & act1;
     if (check_pw) {
         m0 &= ballot(pw.x <= 0.0f);
         m1 &= ballot(pw.y <= 0.0f);
     }
-    const bool b0 = lane_bit(m0), b1 = lane_bit(m1);
-    const f2 ae = f2{b0 ? alpha.x : 0.f, b1 ? alpha.y : 0.f};
-    const f2 Ge = f2{b0 ? G.x : 0.f, b1 ? G.y : 0.f};
+    // the skip applied to G; alpha of a skipped pixel is then min(0.99, o * 0) = 0 exactly
+    const f2 Ge = f2{lane_bit(m0) ? G.x : 0.f, lane_bit(m1) ? G.y : 0.f};
+    const f2 ale = O2 * Ge;
+    const f2 ae = f2{fminf(0.99f, ale.x), fminf(0.99f, ale.y)};
     const f2 om = bc2(1.f) - ae;
     const f2 inv = f2{__builtin_amdgcn_rcpf(om.x), __builtin_amdgcn_rcpf(om.y)};
     const f2 Tn = T * inv;  // backward.cu:503
@@ -503,7 +503,10 @@ __global__ __launch_bounds__(64) void render_backward_kernel(Args a, const uint2
         s_sp[lane].q4 = make_float2(nxt.col.z, nxt.col.z);
         __syncthreads();
         if (end - 64 > 0) fetch(end - 64);
-        for (int j = 0; j < n; j++) {
+        // batches wholly below every inside pixel's n_contrib: the contributor test passes everywhere
+        const bool all_act = (uint32_t)(end - 1) < min_last;
+        // one splat of the reverse walk: both halves, then its 9 per-lane partial sums into v[]
+        auto walk_splat = [&](int j, float *v) {
             const float4 q0 = s_sp[j].q[0], q1 = s_sp[j].q[1], q2 = s_sp[j].q[2], q3 = s_sp[j].q[3];
             const float2 q4 = s_sp[j].q4;
             const uint32_t contributor = (uint32_t)(end - 1 - j);
@@ -516,16 +519,35 @@ __global__ __launch_bounds__(64) void render_backward_kernel(Args a, const uint2
 #pragma unroll
             for (int h = 0; h < 2; h++) {
                 if ((reach[h] >> j) & 1) {
-                    const uint64_t act0 = ballot(contributor < lastc[2 * h]);
-                    const uint64_t act1 = ballot(contributor < lastc[2 * h + 1]);
+                    const uint64_t act0 = all_act ? inside_m[2 * h] : ballot(contributor < lastc[2 * h]);
+                    const uint64_t act1 = all_act ? inside_m[2 * h + 1] : ballot(contributor < lastc[2 * h + 1]);
                     walk_half(st.T[h], st.A[h], st.dp0[h], st.dp1[h], st.dp2[h], st.nTb[h], hi2(q0), lo2(q2),
                               hi2(q2), lo2(q3), hi2(q3), f2{q4.x, q4.y}, pa2, pb2, pfy[h], (nonpd >> j) & 1, act0, act1,
                               U0, U1, U2, W0, W1, W2);
                 }
             }
             const float u0 = U0.x + U0.y, u1 = U1.x + U1.y;
-            const float v[9] = {u0, dx * u0, u1, dx * dx * u0, dx * u1, U2.x + U2.y, W0.x + W0.y, W1.x + W1.y,
-                                W2.x + W2.y};
+            v[0] = u0;
+            v[1] = dx * u0;
+            v[2] = u1;
+            v[3] = dx * dx * u0;
+            v[4] = dx * u1;
+            v[5] = U2.x + U2.y;
+            v[6] = W0.x + W0.y;
+            v[7] = W1.x + W1.y;
+            v[8] = W2.x + W2.y;
+        };
+        // splats in pairs: the two splats' 18 sums share one reduce-scatter
+        int j = 0;
+        for (; j + 1 < n; j += 2) {
+            float v[18];
+            walk_splat(j, v);
+            walk_splat(j + 1, v + 9);
+            wave_sum18_to_lds(v, reinterpret_cast<float *>(s_rec[j]), reinterpret_cast<float *>(s_rec[j + 1]), lane);
+        }
+        if (j < n) {
+            float v[9];
+            walk_splat(j, v);
             wave_sum9_to_lds(v, reinterpret_cast<float *>(s_rec[j]), lane);
         }
         __syncthreads();

@@ -194,6 +194,25 @@ def test_metric_config_properties(C, oracle, dev):
     _check(C, oracle, s, dev)
 
 
+@pytest.mark.parametrize("cfg", ["c4_per_view", "c5_broom"])
+def test_large_configs(C, oracle, dev, cfg):
+    """BASELINE configs C4 (300k Gaussians, 1352x1014, one view of the 8-GPU run) and C5 (1M Gaussians,
+    960x536): full parity with the oracle at those sizes."""
+    from gs4d_train.synthetic import CONFIGS
+    P, W, H = CONFIGS[cfg]
+    s = make_scene(P, W, H, seed=21)
+    _check(C, oracle, s, dev)
+
+
+def test_parity_mid_tiles(C, oracle, dev):
+    """Tile runs between 256 and 4096 instances, the regime of a training scene's early iterations
+    (dense, large, faint splats): sorted in LDS by tile_sort_kernel before the forward blends them."""
+    s = make_scene(20000, 192, 128, seed=22, log_scale=math.log(0.08))
+    s["opacities"] = np.full_like(s["opacities"], 0.1)
+    fwd, _ = _check(C, oracle, s, dev)
+    assert fwd[0] > 96 * 256
+
+
 def test_autograd_api(dev, oracle):
     """Through GaussianRasterizer + autograd, exactly as gaussian_renderer/__init__.py calls it."""
     if not torch.cuda.is_available():
