@@ -305,7 +305,87 @@ __device__ void lds_network(TileSortLds &s, int n, int space, int k_lo, int k_hi
     }
 }
 
-// Tiles with more than kWaveSortMax instances: one workgroup each.
+// Runs of kWaveSortMax < n <= 256*R instances: one 256-thread workgroup, thread (wave w, lane l) holding
+// positions i = w*64R + r*64 + l in R registers, key = depth bits << 32 | emission slot (as the forward's
+// register sort: the slot grows with the id inside a tile, so this is the (depth, id) order and the
+// key carries its value).  The bitonic network's partner i ^ mask is a lane shuffle for mask bits
+// below 64, a register select for bits below 64R and an LDS exchange (two barriers) above: for
+// n = 2048 that is 3 LDS steps of the network's 66.
+template <int R>
+__device__ __forceinline__ void block_sort(uint32_t *__restrict__ seg, int n, const uint32_t *__restrict__ gid_by_e,
+                                           const float *__restrict__ depths, uint64_t *__restrict__ s_x) {
+    constexpr int M = 256 * R;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int base = w * 64 * R;
+    uint64_t key[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const int i = base + r * 64 + lane;
+        const uint32_t e = i < n ? seg[i] : 0u;
+        const uint32_t gid = i < n ? gid_by_e[e] & kGidMask : 0u;
+        key[r] = i < n ? ((uint64_t)__float_as_uint(depths[gid]) << 32) | e : ~0ull;  // depths > 0.2
+    }
+#pragma unroll
+    for (int k = 2; k <= M; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j >= 1; j >>= 1) {
+            const int mask = j == (k >> 1) ? k - 1 : j;  // flip, then half-cleaners
+            const int lx = mask & 63, rx = (mask >> 6) & (R - 1), wx = mask / (64 * R);
+            uint64_t pk[R];
+            if (wx != 0) {
+                // partner in another wave: exchange through LDS
+#pragma unroll
+                for (int r = 0; r < R; r++) s_x[base + r * 64 + lane] = key[r];
+                __syncthreads();
+#pragma unroll
+                for (int r = 0; r < R; r++) pk[r] = s_x[(base + r * 64 + lane) ^ mask];
+                __syncthreads();
+            } else {
+#pragma unroll
+                for (int r = 0; r < R; r++) {
+                    const int rq = r ^ rx;
+                    if (lx == 0) {
+                        pk[r] = key[rq];
+                    } else {
+                        const uint32_t hi = __shfl_xor((uint32_t)(key[rq] >> 32), lx);
+                        const uint32_t lo = __shfl_xor((uint32_t)key[rq], lx);
+                        pk[r] = ((uint64_t)hi << 32) | lo;
+                    }
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                const bool lower = ((base + r * 64 + lane) & j) == 0;
+                const uint64_t kr = key[r];
+                key[r] = lower ? (pk[r] < kr ? pk[r] : kr) : (pk[r] > kr ? pk[r] : kr);
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const int i = base + r * 64 + lane;
+        if (i < n) seg[i] = (uint32_t)key[r];
+    }
+}
+
+// Tiles with kWaveSortMax < n <= 4096 instances (register + LDS bitonic, one workgroup each); longer
+// runs go to tile_sort_kernel.
+__global__ __launch_bounds__(256) void tile_sort_mid_kernel(const uint2 *__restrict__ ranges,
+                                                            const uint32_t *__restrict__ gid_by_e,
+                                                            const float *__restrict__ depths,
+                                                            uint32_t *__restrict__ upos) {
+    __shared__ uint64_t s_x[kSortCap];
+    const uint2 r = ranges[blockIdx.x];
+    const int n = (int)(r.y - r.x);
+    if (n <= kWaveSortMax || n > kSortCap) return;
+    uint32_t *seg = upos + r.x;
+    if (n <= 512) block_sort<2>(seg, n, gid_by_e, depths, s_x);
+    else if (n <= 1024) block_sort<4>(seg, n, gid_by_e, depths, s_x);
+    else if (n <= 2048) block_sort<8>(seg, n, gid_by_e, depths, s_x);
+    else block_sort<16>(seg, n, gid_by_e, depths, s_x);
+}
+
+// Tiles with more than kSortCap instances: one workgroup each.
 __global__ __launch_bounds__(256) void tile_sort_kernel(const uint2 *__restrict__ ranges,
                                                         const uint32_t *__restrict__ gid_by_e,
                                                         const float *__restrict__ depths, uint32_t *__restrict__ upos,
@@ -313,7 +393,7 @@ __global__ __launch_bounds__(256) void tile_sort_kernel(const uint2 *__restrict_
     __shared__ TileSortLds s;
     const uint2 r = ranges[blockIdx.x];
     const int n = (int)(r.y - r.x);
-    if (n <= kWaveSortMax) return;
+    if (n <= kSortCap) return;  // tile_sort_mid_kernel / the render forward
     uint32_t *seg = upos + r.x;
     if (n <= kSortCap) {
         int m = 1;
@@ -399,6 +479,7 @@ hipError_t launch_binning(const Args &a, GeomState g, const int *radii, BinningS
     onesweep_sort<kSortThreads, kItemsL>(keys, vals, L, n_dev, b.key_bits, b.scratch + kZeroHist,
                                          b.scratch + bin_look_off(L), b.scratch + bin_chain_off() + 1, s);
     hipLaunchKernelGGL(tile_ranges_kernel, dim3((L + 255) / 256), dim3(256), 0, s, b.sorted_keys, n_dev, img.ranges);
+    hipLaunchKernelGGL(tile_sort_mid_kernel, dim3(T), dim3(256), 0, s, img.ranges, b.gid_by_e, g.depths, b.upos);
     hipLaunchKernelGGL(tile_sort_kernel, dim3(T), dim3(256), 0, s, img.ranges, b.gid_by_e, g.depths, b.upos,
                        b.tmp_hi, b.tmp_lo);
     return hipGetLastError();
