@@ -144,6 +144,34 @@ constexpr int kWaveSortMax = 256;
 constexpr int kReachShift = 30;
 constexpr uint32_t kGidMask = (1u << kReachShift) - 1u;
 
+// v from lane (lane ^ lx) of the wave, for the bitonic networks' lane masks (lx is a constant once
+// their loops are unrolled): one DPP move where a row pattern matches (quad permutes, row mirrors,
+// row rotate by 8), ds_swizzle inside 32-lane halves, v_permlane32_swap across them, ds_bpermute for
+// the rest.
+__device__ __forceinline__ uint32_t xor_lane(uint32_t v, int lx) {
+    switch (lx) {
+    case 1: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    case 2: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    case 3: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x1B, 0xF, 0xF, false);   // quad_perm [3,2,1,0]
+    case 7: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+    case 8: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, false);  // row_ror:8
+    case 15: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, false); // row_mirror
+    case 4: return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (4 << 10));
+    case 16: return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (16 << 10));
+    case 31: return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (31 << 10));
+    case 32: {
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        return (threadIdx.x & 32) ? r[0] : r[1];
+    }
+    case 63: {  // lane ^ 63 = (lane ^ 32) ^ 31
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        const uint32_t h = (threadIdx.x & 32) ? r[0] : r[1];
+        return (uint32_t)__builtin_amdgcn_ds_swizzle((int)h, 0x1F | (31 << 10));
+    }
+    default: return (uint32_t)__shfl_xor((int)v, lx);
+    }
+}
+
 // ---- launchers (each enqueues on `stream`, returns hipError_t of the launch) ------------------
 hipError_t launch_preprocess(const Args &a, const float *means3D, const float *scales, const float *rotations,
                              const float *opacities, const float *shs, const float *cov3D_precomp,

@@ -123,8 +123,8 @@ __device__ __forceinline__ void sort_run(uint32_t *__restrict__ seg, int n, cons
                 if (lx == 0) {
                     pk[r] = key[rq];
                 } else {
-                    const uint32_t hi = __shfl_xor((uint32_t)(key[rq] >> 32), lx);
-                    const uint32_t lo = __shfl_xor((uint32_t)key[rq], lx);
+                    const uint32_t hi = xor_lane((uint32_t)(key[rq] >> 32), lx);
+                    const uint32_t lo = xor_lane((uint32_t)key[rq], lx);
                     pk[r] = ((uint64_t)hi << 32) | lo;
                 }
             }
