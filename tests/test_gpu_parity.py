@@ -213,6 +213,19 @@ def test_parity_mid_tiles(C, oracle, dev):
     assert fwd[0] > 96 * 256
 
 
+def test_capacity_prediction_both_ways(C, oracle, dev):
+    """The forward launches the binning against a capacity predicted from the previous call: a scene
+    with ~20x more instances than its predecessor overflows it (relaunch at the exact size), and the
+    small scene after it runs in an oversized buffer; both must match the oracle, backward included
+    (the backward re-carves the buffer with the forward's capacity)."""
+    small = make_scene(2000, 256, 192, seed=23)
+    big = make_scene(40000, 512, 384, seed=24, log_scale=math.log(0.05))
+    _check(C, oracle, small, dev)
+    fwd_big, _ = _check(C, oracle, big, dev)
+    fwd_small, _ = _check(C, oracle, small, dev)
+    assert fwd_big[0] > 20 * fwd_small[0]
+
+
 def test_autograd_api(dev, oracle):
     """Through GaussianRasterizer + autograd, exactly as gaussian_renderer/__init__.py calls it."""
     if not torch.cuda.is_available():
