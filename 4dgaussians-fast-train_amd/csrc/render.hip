@@ -64,6 +64,43 @@ __device__ __forceinline__ void load_splat(SplatRegs &r, bool valid, uint32_t ge
     }
 }
 
+// A splat's attributes as loaded (no arithmetic on them), so that the loads of the next batch stay in
+// flight while the current batch is blended; to_regs() forms the blend constants (as load_splat does)
+// when the batch comes up.
+struct RawSplat {
+    float2 p;
+    float4 co;
+    float3 c;
+    uint32_t ge;  // gid_by_e entry: Gaussian id | half-reach bits
+};
+__device__ __forceinline__ void issue_raw(RawSplat &r, bool valid, uint32_t ge, const float2 *__restrict__ xy,
+                                          const float4 *__restrict__ conic_opacity, const float4 *__restrict__ rgbd,
+                                          const float *__restrict__ colors) {
+    r.ge = valid ? ge : 0u;
+    if (valid) {
+        const uint32_t gid = ge & kGidMask;
+        r.p = xy[gid];
+        r.co = conic_opacity[gid];
+        if (colors) {
+            r.c = make_float3(colors[3 * gid], colors[3 * gid + 1], colors[3 * gid + 2]);
+        } else {
+            const float4 c4 = rgbd[gid];
+            r.c = make_float3(c4.x, c4.y, c4.z);
+        }
+    }
+}
+__device__ __forceinline__ void to_regs(SplatRegs &s, bool valid, const RawSplat &r) {
+    if (valid) {
+        s.geo = make_float4(r.p.x, r.p.y, (-0.5f * r.co.x) * kLog2e, (-r.co.y) * kLog2e);
+        s.opc = make_float4((-0.5f * r.co.z) * kLog2e, r.co.w, 0.f, 0.f);
+        s.col = make_float4(r.c.x, r.c.y, r.c.z, 0.f);
+        s.reach = r.ge >> kReachShift;
+    } else {
+        s.geo = s.opc = s.col = make_float4(0.f, 0.f, 0.f, 0.f);
+        s.reach = 0;
+    }
+}
+
 // Falloff of one splat at a pixel pair: exponent (base 2) and G = 2^power2.  Forward and backward use
 // this one sequence, so they take identical blend decisions.
 struct Falloff {
@@ -480,19 +517,43 @@ __global__ __launch_bounds__(64) void render_backward_kernel(Args a, const uint2
         rec[1] = z4;
         rec[2] = z4;
     }
-    SplatRegs nxt;
+    // The walk's instances: emission slot e (where the gradient record goes) and gid_by_e[e] of list
+    // position end-1-lane of each batch, loaded 4 batches at a time (independent loads, one wait per
+    // refill).  The next batch's attributes are issued before the current batch is blended and only
+    // turned into blend constants after it, so their loads are the only ones in flight across the
+    // blend loop.
+    uint32_t ue[4], ug[4];
+    int ids_left = 0;
+    auto refill = [&](int end) {
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int pos = end - 1 - (r * 64 + lane);
+            ue[r] = pos >= 0 ? upos[range.x + pos] : 0u;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int pos = end - 1 - (r * 64 + lane);
+            ug[r] = pos >= 0 ? gid_by_e[ue[r]] : 0u;
+        }
+        ids_left = 4;
+    };
+    RawSplat raw;
     uint32_t unxt = 0;  // where this lane's splat record goes (the instance's emission slot)
-    auto fetch = [&](int end) {
-        const int n = min(64, end);
-        const bool v = lane < n;
-        unxt = v ? upos[range.x + end - 1 - lane] : 0u;
-        const uint32_t gid = v ? gid_by_e[unxt] : 0u;
-        load_splat(nxt, v, gid, xy, conic_opacity, rgbd, colors);  // colour: colors_precomp or rgb
+    auto fetch = [&](int end) {  // ids of the batch ending at `end`, then its attribute loads
+        if (ids_left == 0) refill(end);
+        unxt = ue[0];
+        const uint32_t ge = ug[0];
+        ue[0] = ue[1]; ue[1] = ue[2]; ue[2] = ue[3];
+        ug[0] = ug[1]; ug[1] = ug[2]; ug[2] = ug[3];
+        ids_left--;
+        issue_raw(raw, lane < min(64, end), ge, xy, conic_opacity, rgbd, colors);  // colors_precomp or rgb
     };
     if (max_last > 0) fetch((int)max_last);
     for (int end = (int)max_last; end > 0; end -= 64) {
         const int n = min(64, end);
         const uint32_t ucur = unxt;
+        SplatRegs nxt;
+        to_regs(nxt, lane < n, raw);
         const uint64_t reach[2] = {ballot(nxt.reach & 1u), ballot(nxt.reach & 2u)};
         const uint64_t nonpd = ballot(!conic_pd(nxt.geo, nxt.opc));
         __syncthreads();
