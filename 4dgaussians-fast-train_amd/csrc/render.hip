@@ -45,27 +45,8 @@ struct SplatRegs {
     uint32_t reach;  // bit h: the splat reaches some pixel centre of half tile h (rows 8h..8h+7)
 };
 
-// ge = gid_by_e entry of the instance (Gaussian id | half-reach bits)
-__device__ __forceinline__ void load_splat(SplatRegs &r, bool valid, uint32_t ge, const float2 *__restrict__ xy,
-                                           const float4 *__restrict__ conic_opacity, const float4 *__restrict__ rgbd,
-                                           const float *__restrict__ colors) {
-    if (valid) {
-        const uint32_t gid = ge & kGidMask;
-        const float2 p = xy[gid];
-        const float4 co = conic_opacity[gid];
-        r.geo = make_float4(p.x, p.y, (-0.5f * co.x) * kLog2e, (-co.y) * kLog2e);
-        r.opc = make_float4((-0.5f * co.z) * kLog2e, co.w, 0.f, 0.f);
-        r.col = rgbd[gid];
-        if (colors) r.col = make_float4(colors[3 * gid], colors[3 * gid + 1], colors[3 * gid + 2], r.col.w);
-        r.reach = ge >> kReachShift;
-    } else {
-        r.geo = r.opc = r.col = make_float4(0.f, 0.f, 0.f, 0.f);
-        r.reach = 0;
-    }
-}
-
 // A splat's attributes as loaded (no arithmetic on them), so that the loads of the next batch stay in
-// flight while the current batch is blended; to_regs() forms the blend constants (as load_splat does)
+// flight while the current batch is blended; to_regs() forms the blend constants
 // when the batch comes up.
 struct RawSplat {
     float2 p;
@@ -223,14 +204,55 @@ __global__ __launch_bounds__(64) void render_forward_kernel(Args a, const uint2 
     } else if (n_run == 1 && lane == 0) {
         ev[0] = upos[range.x];
     }
-    SplatRegs nxt;
-    if (range.x < range.y) {
-        const bool v = range.x + lane < range.y;
-        const uint32_t e = in_regs ? ev[0] : (v ? upos[range.x + lane] : 0u);
-        load_splat(nxt, v, v ? gid_by_e[e] : 0u, xy, conic_opacity, rgbd, nullptr);
-    }
+    // gid_by_e of each batch's instances, 4 batches at a time (the short run's are all loaded here);
+    // the next batch's attributes are issued before the current one is blended and only turned into
+    // blend constants when it comes up, so their loads overlap the blend loop
+    uint32_t ug[4];
+    int ids_left = 0;
+    auto refill = [&](uint32_t first) {  // list positions first + r*64 + lane
+        if (!in_regs) {
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const uint32_t i = first + r * 64 + lane;
+                ev[r] = i < range.y ? upos[i] : 0u;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const uint32_t i = first + r * 64 + lane;
+            ug[r] = i < range.y ? gid_by_e[ev[r]] : 0u;
+        }
+        ids_left = 4;
+    };
+    float2 rp;
+    float4 rco, rcd;
+    uint32_t rge = 0;
+    auto fetch = [&](uint32_t first) {
+        if (ids_left == 0) refill(first);
+        rge = ug[0];
+        ev[0] = ev[1]; ev[1] = ev[2]; ev[2] = ev[3];
+        ug[0] = ug[1]; ug[1] = ug[2]; ug[2] = ug[3];
+        ids_left--;
+        if (first + lane < range.y) {
+            const uint32_t gid = rge & kGidMask;
+            rp = xy[gid];
+            rco = conic_opacity[gid];
+            rcd = rgbd[gid];
+        }
+    };
+    if (range.x < range.y) fetch(range.x);
     for (uint32_t base = range.x; base < range.y; base += 64) {
         if ((alive[0] | alive[1] | alive[2] | alive[3]) == 0) break;  // forward.cu:312-314
+        SplatRegs nxt;
+        if (base + lane < range.y) {  // blend constants (as to_regs)
+            nxt.geo = make_float4(rp.x, rp.y, (-0.5f * rco.x) * kLog2e, (-rco.y) * kLog2e);
+            nxt.opc = make_float4((-0.5f * rco.z) * kLog2e, rco.w, 0.f, 0.f);
+            nxt.col = rcd;
+            nxt.reach = rge >> kReachShift;
+        } else {
+            nxt.geo = nxt.opc = nxt.col = make_float4(0.f, 0.f, 0.f, 0.f);
+            nxt.reach = 0;
+        }
         const uint64_t reach[2] = {ballot(nxt.reach & 1u), ballot(nxt.reach & 2u)};
         const uint64_t nonpd = ballot(!conic_pd(nxt.geo, nxt.opc));
         __syncthreads();
@@ -238,17 +260,7 @@ __global__ __launch_bounds__(64) void render_forward_kernel(Args a, const uint2 
         s_sp[lane].opc = nxt.opc;
         s_sp[lane].col = nxt.col;
         __syncthreads();
-        {
-            const uint32_t nb = base + 64;
-            const bool v = nb + lane < range.y;
-            ev[0] = ev[1];
-            ev[1] = ev[2];
-            ev[2] = ev[3];
-            if (nb < range.y) {
-                const uint32_t e = in_regs ? ev[0] : (v ? upos[nb + lane] : 0u);
-                load_splat(nxt, v, v ? gid_by_e[e] : 0u, xy, conic_opacity, rgbd, nullptr);
-            }
-        }
+        if (base + 64 < range.y) fetch(base + 64);
         const uint32_t pos0 = base - range.x;
         // The two half tiles blend independently: each walks only the batch's splats that reach it.
 #pragma unroll
