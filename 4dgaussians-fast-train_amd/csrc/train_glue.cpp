@@ -241,7 +241,38 @@ std::vector<torch::Tensor> hexplane_reg_backward(std::vector<torch::Tensor> plan
     return grads;
 }
 
+// ---- Linear weight gradients: [(dw (n, W), db (n))] for pairs dy (P, n), x (P, W) (row strides kept)
+std::vector<torch::Tensor> linear_dw(const std::vector<torch::Tensor> &dys, const std::vector<torch::Tensor> &xs) {
+    need(!dys.empty() && dys.size() == xs.size() && dys.size() <= 8, "linear_dw: 1-8 (dy, x) pairs");
+    const auto &d0 = dys[0];
+    c10::hip::HIPGuard guard(d0.device().index());
+    const int P = (int)d0.size(0), W = (int)xs[0].size(1), count = (int)dys.size();
+    std::vector<gs4d_dw_problem> probs(count);
+    std::vector<int> ns(count);
+    std::vector<torch::Tensor> out;
+    for (int i = 0; i < count; i++) {
+        const auto &dy = dys[i], &x = xs[i];
+        need(dy.is_cuda() && x.is_cuda() && dy.scalar_type() == torch::kFloat32 && x.scalar_type() == torch::kFloat32,
+             "linear_dw: float32 GPU tensors");
+        need(dy.dim() == 2 && x.dim() == 2 && dy.size(0) == P && x.size(0) == P && x.size(1) == W,
+             "linear_dw: dy (P, n) and x (P, W), same P and W for every pair");
+        need(dy.stride(1) == 1 && x.stride(1) == 1, "linear_dw: rows must be contiguous");
+        auto dw = torch::empty({dy.size(1), W}, dy.options());
+        auto db = torch::empty({dy.size(1)}, dy.options());
+        ns[i] = (int)dy.size(1);
+        probs[i] = gs4d_dw_problem{dy.data_ptr<float>(), x.data_ptr<float>(), dw.data_ptr<float>(), db.data_ptr<float>(),
+                                   ns[i], (int)dy.stride(0), (int)x.stride(0)};
+        out.push_back(dw);
+        out.push_back(db);
+    }
+    const size_t sb = gs4d_linear_dw_scratch_bytes(P, W, count, ns.data());
+    auto scratch = torch::empty({(int64_t)sb}, d0.options().dtype(torch::kUInt8));
+    check(gs4d_linear_dw(P, W, count, probs.data(), scratch.data_ptr(), (void *)stream_of(d0)), "linear_dw");
+    return out;
+}
+
 PYBIND11_MODULE(_C, m) {
+    m.def("linear_dw", &linear_dw);
     m.def("hexplane_reg_forward", &hexplane_reg_forward);
     m.def("hexplane_reg_backward", &hexplane_reg_backward);
     m.def("hexplane_forward", &hexplane_forward);

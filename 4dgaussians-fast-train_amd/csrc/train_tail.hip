@@ -19,6 +19,8 @@
 //           backward: one launch per direction over every plane (plus one fixed-order final sum).
 #include <math.h>
 
+#include <algorithm>
+
 #include "../../include/gs4d_train.h"
 #include "gs4d_internal.h"
 
@@ -213,11 +215,184 @@ __global__ __launch_bounds__(kTailThreads) void reg_backward_kernel(gs4d_reg_bat
     }
 }
 
+// ---- tall-skinny weight gradients -----------------------------------------------------------------
+// dW = dy^T x and db = column sums of dy for Linear layers' backward, reduced over P ~ 1e5 rows with
+// n <= 64 outputs and W in {64, 128, 256} inputs -- the deformation heads' second layers, which the
+// GEMM library tiles only by their small output (~55 us per call whatever n, split-K included).  Up to
+// kDwMaxProblems such products (same P and W) go in one launch, blockIdx.y picking the problem.  A
+// workgroup takes a contiguous block of rows; inside it G = 512 / W thread groups take interleaved
+// runs of kDwUnroll rows; a thread owns column c and accumulates all n outputs: x[p, c] is one
+// coalesced vector load per row, the dy row is wave-uniform (scalar loads, the FMA's SGPR operand).
+// db: lane l of each group's first wave adds dy[p, l].  Groups combine through LDS in group order and
+// the per-workgroup partials are summed in a fixed order by a second launch: deterministic.
+constexpr int kDwMaxProblems = 8;
+constexpr int kDwThreads = 512;
+constexpr int kDwMaxNW = 64 * 128;  // n * W bound (LDS combine buffer)
+
+struct DwProblem {
+    const float *dy;
+    const float *x;
+    float *dw;
+    float *db;
+    int n, ld_dy, ld_x, pad;
+    int64_t part_off;  // floats into the partials buffer
+};
+struct DwBatch {
+    DwProblem q[kDwMaxProblems];
+};
+
+template <int N, bool EXACT, int kDwUnroll>
+__device__ __forceinline__ void dw_block(const DwProblem &q, int P, int W, int rows_per_wg, float *__restrict__ part,
+                                         float *s_red, float *s_bs) {
+    const int tid = threadIdx.x;
+    const int G = kDwThreads / W;
+    const int g = __builtin_amdgcn_readfirstlane(tid / W);  // W is a multiple of 64: wave-uniform
+    const int c = tid - g * W;
+    const bool lead = __builtin_amdgcn_readfirstlane(c) == 0;  // the group's first wave
+    const int n = EXACT ? N : q.n;
+    const float *__restrict__ dy = q.dy;
+    const float *__restrict__ x = q.x;
+    const int64_t p0 = (int64_t)blockIdx.x * rows_per_wg, p1 = min((int64_t)P, p0 + rows_per_wg);
+    float acc[N];
+#pragma unroll
+    for (int j = 0; j < N; j++) acc[j] = 0.f;
+    float bs = 0.f;
+    for (int64_t p = p0 + (int64_t)g * kDwUnroll; p < p1; p += (int64_t)G * kDwUnroll) {
+        float xv[kDwUnroll];
+#pragma unroll
+        for (int u = 0; u < kDwUnroll; u++) xv[u] = p + u < p1 ? x[(p + u) * q.ld_x + c] : 0.f;
+#pragma unroll
+        for (int u = 0; u < kDwUnroll; u++) {
+            if (p + u < p1) {
+                const float *d = dy + (p + u) * q.ld_dy;
+#pragma unroll
+                for (int j = 0; j < N; j++)
+                    if (EXACT || j < n) acc[j] = fmaf(d[j], xv[u], acc[j]);
+                if (lead && c < n) bs += d[c];
+            }
+        }
+    }
+    for (int h = 0; h < G; h++) {
+        if (g == h) {
+#pragma unroll
+            for (int j = 0; j < N; j++)
+                if (EXACT || j < n) s_red[j * W + c] = (h == 0 ? 0.f : s_red[j * W + c]) + acc[j];
+            if (lead && c < n) s_bs[c] = (h == 0 ? 0.f : s_bs[c]) + bs;
+        }
+        __syncthreads();
+    }
+    float *out = part + q.part_off + (int64_t)blockIdx.x * n * (W + 1);
+    for (int e = tid; e < n * (W + 1); e += kDwThreads) {
+        const int r = e / (W + 1), cc = e - r * (W + 1);
+        out[e] = cc < W ? s_red[r * W + cc] : s_bs[r];
+    }
+}
+
+// FAMILY 0: n <= 8 (16 rows in flight per thread); FAMILY 1: n = 48 or n <= 16 (4 rows)
+template <int FAMILY>
+__global__ __launch_bounds__(kDwThreads) void linear_dw_kernel(DwBatch b, int P, int W, int rows_per_wg,
+                                                                float *__restrict__ part) {
+    __shared__ float s_red[kDwMaxNW];
+    __shared__ float s_bs[64];
+    const DwProblem &q = b.q[blockIdx.y];
+    if constexpr (FAMILY == 0) {
+        switch (q.n) {
+        case 1: dw_block<1, true, 16>(q, P, W, rows_per_wg, part, s_red, s_bs); break;
+        case 2: dw_block<2, true, 16>(q, P, W, rows_per_wg, part, s_red, s_bs); break;
+        case 3: dw_block<3, true, 16>(q, P, W, rows_per_wg, part, s_red, s_bs); break;
+        case 4: dw_block<4, true, 16>(q, P, W, rows_per_wg, part, s_red, s_bs); break;
+        default: dw_block<8, false, 8>(q, P, W, rows_per_wg, part, s_red, s_bs);
+        }
+    } else {
+        if (q.n == 48) dw_block<48, true, 4>(q, P, W, rows_per_wg, part, s_red, s_bs);
+        else if (q.n <= 8) dw_block<8, false, 8>(q, P, W, rows_per_wg, part, s_red, s_bs);
+        else dw_block<16, false, 4>(q, P, W, rows_per_wg, part, s_red, s_bs);
+    }
+}
+
+// sum of the per-workgroup partials: 32 outputs (r, c | bias) of problem blockIdx.y per workgroup,
+// 8 interleaved eighths of the workgroups combined in a fixed order
+__global__ __launch_bounds__(256) void linear_dw_reduce_kernel(DwBatch b, int W, int nwg, const float *__restrict__ part) {
+    __shared__ float s_sum[8][32];
+    const DwProblem &q = b.q[blockIdx.y];
+    const int per = q.n * (W + 1);
+    if ((int)blockIdx.x * 32 >= per) return;  // uniform over the workgroup
+    const int o = threadIdx.x & 31, k = threadIdx.x >> 5;
+    const int i = blockIdx.x * 32 + o;
+    const float *src = part + q.part_off;
+    float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;  // four independent chains: loads in flight
+    if (i < per) {
+        int w = k;
+        for (; w + 24 < nwg; w += 32) {
+            v0 += src[(size_t)w * per + i];
+            v1 += src[(size_t)(w + 8) * per + i];
+            v2 += src[(size_t)(w + 16) * per + i];
+            v3 += src[(size_t)(w + 24) * per + i];
+        }
+        for (; w < nwg; w += 8) v0 += src[(size_t)w * per + i];
+    }
+    s_sum[k][o] = (v0 + v1) + (v2 + v3);
+    __syncthreads();
+    if (k == 0 && i < per) {
+        float t = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; e++) t += s_sum[e][o];
+        const int r = i / (W + 1), cc = i - r * (W + 1);
+        if (cc < W) q.dw[(size_t)r * W + cc] = t;
+        else if (q.db) q.db[r] = t;
+    }
+}
+
+static int dw_rows_per_wg(int P, int nmax) {
+    // enough workgroups to cover the chip, few enough that the partials stay small next to x
+    (void)P;
+    return nmax <= 8 ? 256 : 1024;
+}
+
 }  // namespace gs4d
 
 using namespace gs4d;
 
 extern "C" {
+
+size_t gs4d_linear_dw_scratch_bytes(int P, int W, int count, const int *n) {
+    if (P < 0 || W < 1 || count < 1 || count > kDwMaxProblems || !n) return 0;
+    int nmax = 0, nsum = 0;
+    for (int i = 0; i < count; i++) nmax = std::max(nmax, n[i]), nsum += std::max(n[i], 0);
+    const size_t nwg = std::max<size_t>(1, ((size_t)P + dw_rows_per_wg(P, nmax) - 1) / dw_rows_per_wg(P, nmax));
+    return 4 * nwg * (size_t)nsum * (W + 1) + 256;
+}
+
+int gs4d_linear_dw(int P, int W, int count, const gs4d_dw_problem *problems, void *scratch, void *stream) {
+    if (P < 0 || (W != 64 && W != 128 && W != 256) || count < 1 || count > kDwMaxProblems || !problems || !scratch)
+        return 1;
+    DwBatch b{};
+    int nmax = 0, nsum = 0;
+    for (int i = 0; i < count; i++) {
+        const gs4d_dw_problem &p = problems[i];
+        if (p.n < 1 || (p.n > 16 && p.n != 48) || p.n * W > kDwMaxNW || (P > 0 && (!p.dy || !p.x)) || !p.dw || p.ld_dy < p.n || p.ld_x < W)
+            return 1;
+        nmax = std::max(nmax, p.n);
+        b.q[i] = DwProblem{p.dy, p.x, p.dw, p.db, p.n, p.ld_dy, p.ld_x, 0, 0};
+    }
+    hipStream_t s = (hipStream_t)stream;
+    if (P == 0) {
+        for (int i = 0; i < count; i++) {
+            if (hipMemsetAsync(b.q[i].dw, 0, 4 * (size_t)b.q[i].n * W, s) != hipSuccess) return 3;
+            if (b.q[i].db && hipMemsetAsync(b.q[i].db, 0, 4 * (size_t)b.q[i].n, s) != hipSuccess) return 3;
+        }
+        return 0;
+    }
+    const int rows = dw_rows_per_wg(P, nmax);
+    const int nwg = (int)(((int64_t)P + rows - 1) / rows);
+    for (int i = 0; i < count; i++) b.q[i].part_off = (int64_t)nwg * nsum * (W + 1), nsum += b.q[i].n;
+    float *part = (float *)align_up((size_t)scratch, 256);
+    if (nmax <= 8) hipLaunchKernelGGL(linear_dw_kernel<0>, dim3(nwg, count), dim3(kDwThreads), 0, s, b, P, W, rows, part);
+    else hipLaunchKernelGGL(linear_dw_kernel<1>, dim3(nwg, count), dim3(kDwThreads), 0, s, b, P, W, rows, part);
+    hipLaunchKernelGGL(linear_dw_reduce_kernel, dim3((nmax * (W + 1) + 31) / 32, count), dim3(256), 0, s, b, W, nwg,
+                       (const float *)part);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+}
 
 int64_t gs4d_reg_blocks(int C, int H, int W) { return ((int64_t)C * H * W + kRegBlock - 1) / kRegBlock; }
 

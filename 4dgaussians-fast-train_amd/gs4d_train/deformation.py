@@ -167,7 +167,8 @@ class _DeformHeads(torch.autograd.Function):
     input, ONE (P x W) @ (W x kW) GEMM for the k first layers (weights concatenated), one ReLU, then
     the k small second layers on column slices.  The backward mirrors it: the k (P x n) @ (n x W)
     products land in column slices of one (P x kW) gradient, then one ReLU mask, one GEMM with K = kW
-    for the input gradient and one split-K GEMM for the concatenated first-layer weight gradient.
+    for the input gradient and one split-K GEMM for the concatenated first-layer weight gradient; the
+    narrow second layers' weight and bias gradients (n <= 8) come from one gs4d_linear_dw launch.
     Same function as the k separate heads (and the same parameters, concatenated per call); the
     GEMMs sum in a different order, so results agree to fp32 rounding."""
 
@@ -187,14 +188,22 @@ class _DeformHeads(torch.autograd.Function):
         h, a, w1, *w2 = ctx.saved_tensors
         W, k = ctx.W, len(w2)
         da = torch.empty_like(a)
-        dw2, db2 = [], []
+        dw2, db2 = [None] * k, [None] * k
+        small = []  # heads whose (dw, db) one gs4d_linear_dw launch forms (n <= 8)
         for i in range(k):
             do = douts[i] if douts[i] is not None else torch.zeros(a.shape[0], w2[i].shape[0], device=a.device)
             do = do.contiguous()
             sl = a[:, i * W:(i + 1) * W]
             torch.mm(do, w2[i], out=da[:, i * W:(i + 1) * W])
-            dw2.append(_splitk_dw(do, sl))
-            db2.append(do.sum(0))
+            if do.shape[1] <= 8 and W in (64, 128, 256):
+                small.append((i, do, sl))
+            else:
+                dw2[i], db2[i] = _splitk_dw(do, sl), do.sum(0)
+        if small:
+            from . import _C
+            out = _C.linear_dw([d for _, d, _ in small], [x for _, _, x in small])
+            for j, (i, _, _) in enumerate(small):
+                dw2[i], db2[i] = out[2 * j], out[2 * j + 1]
         da = torch.ops.aten.threshold_backward(da, a, 0)  # ReLU backward (a = relu(z): a > 0 <=> z > 0)
         dw1 = _splitk_dw(da, h)
         db1 = da.sum(0)

@@ -117,6 +117,22 @@ size_t gs4d_reg_scratch_bytes(const gs4d_reg_batch *batch);
 int gs4d_hexplane_reg_forward(const gs4d_reg_batch *batch, float *loss, void *scratch, void *stream);
 int gs4d_hexplane_reg_backward(const gs4d_reg_batch *batch, const float *dloss, void *stream);
 
+/* ---- Linear-layer weight gradients over many rows: for each problem, dw (n, W) = dy^T x and db (n)
+ * = column sums of dy (db may be NULL) -- the backward of F.linear as autograd forms it -- for dy (P, n)
+ * and x (P, W) given with row strides ld_dy >= n and ld_x >= W (x may be a column block of a wider
+ * matrix).  Up to 8 problems with the same P and W per call; n <= 16 or n = 48, n * W <= 8192,
+ * W in {64, 128, 256}.  Replaces the weight/bias gradients of the deformation heads' second layers
+ * (scene/deformation.py:73-78, 152-164).  fp32, partial sums reduced in a fixed order. */
+typedef struct gs4d_dw_problem {
+    const float *dy;
+    const float *x;
+    float *dw;
+    float *db;
+    int n, ld_dy, ld_x;
+} gs4d_dw_problem;
+size_t gs4d_linear_dw_scratch_bytes(int P, int W, int count, const int *n);
+int gs4d_linear_dw(int P, int W, int count, const gs4d_dw_problem *problems, void *scratch, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -147,6 +147,28 @@ def test_hexplane_regulation_fused_matches_torch():
         assert float((a.grad - b.grad).abs().max()) <= 1e-5 * scale
 
 
+@pytest.mark.parametrize("P,W,ns", [(100_003, 128, [3, 3, 4, 1]), (777, 64, [2, 5, 8]), (3000, 256, [16, 7]),
+                                     (50_001, 128, [48]), (1, 128, [1, 48]), (0, 128, [3])])
+def test_linear_dw_matches_fp64(P, W, ns):
+    """gs4d_linear_dw (the narrow deformation heads' weight/bias gradients, dW = dy^T x, db = dy.sum(0))
+    vs fp64 torch: to 1e-5 of each result's largest |term sum| (fp32 partial sums over ~1e5 rows); x a
+    column block of a wider matrix as in the heads block; ragged P (not a multiple of the row blocks),
+    P = 1 and P = 0."""
+    from gs4d_train import _C
+    torch.manual_seed(P + W)
+    a = torch.relu(torch.randn(P, len(ns) * W + 5, device="cuda"))
+    dys = [torch.randn(P, n, device="cuda") for n in ns]
+    xs = [a[:, 5 + i * W:5 + (i + 1) * W] for i in range(len(ns))]
+    out = _C.linear_dw(dys, xs)
+    for i, (d, x) in enumerate(zip(dys, xs)):
+        rw, rb = d.double().t() @ x.double(), d.double().sum(0)
+        sw = (d.double().abs().t() @ x.double().abs()).max().clamp_min(1e-30)
+        sb = d.double().abs().sum(0).max().clamp_min(1e-30)
+        assert out[2 * i].shape == (ns[i], W) and out[2 * i + 1].shape == (ns[i],)
+        assert float((out[2 * i].double() - rw).abs().max() / sw) <= 1e-5
+        assert float((out[2 * i + 1].double() - rb).abs().max() / sb) <= 1e-5
+
+
 def test_train_step_fused_matches_torch_tail():
     """One fine-stage step through deformation + rasterizer + loss + densification statistics, fused
     (HexPlane kernel, L1 kernel, stats kernel) vs the reference's torch formulation.  The optimizer is
