@@ -20,10 +20,11 @@
 //   - points are visited in a 3-D Morton order (gs4d_hexplane_order: 24-bit codes of the normalised
 //     coordinates, the library's onesweep sort), so the ~128 points of a backward workgroup cover a
 //     small box of the field and each plane sees only a small window of cells;
-//   - grid gradients are summed in LDS over those windows (one window per plane and level, bounding
-//     box of the workgroup's taps) and added to HBM once per workgroup with hardware float atomics
-//     (no-return); a window that does not fit the LDS budget falls back to direct atomics.  The
-//     channels-last gradient buffer is repacked to the (1, F, H, W) parameter layout by one launch.
+//   - grid gradients are gathered, not scattered: the workgroup's points are bucketed by bilinear
+//     anchor cell in LDS and each touched (cell, feature) sums its neighbouring buckets with plain LDS
+//     reads, then goes to HBM with one no-return float atomic per workgroup; a plane whose anchor box
+//     is too large falls back to direct atomics.  The channels-last gradient buffer is repacked to
+//     the (1, F, H, W) parameter layout by one launch.
 #include <algorithm>
 #include <climits>
 
@@ -133,14 +134,57 @@ __global__ __launch_bounds__(kHexThreads) void hexplane_forward_kernel(int N, co
     }
 }
 
-// Backward.  A workgroup serves kHexPointsPerWG consecutive points of the Morton order.  Per level it
-// first takes, for each of the 6 planes, the bounding box of the cells its points' bilinear taps
-// touch, lays the boxes out in LDS (kHexLdsFloats budget, planes in order; a box that does not fit
-// keeps direct atomics), accumulates the plane gradients there with LDS atomics, then adds each box
-// to the packed gradient buffer with one no-return float atomic per non-zero element.  Time planes
-// get tiny boxes: within one render call every point has the same t, so their taps span two rows.
-constexpr int kHexPointsPerWG = 128;
-constexpr int kHexLdsFloats = 12288;  // 48 KiB: three workgroups per CU
+// Backward.  A workgroup serves NPW consecutive points of the Morton order (hex_points_per_wg: 2048 / F,
+// at least one chunk of 256 / (F/4) points, at most 128), so they cover a small box of the field.  Per
+// level:
+//   1. each point's reverse pass (F/4 lanes) writes its 6 plane gradients dv (F floats each), its
+//      bilinear anchor cell (x0, y0) and unnormalised coordinates (ix, iy) to LDS, and reduces its
+//      coordinate gradient with shuffles;
+//   2. per plane, the points' <= 4 taps (weights as make_tap forms them) are counting-sorted by cell
+//      in LDS over the touched box, and every (cell, 4 features) of it sums its taps' w * dv with
+//      plain LDS reads and adds the sums to HBM with no-return float atomics.  A plane whose box
+//      exceeds kHexMaxCells scatters its points' taps with direct float atomics instead.
+// gfx950 executes LDS float atomics (ds_add_f32) at well under one lane per clock per CU: the previous
+// version, which summed the taps into LDS windows with them, spent 280 of its 620 us in those atomics.
+constexpr int kHexMaxCells = 1024;
+constexpr int kHexDvFloats = 2048;   // NPW * F
+constexpr int kHexLdsWords = 20480;  // 80 KiB: two workgroups per CU, as the registers allow
+
+__host__ __device__ __forceinline__ int hex_points_per_wg(int F) {
+    const int ppc = kHexThreads / (F / 4);
+    const int fit = kHexDvFloats / F;
+    const int want = fit < 128 ? fit : 128;
+    return ppc > want ? ppc : want;  // a whole number of chunks
+}
+// LDS words of the backward's layout (hexplane_backward_kernel); <= kHexLdsWords for every valid F
+__host__ __device__ __forceinline__ int hex_bwd_lds_words(int F) {
+    const int npw = hex_points_per_wg(F);
+    return 6 * npw * F + 6 * npw * 3 + (kHexMaxCells + 1) + kHexMaxCells / 2 + (kHexMaxCells + 2) / 2 + 4 * npw +
+           2 * npw + 6 * 4 + 4 * 6 * 4 + 8;
+}
+
+// exclusive prefix sum over the workgroup (256 threads), `tot` = the sum; s_tmp holds 4 ints
+__device__ __forceinline__ int block_excl_scan(int v, int *s_tmp, int &tot) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) s_tmp[wv] = x;
+    __syncthreads();
+    int base = 0;
+    tot = 0;
+#pragma unroll
+    for (int w = 0; w < kHexThreads / 64; w++) {
+        const int t = s_tmp[w];
+        if (w < wv) base += t;
+        tot += t;
+    }
+    __syncthreads();
+    return base + x - v;
+}
 
 __global__ __launch_bounds__(kHexThreads) void hexplane_backward_kernel(int N, const float *__restrict__ pts,
                                                                         const uint32_t *__restrict__ order,
@@ -149,74 +193,34 @@ __global__ __launch_bounds__(kHexThreads) void hexplane_backward_kernel(int N, c
                                                                         const float *__restrict__ dfeat,
                                                                         float *__restrict__ dpacked,
                                                                         float *__restrict__ dpts) {
-    __shared__ float s_win[kHexLdsFloats];
-    __shared__ int s_box[6][4];  // x0, x1, y0, y1 (inclusive) of the plane's touched cells
-    __shared__ int s_off[6];     // LDS offset of the plane's box, -1: direct atomics
-    __shared__ int s_used;
-    const int F = lay.F, G = F / 4, ppc = kHexThreads / G;  // lanes per point, points per chunk
-    const int cpw = max(1, kHexPointsPerWG / ppc);
+    __shared__ float smem[kHexLdsWords];
+    const int F = lay.F, G = F / 4, ppc = kHexThreads / G;
+    const int npw = hex_points_per_wg(F), cpw = npw / ppc;
+    float *s_dv = smem;                                            // [6][npw][F]
+    int *s_anc = (int *)(s_dv + 6 * npw * F);                      // [6][npw]: y0 << 16 | x0, -1: none
+    float2 *s_ixy = (float2 *)(s_anc + 6 * npw);                   // [6][npw]
+    int *s_off = (int *)(s_ixy + 6 * npw);                         // [kHexMaxCells + 1]: cell -> first tap
+    uint16_t *s_cells = (uint16_t *)(s_off + kHexMaxCells + 1);    // [kHexMaxCells]: touched cells
+    uint16_t *s_cstart = s_cells + kHexMaxCells;                   // [kHexMaxCells + 1]: their first taps
+    float *s_pw = (float *)(s_off + kHexMaxCells + 1 + kHexMaxCells / 2 + (kHexMaxCells + 2) / 2);  // [4 npw]
+    uint16_t *s_pj = (uint16_t *)(s_pw + 4 * npw);                 // [4 npw]: point
+    int *s_box = (int *)(s_pj + 4 * npw);                          // [6][4]: ax0, ay0, aw, ah
+    int *s_wbox = s_box + 24;                                      // [waves][6][4]
+    int *s_tmp = s_wbox + 4 * 24;                                  // [8]
     const int q = threadIdx.x % G, slot = threadIdx.x / G;
-    const int64_t first = (int64_t)blockIdx.x * cpw * ppc;
-    auto point_of = [&](int c) -> int {
-        const int64_t i = first + (int64_t)c * ppc + slot;
-        return i < N ? (order ? (int)order[i] : (int)i) : -1;
-    };
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t first = (int64_t)blockIdx.x * npw;
     for (int l = 0; l < lay.levels; l++) {
-        // 1. the planes' touched-cell boxes
-        if (threadIdx.x < 6) {
-            s_box[threadIdx.x][0] = INT_MAX; s_box[threadIdx.x][1] = INT_MIN;
-            s_box[threadIdx.x][2] = INT_MAX; s_box[threadIdx.x][3] = INT_MIN;
-        }
-        __syncthreads();
-        if (q == 0) {
-            int bx[6][4];
-#pragma unroll
-            for (int p = 0; p < 6; p++) { bx[p][0] = INT_MAX; bx[p][1] = INT_MIN; bx[p][2] = INT_MAX; bx[p][3] = INT_MIN; }
-            for (int c = 0; c < cpw; c++) {
-                const int n = point_of(c);
-                if (n < 0) break;
-                const float4 p4 = reinterpret_cast<const float4 *>(pts)[n];
-                const float pc[4] = {p4.x, p4.y, p4.z, p4.w};
-#pragma unroll
-                for (int p = 0; p < 6; p++) {
-                    const gs4d_hexplane_plane pl = lay.plane[6 * l + p];
-                    const Tap t = make_tap(pc[kPairC0[p]], pc[kPairC1[p]], pl.W, pl.H);
-                    // taps x0, x0 + 1 (y likewise) clipped to the plane: the cells make_tap keeps
-                    bx[p][0] = min(bx[p][0], max(t.x0, 0));
-                    bx[p][1] = max(bx[p][1], min(t.x0 + 1, pl.W - 1));
-                    bx[p][2] = min(bx[p][2], max(t.y0, 0));
-                    bx[p][3] = max(bx[p][3], min(t.y0 + 1, pl.H - 1));
-                }
-            }
-#pragma unroll
-            for (int p = 0; p < 6; p++) {
-                atomicMin(&s_box[p][0], bx[p][0]); atomicMax(&s_box[p][1], bx[p][1]);
-                atomicMin(&s_box[p][2], bx[p][2]); atomicMax(&s_box[p][3], bx[p][3]);
-            }
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            int used = 0;
-            for (int p = 0; p < 6; p++) {
-                const int w = s_box[p][1] - s_box[p][0] + 1, h = s_box[p][3] - s_box[p][2] + 1;
-                const int need = (w > 0 && h > 0) ? w * h * F : 0;
-                if (need > 0 && used + need <= kHexLdsFloats) {
-                    s_off[p] = used;
-                    used += need;
-                } else {
-                    s_off[p] = -1;
-                }
-            }
-            s_used = used;
-        }
-        __syncthreads();
-        const int used = s_used;
-        for (int e = threadIdx.x; e < used; e += kHexThreads) s_win[e] = 0.f;
-        __syncthreads();
-        // 2. gradients
+        // 1. reverse passes
         for (int c = 0; c < cpw; c++) {
-            const int n = point_of(c);
-            if (n < 0) break;
+            const int j = c * ppc + slot;
+            const int64_t i = first + j;
+            const int n = i < N ? (order ? (int)order[i] : (int)i) : -1;
+            if (n < 0) {
+                if (q == 0)
+                    for (int p = 0; p < 6; p++) s_anc[p * npw + j] = -1;
+                continue;
+            }
             const float4 p4 = reinterpret_cast<const float4 *>(pts)[n];
             const float pc[4] = {p4.x, p4.y, p4.z, p4.w};
             float gpt[4] = {0.f, 0.f, 0.f, 0.f};
@@ -259,28 +263,11 @@ __global__ __launch_bounds__(kHexThreads) void hexplane_backward_kernel(int N, c
                     gix += sel(r.v11, k) * (t.iy - y0) * go;
                     giy += sel(r.v11, k) * (t.ix - x0) * go;
                 }
-                const int cells[4] = {t.i00, t.i10, t.i01, t.i11};
-                const float ws[4] = {t.w00, t.w10, t.w01, t.w11};
-                const int off = s_off[p];
-                if (off >= 0) {
-                    const int bx0 = s_box[p][0], by0 = s_box[p][2], bw = s_box[p][1] - bx0 + 1;
-#pragma unroll
-                    for (int cc = 0; cc < 4; cc++) {
-                        if (cells[cc] < 0) continue;
-                        const int cy = cells[cc] / pl.W, cx = cells[cc] - cy * pl.W;
-                        float *dst = s_win + off + ((cy - by0) * bw + (cx - bx0)) * F + 4 * q;
-#pragma unroll
-                        for (int k = 0; k < 4; k++) atomicAdd(dst + k, ws[cc] * dv[k]);
-                    }
-                } else {
-                    float *dpl = dpacked + pl.offset + 4 * q;
-#pragma unroll
-                    for (int cc = 0; cc < 4; cc++) {
-                        if (cells[cc] < 0) continue;
-                        float *dst = dpl + (size_t)cells[cc] * F;
-#pragma unroll
-                        for (int k = 0; k < 4; k++) unsafeAtomicAdd(dst + k, ws[cc] * dv[k]);
-                    }
+                *reinterpret_cast<float4 *>(s_dv + (p * npw + j) * F + 4 * q) = make_float4(dv[0], dv[1], dv[2], dv[3]);
+                if (q == 0) {
+                    const bool ok = t.x0 >= 0 && t.x0 < pl.W && t.y0 >= 0 && t.y0 < pl.H;  // false for NaN
+                    s_anc[p * npw + j] = ok ? (t.y0 << 16) | t.x0 : -1;
+                    s_ixy[p * npw + j] = make_float2(t.ix, t.iy);
                 }
                 gpt[kPairC0[p]] += t.gxm * gix;
                 gpt[kPairC1[p]] += t.gym * giy;
@@ -297,21 +284,165 @@ __global__ __launch_bounds__(kHexThreads) void hexplane_backward_kernel(int N, c
             }
         }
         __syncthreads();
-        // 3. the boxes to HBM (rows of the box are contiguous cells x F floats in the packed layout)
-        for (int p = 0; p < 6; p++) {
-            const int off = s_off[p];
-            if (off < 0) continue;
-            const gs4d_hexplane_plane pl = lay.plane[6 * l + p];
-            const int bx0 = s_box[p][0], by0 = s_box[p][2], bw = s_box[p][1] - bx0 + 1;
-            const int row = bw * F, cnt = row * (s_box[p][3] - by0 + 1);
-            for (int e = threadIdx.x; e < cnt; e += kHexThreads) {
-                const float val = s_win[off + e];
-                if (val == 0.f) continue;
-                const int ry = e / row, rx = e - ry * row;
-                unsafeAtomicAdd(dpacked + pl.offset + ((size_t)(by0 + ry) * pl.W + bx0) * F + rx, val);
+        // 2a. the anchors' boxes of the 6 planes (wave min/max, then over the waves)
+        {
+            int bx[6][4];
+#pragma unroll
+            for (int p = 0; p < 6; p++) {
+                const int a = threadIdx.x < npw ? s_anc[p * npw + threadIdx.x] : -1;
+                const bool ok = a >= 0;
+                bx[p][0] = ok ? (a & 0xFFFF) : INT_MAX;
+                bx[p][1] = ok ? (a >> 16) : INT_MAX;
+                bx[p][2] = ok ? (a & 0xFFFF) : INT_MIN;
+                bx[p][3] = ok ? (a >> 16) : INT_MIN;
             }
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1)
+#pragma unroll
+                for (int p = 0; p < 6; p++) {
+                    bx[p][0] = min(bx[p][0], __shfl_xor(bx[p][0], o, 64));
+                    bx[p][1] = min(bx[p][1], __shfl_xor(bx[p][1], o, 64));
+                    bx[p][2] = max(bx[p][2], __shfl_xor(bx[p][2], o, 64));
+                    bx[p][3] = max(bx[p][3], __shfl_xor(bx[p][3], o, 64));
+                }
+            if (lane == 0)
+#pragma unroll
+                for (int p = 0; p < 6; p++)
+#pragma unroll
+                    for (int k = 0; k < 4; k++) s_wbox[(wv * 6 + p) * 4 + k] = bx[p][k];
         }
         __syncthreads();
+        if (threadIdx.x < 6) {
+            const int p = threadIdx.x;
+            int x0 = INT_MAX, y0 = INT_MAX, x1 = INT_MIN, y1 = INT_MIN;
+            for (int w = 0; w < kHexThreads / 64; w++) {
+                x0 = min(x0, s_wbox[(w * 6 + p) * 4 + 0]);
+                y0 = min(y0, s_wbox[(w * 6 + p) * 4 + 1]);
+                x1 = max(x1, s_wbox[(w * 6 + p) * 4 + 2]);
+                y1 = max(y1, s_wbox[(w * 6 + p) * 4 + 3]);
+            }
+            s_box[p * 4 + 0] = x0;
+            s_box[p * 4 + 1] = y0;
+            s_box[p * 4 + 2] = x1 >= x0 ? x1 - x0 + 1 : 0;
+            s_box[p * 4 + 3] = y1 >= y0 ? y1 - y0 + 1 : 0;
+        }
+        __syncthreads();
+        // 2b. per plane: bucket the points by anchor, gather each touched (cell, feature)
+        for (int p = 0; p < 6; p++) {
+            const gs4d_hexplane_plane pl = lay.plane[6 * l + p];
+            const int ax0 = s_box[p * 4 + 0], ay0 = s_box[p * 4 + 1], aw = s_box[p * 4 + 2], ah = s_box[p * 4 + 3];
+            const int na = aw * ah;
+            if (na == 0) continue;  // uniform
+            const float *dvp = s_dv + p * npw * F;
+            const int *ancp = s_anc + p * npw;
+            const float2 *ixyp = s_ixy + p * npw;
+            float *dpl = dpacked + pl.offset;
+            if ((min(ax0 + aw, pl.W - 1) - ax0 + 1) * (min(ay0 + ah, pl.H - 1) - ay0 + 1) > kHexMaxCells) {
+                // uniform: a box too large for the cell offsets -- direct atomics per (point, feature)
+                for (int e = threadIdx.x; e < npw * F; e += kHexThreads) {
+                    const int j = e / F, f = e - j * F;
+                    const int a = ancp[j];
+                    if (a < 0) continue;
+                    const int x0 = a & 0xFFFF, y0 = a >> 16;
+                    const float2 ixy = ixyp[j];
+                    const float d = dvp[j * F + f];
+                    const float xa = (float)(x0 + 1) - ixy.x, xb = ixy.x - (float)x0;
+                    const float ya = (float)(y0 + 1) - ixy.y, yb = ixy.y - (float)y0;
+                    const bool in_x1 = x0 + 1 < pl.W, in_y1 = y0 + 1 < pl.H;
+                    float *b0 = dpl + ((size_t)y0 * pl.W + x0) * F + f;
+                    unsafeAtomicAdd(b0, (xa * ya) * d);
+                    if (in_x1) unsafeAtomicAdd(b0 + F, (xb * ya) * d);
+                    if (in_y1) unsafeAtomicAdd(b0 + (size_t)pl.W * F, (xa * yb) * d);
+                    if (in_x1 && in_y1) unsafeAtomicAdd(b0 + (size_t)(pl.W + 1) * F, (xb * yb) * d);
+                }
+                continue;
+            }
+            // the touched cells' box; each point's <= 4 taps counting-sorted by cell: s_off <- counts,
+            // the taps' ranks within their cells kept in registers
+            const int cw = min(ax0 + aw, pl.W - 1) - ax0 + 1, ch = min(ay0 + ah, pl.H - 1) - ay0 + 1;
+            const int nc = cw * ch;
+            for (int e = threadIdx.x; e <= nc; e += kHexThreads) s_off[e] = 0;
+            __syncthreads();
+            int tc[4] = {-1, -1, -1, -1}, tr[4] = {0, 0, 0, 0};
+            float tw[4] = {0.f, 0.f, 0.f, 0.f};
+            if (threadIdx.x < npw) {
+                const int a = ancp[threadIdx.x];
+                if (a >= 0) {
+                    const int x0 = a & 0xFFFF, y0 = a >> 16, lx = x0 - ax0, ly = y0 - ay0;
+                    const float2 ixy = ixyp[threadIdx.x];
+                    // make_tap's weights: w00, w10, w01, w11
+                    const float xa = (float)(x0 + 1) - ixy.x, xb = ixy.x - (float)x0;
+                    const float ya = (float)(y0 + 1) - ixy.y, yb = ixy.y - (float)y0;
+                    const bool in_x1 = x0 + 1 < pl.W, in_y1 = y0 + 1 < pl.H;
+                    tc[0] = ly * cw + lx;
+                    tw[0] = xa * ya;
+                    if (in_x1) tc[1] = tc[0] + 1, tw[1] = xb * ya;
+                    if (in_y1) tc[2] = tc[0] + cw, tw[2] = xa * yb;
+                    if (in_x1 && in_y1) tc[3] = tc[0] + cw + 1, tw[3] = xb * yb;
+#pragma unroll
+                    for (int t = 0; t < 4; t++)
+                        if (tc[t] >= 0) tr[t] = atomicAdd(&s_off[tc[t]], 1);
+                }
+            }
+            __syncthreads();
+            int ntouched;
+            {
+                // exclusive scan of s_off[0, nc) (four entries per thread, nc <= kHexMaxCells), the tap
+                // counts in the low 16 bits and the touched-cell flags in the high 16: the cells' first
+                // taps and the compact list of touched cells from one scan
+                const int e0 = 4 * threadIdx.x;
+                int c[4], v = 0;
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    c[u] = e0 + u < nc ? s_off[e0 + u] : 0;
+                    v += c[u] + (c[u] > 0 ? 0x10000 : 0);
+                }
+                int tot;
+                int ex = block_excl_scan(v, s_tmp, tot);
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    if (e0 + u < nc) {
+                        s_off[e0 + u] = ex & 0xFFFF;
+                        if (c[u] > 0) {
+                            s_cells[ex >> 16] = (uint16_t)(e0 + u);
+                            s_cstart[ex >> 16] = (uint16_t)(ex & 0xFFFF);
+                        }
+                    }
+                    ex += c[u] + (c[u] > 0 ? 0x10000 : 0);
+                }
+                ntouched = tot >> 16;
+                if (threadIdx.x == 0) s_cstart[ntouched] = (uint16_t)(tot & 0xFFFF);
+            }
+            __syncthreads();
+#pragma unroll
+            for (int t = 0; t < 4; t++)
+                if (tc[t] >= 0) {
+                    const int k = s_off[tc[t]] + tr[t];
+                    s_pj[k] = (uint16_t)threadIdx.x;
+                    s_pw[k] = tw[t];
+                }
+            __syncthreads();
+            // gather: (touched cell, 4 features) per item, over the cell's taps in LDS
+            const int nb = F / 4;
+            for (int e = threadIdx.x; e < ntouched * nb; e += kHexThreads) {
+                const int r = e / nb, b4 = e - r * nb;
+                const int cell = s_cells[r], k0 = s_cstart[r], k1 = s_cstart[r + 1];
+                float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+                for (int k = k0; k < k1; k++) {
+                    const int j = s_pj[k];
+                    const float w = s_pw[k];
+                    const float4 d = *reinterpret_cast<const float4 *>(dvp + j * F + 4 * b4);
+                    acc.x += w * d.x; acc.y += w * d.y; acc.z += w * d.z; acc.w += w * d.w;
+                }
+                const int ry = cell / cw, rx = cell - ry * cw;
+                float *dst = dpl + ((size_t)(ay0 + ry) * pl.W + ax0 + rx) * F + 4 * b4;
+                if (acc.x != 0.f) unsafeAtomicAdd(dst + 0, acc.x);
+                if (acc.y != 0.f) unsafeAtomicAdd(dst + 1, acc.y);
+                if (acc.z != 0.f) unsafeAtomicAdd(dst + 2, acc.z);
+                if (acc.w != 0.f) unsafeAtomicAdd(dst + 3, acc.w);
+            }
+            __syncthreads();
+        }
     }
 }
 
@@ -383,7 +514,7 @@ int gs4d_hexplane_layout_init(gs4d_hexplane_layout *lay, int levels, int F, cons
     lay->F = F;
     int64_t off = 0;
     for (int i = 0; i < 6 * levels; i++) {
-        if (W[i] < 1 || H[i] < 1) return 1;
+        if (W[i] < 1 || H[i] < 1 || W[i] > 65535 || H[i] > 65535) return 1;  // anchors pack as 16 + 16 bits
         lay->plane[i].W = W[i];
         lay->plane[i].H = H[i];
         lay->plane[i].offset = off;
@@ -462,9 +593,9 @@ int gs4d_hexplane_backward(int N, const float *pts, const uint32_t *order, const
     if (N < 0 || !lay || (N > 0 && (!pts || !packed || !dfeat || !dpacked || !dpts))) return 1;
     if (((size_t)pts & 15) || ((size_t)packed & 15) || ((size_t)dfeat & 15) || ((size_t)dpts & 15)) return 1;
     if (N == 0) return 0;
-    const int ppc = kHexThreads / (lay->F / 4);
-    const int64_t per_wg = (int64_t)std::max(1, kHexPointsPerWG / ppc) * ppc;
+    const int64_t per_wg = hex_points_per_wg(lay->F);
     const int64_t nwg = ((int64_t)N + per_wg - 1) / per_wg;
+    if (hex_bwd_lds_words(lay->F) > kHexLdsWords) return 1;
     hipLaunchKernelGGL(hexplane_backward_kernel, dim3((unsigned)nwg), dim3(kHexThreads), 0, (hipStream_t)stream, N, pts,
                        order, *lay, packed, dfeat, dpacked, dpts);
     return hipGetLastError() == hipSuccess ? 0 : 3;

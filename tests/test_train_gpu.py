@@ -87,12 +87,13 @@ def _field(F=16, reso=(64, 64, 64, 150), multires=(1, 2)):
     return f
 
 
-@pytest.mark.parametrize("F", [16, 32])
-def test_hexplane_fused_matches_grid_sample(F):
+@pytest.mark.parametrize("F,N", [(4, 20000), (8, 20000), (16, 20000), (32, 20000), (16, 100_000)])
+def test_hexplane_fused_matches_grid_sample(F, N):
+    """N = 20000 points spread over the field: many workgroups' cell boxes exceed the LDS bound and take
+    the direct-atomic path; N = 100k: dense enough that most go through the LDS tap sort + gather."""
     from gs4d_train.deformation import interpolate_ms_features
     from gs4d_train.kernels import hexplane
     f = _field(F)
-    N = 20000
     g = torch.Generator(device="cuda").manual_seed(4)
     pts = torch.rand(N, 4, device="cuda", generator=g) * 2.4 - 1.2  # incl. border-clamped coordinates
     pts[:100, 0] = 1.0      # exactly on the border (clipped: zero coordinate gradient)
