@@ -271,7 +271,48 @@ std::vector<torch::Tensor> linear_dw(const std::vector<torch::Tensor> &dys, cons
     return out;
 }
 
+// ---- heads block backward: (da, db1, [dW2_i, db2_i]...) for a (P, kW), g_i (P, n_i), W2_i (n_i, W)
+std::vector<torch::Tensor> heads_backward(const torch::Tensor &a, const std::vector<torch::Tensor> &gs,
+                                          const std::vector<torch::Tensor> &w2s) {
+    const int k = (int)gs.size();
+    need(k >= 1 && k <= GS4D_HEADS_MAX && (int)w2s.size() == k, "heads_backward: 1-8 heads");
+    need(a.is_cuda() && a.scalar_type() == torch::kFloat32 && a.dim() == 2 && a.is_contiguous(),
+         "heads_backward: a contiguous float32 (P, kW) GPU tensor");
+    need(a.size(1) % k == 0, "heads_backward: a must be (P, kW)");
+    c10::hip::HIPGuard guard(a.device().index());
+    gs4d_heads_bwd b{};
+    b.P = (int)a.size(0), b.k = k, b.W = (int)(a.size(1) / k);
+    auto da = torch::empty_like(a);
+    auto db1 = torch::empty({a.size(1)}, a.options());
+    b.a = a.data_ptr<float>(), b.da = da.data_ptr<float>(), b.db1 = db1.data_ptr<float>();
+    std::vector<torch::Tensor> out = {da, db1};
+    std::vector<torch::Tensor> keep;
+    for (int i = 0; i < k; i++) {
+        auto g = gs[i].contiguous();
+        const auto &w2 = w2s[i];
+        need(g.is_cuda() && g.scalar_type() == torch::kFloat32 && g.dim() == 2 && g.size(0) == b.P,
+             "heads_backward: g_i (P, n_i) float32");
+        need(w2.is_cuda() && w2.scalar_type() == torch::kFloat32 && w2.dim() == 2 && w2.is_contiguous() &&
+                 w2.size(0) == g.size(1) && w2.size(1) == b.W,
+             "heads_backward: W2_i (n_i, W) contiguous float32");
+        b.n[i] = (int)g.size(1);
+        b.g[i] = g.data_ptr<float>();
+        b.w2[i] = w2.data_ptr<float>();
+        auto dw2 = torch::empty({g.size(1), b.W}, a.options());
+        auto db2 = torch::empty({g.size(1)}, a.options());
+        b.dw2[i] = dw2.data_ptr<float>(), b.db2[i] = db2.data_ptr<float>();
+        out.push_back(dw2);
+        out.push_back(db2);
+        keep.push_back(g);
+    }
+    const size_t sb = gs4d_heads_backward_scratch_bytes(b.P, b.W, k, b.n);
+    auto scratch = torch::empty({(int64_t)sb}, a.options().dtype(torch::kUInt8));
+    check(gs4d_heads_backward(&b, scratch.data_ptr(), (void *)stream_of(a)), "heads_backward");
+    return out;
+}
+
 PYBIND11_MODULE(_C, m) {
+    m.def("heads_backward", &heads_backward);
     m.def("linear_dw", &linear_dw);
     m.def("hexplane_reg_forward", &hexplane_reg_forward);
     m.def("hexplane_reg_backward", &hexplane_reg_backward);

@@ -343,6 +343,135 @@ __global__ __launch_bounds__(256) void linear_dw_reduce_kernel(DwBatch b, int W,
     }
 }
 
+// ---- the deformation heads' second layers, backward, in one pass over the first layers' output ------
+// For k heads (scene/deformation.py:73-78: ReLU -> Linear(W, W) -> ReLU -> Linear(W, n_i)) evaluated as
+// one block (gs4d_train/deformation.py _DeformHeads): a = relu(h W1^T + b1) is (P, kW), head i's output
+// is a[:, iW:(i+1)W] W2_i^T + b2_i.  Given the output gradients g_i (P, n_i) this forms, reading `a` once:
+//   da[:, iW + c] = (a > 0) * sum_r g_i[:, r] W2_i[r, c]   (mm + threshold_backward in autograd)
+//   db1 = column sums of da,  dW2_i = g_i^T a_i,  db2_i = column sums of g_i.
+// A workgroup takes a block of rows; thread c owns column c of a (kW <= 1024 threads, head = c / W is
+// wave-uniform): its W2_i column and dW2_i accumulators stay in registers, the g_i row is wave-uniform
+// (scalar loads).  Per-workgroup partials are summed in a fixed order by a second launch.
+constexpr int kHbMaxHeads = 8;
+struct HbArgs {
+    int P, W, k, rows_per_wg;
+    int n[kHbMaxHeads];
+    const float *w2[kHbMaxHeads];
+    int poff[kHbMaxHeads + 1];  // head i's partials: n_i * (W + 1) floats from poff[i]; poff[0] = k W
+};
+
+template <int N, bool EXACT, int U>
+__device__ __forceinline__ void heads_bwd_cols(const HbArgs &A, int h, const float *__restrict__ a,
+                                               float *__restrict__ da, const float *__restrict__ g,
+                                               float *__restrict__ part) {
+    const int W = A.W, ld = A.k * W;
+    const int col = threadIdx.x, c = col - h * W;
+    const int lane = threadIdx.x & 63;
+    const bool lead = c < 64;  // the head's first wave: db2 partials
+    const int n = EXACT ? N : A.n[h];
+    const float *__restrict__ w2 = A.w2[h];
+    float w[N], acc[N];
+#pragma unroll
+    for (int r = 0; r < N; r++) {
+        w[r] = (EXACT || r < n) ? w2[r * W + c] : 0.f;
+        acc[r] = 0.f;
+    }
+    float csum = 0.f, bsum = 0.f;
+    const int64_t p0 = (int64_t)blockIdx.x * A.rows_per_wg, p1 = min((int64_t)A.P, p0 + A.rows_per_wg);
+    for (int64_t p = p0; p < p1; p += U) {
+        float x[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) x[u] = p + u < p1 ? a[(p + u) * ld + col] : 0.f;
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            if (p + u < p1) {
+                const float *__restrict__ d = g + (p + u) * n;
+                float sdot = 0.f;
+#pragma unroll
+                for (int r = 0; r < N; r++)
+                    if (EXACT || r < n) {
+                        const float dv = d[r];
+                        sdot = fmaf(dv, w[r], sdot);
+                        acc[r] = fmaf(dv, x[u], acc[r]);
+                    }
+                const float gv = x[u] > 0.f ? sdot : 0.f;
+                da[(p + u) * ld + col] = gv;
+                csum += gv;
+                if (lead && lane < n) bsum += d[lane];
+            }
+        }
+    }
+    float *pw = part + (size_t)blockIdx.x * A.poff[A.k];
+    pw[col] = csum;
+    float *ph = pw + A.poff[h];
+#pragma unroll
+    for (int r = 0; r < N; r++)
+        if (EXACT || r < n) ph[r * (W + 1) + c] = acc[r];
+    if (lead && lane < n) ph[lane * (W + 1) + W] = bsum;
+}
+
+__global__ __launch_bounds__(1024) void heads_bwd_kernel(HbArgs A, const float *__restrict__ a, float *__restrict__ da,
+                                                         const float *__restrict__ g0, const float *__restrict__ g1,
+                                                         const float *__restrict__ g2, const float *__restrict__ g3,
+                                                         const float *__restrict__ g4, const float *__restrict__ g5,
+                                                         const float *__restrict__ g6, const float *__restrict__ g7,
+                                                         float *__restrict__ part) {
+    const int h = __builtin_amdgcn_readfirstlane((int)threadIdx.x / A.W);
+    const float *__restrict__ g = h == 0 ? g0 : h == 1 ? g1 : h == 2 ? g2 : h == 3 ? g3 : h == 4 ? g4 : h == 5 ? g5
+                                : h == 6 ? g6 : g7;
+    switch (A.n[h]) {
+    case 1: heads_bwd_cols<1, true, 8>(A, h, a, da, g, part); break;
+    case 2: heads_bwd_cols<2, true, 8>(A, h, a, da, g, part); break;
+    case 3: heads_bwd_cols<3, true, 8>(A, h, a, da, g, part); break;
+    case 4: heads_bwd_cols<4, true, 8>(A, h, a, da, g, part); break;
+    case 48: heads_bwd_cols<48, true, 4>(A, h, a, da, g, part); break;
+    default:
+        if (A.n[h] <= 8) heads_bwd_cols<8, false, 8>(A, h, a, da, g, part);
+        else heads_bwd_cols<16, false, 4>(A, h, a, da, g, part);
+    }
+}
+
+// the partials summed over the workgroups (32 record entries per workgroup, 8 eighths in a fixed
+// order) and routed to db1 / dW2_i / db2_i
+struct HbOut {
+    float *db1;
+    float *dw2[kHbMaxHeads];
+    float *db2[kHbMaxHeads];
+};
+__global__ __launch_bounds__(256) void heads_bwd_reduce_kernel(HbArgs A, HbOut O, int nwg, const float *__restrict__ part) {
+    __shared__ float s_sum[8][32];
+    const int per = A.poff[A.k];
+    const int o = threadIdx.x & 31, q = threadIdx.x >> 5;
+    const int i = blockIdx.x * 32 + o;
+    float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
+    if (i < per) {
+        int w = q;
+        for (; w + 24 < nwg; w += 32) {
+            v0 += part[(size_t)w * per + i];
+            v1 += part[(size_t)(w + 8) * per + i];
+            v2 += part[(size_t)(w + 16) * per + i];
+            v3 += part[(size_t)(w + 24) * per + i];
+        }
+        for (; w < nwg; w += 8) v0 += part[(size_t)w * per + i];
+    }
+    s_sum[q][o] = (v0 + v1) + (v2 + v3);
+    __syncthreads();
+    if (q == 0 && i < per) {
+        float t = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; e++) t += s_sum[e][o];
+        if (i < A.poff[0]) {
+            O.db1[i] = t;
+        } else {
+            int h = 0;
+            while (h + 1 < A.k && i >= A.poff[h + 1]) h++;
+            const int e = i - A.poff[h], r = e / (A.W + 1), c = e - r * (A.W + 1);
+            if (c < A.W) O.dw2[h][r * A.W + c] = t;
+            else O.db2[h][r] = t;
+        }
+    }
+}
+
 static int dw_rows_per_wg(int P, int nmax) {
     // enough workgroups to cover the chip, few enough that the partials stay small next to x
     (void)P;
@@ -354,6 +483,53 @@ static int dw_rows_per_wg(int P, int nmax) {
 using namespace gs4d;
 
 extern "C" {
+
+static int hb_rows_per_wg(int P) {
+    // about two workgroups per CU, at least 64 rows each
+    return std::max(64, (P + 511) / 512);
+}
+
+size_t gs4d_heads_backward_scratch_bytes(int P, int W, int k, const int *n) {
+    if (P < 0 || W < 1 || k < 1 || k > kHbMaxHeads || !n) return 0;
+    size_t per = (size_t)k * W;
+    for (int i = 0; i < k; i++) per += (size_t)std::max(n[i], 0) * (W + 1);
+    const size_t nwg = std::max<size_t>(1, ((size_t)P + hb_rows_per_wg(P) - 1) / hb_rows_per_wg(P));
+    return 4 * nwg * per + 256;
+}
+
+int gs4d_heads_backward(const gs4d_heads_bwd *args, void *scratch, void *stream) {
+    if (!args || !scratch) return 1;
+    const gs4d_heads_bwd &b = *args;
+    if (b.P < 0 || (b.W != 64 && b.W != 128 && b.W != 256) || b.k < 1 || b.k > kHbMaxHeads || b.k * b.W > 1024 ||
+        !b.db1)
+        return 1;
+    if (b.P > 0 && (!b.a || !b.da)) return 1;
+    HbArgs A{};
+    HbOut O{};
+    A.P = b.P, A.W = b.W, A.k = b.k, A.rows_per_wg = hb_rows_per_wg(b.P);
+    A.poff[0] = b.k * b.W;
+    const float *g[kHbMaxHeads] = {};
+    for (int i = 0; i < b.k; i++) {
+        if (b.n[i] < 1 || (b.n[i] > 16 && b.n[i] != 48) || !b.w2[i] || !b.dw2[i] || !b.db2[i] || (b.P > 0 && !b.g[i]))
+            return 1;
+        A.n[i] = b.n[i], A.w2[i] = b.w2[i], g[i] = b.g[i];
+        A.poff[i + 1] = A.poff[i] + b.n[i] * (b.W + 1);
+        O.dw2[i] = b.dw2[i], O.db2[i] = b.db2[i];
+    }
+    O.db1 = b.db1;
+    hipStream_t s = (hipStream_t)stream;
+    const int nwg = std::max(1, (int)(((int64_t)b.P + A.rows_per_wg - 1) / A.rows_per_wg));
+    float *part = (float *)align_up((size_t)scratch, 256);
+    if (b.P == 0) {  // empty sums: the partials of one empty workgroup
+        if (hipMemsetAsync(part, 0, 4 * (size_t)A.poff[b.k], s) != hipSuccess) return 3;
+    } else {
+        hipLaunchKernelGGL(heads_bwd_kernel, dim3(nwg), dim3(b.k * b.W), 0, s, A, b.a, b.da, g[0], g[1], g[2], g[3],
+                           g[4], g[5], g[6], g[7], part);
+    }
+    hipLaunchKernelGGL(heads_bwd_reduce_kernel, dim3((A.poff[b.k] + 31) / 32), dim3(256), 0, s, A, O, nwg,
+                       (const float *)part);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+}
 
 size_t gs4d_linear_dw_scratch_bytes(int P, int W, int count, const int *n) {
     if (P < 0 || W < 1 || count < 1 || count > kDwMaxProblems || !n) return 0;

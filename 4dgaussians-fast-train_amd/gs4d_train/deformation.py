@@ -167,8 +167,10 @@ class _DeformHeads(torch.autograd.Function):
     input, ONE (P x W) @ (W x kW) GEMM for the k first layers (weights concatenated), one ReLU, then
     the k small second layers on column slices.  The backward mirrors it: the k (P x n) @ (n x W)
     products land in column slices of one (P x kW) gradient, then one ReLU mask, one GEMM with K = kW
-    for the input gradient and one split-K GEMM for the concatenated first-layer weight gradient; the
-    narrow second layers' weight and bias gradients (n <= 8) come from one gs4d_linear_dw launch.
+    for the input gradient and one split-K GEMM for the concatenated first-layer weight gradient.  On
+    the GPU the second layers' backward, the ReLU mask and the first-layer bias gradient are one HIP
+    pass over the first layers' output (gs4d_heads_backward); the PyTorch formulation below it is the
+    CPU path (and the narrow heads' dW/db there come from gs4d_linear_dw when on the GPU).
     Same function as the k separate heads (and the same parameters, concatenated per call); the
     GEMMs sum in a different order, so results agree to fp32 rounding."""
 
@@ -187,12 +189,22 @@ class _DeformHeads(torch.autograd.Function):
     def backward(ctx, *douts):
         h, a, w1, *w2 = ctx.saved_tensors
         W, k = ctx.W, len(w2)
+        douts = [d if d is not None else torch.zeros(a.shape[0], w2[i].shape[0], device=a.device)
+                 for i, d in enumerate(douts)]
+        if a.is_cuda and W in (64, 128, 256) and k * W <= 1024 and all(x.shape[0] <= 16 or x.shape[0] == 48
+                                                                        for x in w2):
+            # second layers' backward + ReLU mask + first-layer bias gradient in one HIP pass over a
+            from . import _C
+            out = _C.heads_backward(a, list(douts), [x.contiguous() for x in w2])
+            da, db1 = out[0], out[1]
+            dw1 = _splitk_dw(da, h)
+            dh = torch.ops.aten.threshold_backward(da @ w1, h, 0)
+            return tuple([dh, dw1, db1] + out[2:])
         da = torch.empty_like(a)
         dw2, db2 = [None] * k, [None] * k
         small = []  # heads whose (dw, db) one gs4d_linear_dw launch forms (n <= 8)
         for i in range(k):
-            do = douts[i] if douts[i] is not None else torch.zeros(a.shape[0], w2[i].shape[0], device=a.device)
-            do = do.contiguous()
+            do = douts[i].contiguous()
             sl = a[:, i * W:(i + 1) * W]
             torch.mm(do, w2[i], out=da[:, i * W:(i + 1) * W])
             if do.shape[1] <= 8 and W in (64, 128, 256):

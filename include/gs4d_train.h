@@ -133,6 +133,28 @@ typedef struct gs4d_dw_problem {
 size_t gs4d_linear_dw_scratch_bytes(int P, int W, int count, const int *n);
 int gs4d_linear_dw(int P, int W, int count, const gs4d_dw_problem *problems, void *scratch, void *stream);
 
+/* ---- The deformation heads' second layers, backward (scene/deformation.py:73-78, evaluated as one
+ * block: a = relu(h W1^T + b1) of shape (P, kW), head i = a[:, iW:(i+1)W] W2_i^T + b2_i), in one pass
+ * over a: da = (a > 0) * [g_0 W2_0 | ... | g_{k-1} W2_{k-1}] (P, kW), db1 = column sums of da, and for each
+ * head dW2_i = g_i^T a_i (n_i, W), db2_i = column sums of g_i -- what autograd forms with k mm, one
+ * threshold_backward, a sum and 2k weight/bias reductions.  W in {64, 128, 256}, k W <= 1024, n_i <= 16
+ * or n_i = 48; g_i (P, n_i) contiguous, a and da (P, kW) contiguous, W2_i (n_i, W).  fp32, partial sums
+ * reduced in a fixed order. */
+#define GS4D_HEADS_MAX 8
+typedef struct gs4d_heads_bwd {
+    int P, W, k;
+    const float *a;
+    float *da;
+    float *db1;
+    int n[GS4D_HEADS_MAX];
+    const float *g[GS4D_HEADS_MAX];
+    const float *w2[GS4D_HEADS_MAX];
+    float *dw2[GS4D_HEADS_MAX];
+    float *db2[GS4D_HEADS_MAX];
+} gs4d_heads_bwd;
+size_t gs4d_heads_backward_scratch_bytes(int P, int W, int k, const int *n);
+int gs4d_heads_backward(const gs4d_heads_bwd *args, void *scratch, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -170,6 +170,37 @@ def test_linear_dw_matches_fp64(P, W, ns):
         assert float((out[2 * i + 1].double() - rb).abs().max() / sb) <= 1e-5
 
 
+@pytest.mark.parametrize("P,W,ns", [(100_003, 128, [3, 3, 4, 1, 48]), (777, 64, [2, 16, 5]), (1, 256, [1, 48]),
+                                     (0, 128, [3, 4])])
+def test_heads_backward_matches_fp64(P, W, ns):
+    """gs4d_heads_backward (the heads block's second layers + ReLU mask + first-layer bias gradient in one
+    pass) vs the same products in fp64 torch: da to 1e-5 of its row's |terms| sum, the reductions to 1e-5 of
+    their largest |term| sum; the mask exact (a > 0, zeros kept); ragged P, P = 1 and P = 0."""
+    from gs4d_train import _C
+    torch.manual_seed(P + W)
+    k = len(ns)
+    a = torch.relu(torch.randn(P, k * W, device="cuda"))
+    gs = [torch.randn(P, n, device="cuda") for n in ns]
+    w2 = [torch.randn(n, W, device="cuda") for n in ns]
+    out = _C.heads_backward(a, gs, w2)
+    da, db1 = out[0], out[1]
+    ad = a.double()
+    ref = torch.cat([g.double() @ w.double() for g, w in zip(gs, w2)], 1) * (ad > 0)
+    scale = torch.cat([g.double().abs() @ w.double().abs() for g, w in zip(gs, w2)], 1)
+    assert da.shape == a.shape and db1.shape == (k * W,)
+    assert bool(((da == 0) == ((a <= 0) | (ref == 0))).all()) or P == 0
+    assert float(((da.double() - ref).abs() - 1e-5 * scale).max().clamp_min(0)) == 0.0 if P else True
+    s1 = (ref.abs().sum(0).max() if P else torch.tensor(1.0)).clamp_min(1e-30)
+    assert float((db1.double() - ref.sum(0)).abs().max() / s1) <= 1e-5
+    for i, (g, w) in enumerate(zip(gs, w2)):
+        x = ad[:, i * W:(i + 1) * W]
+        rw, rb = g.double().t() @ x, g.double().sum(0)
+        sw = (g.double().abs().t() @ x.abs()).max().clamp_min(1e-30)
+        sb = g.double().abs().sum(0).max().clamp_min(1e-30)
+        assert float((out[2 + 2 * i].double() - rw).abs().max() / sw) <= 1e-5
+        assert float((out[3 + 2 * i].double() - rb).abs().max() / sb) <= 1e-5
+
+
 def test_train_step_fused_matches_torch_tail():
     """One fine-stage step through deformation + rasterizer + loss + densification statistics, fused
     (HexPlane kernel, L1 kernel, stats kernel) vs the reference's torch formulation.  The optimizer is

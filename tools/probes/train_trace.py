@@ -60,11 +60,15 @@ def op_profile(cfg="metric", steps=5):
     for i in range(5):
         train_step(g, views, opt, hyper, 3001 + i, bg)
     torch.cuda.synchronize()
-    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes="--shapes" in sys.argv) as prof:
         for i in range(steps):
             train_step(g, views, opt, hyper, 3006 + i, bg)
         torch.cuda.synchronize()
-    print(prof.key_averages().table(sort_by="cuda_time_total", row_limit=45, max_name_column_width=60))
+    if "--shapes" in sys.argv:
+        print(prof.key_averages(group_by_input_shape=True).table(sort_by="cuda_time_total", row_limit=60,
+                                                                 max_name_column_width=40, max_shapes_column_width=70))
+    else:
+        print(prof.key_averages().table(sort_by="cuda_time_total", row_limit=45, max_name_column_width=60))
 
 
 if __name__ == "__main__":
