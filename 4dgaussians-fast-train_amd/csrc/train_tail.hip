@@ -349,23 +349,33 @@ __global__ __launch_bounds__(256) void linear_dw_reduce_kernel(DwBatch b, int W,
 // is a[:, iW:(i+1)W] W2_i^T + b2_i.  Given the output gradients g_i (P, n_i) this forms, reading `a` once:
 //   da[:, iW + c] = (a > 0) * sum_r g_i[:, r] W2_i[r, c]   (mm + threshold_backward in autograd)
 //   db1 = column sums of da,  dW2_i = g_i^T a_i,  db2_i = column sums of g_i.
-// A workgroup takes a block of rows; thread c owns column c of a (kW <= 1024 threads, head = c / W is
+// A workgroup takes a block of rows; thread c owns column c of a (kW <= 768 threads, head = c / W is
 // wave-uniform): its W2_i column and dW2_i accumulators stay in registers, the g_i row is wave-uniform
 // (scalar loads).  Per-workgroup partials are summed in a fixed order by a second launch.
 constexpr int kHbMaxHeads = 8;
+// One launch serves the heads [h0, h0 + hk) (columns h0 W .. (h0 + hk) W of a): the narrow heads and
+// the 48-wide one go in separate launches, each with its own row blocking, so no workgroup waits on a
+// few compute-heavy waves.
 struct HbArgs {
-    int P, W, k, rows_per_wg;
+    int P, W, k, rows_per_wg, h0, hk;
     int n[kHbMaxHeads];
     const float *w2[kHbMaxHeads];
-    int poff[kHbMaxHeads + 1];  // head i's partials: n_i * (W + 1) floats from poff[i]; poff[0] = k W
+    int poff[kHbMaxHeads + 1];  // local head i's partials: n_{h0+i} (W + 1) floats from poff[i]; poff[0] = hk W
 };
 
+// One wave's columns of head h.  The head's output-gradient rows for U rows at a time are one or a few
+// coalesced vector loads (the U x n block is contiguous in g); each value reaches the FMAs as an SGPR
+// through v_readlane.  The next block's loads are issued before the current block is used.  db2: the
+// lead wave adds the blocks elementwise (flattened index i holds output i mod n) and folds them at the
+// end in a fixed order.
 template <int N, bool EXACT, int U>
 __device__ __forceinline__ void heads_bwd_cols(const HbArgs &A, int h, const float *__restrict__ a,
                                                float *__restrict__ da, const float *__restrict__ g,
-                                               float *__restrict__ part) {
-    const int W = A.W, ld = A.k * W;
-    const int col = threadIdx.x, c = col - h * W;
+                                               float *__restrict__ part, float *s_fold) {
+    constexpr int KG = (U * N + 63) / 64;
+    static_assert(EXACT || KG == 1, "runtime widths keep the block in one register");
+    const int W = A.W, ld = A.k * W, hl = h - A.h0;
+    const int col = A.h0 * W + threadIdx.x, c = (int)threadIdx.x - hl * W;
     const int lane = threadIdx.x & 63;
     const bool lead = c < 64;  // the head's first wave: db2 partials
     const int n = EXACT ? N : A.n[h];
@@ -376,59 +386,175 @@ __device__ __forceinline__ void heads_bwd_cols(const HbArgs &A, int h, const flo
         w[r] = (EXACT || r < n) ? w2[r * W + c] : 0.f;
         acc[r] = 0.f;
     }
-    float csum = 0.f, bsum = 0.f;
-    const int64_t p0 = (int64_t)blockIdx.x * A.rows_per_wg, p1 = min((int64_t)A.P, p0 + A.rows_per_wg);
-    for (int64_t p = p0; p < p1; p += U) {
-        float x[U];
+    float gacc[KG];
 #pragma unroll
-        for (int u = 0; u < U; u++) x[u] = p + u < p1 ? a[(p + u) * ld + col] : 0.f;
+    for (int k = 0; k < KG; k++) gacc[k] = 0.f;
+    float csum = 0.f;
+    const int64_t p0 = (int64_t)blockIdx.x * A.rows_per_wg, p1 = min((int64_t)A.P, p0 + A.rows_per_wg);
+    const int64_t gend = p1 * n;
+    float xn[U], gn[KG];
+    auto fetch = [&](int64_t p) {
+#pragma unroll
+        for (int u = 0; u < U; u++) xn[u] = p + u < p1 ? a[(p + u) * ld + col] : 0.f;
+#pragma unroll
+        for (int k = 0; k < KG; k++) {
+            const int64_t i = p * n + lane + 64 * k;
+            gn[k] = (lane + 64 * k < U * n && i < gend) ? g[i] : 0.f;  // this block's U x n values only
+        }
+    };
+    if (p0 < p1) fetch(p0);
+    for (int64_t p = p0; p < p1; p += U) {
+        float x[U], gv[KG];
+#pragma unroll
+        for (int u = 0; u < U; u++) x[u] = xn[u];
+#pragma unroll
+        for (int k = 0; k < KG; k++) gv[k] = gn[k], gacc[k] += gn[k];
+        if (p + U < p1) fetch(p + U);
 #pragma unroll
         for (int u = 0; u < U; u++) {
             if (p + u < p1) {
-                const float *__restrict__ d = g + (p + u) * n;
                 float sdot = 0.f;
 #pragma unroll
                 for (int r = 0; r < N; r++)
                     if (EXACT || r < n) {
-                        const float dv = d[r];
+                        const int idx = EXACT ? u * N + r : u * n + r;
+                        const float dv = __builtin_bit_cast(
+                            float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, gv[EXACT ? idx / 64 : 0]),
+                                                             EXACT ? idx % 64 : idx));
                         sdot = fmaf(dv, w[r], sdot);
                         acc[r] = fmaf(dv, x[u], acc[r]);
                     }
-                const float gv = x[u] > 0.f ? sdot : 0.f;
-                da[(p + u) * ld + col] = gv;
-                csum += gv;
-                if (lead && lane < n) bsum += d[lane];
+                const float gvv = x[u] > 0.f ? sdot : 0.f;
+                da[(p + u) * ld + col] = gvv;
+                csum += gvv;
             }
         }
     }
-    float *pw = part + (size_t)blockIdx.x * A.poff[A.k];
-    pw[col] = csum;
-    float *ph = pw + A.poff[h];
+    float *pw = part + (size_t)blockIdx.x * A.poff[A.hk];
+    pw[threadIdx.x] = csum;
+    float *ph = pw + A.poff[hl];
 #pragma unroll
     for (int r = 0; r < N; r++)
         if (EXACT || r < n) ph[r * (W + 1) + c] = acc[r];
-    if (lead && lane < n) ph[lane * (W + 1) + W] = bsum;
+    if (lead) {
+        // fold the flattened block sums: output r = sum over flattened indices i with i mod n == r
+        float *f = s_fold + (threadIdx.x >> 6) * 64 * KG;
+#pragma unroll
+        for (int k = 0; k < KG; k++) f[lane + 64 * k] = gacc[k];
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        if (lane < n) {
+            float t = 0.f;
+            for (int i = lane; i < 64 * KG; i += n) t += f[i];
+            ph[lane * (W + 1) + W] = t;
+        }
+    }
 }
 
-__global__ __launch_bounds__(1024) void heads_bwd_kernel(HbArgs A, const float *__restrict__ a, float *__restrict__ da,
+__global__ __launch_bounds__(768) void heads_bwd_kernel(HbArgs A, const float *__restrict__ a, float *__restrict__ da,
                                                          const float *__restrict__ g0, const float *__restrict__ g1,
                                                          const float *__restrict__ g2, const float *__restrict__ g3,
                                                          const float *__restrict__ g4, const float *__restrict__ g5,
                                                          const float *__restrict__ g6, const float *__restrict__ g7,
                                                          float *__restrict__ part) {
-    const int h = __builtin_amdgcn_readfirstlane((int)threadIdx.x / A.W);
+    __shared__ float s_fold[16 * 64];  // per wave: the lead waves' flattened db2 block sums
+    const int h = A.h0 + __builtin_amdgcn_readfirstlane((int)threadIdx.x / A.W);
     const float *__restrict__ g = h == 0 ? g0 : h == 1 ? g1 : h == 2 ? g2 : h == 3 ? g3 : h == 4 ? g4 : h == 5 ? g5
                                 : h == 6 ? g6 : g7;
     switch (A.n[h]) {
-    case 1: heads_bwd_cols<1, true, 8>(A, h, a, da, g, part); break;
-    case 2: heads_bwd_cols<2, true, 8>(A, h, a, da, g, part); break;
-    case 3: heads_bwd_cols<3, true, 8>(A, h, a, da, g, part); break;
-    case 4: heads_bwd_cols<4, true, 8>(A, h, a, da, g, part); break;
-    case 48: heads_bwd_cols<48, true, 4>(A, h, a, da, g, part); break;
+    case 1: heads_bwd_cols<1, true, 8>(A, h, a, da, g, part, s_fold); break;
+    case 2: heads_bwd_cols<2, true, 8>(A, h, a, da, g, part, s_fold); break;
+    case 3: heads_bwd_cols<3, true, 8>(A, h, a, da, g, part, s_fold); break;
+    case 4: heads_bwd_cols<4, true, 8>(A, h, a, da, g, part, s_fold); break;
     default:
-        if (A.n[h] <= 8) heads_bwd_cols<8, false, 8>(A, h, a, da, g, part);
-        else heads_bwd_cols<16, false, 4>(A, h, a, da, g, part);
+        if (A.n[h] <= 8) heads_bwd_cols<8, false, 8>(A, h, a, da, g, part, s_fold);
+        else heads_bwd_cols<16, false, 4>(A, h, a, da, g, part, s_fold);
     }
+}
+
+// The wide head (n = 48: the SH-coefficient deformation): the same products, VALU-bound rather than
+// streaming (96 FMAs per row and column).  Thread c owns column c of the head (W threads); the head's
+// output-gradient rows are staged in LDS in tiles of kWideTile rows (one coalesced load of a contiguous
+// block of g) and read back as broadcasts, four values per ds_read_b128; the dot product (da) and the
+// weight-gradient update (dW2) each take output pairs per v_pk_fma_f32.
+constexpr int kWideTile = 8;
+typedef float hf2 __attribute__((ext_vector_type(2)));
+
+template <int N>
+__global__ __launch_bounds__(256) void heads_bwd_wide_kernel(HbArgs A, const float *__restrict__ a,
+                                                              float *__restrict__ da, const float *__restrict__ g,
+                                                              float *__restrict__ part) {
+    static_assert(N % 4 == 0, "rows of g read as float4");
+    __shared__ float4 s_g[kWideTile * N / 4];
+    const int W = A.W, ld = A.k * W, h = A.h0;
+    const int c = threadIdx.x, col = h * W + c;
+    const float *__restrict__ w2 = A.w2[h];
+    hf2 w[N / 2], acc[N / 2];
+#pragma unroll
+    for (int r = 0; r < N / 2; r++) {
+        w[r] = hf2{w2[(2 * r) * W + c], w2[(2 * r + 1) * W + c]};
+        acc[r] = hf2{0.f, 0.f};
+    }
+    float csum = 0.f, bsum = 0.f;
+    const int64_t p0 = (int64_t)blockIdx.x * A.rows_per_wg, p1 = min((int64_t)A.P, p0 + A.rows_per_wg);
+    // software pipeline: the next tile's x values and g block are in registers while this tile computes
+    constexpr int kG4 = kWideTile * N / 4;  // float4 of g per tile
+    constexpr int kGPer = (kG4 + 63) / 64;  // per thread, for W >= 64 threads
+    float xn[kWideTile];
+    float4 gn[kGPer];
+    auto fetch = [&](int64_t t0) {
+        const int nr = (int)min((int64_t)kWideTile, p1 - t0);
+#pragma unroll
+        for (int u = 0; u < kWideTile; u++) xn[u] = u < nr ? a[(t0 + u) * ld + col] : 0.f;
+        const float4 *src = reinterpret_cast<const float4 *>(g + t0 * N);
+#pragma unroll
+        for (int k = 0; k < kGPer; k++) {
+            const int e = threadIdx.x + W * k;
+            gn[k] = e < nr * N / 4 ? src[e] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    if (p0 < p1) fetch(p0);
+    for (int64_t t0 = p0; t0 < p1; t0 += kWideTile) {
+        const int nr = (int)min((int64_t)kWideTile, p1 - t0);
+        float x[kWideTile];
+#pragma unroll
+        for (int u = 0; u < kWideTile; u++) x[u] = xn[u];
+        __syncthreads();  // the previous tile's LDS reads are done
+#pragma unroll
+        for (int k = 0; k < kGPer; k++) {
+            const int e = threadIdx.x + W * k;
+            if (e < kG4) s_g[e] = gn[k];
+        }
+        __syncthreads();
+        if (t0 + kWideTile < p1) fetch(t0 + kWideTile);
+        if (c < N)
+            for (int u = 0; u < nr; u++) bsum += reinterpret_cast<const float *>(s_g)[u * N + c];
+        for (int u = 0; u < nr; u++) {
+            hf2 sd0 = hf2{0.f, 0.f}, sd1 = hf2{0.f, 0.f};
+            const hf2 xx = hf2{x[u], x[u]};
+#pragma unroll
+            for (int q = 0; q < N / 4; q++) {
+                const float4 gv = s_g[u * (N / 4) + q];
+                const hf2 ga = hf2{gv.x, gv.y}, gb = hf2{gv.z, gv.w};
+                sd0 = __builtin_elementwise_fma(ga, w[2 * q], sd0);
+                sd1 = __builtin_elementwise_fma(gb, w[2 * q + 1], sd1);
+                acc[2 * q] = __builtin_elementwise_fma(ga, xx, acc[2 * q]);
+                acc[2 * q + 1] = __builtin_elementwise_fma(gb, xx, acc[2 * q + 1]);
+            }
+            const float gvv = x[u] > 0.f ? (sd0.x + sd0.y) + (sd1.x + sd1.y) : 0.f;
+            da[(t0 + u) * ld + col] = gvv;
+            csum += gvv;
+        }
+    }
+    float *pw = part + (size_t)blockIdx.x * A.poff[1];
+    pw[c] = csum;
+    float *ph = pw + A.poff[0];
+#pragma unroll
+    for (int r = 0; r < N / 2; r++) {
+        ph[(2 * r) * (W + 1) + c] = acc[r].x;
+        ph[(2 * r + 1) * (W + 1) + c] = acc[r].y;
+    }
+    if (c < N) ph[c * (W + 1) + W] = bsum;
 }
 
 // the partials summed over the workgroups (32 record entries per workgroup, 8 eighths in a fixed
@@ -440,7 +566,7 @@ struct HbOut {
 };
 __global__ __launch_bounds__(256) void heads_bwd_reduce_kernel(HbArgs A, HbOut O, int nwg, const float *__restrict__ part) {
     __shared__ float s_sum[8][32];
-    const int per = A.poff[A.k];
+    const int per = A.poff[A.hk];
     const int o = threadIdx.x & 31, q = threadIdx.x >> 5;
     const int i = blockIdx.x * 32 + o;
     float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
@@ -461,13 +587,13 @@ __global__ __launch_bounds__(256) void heads_bwd_reduce_kernel(HbArgs A, HbOut O
 #pragma unroll
         for (int e = 0; e < 8; e++) t += s_sum[e][o];
         if (i < A.poff[0]) {
-            O.db1[i] = t;
+            O.db1[A.h0 * A.W + i] = t;
         } else {
-            int h = 0;
-            while (h + 1 < A.k && i >= A.poff[h + 1]) h++;
-            const int e = i - A.poff[h], r = e / (A.W + 1), c = e - r * (A.W + 1);
-            if (c < A.W) O.dw2[h][r * A.W + c] = t;
-            else O.db2[h][r] = t;
+            int hl = 0;
+            while (hl + 1 < A.hk && i >= A.poff[hl + 1]) hl++;
+            const int e = i - A.poff[hl], r = e / (A.W + 1), c = e - r * (A.W + 1);
+            if (c < A.W) O.dw2[A.h0 + hl][r * A.W + c] = t;
+            else O.db2[A.h0 + hl][r] = t;
         }
     }
 }
@@ -484,50 +610,81 @@ using namespace gs4d;
 
 extern "C" {
 
-static int hb_rows_per_wg(int P) {
-    // about two workgroups per CU, at least 64 rows each
-    return std::max(64, (P + 511) / 512);
+// the launches: maximal runs of heads of one class (narrow: n <= 16; wide: n = 48)
+static bool hb_wide(int n) { return n > 16; }  // n = 48 (validated), one head per launch
+static int hb_rows_per_wg(int P, bool wide) {
+    // narrow heads stream a: about two workgroups per CU; the wide head's waves are compute-heavy and
+    // its per-workgroup partials large: 256-row blocks
+    return wide ? 128 : std::max(64, (P + 511) / 512);
+}
+extern "C++" {
+template <class Fn>
+static void hb_groups(int k, const int *n, Fn fn) {  // fn(h0, hk)
+    for (int h0 = 0; h0 < k;) {
+        int h1 = h0 + 1;
+        while (h1 < k && !hb_wide(n[h0]) && !hb_wide(n[h1])) h1++;
+        fn(h0, h1 - h0);
+        h0 = h1;
+    }
+}
 }
 
 size_t gs4d_heads_backward_scratch_bytes(int P, int W, int k, const int *n) {
     if (P < 0 || W < 1 || k < 1 || k > kHbMaxHeads || !n) return 0;
-    size_t per = (size_t)k * W;
-    for (int i = 0; i < k; i++) per += (size_t)std::max(n[i], 0) * (W + 1);
-    const size_t nwg = std::max<size_t>(1, ((size_t)P + hb_rows_per_wg(P) - 1) / hb_rows_per_wg(P));
-    return 4 * nwg * per + 256;
+    size_t total = 256;
+    hb_groups(k, n, [&](int h0, int hk) {
+        size_t per = (size_t)hk * W;
+        for (int i = h0; i < h0 + hk; i++) per += (size_t)std::max(n[i], 0) * (W + 1);
+        const int rows = hb_rows_per_wg(P, hb_wide(n[h0]));
+        const size_t nwg = std::max<size_t>(1, ((size_t)P + rows - 1) / rows);
+        total += align_up(4 * nwg * per, 256);
+    });
+    return total;
 }
 
 int gs4d_heads_backward(const gs4d_heads_bwd *args, void *scratch, void *stream) {
     if (!args || !scratch) return 1;
     const gs4d_heads_bwd &b = *args;
-    if (b.P < 0 || (b.W != 64 && b.W != 128 && b.W != 256) || b.k < 1 || b.k > kHbMaxHeads || b.k * b.W > 1024 ||
+    if (b.P < 0 || (b.W != 64 && b.W != 128 && b.W != 256) || b.k < 1 || b.k > kHbMaxHeads || b.k * b.W > 768 ||
         !b.db1)
         return 1;
     if (b.P > 0 && (!b.a || !b.da)) return 1;
     HbArgs A{};
     HbOut O{};
-    A.P = b.P, A.W = b.W, A.k = b.k, A.rows_per_wg = hb_rows_per_wg(b.P);
-    A.poff[0] = b.k * b.W;
+    A.P = b.P, A.W = b.W, A.k = b.k;
     const float *g[kHbMaxHeads] = {};
     for (int i = 0; i < b.k; i++) {
         if (b.n[i] < 1 || (b.n[i] > 16 && b.n[i] != 48) || !b.w2[i] || !b.dw2[i] || !b.db2[i] || (b.P > 0 && !b.g[i]))
             return 1;
+        if (b.n[i] == 48 && ((size_t)b.g[i] & 15)) return 1;  // the wide head's rows are read as float4
         A.n[i] = b.n[i], A.w2[i] = b.w2[i], g[i] = b.g[i];
-        A.poff[i + 1] = A.poff[i] + b.n[i] * (b.W + 1);
         O.dw2[i] = b.dw2[i], O.db2[i] = b.db2[i];
     }
     O.db1 = b.db1;
     hipStream_t s = (hipStream_t)stream;
-    const int nwg = std::max(1, (int)(((int64_t)b.P + A.rows_per_wg - 1) / A.rows_per_wg));
-    float *part = (float *)align_up((size_t)scratch, 256);
-    if (b.P == 0) {  // empty sums: the partials of one empty workgroup
-        if (hipMemsetAsync(part, 0, 4 * (size_t)A.poff[b.k], s) != hipSuccess) return 3;
-    } else {
-        hipLaunchKernelGGL(heads_bwd_kernel, dim3(nwg), dim3(b.k * b.W), 0, s, A, b.a, b.da, g[0], g[1], g[2], g[3],
-                           g[4], g[5], g[6], g[7], part);
-    }
-    hipLaunchKernelGGL(heads_bwd_reduce_kernel, dim3((A.poff[b.k] + 31) / 32), dim3(256), 0, s, A, O, nwg,
-                       (const float *)part);
+    char *q = (char *)align_up((size_t)scratch, 256);
+    int err = 0;
+    hb_groups(b.k, b.n, [&](int h0, int hk) {
+        A.h0 = h0, A.hk = hk;
+        A.rows_per_wg = hb_rows_per_wg(b.P, hb_wide(b.n[h0]));
+        A.poff[0] = hk * b.W;
+        for (int i = 0; i < hk; i++) A.poff[i + 1] = A.poff[i] + b.n[h0 + i] * (b.W + 1);
+        const int nwg = std::max(1, (int)(((int64_t)b.P + A.rows_per_wg - 1) / A.rows_per_wg));
+        float *part = (float *)q;
+        q += align_up(4 * (size_t)nwg * A.poff[hk], 256);
+        if (b.P == 0) {  // empty sums: the partials of one empty workgroup
+            if (hipMemsetAsync(part, 0, 4 * (size_t)A.poff[hk], s) != hipSuccess) err = 3;
+        } else {
+            if (hb_wide(b.n[h0]))
+                hipLaunchKernelGGL(heads_bwd_wide_kernel<48>, dim3(nwg), dim3(b.W), 0, s, A, b.a, b.da, g[h0], part);
+            else
+                hipLaunchKernelGGL(heads_bwd_kernel, dim3(nwg), dim3(hk * b.W), 0, s, A, b.a, b.da, g[0], g[1], g[2],
+                                   g[3], g[4], g[5], g[6], g[7], part);
+        }
+        hipLaunchKernelGGL(heads_bwd_reduce_kernel, dim3((A.poff[hk] + 31) / 32), dim3(256), 0, s, A, O, nwg,
+                           (const float *)part);
+    });
+    if (err) return err;
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
