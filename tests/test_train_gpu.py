@@ -237,6 +237,9 @@ def test_train_step_fused_matches_torch_tail():
         scale = max(a.abs().max().item(), 1e-30)
         err = (a - b).abs().max().item() / scale
         assert err < 1e-4, (k, err)
-    torch.testing.assert_close(gb.xyz_gradient_accum, ga.xyz_gradient_accum, rtol=1e-4, atol=1e-9)
+    # the statistic sums |d loss / d mean2D| per point: fp32 rounding of the deformation MLP moves it by
+    # ~1e-9 absolute (1e-4 of the tensor's max, the same bar as the gradients above)
+    acc_scale = max(ga.xyz_gradient_accum.abs().max().item(), 1e-30)
+    torch.testing.assert_close(gb.xyz_gradient_accum, ga.xyz_gradient_accum, rtol=1e-4, atol=1e-4 * acc_scale)
     torch.testing.assert_close(gb.denom, ga.denom, rtol=0, atol=0)
     torch.testing.assert_close(gb.max_radii2D, ga.max_radii2D, rtol=0, atol=0)
