@@ -480,14 +480,18 @@ __global__ __launch_bounds__(768) void heads_bwd_kernel(HbArgs A, const float *_
 constexpr int kWideTile = 8;
 typedef float hf2 __attribute__((ext_vector_type(2)));
 
+constexpr int kWideGroups = 2;  // row groups per workgroup: 2 x W threads (3 workgroups per CU at 152 VGPRs)
+
 template <int N>
-__global__ __launch_bounds__(256) void heads_bwd_wide_kernel(HbArgs A, const float *__restrict__ a,
+__global__ __launch_bounds__(512) void heads_bwd_wide_kernel(HbArgs A, const float *__restrict__ a,
                                                               float *__restrict__ da, const float *__restrict__ g,
                                                               float *__restrict__ part) {
     static_assert(N % 4 == 0, "rows of g read as float4");
-    __shared__ float4 s_g[kWideTile * N / 4];
+    __shared__ float4 s_g[kWideGroups][kWideTile * N / 4];
+    __shared__ float s_red[N * 128 + 2 * 128];  // row-group combine (W <= 128)
     const int W = A.W, ld = A.k * W, h = A.h0;
-    const int c = threadIdx.x, col = h * W + c;
+    const int rg = __builtin_amdgcn_readfirstlane((int)threadIdx.x / W);  // row group (wave-uniform)
+    const int c = (int)threadIdx.x - rg * W, col = h * W + c;
     const float *__restrict__ w2 = A.w2[h];
     hf2 w[N / 2], acc[N / 2];
 #pragma unroll
@@ -497,44 +501,48 @@ __global__ __launch_bounds__(256) void heads_bwd_wide_kernel(HbArgs A, const flo
     }
     float csum = 0.f, bsum = 0.f;
     const int64_t p0 = (int64_t)blockIdx.x * A.rows_per_wg, p1 = min((int64_t)A.P, p0 + A.rows_per_wg);
-    // software pipeline: the next tile's x values and g block are in registers while this tile computes
+    // row group rg takes the tiles rg, rg + G, ... of the block; the next tile's x values and g block are
+    // in registers while this one computes
     constexpr int kG4 = kWideTile * N / 4;  // float4 of g per tile
     constexpr int kGPer = (kG4 + 63) / 64;  // per thread, for W >= 64 threads
+    const int64_t step = (int64_t)kWideGroups * kWideTile;
     float xn[kWideTile];
     float4 gn[kGPer];
     auto fetch = [&](int64_t t0) {
-        const int nr = (int)min((int64_t)kWideTile, p1 - t0);
+        const int nr = t0 < p1 ? (int)min((int64_t)kWideTile, p1 - t0) : 0;
 #pragma unroll
         for (int u = 0; u < kWideTile; u++) xn[u] = u < nr ? a[(t0 + u) * ld + col] : 0.f;
         const float4 *src = reinterpret_cast<const float4 *>(g + t0 * N);
 #pragma unroll
         for (int k = 0; k < kGPer; k++) {
-            const int e = threadIdx.x + W * k;
+            const int e = c + W * k;
             gn[k] = e < nr * N / 4 ? src[e] : make_float4(0.f, 0.f, 0.f, 0.f);
         }
     };
-    if (p0 < p1) fetch(p0);
-    for (int64_t t0 = p0; t0 < p1; t0 += kWideTile) {
-        const int nr = (int)min((int64_t)kWideTile, p1 - t0);
+    fetch(p0 + rg * kWideTile);
+    for (int64_t base = p0; base < p1; base += step) {  // uniform trip count over the workgroup
+        const int64_t t0 = base + rg * kWideTile;
+        const int nr = t0 < p1 ? (int)min((int64_t)kWideTile, p1 - t0) : 0;
         float x[kWideTile];
 #pragma unroll
         for (int u = 0; u < kWideTile; u++) x[u] = xn[u];
         __syncthreads();  // the previous tile's LDS reads are done
 #pragma unroll
         for (int k = 0; k < kGPer; k++) {
-            const int e = threadIdx.x + W * k;
-            if (e < kG4) s_g[e] = gn[k];
+            const int e = c + W * k;
+            if (e < kG4) s_g[rg][e] = gn[k];
         }
         __syncthreads();
-        if (t0 + kWideTile < p1) fetch(t0 + kWideTile);
+        if (t0 + step < p1) fetch(t0 + step);
+        const float4 *sg = s_g[rg];
         if (c < N)
-            for (int u = 0; u < nr; u++) bsum += reinterpret_cast<const float *>(s_g)[u * N + c];
+            for (int u = 0; u < nr; u++) bsum += reinterpret_cast<const float *>(sg)[u * N + c];
         for (int u = 0; u < nr; u++) {
             hf2 sd0 = hf2{0.f, 0.f}, sd1 = hf2{0.f, 0.f};
             const hf2 xx = hf2{x[u], x[u]};
 #pragma unroll
             for (int q = 0; q < N / 4; q++) {
-                const float4 gv = s_g[u * (N / 4) + q];
+                const float4 gv = sg[u * (N / 4) + q];
                 const hf2 ga = hf2{gv.x, gv.y}, gb = hf2{gv.z, gv.w};
                 sd0 = __builtin_elementwise_fma(ga, w[2 * q], sd0);
                 sd1 = __builtin_elementwise_fma(gb, w[2 * q + 1], sd1);
@@ -546,6 +554,30 @@ __global__ __launch_bounds__(256) void heads_bwd_wide_kernel(HbArgs A, const flo
             csum += gvv;
         }
     }
+    // combine the row groups in group order (deterministic) into group 0's registers
+    for (int sgp = 1; sgp < kWideGroups; sgp++) {
+        __syncthreads();
+        if (rg == sgp) {
+#pragma unroll
+            for (int r = 0; r < N / 2; r++) {
+                s_red[(2 * r) * 128 + c] = acc[r].x;
+                s_red[(2 * r + 1) * 128 + c] = acc[r].y;
+            }
+            s_red[N * 128 + c] = csum;
+            s_red[N * 128 + 128 + c] = bsum;
+        }
+        __syncthreads();
+        if (rg == 0) {
+#pragma unroll
+            for (int r = 0; r < N / 2; r++) {
+                acc[r].x += s_red[(2 * r) * 128 + c];
+                acc[r].y += s_red[(2 * r + 1) * 128 + c];
+            }
+            csum += s_red[N * 128 + c];
+            bsum += s_red[N * 128 + 128 + c];
+        }
+    }
+    if (rg != 0) return;
     float *pw = part + (size_t)blockIdx.x * A.poff[1];
     pw[c] = csum;
     float *ph = pw + A.poff[0];
@@ -656,7 +688,7 @@ int gs4d_heads_backward(const gs4d_heads_bwd *args, void *scratch, void *stream)
     for (int i = 0; i < b.k; i++) {
         if (b.n[i] < 1 || (b.n[i] > 16 && b.n[i] != 48) || !b.w2[i] || !b.dw2[i] || !b.db2[i] || (b.P > 0 && !b.g[i]))
             return 1;
-        if (b.n[i] == 48 && ((size_t)b.g[i] & 15)) return 1;  // the wide head's rows are read as float4
+        if (b.n[i] == 48 && (((size_t)b.g[i] & 15) || b.W > 128)) return 1;  // rows read as float4; LDS combine
         A.n[i] = b.n[i], A.w2[i] = b.w2[i], g[i] = b.g[i];
         O.dw2[i] = b.dw2[i], O.db2[i] = b.db2[i];
     }
@@ -676,7 +708,8 @@ int gs4d_heads_backward(const gs4d_heads_bwd *args, void *scratch, void *stream)
             if (hipMemsetAsync(part, 0, 4 * (size_t)A.poff[hk], s) != hipSuccess) err = 3;
         } else {
             if (hb_wide(b.n[h0]))
-                hipLaunchKernelGGL(heads_bwd_wide_kernel<48>, dim3(nwg), dim3(b.W), 0, s, A, b.a, b.da, g[h0], part);
+                hipLaunchKernelGGL(heads_bwd_wide_kernel<48>, dim3(nwg), dim3(kWideGroups * b.W), 0, s, A, b.a, b.da,
+                                   g[h0], part);
             else
                 hipLaunchKernelGGL(heads_bwd_kernel, dim3(nwg), dim3(hk * b.W), 0, s, A, b.a, b.da, g[0], g[1], g[2],
                                    g[3], g[4], g[5], g[6], g[7], part);

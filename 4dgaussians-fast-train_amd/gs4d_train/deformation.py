@@ -191,7 +191,7 @@ class _DeformHeads(torch.autograd.Function):
         W, k = ctx.W, len(w2)
         douts = [d if d is not None else torch.zeros(a.shape[0], w2[i].shape[0], device=a.device)
                  for i, d in enumerate(douts)]
-        if a.is_cuda and W in (64, 128, 256) and k * W <= 768 and all(x.shape[0] <= 16 or x.shape[0] == 48
+        if a.is_cuda and W in (64, 128, 256) and k * W <= 768 and all(x.shape[0] <= 16 or (x.shape[0] == 48 and W <= 128)
                                                                         for x in w2):
             # second layers' backward + ReLU mask + first-layer bias gradient in one HIP pass over a
             from . import _C

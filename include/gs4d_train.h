@@ -138,7 +138,7 @@ int gs4d_linear_dw(int P, int W, int count, const gs4d_dw_problem *problems, voi
  * over a: da = (a > 0) * [g_0 W2_0 | ... | g_{k-1} W2_{k-1}] (P, kW), db1 = column sums of da, and for each
  * head dW2_i = g_i^T a_i (n_i, W), db2_i = column sums of g_i -- what autograd forms with k mm, one
  * threshold_backward, a sum and 2k weight/bias reductions.  W in {64, 128, 256}, k W <= 768, n_i <= 16
- * or n_i = 48; g_i (P, n_i) contiguous (16-byte aligned when n_i = 48), a and da (P, kW) contiguous,
+ * or n_i = 48 (then W <= 128); g_i (P, n_i) contiguous (16-byte aligned when n_i = 48), a and da (P, kW) contiguous,
  * W2_i (n_i, W).  fp32, partial sums
  * reduced in a fixed order. */
 #define GS4D_HEADS_MAX 8

@@ -170,8 +170,8 @@ def test_linear_dw_matches_fp64(P, W, ns):
         assert float((out[2 * i + 1].double() - rb).abs().max() / sb) <= 1e-5
 
 
-@pytest.mark.parametrize("P,W,ns", [(100_003, 128, [3, 3, 4, 1, 48]), (777, 64, [2, 16, 5]), (1, 256, [1, 48]),
-                                     (0, 128, [3, 4]), (1001, 64, [48, 3, 48])])
+@pytest.mark.parametrize("P,W,ns", [(100_003, 128, [3, 3, 4, 1, 48]), (777, 64, [2, 16, 5]), (1, 128, [1, 48]),
+                                     (0, 128, [3, 4]), (1001, 64, [48, 3, 48]), (300, 256, [16, 1])])
 def test_heads_backward_matches_fp64(P, W, ns):
     """gs4d_heads_backward (the heads block's second layers + ReLU mask + first-layer bias gradient in one
     pass) vs the same products in fp64 torch: da to 1e-5 of its row's |terms| sum, the reductions to 1e-5 of
