@@ -368,24 +368,10 @@ __device__ __forceinline__ void block_sort(uint32_t *__restrict__ seg, int n, co
     }
 }
 
-// Tiles with kWaveSortMax < n <= 4096 instances (register + LDS bitonic, one workgroup each); longer
-// runs go to tile_sort_kernel.
-__global__ __launch_bounds__(256) void tile_sort_mid_kernel(const uint2 *__restrict__ ranges,
-                                                            const uint32_t *__restrict__ gid_by_e,
-                                                            const float *__restrict__ depths,
-                                                            uint32_t *__restrict__ upos) {
-    __shared__ uint64_t s_x[kSortCap];
-    const uint2 r = ranges[blockIdx.x];
-    const int n = (int)(r.y - r.x);
-    if (n <= kWaveSortMax || n > kSortCap) return;
-    uint32_t *seg = upos + r.x;
-    if (n <= 512) block_sort<2>(seg, n, gid_by_e, depths, s_x);
-    else if (n <= 1024) block_sort<4>(seg, n, gid_by_e, depths, s_x);
-    else if (n <= 2048) block_sort<8>(seg, n, gid_by_e, depths, s_x);
-    else block_sort<16>(seg, n, gid_by_e, depths, s_x);
-}
-
-// Tiles with more than kSortCap instances: one workgroup each.
+// Tiles with more than kWaveSortMax instances (shorter runs are sorted in registers by the render
+// forward): one workgroup each.  Up to kSortCap: register + LDS bitonic (block_sort); longer: runs of
+// kSortCap in LDS merged by the network's global steps.  One launch for both (an empty launch costs
+// ~4 us of the timeline).
 __global__ __launch_bounds__(256) void tile_sort_kernel(const uint2 *__restrict__ ranges,
                                                         const uint32_t *__restrict__ gid_by_e,
                                                         const float *__restrict__ depths, uint32_t *__restrict__ upos,
@@ -393,19 +379,13 @@ __global__ __launch_bounds__(256) void tile_sort_kernel(const uint2 *__restrict_
     __shared__ TileSortLds s;
     const uint2 r = ranges[blockIdx.x];
     const int n = (int)(r.y - r.x);
-    if (n <= kSortCap) return;  // tile_sort_mid_kernel / the render forward
+    if (n <= kWaveSortMax) return;  // the render forward sorts these
     uint32_t *seg = upos + r.x;
     if (n <= kSortCap) {
-        int m = 1;
-        while (m < n) m <<= 1;
-        for (int i = threadIdx.x; i < n; i += blockDim.x) {
-            const uint32_t e = seg[i];
-            s.key[i] = inst_key(e, gid_by_e, depths);
-            s.val[i] = e;
-        }
-        __syncthreads();
-        lds_network(s, n, m, 2, m, 2 >> 1);
-        for (int i = threadIdx.x; i < n; i += blockDim.x) seg[i] = s.val[i];
+        if (n <= 512) block_sort<2>(seg, n, gid_by_e, depths, s.key);
+        else if (n <= 1024) block_sort<4>(seg, n, gid_by_e, depths, s.key);
+        else if (n <= 2048) block_sort<8>(seg, n, gid_by_e, depths, s.key);
+        else block_sort<16>(seg, n, gid_by_e, depths, s.key);
         return;
     }
     // long tile: sort runs of kSortCap in LDS, then continue the network with its global steps
@@ -479,7 +459,6 @@ hipError_t launch_binning(const Args &a, GeomState g, const int *radii, BinningS
     onesweep_sort<kSortThreads, kItemsL>(keys, vals, L, n_dev, b.key_bits, b.scratch + kZeroHist,
                                          b.scratch + bin_look_off(L), b.scratch + bin_chain_off() + 1, s);
     hipLaunchKernelGGL(tile_ranges_kernel, dim3((L + 255) / 256), dim3(256), 0, s, b.sorted_keys, n_dev, img.ranges);
-    hipLaunchKernelGGL(tile_sort_mid_kernel, dim3(T), dim3(256), 0, s, img.ranges, b.gid_by_e, g.depths, b.upos);
     hipLaunchKernelGGL(tile_sort_kernel, dim3(T), dim3(256), 0, s, img.ranges, b.gid_by_e, g.depths, b.upos,
                        b.tmp_hi, b.tmp_lo);
     return hipGetLastError();
