@@ -128,7 +128,11 @@ hipError_t launch_visible_scan(const Args &a, GeomState g, hipStream_t s) {
 __global__ __launch_bounds__(256) void emit_instances_kernel(Args a, GeomState g, const int *__restrict__ radii,
                                                              int L, int npass, uint32_t *__restrict__ keys,
                                                              uint32_t *__restrict__ gid_by_e,
-                                                             uint32_t *__restrict__ zero) {
+                                                             uint32_t *__restrict__ zero, uint2 *__restrict__ ranges,
+                                                             int T) {
+    // the tile ranges start empty (tile_ranges_kernel writes the non-empty ones): zeroed here instead of
+    // by a memset launch of their own
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < T; i += gridDim.x * 256) ranges[i] = make_uint2(0u, 0u);
     __shared__ uint32_t s_own[kEmitChunk];
     __shared__ uint32_t s_off[kEmitChunk + 2];
     __shared__ uint32_t s_n[kEmitChunk + 1];
@@ -448,11 +452,10 @@ hipError_t launch_binning(const Args &a, GeomState g, const int *radii, BinningS
     const int T = a.gx * a.gy;
     hipError_t e = hipMemsetAsync(b.scratch, 0, 4 * binning_zero_words(L, T), s);
     if (e != hipSuccess) return e;
-    e = hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)T, s);
-    if (e != hipSuccess || L == 0) return e;
+    if (L == 0) return hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)T, s);
     const int npass = (b.key_bits + 7) / 8;
     hipLaunchKernelGGL(emit_instances_kernel, dim3((unsigned)nchunk_emit(L)), dim3(256), 0, s, a, g, radii, L, npass,
-                       b.keys[0], b.gid_by_e, b.scratch);
+                       b.keys[0], b.gid_by_e, b.scratch, img.ranges, T);
     const uint32_t *n_dev = b.scratch;  // L' <= L reached instances
     uint32_t *keys[2] = {b.keys[0], b.keys[1]};
     uint32_t *vals[2] = {b.vals[0], b.vals[1]};
