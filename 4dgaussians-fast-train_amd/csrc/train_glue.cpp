@@ -143,8 +143,11 @@ static gs4d_hexplane_layout hex_layout(const std::vector<torch::Tensor> &planes)
 }
 
 // returns (feat (N, levels*F), packed channels-last planes and the point order for the backward)
+// order_in: a point order (N int32 indices) to reuse -- any permutation gives the same field; the
+// Morton order only buys locality, so a caller may keep one across calls while N is unchanged
 std::tuple<torch::Tensor, torch::Tensor, torch::Tensor> hexplane_forward(const torch::Tensor &pts_,
-                                                                         std::vector<torch::Tensor> planes) {
+                                                                         std::vector<torch::Tensor> planes,
+                                                                         c10::optional<torch::Tensor> order_in) {
     need(pts_.dim() == 2 && pts_.size(1) == 4 && pts_.is_cuda(), "hexplane: pts must be (N, 4) on the GPU");
     c10::hip::HIPGuard guard(pts_.device().index());
     torch::Tensor pts = pts_.to(torch::kFloat32).contiguous();
@@ -152,12 +155,22 @@ std::tuple<torch::Tensor, torch::Tensor, torch::Tensor> hexplane_forward(const t
     const int N = (int)pts.size(0);
     torch::Tensor packed = torch::empty({lay.total}, pts.options());
     torch::Tensor feat = torch::empty({N, (int64_t)lay.levels * lay.F}, pts.options());
-    torch::Tensor order = torch::empty({N}, pts.options().dtype(torch::kInt32));
-    torch::Tensor scratch = torch::empty({(int64_t)gs4d_hexplane_order_scratch_bytes(N)}, pts.options().dtype(torch::kUInt8));
     hipStream_t s = stream_of(pts);
     check(gs4d_hexplane_pack(&lay, packed.data_ptr<float>(), (void *)s), "hexplane pack");
-    check(gs4d_hexplane_order(N, pts.data_ptr<float>(), (uint32_t *)order.data_ptr<int>(), scratch.data_ptr(), (void *)s),
-          "hexplane order");
+    torch::Tensor order;
+    if (order_in.has_value() && order_in->defined() && order_in->numel() == N) {
+        need(order_in->is_cuda() && order_in->scalar_type() == torch::kInt32 && order_in->is_contiguous() &&
+                 order_in->device() == pts.device(),
+             "hexplane: order must be a contiguous int32 GPU tensor of N indices");
+        order = *order_in;
+    } else {
+        order = torch::empty({N}, pts.options().dtype(torch::kInt32));
+        torch::Tensor scratch =
+            torch::empty({(int64_t)gs4d_hexplane_order_scratch_bytes(N)}, pts.options().dtype(torch::kUInt8));
+        check(gs4d_hexplane_order(N, pts.data_ptr<float>(), (uint32_t *)order.data_ptr<int>(), scratch.data_ptr(),
+                                  (void *)s),
+              "hexplane order");
+    }
     check(gs4d_hexplane_forward(N, pts.data_ptr<float>(), (const uint32_t *)order.data_ptr<int>(), &lay,
                                 packed.data_ptr<float>(), feat.data_ptr<float>(), (void *)s),
           "hexplane forward");
@@ -316,7 +329,7 @@ PYBIND11_MODULE(_C, m) {
     m.def("linear_dw", &linear_dw);
     m.def("hexplane_reg_forward", &hexplane_reg_forward);
     m.def("hexplane_reg_backward", &hexplane_reg_backward);
-    m.def("hexplane_forward", &hexplane_forward);
+    m.def("hexplane_forward", &hexplane_forward, py::arg("pts"), py::arg("planes"), py::arg("order") = py::none());
     m.def("hexplane_backward", &hexplane_backward);
     m.def("l1_forward", &l1_forward);
     m.def("l1_backward", &l1_backward);

@@ -93,11 +93,27 @@ class FusedAdam(torch.optim.Optimizer):
 
 
 class _HexPlane(torch.autograd.Function):
-    """scene/hexplane.py:75-110 interpolate_ms_features over all levels in one launch each way."""
+    """scene/hexplane.py:75-110 interpolate_ms_features over all levels in one launch each way.
+
+    The points are visited in a Morton order of their coordinates; the field is evaluated at the
+    Gaussians' canonical means, which the optimizer moves little per step, so the order (any
+    permutation gives the same field -- it only buys locality) is kept across calls while the point
+    count is unchanged and refreshed every `order_refresh` calls."""
+
+    order_refresh = 100
+    _order = None
+    _calls = 0
 
     @staticmethod
     def forward(ctx, pts, *planes):
-        feat, packed, order = _C.hexplane_forward(pts, list(planes))
+        cls = _HexPlane
+        cached = cls._order
+        if (cached is None or cached.numel() != pts.shape[0] or cached.device != pts.device
+                or cls._calls % cls.order_refresh == 0):
+            cached = None
+        cls._calls += 1
+        feat, packed, order = _C.hexplane_forward(pts, list(planes), cached)
+        cls._order = order
         ctx.save_for_backward(pts, packed, order, *planes)
         return feat
 

@@ -87,6 +87,31 @@ def _field(F=16, reso=(64, 64, 64, 150), multires=(1, 2)):
     return f
 
 
+def test_hexplane_point_order_is_only_locality():
+    """_C.hexplane_forward with a caller-kept point order (kernels._HexPlane keeps one across calls): any
+    permutation gives bit-identical features (each point is evaluated alone) and the same gradients to
+    fp32 summation order (1e-5 of each tensor's max); a stale order of the wrong length is recomputed."""
+    from gs4d_train import _C
+    f = _field(16)
+    planes = [p.detach() for l in f.grids for p in l]
+    N = 30000
+    g = torch.Generator(device="cuda").manual_seed(7)
+    pts = torch.rand(N, 4, device="cuda", generator=g) * 2 - 1
+    feat0, packed0, order0 = _C.hexplane_forward(pts, planes)
+    perm = torch.randperm(N, device="cuda", generator=g).to(torch.int32)
+    feat1, packed1, order1 = _C.hexplane_forward(pts, planes, perm)
+    assert order1.data_ptr() == perm.data_ptr()
+    assert torch.equal(feat0, feat1)
+    dfeat = torch.randn_like(feat0)
+    d0, g0 = _C.hexplane_backward(pts, planes, packed0, dfeat, order0)
+    d1, g1 = _C.hexplane_backward(pts, planes, packed1, dfeat, order1)
+    torch.testing.assert_close(d1, d0, rtol=0, atol=1e-5 * d0.abs().max().item())
+    for a, b in zip(g0, g1):
+        torch.testing.assert_close(b, a, rtol=0, atol=1e-5 * max(a.abs().max().item(), 1e-30))
+    _, _, order2 = _C.hexplane_forward(pts[:100], planes, perm)  # wrong length: a fresh order
+    assert order2.numel() == 100 and order2.data_ptr() != perm.data_ptr()
+
+
 @pytest.mark.parametrize("F,N", [(4, 20000), (8, 20000), (16, 20000), (32, 20000), (16, 100_000)])
 def test_hexplane_fused_matches_grid_sample(F, N):
     """N = 20000 points spread over the field: many workgroups' cell boxes exceed the LDS bound and take
