@@ -81,8 +81,8 @@ int gs4d_hexplane_layout_init(gs4d_hexplane_layout *lay, int levels, int F, cons
 int gs4d_hexplane_pack(const gs4d_hexplane_layout *lay, float *packed, void *stream);
 int gs4d_hexplane_unpack(const gs4d_hexplane_layout *lay, const float *packed, void *stream);
 /* Visiting order of the points (a 3-D Morton order of the normalised x, y, z; any permutation of 0..N-1
- * gives the same results up to float summation order, NULL = identity).  The backward sums plane
- * gradients in LDS over the small windows of cells that Morton-consecutive points touch. */
+ * gives the same results up to float summation order, NULL = identity).  Morton-consecutive points touch
+ * small boxes of cells, which the backward's per-workgroup tap sort and gather exploit. */
 size_t gs4d_hexplane_order_scratch_bytes(int N);
 int gs4d_hexplane_order(int N, const float *pts, uint32_t *order, void *scratch, void *stream);
 int gs4d_hexplane_forward(int N, const float *pts, const uint32_t *order, const gs4d_hexplane_layout *lay,
