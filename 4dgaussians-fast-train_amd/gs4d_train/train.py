@@ -41,11 +41,19 @@ def train_step(gaussians, views, opt, hyper, iteration, background, stage="fine"
         vs_list.append(pkg["viewspace_points"])
     P = gaussians.get_xyz.shape[0]
     dev = gaussians.get_xyz.device
-    radii = torch.cat(radii_list, 0).max(dim=0).values if radii_list else torch.zeros(P, dtype=torch.int32, device=dev)
-    visibility_filter = torch.cat(vis_list).any(dim=0) if vis_list else torch.zeros(P, dtype=torch.bool, device=dev)
+    # train.py:221-228 batches the views with torch.cat and reduces radii / visibility over them; with one view
+    # per rank those are the view's own tensors (no copies, no reductions)
+    one = len(mine) == 1
+    if one:
+        radii, visibility_filter = radii_list[0][0], vis_list[0][0]
+    else:
+        radii = torch.cat(radii_list, 0).max(dim=0).values if radii_list else torch.zeros(P, dtype=torch.int32,
+                                                                                       device=dev)
+        visibility_filter = torch.cat(vis_list).any(dim=0) if vis_list else torch.zeros(P, dtype=torch.bool,
+                                                                                      device=dev)
     if images:
-        image_tensor = torch.cat(images, 0)
-        gt_image_tensor = torch.cat(gts, 0)
+        image_tensor = images[0] if one else torch.cat(images, 0)
+        gt_image_tensor = gts[0] if one else torch.cat(gts, 0)
         if fused:
             from .kernels import l1_loss
             Ll1 = l1_loss(image_tensor, gt_image_tensor[:, :3, :, :])
@@ -63,9 +71,12 @@ def train_step(gaussians, views, opt, hyper, iteration, background, stage="fine"
         loss = loss + opt.lambda_dssim * (1.0 - ssim(image_tensor, gt_image_tensor)) * (
             len(mine) / len(views) if data_parallel else 1.0)
     loss.backward()
-    viewspace_grad = torch.zeros_like(gaussians.get_xyz)
-    for t in vs_list:
-        viewspace_grad = viewspace_grad + t.grad
+    if len(vs_list) == 1 and vs_list[0].grad is not None:
+        viewspace_grad = vs_list[0].grad
+    else:
+        viewspace_grad = torch.zeros_like(gaussians.get_xyz)
+        for t in vs_list:
+            viewspace_grad = viewspace_grad + t.grad
     loss_out = loss.detach().reshape(1).clone()
     if data_parallel and dp.world() > 1:
         params = [p for g in gaussians.optimizer.param_groups for p in g["params"]]
