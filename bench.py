@@ -240,7 +240,7 @@ def train_step_timing(P, W, H, dev, world, rank, steps, warmup, dist, unfused=Tr
     res = {"ms": round(ms, 3), "views_per_gpu": 1, "global_batch": world, "gaussians": P,
            "image": f"{W}x{H}", "loss": round(loss, 6),
            "config": "arguments/dynerf/default.py (HexPlane 16 x [64,64,64,150], multires [1,2], MLP width 128, "
-                     "opacity+SH deform), fused libgs4d HexPlane field + regularisers / L1 / densification stats / Adam kernels, deformation heads as one GEMM block"}
+                     "opacity+SH deform), fused libgs4d HexPlane field + regularisers / L1 / densification stats / Adam kernels, deformation heads as one GEMM block with their second-layer backward in HIP (gs4d_heads_backward)"}
     if unfused and world == 1:
         ums, _ = run(False, max(3, steps // 4), 2)
         res["reference_torch_tail_ms"] = round(ums, 3)
