@@ -63,7 +63,20 @@ __global__ __launch_bounds__(kPreprocessBlock) void preprocess_kernel(
                         V3 dir = p_orig - load_v3(a.campos);
                         float len = sqrtf(dot(dir, dir));
                         dir = v3(dir.x / len, dir.y / len, dir.z / len);
-                        V3 res = sh_eval(a.D, sh, dir);
+                        V3 res;
+                        if (a.M == 16 && ((size_t)shs & 15) == 0) {
+                            // degree-3 layout: 12 float4 loads instead of 48 scalar loads strided 192 B
+                            float shl[48];
+                            const float4 *s4 = reinterpret_cast<const float4 *>(sh);
+#pragma unroll
+                            for (int q = 0; q < 12; q++) {
+                                const float4 v = s4[q];
+                                shl[4 * q] = v.x, shl[4 * q + 1] = v.y, shl[4 * q + 2] = v.z, shl[4 * q + 3] = v.w;
+                            }
+                            res = sh_eval(a.D, shl, dir);
+                        } else {
+                            res = sh_eval(a.D, sh, dir);
+                        }
                         cl = (uint8_t)((res.x < 0) | ((res.y < 0) << 1) | ((res.z < 0) << 2));
                         rgb = make_float3(fmaxf(res.x, 0.0f), fmaxf(res.y, 0.0f), fmaxf(res.z, 0.0f));
                     } else {

@@ -192,8 +192,27 @@ __global__ __launch_bounds__(256) void gaussian_backward_kernel(
             V3 dRGB = v3(dL_dcolor[3 * idx] * ((cl & 1) ? 0.f : 1.f), dL_dcolor[3 * idx + 1] * ((cl & 2) ? 0.f : 1.f),
                          dL_dcolor[3 * idx + 2] * ((cl & 4) ? 0.f : 1.f));
             V3 dir_orig = m - load_v3(a.campos);
-            dmean = dmean + sh_backward(a.D, sh, dir_orig, dRGB, dsh);
-            nsh_written = (a.D + 1) * (a.D + 1);
+            if (a.M == 16 && (((size_t)shs | (size_t)dL_dsh) & 15) == 0) {
+                // degree-3 layout (192 B per Gaussian, 16-byte aligned): the coefficients in and their
+                // gradients out as 12 float4 each instead of 48 scalar accesses strided 192 B over the lanes
+                float shl[48], dl[48];
+                const float4 *s4 = reinterpret_cast<const float4 *>(sh);
+#pragma unroll
+                for (int q = 0; q < 12; q++) {
+                    const float4 v = s4[q];
+                    shl[4 * q] = v.x, shl[4 * q + 1] = v.y, shl[4 * q + 2] = v.z, shl[4 * q + 3] = v.w;
+                }
+#pragma unroll
+                for (int q = 0; q < 48; q++) dl[q] = 0.f;
+                dmean = dmean + sh_backward(a.D, shl, dir_orig, dRGB, dl);
+                float4 *d4 = reinterpret_cast<float4 *>(dsh);
+#pragma unroll
+                for (int q = 0; q < 12; q++) d4[q] = make_float4(dl[4 * q], dl[4 * q + 1], dl[4 * q + 2], dl[4 * q + 3]);
+                nsh_written = 16;  // zeros included
+            } else {
+                dmean = dmean + sh_backward(a.D, sh, dir_orig, dRGB, dsh);
+                nsh_written = (a.D + 1) * (a.D + 1);
+            }
         }
         // cov3D part (backward.cu:394-395)
         if (scales) {
