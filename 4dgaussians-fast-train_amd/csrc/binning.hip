@@ -39,7 +39,8 @@ constexpr int kSortCap = 4096;              // tile runs sorted in LDS by one wo
 
 // ---------------------------------------------------------------------------------------------
 // Zero-region layouts (u32 words).
-__host__ __device__ static size_t nchunk_scan(int P) { return ((size_t)P + 255) / 256; }
+constexpr int kScanPer = 4;  // Gaussians per thread of the visible scan (1024 per workgroup)
+__host__ __device__ static size_t nchunk_scan(int P) { return ((size_t)P + 256 * kScanPer - 1) / (256 * kScanPer); }
 __host__ __device__ static size_t nchunk_emit(int L) { return ((size_t)L + kEmitChunk - 1) / kEmitChunk; }
 // geometry: counters | visible-count chain (+ err) | area chain (+ err)
 __host__ __device__ static size_t geom_vis_chain_off() { return 64; }
@@ -88,26 +89,39 @@ __device__ __forceinline__ uint32_t wg_exclusive(uint32_t v, uint32_t *s_w, uint
 __global__ __launch_bounds__(256) void visible_scan_kernel(GeomState g, int P, uint32_t jmax) {
     __shared__ uint32_t s_w[4], s_tmp[4];
     const uint32_t b = blockIdx.x;
-    const int idx = (int)b * 256 + threadIdx.x;
-    const uint32_t t = idx < P ? g.tiles_touched[idx] : 0u;
-    const uint32_t vis = t > 0;
+    const int i0 = ((int)b * 256 + threadIdx.x) * kScanPer;  // this thread's kScanPer consecutive Gaussians
+    uint32_t t[kScanPer], vsum = 0, asum = 0;
+#pragma unroll
+    for (int k = 0; k < kScanPer; k++) {
+        t[k] = i0 + k < P ? g.tiles_touched[i0 + k] : 0u;
+        vsum += t[k] > 0;
+        asum += t[k];
+    }
     uint32_t vtot, atot;
-    const uint32_t vx = wg_exclusive(vis, s_w, &vtot);
-    const uint32_t ax = wg_exclusive(t, s_w, &atot);
+    const uint32_t vx = wg_exclusive(vsum, s_w, &vtot);
+    const uint32_t ax = wg_exclusive(asum, s_w, &atot);
     uint32_t *vchain = g.zero + geom_vis_chain_off(), *achain = g.zero + geom_area_chain_off(P);
     const uint32_t vpre = block_prefix(vchain + 64, b, vtot, vchain + 1, s_tmp);
     const uint32_t apre = block_prefix(achain + 64, b, atot, achain + 1, s_tmp);
-    const uint32_t v = vpre + vx, run = apre + ax;
-    if (vis) {
-        g.vis_gid[v] = (uint32_t)idx;
-        g.cand_off[v] = run;
-        // emission chunks starting inside this Gaussian's candidates
-        for (uint32_t j = (run + kEmitChunk - 1) / kEmitChunk; j * (uint32_t)kEmitChunk < run + t && j < jmax; j++)
-            g.first_vis[j] = v;
-    }
-    if (idx == P - 1) {
-        g.cand_off[v + vis] = run + t;  // cand_off[V] = num_rendered
-        g.zero[kZeroV] = v + vis;       // V
+    uint32_t v = vpre + vx, run = apre + ax;
+#pragma unroll
+    for (int k = 0; k < kScanPer; k++) {
+        const int idx = i0 + k;
+        if (idx >= P) break;
+        if (t[k] > 0) {
+            g.vis_gid[v] = (uint32_t)idx;
+            g.cand_off[v] = run;
+            // emission chunks starting inside this Gaussian's candidates
+            for (uint32_t j = (run + kEmitChunk - 1) / kEmitChunk; j * (uint32_t)kEmitChunk < run + t[k] && j < jmax;
+                 j++)
+                g.first_vis[j] = v;
+            v++;
+        }
+        run += t[k];
+        if (idx == P - 1) {
+            g.cand_off[v] = run;  // cand_off[V] = num_rendered
+            g.zero[kZeroV] = v;   // V
+        }
     }
 }
 
