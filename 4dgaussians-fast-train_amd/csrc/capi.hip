@@ -235,10 +235,21 @@ int gs4d_forward(gs4d_alloc_fn geometry_alloc, void *geometry_ctx, gs4d_alloc_fn
     // H1: the single device->host synchronisation of the forward (rasterizer_impl.cu:282).  The scan of
     // the visible Gaussians is enqueued before the host waits, so the GPU keeps working during the
     // round trip.
-    static thread_local uint32_t *pinned = nullptr;
-    static thread_local hipEvent_t copied = nullptr;
-    if (!pinned) GS4D_HIP(hipHostMalloc((void **)&pinned, 128, hipHostMallocDefault));
-    if (!copied) GS4D_HIP(hipEventCreateWithFlags(&copied, hipEventDisableTiming));
+    // The staging word and its event belong to the device the stream runs on: a thread may call the
+    // forward on several devices (the caller switches the current device per call).
+    struct Readback {
+        uint32_t *pinned = nullptr;
+        hipEvent_t copied = nullptr;
+    };
+    static thread_local Readback readback[kMaxDevices];
+    int dev = 0;
+    GS4D_HIP(hipGetDevice(&dev));
+    if (dev < 0 || dev >= kMaxDevices) return fail(GS4D_ERR_ARG, "forward: device index out of range");
+    Readback &rb = readback[dev];
+    if (!rb.pinned) GS4D_HIP(hipHostMalloc((void **)&rb.pinned, 128, hipHostMallocDefault));
+    if (!rb.copied) GS4D_HIP(hipEventCreateWithFlags(&rb.copied, hipEventDisableTiming));
+    uint32_t *pinned = rb.pinned;
+    hipEvent_t copied = rb.copied;
     GS4D_HIP(hipMemcpyAsync(pinned, g.zero, 4 * (kZeroL + 16), hipMemcpyDeviceToHost, stream));
     GS4D_HIP(hipEventRecord(copied, stream));
     GS4D_STAGE("visible_scan", launch_visible_scan(a, g, stream));

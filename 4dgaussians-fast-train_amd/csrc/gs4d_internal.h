@@ -10,6 +10,7 @@ namespace gs4d {
 
 constexpr int kTilePixels = kBlockX * kBlockY;  // 256 pixels per 16x16 tile
 constexpr int kPreprocessBlock = 256;           // Gaussians per preprocess / duplicate workgroup
+constexpr int kMaxDevices = 64;                 // per-device host state (the forward's readback word)
 // Per-instance gradient record written by the render backward at the instance's emission slot:
 // m2x m2y conic_a conic_b conic_c opacity r g b + 3 pad (48 bytes = three 16-byte stores)
 constexpr int kContribStride = 12;

@@ -125,6 +125,27 @@ class GaussianModel:
         if self.active_sh_degree < self.max_sh_degree:
             self.active_sh_degree += 1
 
+    # ---- checkpoints (gaussian_model.py:66-106; train.py:49-57 restores, :393-395 saves)
+    def capture(self):
+        """The reference's checkpoint tuple, in its order; saved as torch.save((capture(), iteration))."""
+        return (self.active_sh_degree, self._xyz, self._deformation.state_dict(), self._deformation_table,
+                self._features_dc, self._features_rest, self._scaling, self._rotation, self._opacity,
+                self.max_radii2D, self.xyz_gradient_accum, self.denom, self.optimizer.state_dict(),
+                self.spatial_lr_scale)
+
+    def restore(self, model_args, training_args):
+        """Inverse of capture(): parameters, deformation network, statistics, then a fresh optimizer
+        (training_setup) loaded with the saved state -- torch.optim.Adam and FusedAdam state dicts are
+        interchangeable."""
+        (self.active_sh_degree, self._xyz, deform_state, self._deformation_table, self._features_dc,
+         self._features_rest, self._scaling, self._rotation, self._opacity, self.max_radii2D, xyz_gradient_accum,
+         denom, opt_dict, self.spatial_lr_scale) = model_args
+        self._deformation.load_state_dict(deform_state)
+        self.training_setup(training_args)
+        self.xyz_gradient_accum = xyz_gradient_accum
+        self.denom = denom
+        self.optimizer.load_state_dict(opt_dict)
+
     # ---- initialisation (gaussian_model.py:137-163)
     def create_from_pcd(self, points, colors, spatial_lr_scale, device="cuda"):
         from simple_knn._C import distCUDA2
@@ -294,6 +315,11 @@ class GaussianModel:
             return
         stds = self.get_scaling[sel].repeat(N, 1)
         samples = torch.normal(mean=torch.zeros((stds.size(0), 3), device=dev), std=stds)
+        # data-parallel replicas select the same Gaussians (their statistics are all-reduced) but draw
+        # from their own RNGs: rank 0's draws are the ones every replica uses
+        from . import dp
+        if dp.world() > 1:
+            torch.distributed.broadcast(samples, src=0)
         rots = build_rotation(self._rotation[sel]).repeat(N, 1, 1)
         new_xyz = torch.bmm(rots, samples.unsqueeze(-1)).squeeze(-1) + self.get_xyz[sel].repeat(N, 1)
         new_scaling = self.scaling_inverse_activation(self.get_scaling[sel].repeat(N, 1) / (0.8 * N))

@@ -14,17 +14,17 @@ radii and visibility are reduced so every replica takes the single-process step.
 import torch
 
 from . import dp
-from .render import render
-
-
-def l1_loss_torch(network_output, gt):
-    """utils/loss_utils.py:20-21"""
-    return torch.abs((network_output - gt)).mean()
+from .losses import l1_loss_torch
 
 
 def train_step(gaussians, views, opt, hyper, iteration, background, stage="fine", fused_loss=None,
-               data_parallel=False):
-    """views: list of (camera, gt_image (3, H, W)).  Returns the (detached) batch loss tensor."""
+               data_parallel=False, render_fn=None):
+    """views: list of (camera, gt_image (3, H, W)).  Returns the (detached) batch loss tensor.
+
+    render_fn(camera, gaussians, debug, bg, stage=...) -> render()'s dict; defaults to
+    gs4d_train.render.render (the HIP rasterizer).  The multi-process CPU tests pass a torch stand-in."""
+    if render_fn is None:
+        from .render import render as render_fn
     fused = gaussians.fused if fused_loss is None else fused_loss
     gaussians.update_learning_rate(iteration)
     if iteration % 1000 == 0:
@@ -33,7 +33,7 @@ def train_step(gaussians, views, opt, hyper, iteration, background, stage="fine"
     images, gts, radii_list, vis_list, vs_list = [], [], [], [], []
     for v in mine:
         cam, gt = views[v]
-        pkg = render(cam, gaussians, False, background, stage=stage)
+        pkg = render_fn(cam, gaussians, False, background, stage=stage)
         images.append(pkg["render"].unsqueeze(0))
         gts.append(gt.unsqueeze(0))
         radii_list.append(pkg["radii"].unsqueeze(0))
@@ -70,16 +70,26 @@ def train_step(gaussians, views, opt, hyper, iteration, background, stage="fine"
         from .losses import ssim
         loss = loss + opt.lambda_dssim * (1.0 - ssim(image_tensor, gt_image_tensor)) * (
             len(mine) / len(views) if data_parallel else 1.0)
-    loss.backward()
+    # a data-parallel rank with no view of the batch (len(views) < world) and no regulariser has a
+    # constant loss: nothing to back-propagate, its gradients are the zeros filled in below
+    if loss.requires_grad:
+        loss.backward()
     if len(vs_list) == 1 and vs_list[0].grad is not None:
         viewspace_grad = vs_list[0].grad
     else:
         viewspace_grad = torch.zeros_like(gaussians.get_xyz)
         for t in vs_list:
-            viewspace_grad = viewspace_grad + t.grad
+            if t.grad is not None:
+                viewspace_grad = viewspace_grad + t.grad
     loss_out = loss.detach().reshape(1).clone()
     if data_parallel and dp.world() > 1:
+        # a parameter gets a gradient on every replica iff some rank produced one (a rank without views
+        # produces none); parameters no rank touched keep grad None, so the optimizer skips them as the
+        # single-process step does (their Adam step counts stay in step)
         params = [p for g in gaussians.optimizer.param_groups for p in g["params"]]
+        has = torch.tensor([p.grad is not None for p in params], dtype=torch.int32, device=dev)
+        torch.distributed.all_reduce(has, op=torch.distributed.ReduceOp.MAX)
+        params = [p for p, h in zip(params, has.tolist()) if h]
         for p in params:
             if p.grad is None:
                 p.grad = torch.zeros_like(p)

@@ -222,3 +222,98 @@ def test_deform_heads_block_matches_separate_heads():
         torch.testing.assert_close(a, b, rtol=1e-10, atol=1e-10)
     for a, b in zip(ga, gb):
         torch.testing.assert_close(a, b, rtol=1e-10, atol=1e-10)
+
+
+def test_checkpoint_capture_restore_round_trip(tmp_path):
+    """gaussian_model.py:66-106: capture() -> torch.save((capture(), iteration)) -> restore(); the
+    optimizer state comes back bound to the restored parameters (train.py:49-57, 393-395)."""
+    g, opt = _cpu_model(P=120)
+    g.training_setup(opt)
+    loss = sum((p ** 2).sum() for grp in g.optimizer.param_groups for p in grp["params"])
+    loss.backward()
+    g.optimizer.step()
+    g.xyz_gradient_accum = torch.rand(120, 1)
+    g.denom = torch.ones(120, 1) * 3
+    g.active_sh_degree = 2
+    path = os.path.join(tmp_path, "chkpnt_fine_7.pth")
+    torch.save((g.capture(), 7), path)
+    model_args, it = torch.load(path, weights_only=True)
+    assert it == 7
+    h, _ = _cpu_model(P=5, seed=4)
+    h.restore(model_args, opt)
+    assert h.active_sh_degree == 2 and h.spatial_lr_scale == g.spatial_lr_scale
+    for k in ("_xyz", "_features_dc", "_features_rest", "_scaling", "_rotation", "_opacity", "xyz_gradient_accum",
+              "denom", "max_radii2D"):
+        torch.testing.assert_close(getattr(h, k), getattr(g, k), rtol=0, atol=0)
+    for (ka, a), (kb, b) in zip(g._deformation.state_dict().items(), h._deformation.state_dict().items()):
+        assert ka == kb and torch.equal(a, b)
+    for pa, pb in zip([p for grp in g.optimizer.param_groups for p in grp["params"]],
+                      [p for grp in h.optimizer.param_groups for p in grp["params"]]):
+        sa, sb = g.optimizer.state[pa], h.optimizer.state[pb]
+        if not pa.requires_grad:          # the HexPlane aabb buffer-parameter never steps
+            assert len(sa) == len(sb) == 0
+            continue
+        assert torch.equal(sa["exp_avg"], sb["exp_avg"]) and torch.equal(sa["exp_avg_sq"], sb["exp_avg_sq"])
+        assert float(sa["step"]) == float(sb["step"]) == 1.0
+
+
+def test_fused_adam_state_dict_interchanges_with_torch_adam():
+    """kernels.FusedAdam keeps torch.optim.Adam's state layout: a state dict saved by either loads
+    into the other (the reference's checkpoints hold torch.optim.Adam state), with no kernel call."""
+    from gs4d_train.kernels import FusedAdam
+    torch.manual_seed(0)
+    ps = [torch.nn.Parameter(torch.randn(5, 3)), torch.nn.Parameter(torch.randn(7))]
+    adam = torch.optim.Adam([{"params": [ps[0]], "lr": 1e-2, "name": "a"},
+                             {"params": [ps[1]], "lr": 1e-3, "name": "b"}], lr=0.0, eps=1e-15)
+    (ps[0].sum() ** 2 + (ps[1] ** 3).sum()).backward()
+    adam.step()
+    sd = adam.state_dict()
+    qs = [torch.nn.Parameter(p.detach().clone()) for p in ps]
+    fused = FusedAdam([{"params": [qs[0]], "lr": 0.5, "name": "a"}, {"params": [qs[1]], "lr": 0.5, "name": "b"}],
+                      lr=0.0, eps=1e-15)
+    fused.load_state_dict(sd)
+    assert [g["lr"] for g in fused.param_groups] == [1e-2, 1e-3]
+    assert [g["name"] for g in fused.param_groups] == ["a", "b"]
+    for p, q in zip(ps, qs):
+        a, b = adam.state[p], fused.state[q]
+        assert torch.equal(a["exp_avg"], b["exp_avg"]) and torch.equal(a["exp_avg_sq"], b["exp_avg_sq"])
+        assert float(b["step"]) == 1.0 and b["step"].dtype == torch.float32
+    # and back: FusedAdam's state dict into a fresh torch Adam, which then steps normally
+    back = torch.optim.Adam([{"params": [p], "lr": 0.0, "name": n} for p, n in zip(ps, "ab")], lr=0.0, eps=1e-15)
+    back.load_state_dict(fused.state_dict())
+    assert back.param_groups[0]["amsgrad"] is False and back.param_groups[1]["lr"] == 1e-3
+    (ps[0].sum() ** 2 + (ps[1] ** 3).sum()).backward()
+    back.step()
+    assert float(back.state[ps[0]]["step"]) == 2.0
+
+
+def test_ssim_restatement():
+    """utils/loss_utils.py:26-66: window taps, ssim(x, x) = 1, and a direct float64 evaluation of the
+    same formula (zero-padded 11x11 Gaussian window) on a small image."""
+    from gs4d_train.losses import create_window, gaussian, ssim
+    g = gaussian(11, 1.5)
+    assert abs(float(g.sum()) - 1) < 1e-6 and int(g.argmax()) == 5
+    w = create_window(11, 3)
+    assert tuple(w.shape) == (3, 1, 11, 11)
+    rng = np.random.default_rng(0)
+    a = rng.uniform(size=(1, 3, 13, 17)).astype(np.float32)
+    b = np.clip(a + rng.normal(0, 0.1, a.shape), 0, 1).astype(np.float32)
+    assert abs(float(ssim(torch.tensor(a), torch.tensor(a))) - 1) < 1e-5
+    k = w[0, 0].double().numpy()
+
+    def filt(x):
+        pad = np.pad(x, ((0, 0), (5, 5), (5, 5)))
+        out = np.zeros_like(x)
+        for i in range(x.shape[1]):
+            for j in range(x.shape[2]):
+                out[:, i, j] = (pad[:, i:i + 11, j:j + 11] * k).sum((1, 2))
+        return out
+
+    x, y = a[0].astype(np.float64), b[0].astype(np.float64)
+    m1, m2 = filt(x), filt(y)
+    s1, s2, s12 = filt(x * x) - m1 ** 2, filt(y * y) - m2 ** 2, filt(x * y) - m1 * m2
+    C1, C2 = 0.01 ** 2, 0.03 ** 2
+    ref = (((2 * m1 * m2 + C1) * (2 * s12 + C2)) / ((m1 ** 2 + m2 ** 2 + C1) * (s1 + s2 + C2))).mean()
+    assert abs(float(ssim(torch.tensor(a), torch.tensor(b))) - ref) < 1e-5
+    per_image = ssim(torch.tensor(a), torch.tensor(b), size_average=False)
+    assert per_image.shape == (1,)

@@ -14,7 +14,7 @@ pytestmark = pytest.mark.gpu
 
 def test_l1_loss_matches_torch():
     from gs4d_train.kernels import l1_loss
-    from gs4d_train.train import l1_loss_torch
+    from gs4d_train.losses import l1_loss_torch
     g = torch.Generator(device="cuda").manual_seed(0)
     x = torch.rand(2, 3, 101, 77, device="cuda", generator=g).requires_grad_(True)
     y = torch.rand(2, 3, 101, 77, device="cuda", generator=g)
