@@ -386,6 +386,79 @@ __device__ __forceinline__ void block_sort(uint32_t *__restrict__ seg, int n, co
     }
 }
 
+// The blend kernels run one wave per tile, more waves than fit on the chip at once: the last ones to
+// start run at low occupancy, so a long tile started late ends the kernel late.  tile_order_kernel
+// (one workgroup) orders the tiles longest run first (a counting sort on min(run, 1023), the order
+// inside a length arbitrary: it only schedules, every tile's result is its own).
+constexpr int kOrderBins = 1024, kOrderBatch = 8;
+__device__ void order_tiles(const uint2 *__restrict__ ranges, int T, uint32_t *__restrict__ order, uint32_t *s_bin) {
+    const int tid = threadIdx.x, nt = blockDim.x;
+    for (int i = tid; i < kOrderBins; i += nt) s_bin[i] = 0;
+    __syncthreads();
+    // kOrderBatch tiles per thread per round, their loads all in flight before the first use
+    auto bins_of = [&](int base, int bin[kOrderBatch]) {
+        uint2 r[kOrderBatch];
+#pragma unroll
+        for (int k = 0; k < kOrderBatch; k++) {
+            const int t = base + k * nt + tid;
+            r[k] = t < T ? ranges[t] : make_uint2(0u, 0u);
+        }
+#pragma unroll
+        for (int k = 0; k < kOrderBatch; k++)  // longest first
+            bin[k] = kOrderBins - 1 - (int)min(r[k].y - r[k].x, (uint32_t)(kOrderBins - 1));
+    };
+    // up to kOrderBatch * nt tiles (8192 at 1024 threads) keep their bins in registers between the
+    // histogram and the scatter; larger grids load their ranges again
+    const bool one_round = T <= kOrderBatch * nt;
+    int bin0[kOrderBatch];
+    for (int base = 0; base < T; base += kOrderBatch * nt) {
+        int bin[kOrderBatch];
+        bins_of(base, bin);
+#pragma unroll
+        for (int k = 0; k < kOrderBatch; k++) {
+            if (base + k * nt + tid < T) atomicAdd(&s_bin[bin[k]], 1u);
+            bin0[k] = bin[k];
+        }
+    }
+    __syncthreads();
+    if (tid < 64) {  // exclusive scan of the bins by one wave, 16 bins per lane
+        constexpr int per = kOrderBins / 64;
+        uint32_t v[per], sum = 0;
+#pragma unroll
+        for (int k = 0; k < per; k++) { v[k] = s_bin[tid * per + k]; sum += v[k]; }
+        uint32_t incl = sum;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t o = __shfl_up(incl, off);
+            if (tid >= off) incl += o;
+        }
+        uint32_t run = incl - sum;
+#pragma unroll
+        for (int k = 0; k < per; k++) { s_bin[tid * per + k] = run; run += v[k]; }
+    }
+    __syncthreads();
+    for (int base = 0; base < T; base += kOrderBatch * nt) {
+        int bin[kOrderBatch];
+        if (one_round) {
+#pragma unroll
+            for (int k = 0; k < kOrderBatch; k++) bin[k] = bin0[k];
+        } else {
+            bins_of(base, bin);
+        }
+#pragma unroll
+        for (int k = 0; k < kOrderBatch; k++) {
+            const int t = base + k * nt + tid;
+            if (t < T) order[atomicAdd(&s_bin[bin[k]], 1u)] = (uint32_t)t;
+        }
+    }
+}
+
+__global__ __launch_bounds__(1024) void tile_order_kernel(const uint2 *__restrict__ ranges, int T,
+                                                          uint32_t *__restrict__ order) {
+    __shared__ uint32_t s_bin[kOrderBins];
+    order_tiles(ranges, T, order, s_bin);
+}
+
 // Tiles with more than kWaveSortMax instances (shorter runs are sorted in registers by the render
 // forward): one workgroup each.  Up to kSortCap: register + LDS bitonic (block_sort); longer: runs of
 // kSortCap in LDS merged by the network's global steps.  One launch for both (an empty launch costs
@@ -466,7 +539,12 @@ hipError_t launch_binning(const Args &a, GeomState g, const int *radii, BinningS
     const int T = a.gx * a.gy;
     hipError_t e = hipMemsetAsync(b.scratch, 0, 4 * binning_zero_words(L, T), s);
     if (e != hipSuccess) return e;
-    if (L == 0) return hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)T, s);
+    if (L == 0) {
+        e = hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)T, s);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, s, img.ranges, T, img.order);
+        return hipGetLastError();
+    }
     const int npass = (b.key_bits + 7) / 8;
     hipLaunchKernelGGL(emit_instances_kernel, dim3((unsigned)nchunk_emit(L)), dim3(256), 0, s, a, g, radii, L, npass,
                        b.keys[0], b.gid_by_e, b.scratch, img.ranges, T);
@@ -476,6 +554,7 @@ hipError_t launch_binning(const Args &a, GeomState g, const int *radii, BinningS
     onesweep_sort<kSortThreads, kItemsL>(keys, vals, L, n_dev, b.key_bits, b.scratch + kZeroHist,
                                          b.scratch + bin_look_off(L), b.scratch + bin_chain_off() + 1, s);
     hipLaunchKernelGGL(tile_ranges_kernel, dim3((L + 255) / 256), dim3(256), 0, s, b.sorted_keys, n_dev, img.ranges);
+    hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, s, img.ranges, T, img.order);
     hipLaunchKernelGGL(tile_sort_kernel, dim3(T), dim3(256), 0, s, img.ranges, b.gid_by_e, g.depths, b.upos,
                        b.tmp_hi, b.tmp_lo);
     return hipGetLastError();

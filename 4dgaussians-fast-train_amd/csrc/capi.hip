@@ -94,7 +94,7 @@ GeomState GeomState::carve(char *base, int P, int T) {
     return g;
 }
 
-size_t ImageState::required(int W, int H) { return (size_t)carve(nullptr, W, H).ranges + 8 * (size_t)((W + 15) / 16) * ((H + 15) / 16) + 512; }
+size_t ImageState::required(int W, int H) { return (size_t)carve(nullptr, W, H).order + 4 * (size_t)((W + 15) / 16) * ((H + 15) / 16) + 512; }
 ImageState ImageState::carve(char *base, int W, int H) {
     char *p = (char *)align_up((size_t)base, 256);
     const size_t N = (size_t)W * H;
@@ -103,6 +103,7 @@ ImageState ImageState::carve(char *base, int W, int H) {
     s.final_T = (float *)gs4d::carve(p, 4 * N);
     s.n_contrib = (uint32_t *)gs4d::carve(p, 4 * N);
     s.ranges = (uint2 *)gs4d::carve(p, 8 * T);
+    s.order = (uint32_t *)gs4d::carve(p, 4 * T);
     return s;
 }
 

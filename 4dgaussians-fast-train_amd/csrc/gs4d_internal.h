@@ -50,6 +50,7 @@ struct ImageState {
     float *final_T;       // W*H
     uint32_t *n_contrib;  // W*H
     uint2 *ranges;        // T tiles
+    uint32_t *order;      // T tiles, longest run first: the blend kernels' workgroup -> tile map
     static size_t required(int W, int H);
     static ImageState carve(char *base, int W, int H);
 };

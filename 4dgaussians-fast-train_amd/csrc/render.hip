@@ -163,6 +163,7 @@ __device__ __forceinline__ void sort_run(uint32_t *__restrict__ seg, int n, cons
 }
 
 __global__ __launch_bounds__(64) void render_forward_kernel(Args a, const uint2 *__restrict__ ranges,
+                                                            const uint32_t *__restrict__ order,
                                                             uint32_t *__restrict__ upos,
                                                             const float *__restrict__ depths,
                                                             const uint32_t *__restrict__ gid_by_e,
@@ -174,7 +175,7 @@ __global__ __launch_bounds__(64) void render_forward_kernel(Args a, const uint2 
                                                             float *__restrict__ out_color,
                                                             float *__restrict__ out_depth) {
     __shared__ SplatLDS s_sp[64];
-    const int tile = blockIdx.x;
+    const int tile = (int)__builtin_amdgcn_readfirstlane(order[blockIdx.x]);  // longest runs first
     const int tx = tile % a.gx, ty = tile / a.gx;
     const int lane = threadIdx.x;
     const int px = tx * kBlockX + (lane & 15);
@@ -324,7 +325,7 @@ __global__ __launch_bounds__(64) void render_forward_kernel(Args a, const uint2 
 hipError_t launch_render_forward(const Args &a, GeomState g, BinningState b, ImageState img, float *out_color,
                                  float *out_depth, hipStream_t s) {
     const int T = a.gx * a.gy;
-    hipLaunchKernelGGL(render_forward_kernel, dim3(T), dim3(64), 0, s, a, img.ranges, b.upos, g.depths, b.gid_by_e, g.xy,
+    hipLaunchKernelGGL(render_forward_kernel, dim3(T), dim3(64), 0, s, a, img.ranges, img.order, b.upos, g.depths, b.gid_by_e, g.xy,
                        g.conic_opacity, g.rgbd, img.final_T, img.n_contrib, out_color, out_depth);
     return hipGetLastError();
 }
@@ -353,51 +354,49 @@ __device__ __forceinline__ float swap16_add(float a, float b) {
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
-// Wave64 totals of 9 per-lane values, left in LDS: dst[q] = sum over lanes of v[q].  After the two
-// swap stages and the row sums, row r of q0 holds the total of v0,v2,v1,v3 (r = 0..3), of q1 v4,v6,
-// v5,v7 and of q2 v8; the first lane of each row stores it.
-__device__ __forceinline__ void wave_sum9_to_lds(const float v[9], float *dst, int lane) {
-    const float h0 = swap32_add(v[0], v[1]);  // lo: v0, hi: v1
-    const float h1 = swap32_add(v[2], v[3]);  // lo: v2, hi: v3
-    const float h2 = swap32_add(v[4], v[5]);
-    const float h3 = swap32_add(v[6], v[7]);
-    const float h4 = swap32_add(v[8], 0.f);   // lo: v8, hi: 0
-    const float q0 = row_sum(swap16_add(h0, h1));  // rows: v0, v2, v1, v3
-    const float q1 = row_sum(swap16_add(h2, h3));  // rows: v4, v6, v5, v7
-    const float q2 = row_sum(swap16_add(h4, 0.f)); // rows: v8, 0, 0, 0
-    if ((lane & 15) == 0) {
-        const int r = lane >> 4;
-        const int slot = ((r & 1) << 1) | (r >> 1);  // row -> value index {0, 2, 1, 3}
-        dst[slot] = q0;
-        dst[4 + slot] = q1;
-        if (r == 0) dst[8] = q2;
-    }
-}
+// Per-lane partial sums of one splat of the reverse walk, its pixel pair already added: the moments
+// of u = G dL/dalpha in the tile-centred row coordinate yl (sum u, sum u yl, sum u yl^2) and the
+// colour sums (sum w dL/dpix_c, w = alpha T).
+struct SplatPart {
+    float u0, u1, u2, w0, w1, w2;
+};
 
-// Wave64 totals of the 18 per-lane values of two splats (9 each), left in LDS:
-// dst0[q] = sum over lanes of v[q] (q < 9), dst1[q - 9] likewise (q >= 9).  v_permlane32_swap then
-// v_permlane16_swap halve pairs of values (reduce-scatter: after them row r of register i holds value
-// 4i + {0, 2, 1, 3}[r]); a 16-lane DPP tree finishes each register, and the first lane of each row
-// stores its value.
-__device__ __forceinline__ void wave_sum18_to_lds(const float v[18], float *dst0, float *dst1, int lane) {
-    float h[9];
-#pragma unroll
-    for (int m = 0; m < 9; m++) h[m] = swap32_add(v[2 * m], v[2 * m + 1]);
-    float q[5];
-#pragma unroll
-    for (int i = 0; i < 4; i++) q[i] = row_sum(swap16_add(h[2 * i], h[2 * i + 1]));
-    q[4] = row_sum(swap16_add(h[8], 0.f));
+// Wave64 totals of two splats' partial sums, left in LDS as their 9 record values:
+//   0 sum u, 1 sum dx u, 2 sum u yl, 3 sum dx^2 u, 4 sum dx u yl, 5 sum u yl^2, 6-8 colour sums
+// (dx = mean.x - pixel x, per lane column).  v_permlane32_swap then v_permlane16_swap sum each value
+// over the 4 lanes of a column (reduce-scatter: row r of r1 ends with (a.u0, a.u1, b.u0, b.u1)[r], of r2
+// (a.u2, a.w0, b.u2, b.w0)[r], of r3 (a.w1, a.w2, b.w1, b.w2)[r]); the dx-weighted moments are formed
+// on those column sums, and a 16-lane DPP tree sums the columns.  The first lane of each row stores.
+__device__ __forceinline__ void wave_sum_pair_to_lds(const SplatPart &a, const SplatPart &b, float dxa, float dxb,
+                                                     float *dst0, float *dst1, int lane) {
+    const float h0 = swap32_add(a.u0, b.u0);  // lanes 0-31: a, 32-63: b
+    const float h1 = swap32_add(a.u1, b.u1);
+    const float h2 = swap32_add(a.u2, b.u2);
+    const float h3 = swap32_add(a.w0, b.w0);
+    const float h4 = swap32_add(a.w1, b.w1);
+    const float h5 = swap32_add(a.w2, b.w2);
+    const float r1 = swap16_add(h0, h1);
+    const float r2 = swap16_add(h2, h3);
+    const float r3 = swap16_add(h4, h5);
+    const float dxs = lane < 32 ? dxa : dxb;  // rows 0-1 hold splat a, rows 2-3 splat b
+    const float r4 = r1 * dxs;                 // (dx a.u0, dx a.u1, dx b.u0, dx b.u1)
+    const float r5 = r4 * dxs;                 // (dx^2 a.u0, -, dx^2 b.u0, -)
+    const float s1 = row_sum(r1), s2 = row_sum(r2), s3 = row_sum(r3), s4 = row_sum(r4), s5 = row_sum(r5);
     if ((lane & 15) == 0) {
         const int r = lane >> 4;
-        const int slot = ((r & 1) << 1) | (r >> 1);  // row -> value offset {0, 2, 1, 3}
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const int k = 4 * i + slot;
-            float *d = k < 9 ? dst0 + k : dst1 + (k - 9);
-            *d = q[i];
+        float *d = r < 2 ? dst0 : dst1;
+        if (r & 1) {
+            d[2] = s1;
+            d[4] = s4;
+            d[6] = s2;
+            d[8] = s3;
+        } else {
+            d[0] = s1;
+            d[1] = s4;
+            d[3] = s5;
+            d[5] = s2;
+            d[7] = s3;
         }
-        if (r == 0) dst1[7] = q[4];  // value 16
-        if (r == 2) dst1[8] = q[4];  // value 17
     }
 }
 
@@ -420,29 +419,38 @@ __device__ __forceinline__ f2 lo2(const float4 &v) { return f2{v.x, v.y}; }
 __device__ __forceinline__ f2 hi2(const float4 &v) { return f2{v.z, v.w}; }
 
 // One half tile of one splat of the reverse walk: updates the half's pixel state and adds its
-// per-lane partial sums (moments of u = G dL/dalpha, and the colour sums) to U0..U2 / W0..W2.
-// The falloff is the forward's sequence (falloff()) on operand pairs: identical blend decisions.
-__device__ __forceinline__ void walk_half(f2 &T, f2 &A, const f2 dp0, const f2 dp1, const f2 dp2, const f2 nTb,
+// per-lane partial sums (moments of u = G dL/dalpha in the tile-centred row coordinate yl, and the
+// colour sums) to U0..U2 / W0..W2.  The falloff is the forward's sequence (falloff()) on operand pairs:
+// identical blend decisions.  Branch-free, so that the pair walk below is one basic block.
+//   ALL: the splat lies below every pixel's n_contrib (the contributor test passes; pixels outside
+//        the image have T = dL/dpix = 0 and contribute exact zeros).
+//   GEN: the general splat: `chk` = its conic is not positive definite (power > 0 skips, forward.cu:341),
+//        and the 0.99 cap applies; without GEN the opacity is <= 0.9, so o * G never reaches the cap.
+template <bool ALL, bool GEN>
+__device__ __forceinline__ void half_step(f2 &T, f2 &A, const f2 dp0, const f2 dp1, const f2 dp2, const f2 nTb,
                                           const f2 Y2, const f2 C2, const f2 O2, const f2 R2, const f2 G2,
-                                          const f2 B2, const f2 pa2, const f2 pb2, f2 pfy, bool check_pw,
-                                          uint64_t act0, uint64_t act1, f2 &U0, f2 &U1, f2 &U2, f2 &W0, f2 &W1,
-                                          f2 &W2) {
+                                          const f2 B2, const f2 pa2, const f2 pb2, f2 pfy, f2 yl, f2 yl2, bool chk,
+                                          uint32_t contributor, uint32_t last0, uint32_t last1, f2 &U0, f2 &U1,
+                                          f2 &U2, f2 &W0, f2 &W1, f2 &W2) {
     const f2 dy = Y2 - pfy;
     const f2 pw = fma2(dy, fma2(C2, dy, pb2), pa2);
     const f2 G = f2{__builtin_amdgcn_exp2f(pw.x), __builtin_amdgcn_exp2f(pw.y)};
     const f2 al = O2 * G;
-    // backward.cu:486-497: contributor test, alpha < 1/255 and (for a conic that is not positive
-    // definite) power > 0 skips -- the same decisions as the forward (min(0.99, x) >= 1/255 <=> x >= 1/255)
-    uint64_t m0 = ballot(al.x >= 1.0f / 255.0f) & act0;
-    uint64_t m1 = ballot(al.y >= 1.0f / 255.0f) & act1;
-    if (check_pw) {
-        m0 &= ballot(pw.x <= 0.0f);
-        m1 &= ballot(pw.y <= 0.0f);
+    // backward.cu:486-497: contributor test, alpha < 1/255 and power > 0 skips -- the same decisions
+    // as the forward (min(0.99, x) >= 1/255 <=> x >= 1/255)
+    bool k0 = al.x >= 1.0f / 255.0f, k1 = al.y >= 1.0f / 255.0f;
+    if (!ALL) {
+        k0 = k0 && contributor < last0;
+        k1 = k1 && contributor < last1;
+    }
+    if (GEN) {
+        k0 = k0 && (!chk || pw.x <= 0.0f);
+        k1 = k1 && (!chk || pw.y <= 0.0f);
     }
     // the skip applied to G; alpha of a skipped pixel is then min(0.99, o * 0) = 0 exactly
-    const f2 Ge = f2{lane_bit(m0) ? G.x : 0.f, lane_bit(m1) ? G.y : 0.f};
-    const f2 ale = O2 * Ge;
-    const f2 ae = f2{fminf(0.99f, ale.x), fminf(0.99f, ale.y)};
+    const f2 Ge = f2{k0 ? G.x : 0.f, k1 ? G.y : 0.f};
+    f2 ae = O2 * Ge;
+    if (GEN) ae = f2{fminf(0.99f, ae.x), fminf(0.99f, ae.y)};
     const f2 om = bc2(1.f) - ae;
     const f2 inv = f2{__builtin_amdgcn_rcpf(om.x), __builtin_amdgcn_rcpf(om.y)};
     const f2 Tn = T * inv;  // backward.cu:503
@@ -453,26 +461,25 @@ __device__ __forceinline__ void walk_half(f2 &T, f2 &A, const f2 dp0, const f2 d
     A = fma2(ae, diff, A);                      // accum_rec for the next splat in front
     const f2 u = Ge * dLda;
     const f2 w = ae * Tn;                       // dchannel_dcolor (backward.cu:521)
-    const f2 ud = u * dy;
     U0 += u;
-    U1 += ud;
-    U2 = fma2(ud, dy, U2);
+    U1 = fma2(u, yl, U1);
+    U2 = fma2(u, yl2, U2);
     W0 = fma2(w, dp0, W0);
     W1 = fma2(w, dp1, W1);
     W2 = fma2(w, dp2, W2);
 }
 
-// No occupancy attribute: 98 VGPRs (4 waves/SIMD, every tile's wave resident within two rounds) ran
-// as fast as a spilling 80-VGPR build at 6 waves/SIMD.
-__global__ __launch_bounds__(64) void render_backward_kernel(Args a, const uint2 *__restrict__ ranges, const uint32_t *__restrict__ gid_by_e,
+// 3 waves per SIMD (166 VGPRs): the pair walk's four falloff chains need the registers; at 4 waves it spills.
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void render_backward_kernel(Args a, const uint2 *__restrict__ ranges, const uint32_t *__restrict__ order,
+                            const uint32_t *__restrict__ gid_by_e,
                             const uint32_t *__restrict__ upos, const float2 *__restrict__ xy,
                             const float4 *__restrict__ conic_opacity, const float4 *__restrict__ rgbd,
                             const float *__restrict__ colors, const float *__restrict__ final_Ts,
                             const uint32_t *__restrict__ n_contrib, const float *__restrict__ dL_dpixels,
                             float *__restrict__ contrib) {
     __shared__ SplatPairsLDS s_sp[64];
-    __shared__ float4 s_rec[64][3];  // reduced moments of the batch's splats
-    const int tile = blockIdx.x;
+    __shared__ float4 s_rec[64][3];  // reduced sums of the batch's splats
+    const int tile = (int)__builtin_amdgcn_readfirstlane(order[blockIdx.x]);  // longest runs first
     const int tx = tile % a.gx, ty = tile / a.gx;
     const int lane = threadIdx.x;
     const int px = tx * kBlockX + (lane & 15);
@@ -485,6 +492,11 @@ __global__ __launch_bounds__(64) void render_backward_kernel(Args a, const uint2
     if (range.y <= range.x) return;
     const V3 bg = load_v3(a.bg);
     const f2 pfy[2] = {f2{(float)py0, (float)(py0 + 4)}, f2{(float)(py0 + 8), (float)(py0 + 12)}};
+    // rows relative to the tile's centre row (ty*16 + 7.5): the y moments are accumulated in them
+    const float ylane = (float)(lane >> 4) - 7.5f;
+    const f2 yl[2] = {f2{ylane, ylane + 4.f}, f2{ylane + 8.f, ylane + 12.f}};
+    const f2 yl2[2] = {yl[0] * yl[0], yl[1] * yl[1]};
+    const float yc = (float)(ty * kBlockY) + 7.5f;
 
     BwdPixels st;
     uint32_t lastc[4];
@@ -566,8 +578,10 @@ __global__ __launch_bounds__(64) void render_backward_kernel(Args a, const uint2
         const uint32_t ucur = unxt;
         SplatRegs nxt;
         to_regs(nxt, lane < n, raw);
-        const uint64_t reach[2] = {ballot(nxt.reach & 1u), ballot(nxt.reach & 2u)};
-        const uint64_t nonpd = ballot(!conic_pd(nxt.geo, nxt.opc));
+        const float my_l = nxt.geo.y - yc;  // this lane's splat: its record's y moments are shifted by it
+        // per-splat wave masks (the staged zero splats past n are neither)
+        const uint64_t nonpd = ballot(lane < n && !conic_pd(nxt.geo, nxt.opc));
+        const uint64_t hiop = ballot(nxt.opc.y > 0.9f);
         __syncthreads();
         s_sp[lane].q[0] = make_float4(nxt.geo.x, nxt.geo.x, nxt.geo.y, nxt.geo.y);
         s_sp[lane].q[1] = make_float4(nxt.geo.z, nxt.geo.z, nxt.geo.w, nxt.geo.w);
@@ -576,59 +590,72 @@ __global__ __launch_bounds__(64) void render_backward_kernel(Args a, const uint2
         s_sp[lane].q4 = make_float2(nxt.col.z, nxt.col.z);
         __syncthreads();
         if (end - 64 > 0) fetch(end - 64);
-        // batches wholly below every inside pixel's n_contrib: the contributor test passes everywhere
-        const bool all_act = (uint32_t)(end - 1) < min_last;
-        // one splat of the reverse walk: both halves, then its 9 per-lane partial sums into v[]
-        auto walk_splat = [&](int j, float *v) {
-            const float4 q0 = s_sp[j].q[0], q1 = s_sp[j].q[1], q2 = s_sp[j].q[2], q3 = s_sp[j].q[3];
-            const float2 q4 = s_sp[j].q4;
-            const uint32_t contributor = (uint32_t)(end - 1 - j);
-            const f2 dx2 = lo2(q0) - pfx2;
-            const f2 pa2 = lo2(q1) * dx2 * dx2, pb2 = hi2(q1) * dx2;  // forward: geo.z * dx * dx, geo.w * dx
-            const float dx = dx2.x;
-            f2 U0 = bc2(0.f), U1 = bc2(0.f), U2 = bc2(0.f), W0 = bc2(0.f), W1 = bc2(0.f), W2 = bc2(0.f);
-            // a half tile the splat does not reach has alpha = G = 0 at all its pixels: T and A stay,
-            // nothing is added
+        // Splats in pairs, each pair one branch-free block over both halves (a half a splat does not
+        // reach has alpha < 1/255 at every pixel, so walking it changes nothing): the four (splat, half)
+        // falloffs are independent and only the short T / A updates chain, which gives the scheduler
+        // four chains to interleave.  An odd batch's last splat pairs with the zero splat staged past
+        // it (opacity 0: alpha = 0 everywhere, an exact no-op).  The two splats' sums share one
+        // reduce-scatter.
+        auto walk_pair = [&](int j, auto all, auto gen) {
+            constexpr bool ALL = decltype(all)::value, GEN = decltype(gen)::value;
+            SplatPart part[2];
+            float dxs[2];
+            f2 pa2[2], pb2[2];
+            float4 q0[2], q1[2], q2[2], q3[2];
+            float2 q4[2];
 #pragma unroll
-            for (int h = 0; h < 2; h++) {
-                if ((reach[h] >> j) & 1) {
-                    const uint64_t act0 = all_act ? inside_m[2 * h] : ballot(contributor < lastc[2 * h]);
-                    const uint64_t act1 = all_act ? inside_m[2 * h + 1] : ballot(contributor < lastc[2 * h + 1]);
-                    walk_half(st.T[h], st.A[h], st.dp0[h], st.dp1[h], st.dp2[h], st.nTb[h], hi2(q0), lo2(q2),
-                              hi2(q2), lo2(q3), hi2(q3), f2{q4.x, q4.y}, pa2, pb2, pfy[h], (nonpd >> j) & 1, act0, act1,
-                              U0, U1, U2, W0, W1, W2);
-                }
+            for (int i = 0; i < 2; i++) {
+                q0[i] = s_sp[j + i].q[0]; q1[i] = s_sp[j + i].q[1]; q2[i] = s_sp[j + i].q[2];
+                q3[i] = s_sp[j + i].q[3]; q4[i] = s_sp[j + i].q4;
+                const f2 dx2 = lo2(q0[i]) - pfx2;
+                pa2[i] = lo2(q1[i]) * dx2 * dx2;  // forward: geo.z * dx * dx, geo.w * dx
+                pb2[i] = hi2(q1[i]) * dx2;
+                dxs[i] = dx2.x;
             }
-            const float u0 = U0.x + U0.y, u1 = U1.x + U1.y;
-            v[0] = u0;
-            v[1] = dx * u0;
-            v[2] = u1;
-            v[3] = dx * dx * u0;
-            v[4] = dx * u1;
-            v[5] = U2.x + U2.y;
-            v[6] = W0.x + W0.y;
-            v[7] = W1.x + W1.y;
-            v[8] = W2.x + W2.y;
+            f2 U[2][6];
+#pragma unroll
+            for (int i = 0; i < 2; i++)
+#pragma unroll
+                for (int k = 0; k < 6; k++) U[i][k] = bc2(0.f);
+#pragma unroll
+            for (int h = 0; h < 2; h++)
+#pragma unroll
+                for (int i = 0; i < 2; i++)
+                    half_step<ALL, GEN>(st.T[h], st.A[h], st.dp0[h], st.dp1[h], st.dp2[h], st.nTb[h], hi2(q0[i]),
+                                        lo2(q2[i]), hi2(q2[i]), lo2(q3[i]), hi2(q3[i]), f2{q4[i].x, q4[i].y}, pa2[i],
+                                        pb2[i], pfy[h], yl[h], yl2[h], (nonpd >> (j + i)) & 1,
+                                        (uint32_t)(end - 1 - (j + i)), lastc[2 * h], lastc[2 * h + 1], U[i][0],
+                                        U[i][1], U[i][2], U[i][3], U[i][4], U[i][5]);
+#pragma unroll
+            for (int i = 0; i < 2; i++)
+                part[i] = SplatPart{U[i][0].x + U[i][0].y, U[i][1].x + U[i][1].y, U[i][2].x + U[i][2].y,
+                                    U[i][3].x + U[i][3].y, U[i][4].x + U[i][4].y, U[i][5].x + U[i][5].y};
+            wave_sum_pair_to_lds(part[0], part[1], dxs[0], dxs[1], reinterpret_cast<float *>(s_rec[j]),
+                                 reinterpret_cast<float *>(s_rec[j + 1]), lane);
         };
-        // splats in pairs: the two splats' 18 sums share one reduce-scatter
-        int j = 0;
-        for (; j + 1 < n; j += 2) {
-            float v[18];
-            walk_splat(j, v);
-            walk_splat(j + 1, v + 9);
-            wave_sum18_to_lds(v, reinterpret_cast<float *>(s_rec[j]), reinterpret_cast<float *>(s_rec[j + 1]), lane);
-        }
-        if (j < n) {
-            float v[9];
-            walk_splat(j, v);
-            wave_sum9_to_lds(v, reinterpret_cast<float *>(s_rec[j]), lane);
-        }
+        auto walk_batch = [&](auto all) {
+            for (int j = 0; j < n; j += 2) {
+                if (((nonpd | hiop) >> j) & 3) walk_pair(j, all, std::true_type{});
+                else walk_pair(j, all, std::false_type{});
+            }
+        };
+        // batches wholly below every inside pixel's n_contrib: the contributor test passes everywhere
+        if ((uint32_t)(end - 1) < min_last) walk_batch(std::true_type{});
+        else walk_batch(std::false_type{});
         __syncthreads();
         if (lane < n) {
+            // lane j writes splat j's record, its y moments moved from the tile centre to the splat's
+            // centre row: dy = my_l - yl (backward.cu:545-551 moments of dy)
+            const float4 r0 = s_rec[lane][0], r1 = s_rec[lane][1], r2 = s_rec[lane][2];
+            // r0 = (S u, S dx u, S u yl, S dx^2 u), r1 = (S dx u yl, S u yl^2, W0, W1), r2 = (W2, -, -, -)
+            const float s_u = r0.x, s_uyl = r0.z;
+            const float v2 = my_l * s_u - s_uyl;                 // S u dy
+            const float v4 = my_l * r0.y - r1.x;                 // S dx u dy
+            const float v5 = my_l * v2 - (my_l * s_uyl - r1.y);  // S u dy^2
             float4 *rec = reinterpret_cast<float4 *>(contrib + (size_t)ucur * kContribStride);
-            rec[0] = s_rec[lane][0];
-            rec[1] = s_rec[lane][1];
-            rec[2] = s_rec[lane][2];
+            rec[0] = make_float4(s_u, r0.y, v2, r0.w);
+            rec[1] = make_float4(v4, v5, r1.z, r1.w);
+            rec[2] = r2;
         }
     }
 }
@@ -637,7 +664,7 @@ hipError_t launch_render_backward(const Args &a, GeomState g, const uint32_t *gi
                                   ImageState img, const float *colors, const float *dL_dpix, float *contrib,
                                   hipStream_t s) {
     const int T = a.gx * a.gy;
-    hipLaunchKernelGGL(render_backward_kernel, dim3(T), dim3(64), 0, s, a, img.ranges, gid_by_e, upos, g.xy,
+    hipLaunchKernelGGL(render_backward_kernel, dim3(T), dim3(64), 0, s, a, img.ranges, img.order, gid_by_e, upos, g.xy,
                        g.conic_opacity, g.rgbd, colors, img.final_T, img.n_contrib, dL_dpix, contrib);
     return hipGetLastError();
 }

@@ -254,3 +254,35 @@ def test_autograd_api(dev, oracle):
         assert efrac <= GRAD_FRAC, f"{name}: {efrac:.3e} beyond tol (max {emax:.3e})"
     vis = raster.markVisible(leaves["means3D"].detach())
     assert vis.dtype == torch.bool and vis.shape == (3000,)
+
+
+def _image_buffer_views(ib, W, H):
+    """final_T, n_contrib, ranges and order carved from the forward's image buffer (capi.hip
+    ImageState::carve: 256-byte aligned arrays in this order)."""
+    T = ((W + 15) // 16) * ((H + 15) // 16)
+    N = W * H
+    al = lambda x: (x + 255) // 256 * 256
+    base = al(ib.data_ptr()) - ib.data_ptr()
+    raw = ib.cpu().numpy().view(np.uint8)
+    off_r = base + 2 * al(4 * N)
+    ranges = raw[off_r:off_r + 8 * T].view(np.uint32).reshape(T, 2)
+    off_o = off_r + al(8 * T)
+    order = raw[off_o:off_o + 4 * T].view(np.uint32)
+    return ranges, order
+
+
+@pytest.mark.parametrize("W,H", [(1352, 1014), (2304, 1296)])
+def test_tile_order_longest_first(C, oracle, dev, W, H):
+    """The blend kernels take tiles longest run first (tile_order_kernel): the order is a permutation
+    of the tiles with non-increasing run lengths (capped at 1023).  2304x1296 has 11,664 tiles, more than
+    the order kernel keeps in registers (8192), and is checked against the oracle as well."""
+    s = make_scene(100_000 if W == 1352 else 3000, W, H, seed=25)
+    if W == 1352:
+        fwd = c_forward(C, s, to_dev(s, dev))
+    else:
+        fwd, _ = _check(C, oracle, s, dev)
+    ranges, order = _image_buffer_views(fwd[6], W, H)
+    T = ranges.shape[0]
+    assert np.array_equal(np.sort(order), np.arange(T))
+    lens = np.minimum(ranges[order, 1] - ranges[order, 0], 1023)
+    assert np.all(np.diff(lens.astype(np.int64)) <= 0)
