@@ -35,8 +35,10 @@ __device__ __forceinline__ f2 bc2(float x) { return f2{x, x}; }
 
 constexpr float kLog2e = 1.4426950408889634f;
 
-// Blend-ready splat constants.  geo = (x, y, -a/2 log2e, -b log2e), opc = (-c/2 log2e, opacity, -, -),
+// Blend-ready splat constants.  geo = (x, y - yc, -a/2 log2e, -b log2e), opc = (-c/2 log2e, opacity, -, -),
 // col = (r, g, b, depth).  power2 = log2(e) * power (forward.cu:340-342) at offset d = mean - pixel.
+// Rows are measured from the tile's centre row yc = 16 ty + 7.5 (pixel row py = yc + yl, yl a
+// half-integer in [-7.5, 7.5]): dy = (my - yc) - yl, the same two roundings in both kernels.
 struct SplatLDS {
     float4 geo, opc, col;
 };
@@ -82,14 +84,54 @@ __device__ __forceinline__ void to_regs(SplatRegs &s, bool valid, const RawSplat
     }
 }
 
+// The backward's next batch of raw splat attributes, gathered straight into LDS by LDS-DMA loads
+// (global_load_lds: per-lane global address, destination base + lane * size), so the prefetch spans
+// the current batch's walk without holding registers.  cd holds rgbd (16 B per lane) or the caller's
+// colors (three 4-B loads into cd[0..63], cd[64..127], cd[128..191]).
+struct RawLDS {
+    float4 co[64];
+    float cd[64 * 4];
+    float x[64], y[64];
+};
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void gbl_void_t;
+__device__ __forceinline__ void issue_raw_lds(RawLDS &r, bool valid, uint32_t gid, const float2 *__restrict__ xy,
+                                              const float4 *__restrict__ conic_opacity,
+                                              const float4 *__restrict__ rgbd, const float *__restrict__ colors) {
+    if (valid) {
+        __builtin_amdgcn_global_load_lds((gbl_void_t *)(conic_opacity + gid), (lds_void_t *)r.co, 16, 0, 0);
+        if (colors) {
+            const float *c = colors + 3 * (size_t)gid;
+            __builtin_amdgcn_global_load_lds((gbl_void_t *)c, (lds_void_t *)r.cd, 4, 0, 0);
+            __builtin_amdgcn_global_load_lds((gbl_void_t *)(c + 1), (lds_void_t *)(r.cd + 64), 4, 0, 0);
+            __builtin_amdgcn_global_load_lds((gbl_void_t *)(c + 2), (lds_void_t *)(r.cd + 128), 4, 0, 0);
+        } else
+            __builtin_amdgcn_global_load_lds((gbl_void_t *)(rgbd + gid), (lds_void_t *)r.cd, 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((gbl_void_t *)&xy[gid].x, (lds_void_t *)r.x, 4, 0, 0);
+        __builtin_amdgcn_global_load_lds((gbl_void_t *)&xy[gid].y, (lds_void_t *)r.y, 4, 0, 0);
+    }
+}
+// waits for the LDS-DMA loads, then lane l reads its splat of the staged batch
+__device__ __forceinline__ RawSplat read_raw_lds(const RawLDS &r, int lane, bool colors) {
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): the LDS-DMA writes have landed (lgkm/exp counters not waited)
+    __builtin_amdgcn_s_barrier();
+    RawSplat w;
+    w.co = r.co[lane];
+    w.c = colors ? make_float3(r.cd[lane], r.cd[64 + lane], r.cd[128 + lane])
+                 : make_float3(r.cd[4 * lane], r.cd[4 * lane + 1], r.cd[4 * lane + 2]);
+    w.p = make_float2(r.x[lane], r.y[lane]);
+    w.ge = 0;
+    return w;
+}
+
 // Falloff of one splat at a pixel pair: exponent (base 2) and G = 2^power2.  Forward and backward use
 // this one sequence, so they take identical blend decisions.
 struct Falloff {
     f2 dy, pw, G, alpha;
 };
-__device__ __forceinline__ Falloff falloff(const float4 &geo, const float4 &opc, float pa, float pb, f2 pfy) {
+__device__ __forceinline__ Falloff falloff(const float4 &geo, const float4 &opc, float pa, float pb, f2 yl) {
     Falloff f;
-    f.dy = bc2(geo.y) - pfy;
+    f.dy = bc2(geo.y) - yl;
     f.pw = fma2(f.dy, fma2(bc2(opc.x), f.dy, bc2(pb)), bc2(pa));
     f.G = f2{__builtin_amdgcn_exp2f(f.pw.x), __builtin_amdgcn_exp2f(f.pw.y)};
     const f2 al = bc2(opc.y) * f.G;
@@ -181,7 +223,9 @@ __global__ __launch_bounds__(64) void render_forward_kernel(Args a, const uint2 
     const int px = tx * kBlockX + (lane & 15);
     const int py0 = ty * kBlockY + (lane >> 4);
     const float pfx = (float)px;
-    const f2 pfy[2] = {f2{(float)py0, (float)(py0 + 4)}, f2{(float)(py0 + 8), (float)(py0 + 12)}};
+    const float yc = (float)(ty * kBlockY) + 7.5f;
+    const float ylane = (float)(lane >> 4) - 7.5f;
+    const f2 yl[2] = {f2{ylane, ylane + 4.f}, f2{ylane + 8.f, ylane + 12.f}};
     // live pixels (forward.cu:287-289: pixels outside the image never blend)
     uint64_t alive[4];
 #pragma unroll
@@ -246,7 +290,7 @@ __global__ __launch_bounds__(64) void render_forward_kernel(Args a, const uint2 
         if ((alive[0] | alive[1] | alive[2] | alive[3]) == 0) break;  // forward.cu:312-314
         SplatRegs nxt;
         if (base + lane < range.y) {  // blend constants (as to_regs)
-            nxt.geo = make_float4(rp.x, rp.y, (-0.5f * rco.x) * kLog2e, (-rco.y) * kLog2e);
+            nxt.geo = make_float4(rp.x, rp.y - yc, (-0.5f * rco.x) * kLog2e, (-rco.y) * kLog2e);
             nxt.opc = make_float4((-0.5f * rco.z) * kLog2e, rco.w, 0.f, 0.f);
             nxt.col = rcd;
             nxt.reach = rge >> kReachShift;
@@ -271,7 +315,7 @@ __global__ __launch_bounds__(64) void render_forward_kernel(Args a, const uint2 
                 const float4 geo = s_sp[j].geo, opc = s_sp[j].opc, col = s_sp[j].col;
                 const float dx = geo.x - pfx;
                 const float pa = geo.z * dx * dx, pb = geo.w * dx;
-                const Falloff f = falloff(geo, opc, pa, pb, pfy[h]);
+                const Falloff f = falloff(geo, opc, pa, pb, yl[h]);
                 uint64_t m0 = ballot(f.alpha.x >= 1.0f / 255.0f) & alive[2 * h];
                 uint64_t m1 = ballot(f.alpha.y >= 1.0f / 255.0f) & alive[2 * h + 1];
                 if ((nonpd >> j) & 1) {  // forward.cu:341-342
@@ -400,23 +444,14 @@ __device__ __forceinline__ void wave_sum_pair_to_lds(const SplatPart &a, const S
     }
 }
 
-// Per-pixel state of the reverse walk (pairs): T (recovered backwards), A = accum_rec . dL/dpix,
-// dL/dpix and the background term -T_final (bg . dL/dpix) (backward.cu:534).
+// Per-pixel state of the reverse walk (pairs): T (recovered backwards), A = accum_rec . dL/dpix and
+// dL/dpix.  The background term of backward.cu:534, -T_final / (1 - alpha) (bg . dL/dpix), is the
+// background taken as one more layer behind the last contributor (colour bg, alpha 1): A starts at
+// bg . dL/dpix instead of 0, and T_final / (1 - alpha_i) = T_i prod_{i<j} (1 - alpha_j) follows from
+// the walk's own T -- the same value up to rounding, without a per-pixel constant.
 struct BwdPixels {
-    f2 T[2], A[2], dp0[2], dp1[2], dp2[2], nTb[2];
+    f2 T[2], A[2], dp0[2], dp1[2], dp2[2];
 };
-
-// Backward splat constants in LDS, every value stored twice so that a broadcast ds_read_b128 yields
-// the (x, x) operand pairs of the packed-f32 pixel math directly:
-// q0 = (mx, mx, my, my), q1 = (A, A, B, B), q2 = (Cc, Cc, o, o), q3 = (r, r, g, g), q4 = (b, b)
-// with A = -a/2 log2e, B = -b log2e, Cc = -c/2 log2e.
-struct SplatPairsLDS {
-    float4 q[4];
-    float2 q4;
-    float2 pad;
-};
-__device__ __forceinline__ f2 lo2(const float4 &v) { return f2{v.x, v.y}; }
-__device__ __forceinline__ f2 hi2(const float4 &v) { return f2{v.z, v.w}; }
 
 // One half tile of one splat of the reverse walk: updates the half's pixel state and adds its
 // per-lane partial sums (moments of u = G dL/dalpha in the tile-centred row coordinate yl, and the
@@ -427,12 +462,12 @@ __device__ __forceinline__ f2 hi2(const float4 &v) { return f2{v.z, v.w}; }
 //   GEN: the general splat: `chk` = its conic is not positive definite (power > 0 skips, forward.cu:341),
 //        and the 0.99 cap applies; without GEN the opacity is <= 0.9, so o * G never reaches the cap.
 template <bool ALL, bool GEN>
-__device__ __forceinline__ void half_step(f2 &T, f2 &A, const f2 dp0, const f2 dp1, const f2 dp2, const f2 nTb,
+__device__ __forceinline__ void half_step(f2 &T, f2 &A, const f2 dp0, const f2 dp1, const f2 dp2,
                                           const f2 Y2, const f2 C2, const f2 O2, const f2 R2, const f2 G2,
-                                          const f2 B2, const f2 pa2, const f2 pb2, f2 pfy, f2 yl, f2 yl2, bool chk,
+                                          const f2 B2, const f2 pa2, const f2 pb2, f2 yl, f2 yl2, bool chk,
                                           uint32_t contributor, uint32_t last0, uint32_t last1, f2 &U0, f2 &U1,
                                           f2 &U2, f2 &W0, f2 &W1, f2 &W2) {
-    const f2 dy = Y2 - pfy;
+    const f2 dy = Y2 - yl;  // Y2 = my - yc
     const f2 pw = fma2(dy, fma2(C2, dy, pb2), pa2);
     const f2 G = f2{__builtin_amdgcn_exp2f(pw.x), __builtin_amdgcn_exp2f(pw.y)};
     const f2 al = O2 * G;
@@ -457,7 +492,7 @@ __device__ __forceinline__ void half_step(f2 &T, f2 &A, const f2 dp0, const f2 d
     T = Tn;
     const f2 CD = fma2(B2, dp2, fma2(G2, dp1, R2 * dp0));
     const f2 diff = CD - A;
-    const f2 dLda = fma2(diff, Tn, nTb * inv);  // backward.cu:519-534
+    const f2 dLda = diff * Tn;                  // backward.cu:519-534 (bg term in A's start value)
     A = fma2(ae, diff, A);                      // accum_rec for the next splat in front
     const f2 u = Ge * dLda;
     const f2 w = ae * Tn;                       // dchannel_dcolor (backward.cu:521)
@@ -477,21 +512,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
                             const float *__restrict__ colors, const float *__restrict__ final_Ts,
                             const uint32_t *__restrict__ n_contrib, const float *__restrict__ dL_dpixels,
                             float *__restrict__ contrib) {
-    __shared__ SplatPairsLDS s_sp[64];
+    __shared__ SplatLDS s_sp[64];
     __shared__ float4 s_rec[64][3];  // reduced sums of the batch's splats
     const int tile = (int)__builtin_amdgcn_readfirstlane(order[blockIdx.x]);  // longest runs first
     const int tx = tile % a.gx, ty = tile / a.gx;
     const int lane = threadIdx.x;
     const int px = tx * kBlockX + (lane & 15);
     const int py0 = ty * kBlockY + (lane >> 4);
-    const f2 pfx2 = bc2((float)px);
+    const float pfx = (float)px;
     const size_t HW = (size_t)a.W * a.H;
     uint2 range = ranges[tile];
     range.x = __builtin_amdgcn_readfirstlane(range.x);
     range.y = __builtin_amdgcn_readfirstlane(range.y);
     if (range.y <= range.x) return;
     const V3 bg = load_v3(a.bg);
-    const f2 pfy[2] = {f2{(float)py0, (float)(py0 + 4)}, f2{(float)(py0 + 8), (float)(py0 + 12)}};
     // rows relative to the tile's centre row (ty*16 + 7.5): the y moments are accumulated in them
     const float ylane = (float)(lane >> 4) - 7.5f;
     const f2 yl[2] = {f2{ylane, ylane + 4.f}, f2{ylane + 8.f, ylane + 12.f}};
@@ -513,12 +547,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
         const float d2 = inside ? dL_dpixels[2 * HW + pix] : 0.f;
         lastc[k] = inside ? n_contrib[pix] : 0u;
         inside_m[k] = ballot(inside);
-        const float nb = -tf * (bg.x * d0 + bg.y * d1 + bg.z * d2);
+        const float a0 = bg.x * d0 + bg.y * d1 + bg.z * d2;  // the background layer behind the last splat
         const int h = k >> 1;
         if (k & 1) {
-            st.T[h].y = tf; st.dp0[h].y = d0; st.dp1[h].y = d1; st.dp2[h].y = d2; st.nTb[h].y = nb; st.A[h].y = 0.f;
+            st.T[h].y = tf; st.dp0[h].y = d0; st.dp1[h].y = d1; st.dp2[h].y = d2; st.A[h].y = a0;
         } else {
-            st.T[h].x = tf; st.dp0[h].x = d0; st.dp1[h].x = d1; st.dp2[h].x = d2; st.nTb[h].x = nb; st.A[h].x = 0.f;
+            st.T[h].x = tf; st.dp0[h].x = d0; st.dp1[h].x = d1; st.dp2[h].x = d2; st.A[h].x = a0;
         }
         max_last = max(max_last, lastc[k]);
         if (inside) min_last = min(min_last, lastc[k]);
@@ -542,75 +576,78 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
         rec[2] = z4;
     }
     // The walk's instances: emission slot e (where the gradient record goes) and gid_by_e[e] of list
-    // position end-1-lane of each batch, loaded 4 batches at a time (independent loads, one wait per
+    // position end-1-lane of each batch, loaded 2 batches at a time (independent loads, one wait per
     // refill).  The next batch's attributes are issued before the current batch is blended and only
     // turned into blend constants after it, so their loads are the only ones in flight across the
     // blend loop.
-    uint32_t ue[4], ug[4];
+    constexpr int kRing = 2;
+    uint32_t ue[kRing], ug[kRing];
     int ids_left = 0;
     auto refill = [&](int end) {
 #pragma unroll
-        for (int r = 0; r < 4; r++) {
+        for (int r = 0; r < kRing; r++) {
             const int pos = end - 1 - (r * 64 + lane);
             ue[r] = pos >= 0 ? upos[range.x + pos] : 0u;
         }
 #pragma unroll
-        for (int r = 0; r < 4; r++) {
+        for (int r = 0; r < kRing; r++) {
             const int pos = end - 1 - (r * 64 + lane);
             ug[r] = pos >= 0 ? gid_by_e[ue[r]] : 0u;
         }
-        ids_left = 4;
+        ids_left = kRing;
     };
-    RawSplat raw;
+    __shared__ RawLDS s_raw;
     uint32_t unxt = 0;  // where this lane's splat record goes (the instance's emission slot)
+    uint32_t rnxt = 0;  // its half-reach bits
     auto fetch = [&](int end) {  // ids of the batch ending at `end`, then its attribute loads
         if (ids_left == 0) refill(end);
         unxt = ue[0];
         const uint32_t ge = ug[0];
-        ue[0] = ue[1]; ue[1] = ue[2]; ue[2] = ue[3];
-        ug[0] = ug[1]; ug[1] = ug[2]; ug[2] = ug[3];
+        rnxt = ge >> kReachShift;
+#pragma unroll
+        for (int r = 0; r + 1 < kRing; r++) {
+            ue[r] = ue[r + 1];
+            ug[r] = ug[r + 1];
+        }
         ids_left--;
-        issue_raw(raw, lane < min(64, end), ge, xy, conic_opacity, rgbd, colors);  // colors_precomp or rgb
+        issue_raw_lds(s_raw, lane < min(64, end), ge & kGidMask, xy, conic_opacity, rgbd, colors);  // colors_precomp or rgb
     };
     if (max_last > 0) fetch((int)max_last);
     for (int end = (int)max_last; end > 0; end -= 64) {
         const int n = min(64, end);
         const uint32_t ucur = unxt;
+        const uint64_t reach[2] = {ballot(lane < n && (rnxt & 1u)), ballot(lane < n && (rnxt & 2u))};
         SplatRegs nxt;
-        to_regs(nxt, lane < n, raw);
-        const float my_l = nxt.geo.y - yc;  // this lane's splat: its record's y moments are shifted by it
+        to_regs(nxt, lane < n, read_raw_lds(s_raw, lane, colors != nullptr));
+        nxt.geo.y -= yc;                    // my - yc, as the forward stages it
         // per-splat wave masks (the staged zero splats past n are neither)
         const uint64_t nonpd = ballot(lane < n && !conic_pd(nxt.geo, nxt.opc));
         const uint64_t hiop = ballot(nxt.opc.y > 0.9f);
         __syncthreads();
-        s_sp[lane].q[0] = make_float4(nxt.geo.x, nxt.geo.x, nxt.geo.y, nxt.geo.y);
-        s_sp[lane].q[1] = make_float4(nxt.geo.z, nxt.geo.z, nxt.geo.w, nxt.geo.w);
-        s_sp[lane].q[2] = make_float4(nxt.opc.x, nxt.opc.x, nxt.opc.y, nxt.opc.y);
-        s_sp[lane].q[3] = make_float4(nxt.col.x, nxt.col.x, nxt.col.y, nxt.col.y);
-        s_sp[lane].q4 = make_float2(nxt.col.z, nxt.col.z);
+        s_sp[lane].geo = nxt.geo;
+        s_sp[lane].opc = nxt.opc;
+        s_sp[lane].col = nxt.col;
         __syncthreads();
         if (end - 64 > 0) fetch(end - 64);
-        // Splats in pairs, each pair one branch-free block over both halves (a half a splat does not
-        // reach has alpha < 1/255 at every pixel, so walking it changes nothing): the four (splat, half)
-        // falloffs are independent and only the short T / A updates chain, which gives the scheduler
-        // four chains to interleave.  An odd batch's last splat pairs with the zero splat staged past
-        // it (opacity 0: alpha = 0 everywhere, an exact no-op).  The two splats' sums share one
-        // reduce-scatter.
-        auto walk_pair = [&](int j, auto all, auto gen) {
+        // Splats in pairs, each pair one branch-free block over the (splat, half) steps it needs: the
+        // falloffs are independent and only the short T / A updates chain, which gives the scheduler up
+        // to four chains to interleave.  M0 / M1 = the splats (bit 0: j, bit 1: j + 1) walked on half 0 /
+        // half 1: the halves each splat reaches in the common case, all four otherwise (a half a splat
+        // does not reach has alpha < 1/255 at every pixel, so walking it changes nothing).  An odd
+        // batch's last splat pairs with the zero splat staged past it (opacity 0: an exact no-op).  The
+        // two splats' sums share one reduce-scatter.
+        auto walk_pair = [&](int j, auto all, auto gen, auto m0, auto m1) {
             constexpr bool ALL = decltype(all)::value, GEN = decltype(gen)::value;
+            constexpr int M[2] = {decltype(m0)::value, decltype(m1)::value};
             SplatPart part[2];
-            float dxs[2];
-            f2 pa2[2], pb2[2];
-            float4 q0[2], q1[2], q2[2], q3[2];
-            float2 q4[2];
+            float dxs[2], pa[2], pb[2];
+            float4 geo[2], opc[2], col[2];
 #pragma unroll
             for (int i = 0; i < 2; i++) {
-                q0[i] = s_sp[j + i].q[0]; q1[i] = s_sp[j + i].q[1]; q2[i] = s_sp[j + i].q[2];
-                q3[i] = s_sp[j + i].q[3]; q4[i] = s_sp[j + i].q4;
-                const f2 dx2 = lo2(q0[i]) - pfx2;
-                pa2[i] = lo2(q1[i]) * dx2 * dx2;  // forward: geo.z * dx * dx, geo.w * dx
-                pb2[i] = hi2(q1[i]) * dx2;
-                dxs[i] = dx2.x;
+                geo[i] = s_sp[j + i].geo; opc[i] = s_sp[j + i].opc; col[i] = s_sp[j + i].col;
+                dxs[i] = geo[i].x - pfx;
+                pa[i] = geo[i].z * dxs[i] * dxs[i];  // forward: geo.z * dx * dx, geo.w * dx
+                pb[i] = geo[i].w * dxs[i];
             }
             f2 U[2][6];
 #pragma unroll
@@ -621,9 +658,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
             for (int h = 0; h < 2; h++)
 #pragma unroll
                 for (int i = 0; i < 2; i++)
-                    half_step<ALL, GEN>(st.T[h], st.A[h], st.dp0[h], st.dp1[h], st.dp2[h], st.nTb[h], hi2(q0[i]),
-                                        lo2(q2[i]), hi2(q2[i]), lo2(q3[i]), hi2(q3[i]), f2{q4[i].x, q4[i].y}, pa2[i],
-                                        pb2[i], pfy[h], yl[h], yl2[h], (nonpd >> (j + i)) & 1,
+                    if ((M[h] >> i) & 1)
+                    half_step<ALL, GEN>(st.T[h], st.A[h], st.dp0[h], st.dp1[h], st.dp2[h], bc2(geo[i].y),
+                                        bc2(opc[i].x), bc2(opc[i].y), bc2(col[i].x), bc2(col[i].y), bc2(col[i].z),
+                                        bc2(pa[i]), bc2(pb[i]), yl[h], yl2[h], (nonpd >> (j + i)) & 1,
                                         (uint32_t)(end - 1 - (j + i)), lastc[2 * h], lastc[2 * h + 1], U[i][0],
                                         U[i][1], U[i][2], U[i][3], U[i][4], U[i][5]);
 #pragma unroll
@@ -633,10 +671,38 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
             wave_sum_pair_to_lds(part[0], part[1], dxs[0], dxs[1], reinterpret_cast<float *>(s_rec[j]),
                                  reinterpret_cast<float *>(s_rec[j + 1]), lane);
         };
+        using I3 = std::integral_constant<int, 3>;
         auto walk_batch = [&](auto all) {
             for (int j = 0; j < n; j += 2) {
-                if (((nonpd | hiop) >> j) & 3) walk_pair(j, all, std::true_type{});
-                else walk_pair(j, all, std::false_type{});
+                if (((nonpd | hiop) >> j) & 3) {
+                    walk_pair(j, all, std::true_type{}, I3{}, I3{});
+                } else if (!decltype(all)::value) {
+                    walk_pair(j, all, std::false_type{}, I3{}, I3{});
+                } else {
+                    const uint32_t combo = (uint32_t)((reach[0] >> j) & 3u) | (uint32_t)(((reach[1] >> j) & 3u) << 2);
+                    auto go = [&](auto c) {
+                        constexpr int C = decltype(c)::value;
+                        walk_pair(j, all, std::false_type{}, std::integral_constant<int, C & 3>{},
+                                  std::integral_constant<int, (C >> 2)>{});
+                    };
+                    switch (combo) {
+                    case 1: go(std::integral_constant<int, 1>{}); break;
+                    case 2: go(std::integral_constant<int, 2>{}); break;
+                    case 3: go(std::integral_constant<int, 3>{}); break;
+                    case 4: go(std::integral_constant<int, 4>{}); break;
+                    case 5: go(std::integral_constant<int, 5>{}); break;
+                    case 6: go(std::integral_constant<int, 6>{}); break;
+                    case 7: go(std::integral_constant<int, 7>{}); break;
+                    case 8: go(std::integral_constant<int, 8>{}); break;
+                    case 9: go(std::integral_constant<int, 9>{}); break;
+                    case 10: go(std::integral_constant<int, 10>{}); break;
+                    case 11: go(std::integral_constant<int, 11>{}); break;
+                    case 12: go(std::integral_constant<int, 12>{}); break;
+                    case 13: go(std::integral_constant<int, 13>{}); break;
+                    case 14: go(std::integral_constant<int, 14>{}); break;
+                    default: go(std::integral_constant<int, 15>{}); break;
+                    }
+                }
             }
         };
         // batches wholly below every inside pixel's n_contrib: the contributor test passes everywhere
@@ -647,6 +713,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
             // lane j writes splat j's record, its y moments moved from the tile centre to the splat's
             // centre row: dy = my_l - yl (backward.cu:545-551 moments of dy)
             const float4 r0 = s_rec[lane][0], r1 = s_rec[lane][1], r2 = s_rec[lane][2];
+            const float my_l = s_sp[lane].geo.y;  // this lane's splat, my - yc
             // r0 = (S u, S dx u, S u yl, S dx^2 u), r1 = (S dx u yl, S u yl^2, W0, W1), r2 = (W2, -, -, -)
             const float s_u = r0.x, s_uyl = r0.z;
             const float v2 = my_l * s_u - s_uyl;                 // S u dy
