@@ -184,22 +184,26 @@ int gs4d_last_timings(const char **names, float *ms, int max_entries) {
     return n;
 }
 
-int gs4d_mark_visible(int P, const float *means3D, const float *viewmatrix, const float *projmatrix,
-                      uint8_t *present, void *stream_) {
+int gs4d_mark_visible_ex(int P, const float *means3D, const float *viewmatrix, const float *projmatrix,
+                         uint8_t *present, void *stream_, int view_transposed) {
     hipStream_t stream = (hipStream_t)stream_;
     if (P < 0 || (P > 0 && (!means3D || !viewmatrix || !present))) return fail(GS4D_ERR_ARG, "mark_visible: bad args");
     if (P == 0) return GS4D_OK;
-    GS4D_HIP(launch_mark_visible(P, means3D, viewmatrix, present, stream));
+    GS4D_HIP(launch_mark_visible(P, means3D, viewmatrix, view_transposed ? 1 : 0, present, stream));
     return GS4D_OK;
 }
+int gs4d_mark_visible(int P, const float *means3D, const float *viewmatrix, const float *projmatrix,
+                      uint8_t *present, void *stream) {
+    return gs4d_mark_visible_ex(P, means3D, viewmatrix, projmatrix, present, stream, 0);
+}
 
-int gs4d_forward(gs4d_alloc_fn geometry_alloc, void *geometry_ctx, gs4d_alloc_fn binning_alloc, void *binning_ctx,
-                 gs4d_alloc_fn image_alloc, void *image_ctx, int P, int D, int M, const float *background, int width,
-                 int height, const float *means3D, const float *shs, const float *colors_precomp,
-                 const float *opacities, const float *scales, float scale_modifier, const float *rotations,
-                 const float *cov3D_precomp, const float *viewmatrix, const float *projmatrix, const float *cam_pos,
-                 float tan_fovx, float tan_fovy, int prefiltered, float *out_color, float *out_depth, int *radii,
-                 int debug, void *stream_, int *num_rendered) {
+int gs4d_forward_ex(gs4d_alloc_fn geometry_alloc, void *geometry_ctx, gs4d_alloc_fn binning_alloc, void *binning_ctx,
+                    gs4d_alloc_fn image_alloc, void *image_ctx, int P, int D, int M, const float *background,
+                    int width, int height, const float *means3D, const float *shs, const float *colors_precomp,
+                    const float *opacities, const float *scales, float scale_modifier, const float *rotations,
+                    const float *cov3D_precomp, const float *viewmatrix, const float *projmatrix,
+                    const float *cam_pos, float tan_fovx, float tan_fovy, int prefiltered, float *out_color,
+                    float *out_depth, int *radii, int debug, void *stream_, int *num_rendered, int view_transposed) {
     hipStream_t stream = (hipStream_t)stream_;
     *num_rendered = 0;
     if (P < 0 || width <= 0 || height <= 0) return fail(GS4D_ERR_ARG, "forward: P must be >= 0 and the image non-empty");
@@ -217,6 +221,7 @@ int gs4d_forward(gs4d_alloc_fn geometry_alloc, void *geometry_ctx, gs4d_alloc_fn
 
     Args a = make_args(P, D, M, width, height, background, scale_modifier, viewmatrix, projmatrix, cam_pos, tan_fovx,
                        tan_fovy, prefiltered);
+    a.view_transposed = view_transposed ? 1 : 0;
     begin_marks(stream);
 
     const int T = a.gx * a.gy;
@@ -275,14 +280,15 @@ int gs4d_forward(gs4d_alloc_fn geometry_alloc, void *geometry_ctx, gs4d_alloc_fn
     return GS4D_OK;
 }
 
-int gs4d_backward(int P, int D, int M, int R, const float *background, int width, int height, const float *means3D,
-                  const float *shs, const float *colors_precomp, const float *scales, float scale_modifier,
-                  const float *rotations, const float *cov3D_precomp, const float *viewmatrix,
-                  const float *projmatrix, const float *campos, float tan_fovx, float tan_fovy, const int *radii,
-                  char *geom_buffer, char *binning_buffer, char *image_buffer, const float *dL_dpix,
-                  float *dL_dmean2D, float *dL_dconic, float *dL_dopacity, float *dL_dcolor, float *dL_dmean3D,
-                  float *dL_dcov3D, float *dL_dsh, float *dL_dscale, float *dL_drot, gs4d_alloc_fn scratch_alloc,
-                  void *scratch_ctx, int debug, void *stream_) {
+int gs4d_backward_ex(int P, int D, int M, int R, const float *background, int width, int height,
+                     const float *means3D, const float *shs, const float *colors_precomp, const float *scales,
+                     float scale_modifier, const float *rotations, const float *cov3D_precomp,
+                     const float *viewmatrix, const float *projmatrix, const float *campos, float tan_fovx,
+                     float tan_fovy, const int *radii, char *geom_buffer, char *binning_buffer, char *image_buffer,
+                     const float *dL_dpix, float *dL_dmean2D, float *dL_dconic, float *dL_dopacity,
+                     float *dL_dcolor, float *dL_dmean3D, float *dL_dcov3D, float *dL_dsh, float *dL_dscale,
+                     float *dL_drot, gs4d_alloc_fn scratch_alloc, void *scratch_ctx, int debug, void *stream_,
+                     int view_transposed) {
     hipStream_t stream = (hipStream_t)stream_;
     if (P < 0 || R < 0) return fail(GS4D_ERR_ARG, "backward: bad sizes");
     if (P == 0) return GS4D_OK;
@@ -296,6 +302,7 @@ int gs4d_backward(int P, int D, int M, int R, const float *background, int width
         return fail(GS4D_ERR_ARG, "backward: missing camera inputs");
     Args a = make_args(P, D, M, width, height, background, scale_modifier, viewmatrix, projmatrix, campos, tan_fovx,
                        tan_fovy, 0);
+    a.view_transposed = view_transposed ? 1 : 0;
     begin_marks(stream);
     const int T = a.gx * a.gy;
     GeomState g = GeomState::carve(geom_buffer, P, T);
@@ -328,6 +335,34 @@ int gs4d_backward(int P, int D, int M, int R, const float *background, int width
                                         dconic, dL_dcolor, dL_dmean3D, dL_dcov3D, dL_dsh, dL_dscale, dL_drot, stream));
     end_marks();
     return GS4D_OK;
+}
+
+int gs4d_forward(gs4d_alloc_fn geometry_alloc, void *geometry_ctx, gs4d_alloc_fn binning_alloc, void *binning_ctx,
+                 gs4d_alloc_fn image_alloc, void *image_ctx, int P, int D, int M, const float *background, int width,
+                 int height, const float *means3D, const float *shs, const float *colors_precomp,
+                 const float *opacities, const float *scales, float scale_modifier, const float *rotations,
+                 const float *cov3D_precomp, const float *viewmatrix, const float *projmatrix, const float *cam_pos,
+                 float tan_fovx, float tan_fovy, int prefiltered, float *out_color, float *out_depth, int *radii,
+                 int debug, void *stream, int *num_rendered) {
+    return gs4d_forward_ex(geometry_alloc, geometry_ctx, binning_alloc, binning_ctx, image_alloc, image_ctx, P, D, M,
+                           background, width, height, means3D, shs, colors_precomp, opacities, scales, scale_modifier,
+                           rotations, cov3D_precomp, viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, prefiltered,
+                           out_color, out_depth, radii, debug, stream, num_rendered, 0);
+}
+
+int gs4d_backward(int P, int D, int M, int R, const float *background, int width, int height, const float *means3D,
+                  const float *shs, const float *colors_precomp, const float *scales, float scale_modifier,
+                  const float *rotations, const float *cov3D_precomp, const float *viewmatrix,
+                  const float *projmatrix, const float *campos, float tan_fovx, float tan_fovy, const int *radii,
+                  char *geom_buffer, char *binning_buffer, char *image_buffer, const float *dL_dpix,
+                  float *dL_dmean2D, float *dL_dconic, float *dL_dopacity, float *dL_dcolor, float *dL_dmean3D,
+                  float *dL_dcov3D, float *dL_dsh, float *dL_dscale, float *dL_drot, gs4d_alloc_fn scratch_alloc,
+                  void *scratch_ctx, int debug, void *stream) {
+    return gs4d_backward_ex(P, D, M, R, background, width, height, means3D, shs, colors_precomp, scales,
+                            scale_modifier, rotations, cov3D_precomp, viewmatrix, projmatrix, campos, tan_fovx,
+                            tan_fovy, radii, geom_buffer, binning_buffer, image_buffer, dL_dpix, dL_dmean2D,
+                            dL_dconic, dL_dopacity, dL_dcolor, dL_dmean3D, dL_dcov3D, dL_dsh, dL_dscale, dL_drot,
+                            scratch_alloc, scratch_ctx, debug, stream, 0);
 }
 
 int gs4d_knn_mean_dist(int P, const float *points, float *mean_dists, gs4d_alloc_fn scratch_alloc, void *scratch_ctx,

@@ -81,11 +81,14 @@ struct Args {
     float scale_modifier, tan_fovx, tan_fovy, focal_x, focal_y;
     const float *viewmatrix, *projmatrix, *campos, *bg;
     int prefiltered;
+    int view_transposed;  // the 16 view-matrix floats are stored transposed (a (1, 4)-strided 4x4 view)
 };
-__device__ __forceinline__ Mat4 load_mat4(const float *__restrict__ p) {
+// The 4x4 column-major flat matrix m[0..15]; `transposed`: p holds its transpose (p[4 r + c] = m[4 c + r]),
+// which is how the reference's callers hand over world_view_transform (a transposed torch view).
+__device__ __forceinline__ Mat4 load_mat4(const float *__restrict__ p, bool transposed = false) {
     Mat4 m;
 #pragma unroll
-    for (int i = 0; i < 16; i++) m.m[i] = p[i];
+    for (int i = 0; i < 16; i++) m.m[i] = transposed ? p[(i & 3) * 4 + (i >> 2)] : p[i];
     return m;
 }
 __device__ __forceinline__ V3 load_v3(const float *__restrict__ p) { return v3(p[0], p[1], p[2]); }
@@ -178,7 +181,8 @@ __device__ __forceinline__ uint32_t xor_lane(uint32_t v, int lx) {
 hipError_t launch_preprocess(const Args &a, const float *means3D, const float *scales, const float *rotations,
                              const float *opacities, const float *shs, const float *cov3D_precomp,
                              const float *colors_precomp, int *radii, GeomState g, int *err_flag, hipStream_t s);
-hipError_t launch_mark_visible(int P, const float *means3D, const float *viewmatrix, uint8_t *present, hipStream_t s);
+hipError_t launch_mark_visible(int P, const float *means3D, const float *viewmatrix, int view_transposed,
+                               uint8_t *present, hipStream_t s);
 hipError_t launch_visible_scan(const Args &a, GeomState g, hipStream_t s);
 hipError_t launch_binning(const Args &a, GeomState g, const int *radii, BinningState b, int L, ImageState img,
                           hipStream_t s);

@@ -15,7 +15,7 @@ __global__ __launch_bounds__(kPreprocessBlock) void preprocess_kernel(
     const float *__restrict__ colors_precomp, int *__restrict__ radii, GeomState g, int *__restrict__ err_flag) {
     __shared__ uint32_t s_wave[kPreprocessBlock / 64];
     const int idx = blockIdx.x * kPreprocessBlock + threadIdx.x;
-    const Mat4 view = load_mat4(a.viewmatrix), proj = load_mat4(a.projmatrix);
+    const Mat4 view = load_mat4(a.viewmatrix, a.view_transposed), proj = load_mat4(a.projmatrix);
     uint32_t touched = 0;
     if (idx < a.P) {
         int my_r = 0;
@@ -124,17 +124,20 @@ hipError_t launch_preprocess(const Args &a, const float *means3D, const float *s
 
 // rasterizer_impl.cu:54-66 checkFrustum
 __global__ void mark_visible_kernel(int P, const float *__restrict__ means3D, const float *__restrict__ viewmatrix,
+                                    int view_transposed,
                                     uint8_t *__restrict__ present) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= P) return;
-    const Mat4 view = load_mat4(viewmatrix);
+    const Mat4 view = load_mat4(viewmatrix, view_transposed);
     V3 p = v3(means3D[3 * idx], means3D[3 * idx + 1], means3D[3 * idx + 2]);
     V3 pv = transformPoint4x3(p, view);
     present[idx] = !(pv.z <= 0.2f);
 }
 
-hipError_t launch_mark_visible(int P, const float *means3D, const float *viewmatrix, uint8_t *present, hipStream_t s) {
-    hipLaunchKernelGGL(mark_visible_kernel, dim3((P + 255) / 256), dim3(256), 0, s, P, means3D, viewmatrix, present);
+hipError_t launch_mark_visible(int P, const float *means3D, const float *viewmatrix, int view_transposed,
+                               uint8_t *present, hipStream_t s) {
+    hipLaunchKernelGGL(mark_visible_kernel, dim3((P + 255) / 256), dim3(256), 0, s, P, means3D, viewmatrix,
+                       view_transposed, present);
     return hipGetLastError();
 }
 

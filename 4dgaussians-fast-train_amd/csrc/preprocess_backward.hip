@@ -164,7 +164,7 @@ __global__ __launch_bounds__(256) void gaussian_backward_kernel(
     float *dsh = shs ? dL_dsh + (size_t)idx * a.M * 3 : nullptr;
     int nsh_written = 0;
     if (radii[idx] > 0) {
-        const Mat4 view = load_mat4(a.viewmatrix), projm = load_mat4(a.projmatrix);
+        const Mat4 view = load_mat4(a.viewmatrix, a.view_transposed), projm = load_mat4(a.projmatrix);
         const V3 m = v3(means3D[3 * idx], means3D[3 * idx + 1], means3D[3 * idx + 2]);
         float cov3D[6];
 #pragma unroll

@@ -47,6 +47,20 @@ torch::Tensor prep(const torch::Tensor &t, const char *name, const torch::Device
 }
 const float *fptr(const torch::Tensor &t) { return t.numel() ? t.data_ptr<float>() : nullptr; }
 
+// The view matrix as the reference's callers pass it: world_view_transform is a transposed 4x4 view
+// (strides (1, 4)); such a matrix is read in place by the kernels (view_transposed = 1) instead of
+// being copied by .contiguous().  Anything else goes through prep().
+torch::Tensor prep_view(const torch::Tensor &t, const torch::Device &dev, int &transposed) {
+    transposed = 0;
+    if (t.numel() == 16 && t.dim() >= 2 && t.size(-1) == 4 && t.size(-2) == 4 && t.stride(-1) == 4 &&
+        t.stride(-2) == 1 && t.is_cuda() && t.device() == dev && t.scalar_type() == torch::kFloat32 &&
+        (reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0) {
+        transposed = 1;
+        return t;
+    }
+    return prep(t, "viewmatrix", dev);
+}
+
 }  // namespace
 
 // rasterize_points.cu:35-117
@@ -85,17 +99,19 @@ RasterizeGaussians(const torch::Tensor &background, const torch::Tensor &means3D
     if (sh.size(0) != 0) M = sh.size(1);
     auto bg = prep(background, "bg", dev), m3 = prep(means3D, "means3D", dev), col = prep(colors, "colors_precomp", dev),
          op = prep(opacity, "opacities", dev), sc = prep(scales, "scales", dev), rot = prep(rotations, "rotations", dev),
-         c3 = prep(cov3D_precomp, "cov3D_precomp", dev), vm = prep(viewmatrix, "viewmatrix", dev),
-         pm = prep(projmatrix, "projmatrix", dev), shc = prep(sh, "sh", dev), cp = prep(campos, "campos", dev);
+         c3 = prep(cov3D_precomp, "cov3D_precomp", dev), pm = prep(projmatrix, "projmatrix", dev),
+         shc = prep(sh, "sh", dev), cp = prep(campos, "campos", dev);
+    int vt = 0;
+    auto vm = prep_view(viewmatrix, dev, vt);
 
     Resizer rg{&geomBuffer}, rb{&binningBuffer}, ri{&imgBuffer};
     hipStream_t stream = c10::hip::getCurrentHIPStream(dev.index()).stream();
     int rendered = 0;
-    int st = gs4d_forward(resize_cb, &rg, resize_cb, &rb, resize_cb, &ri, P, degree, M, fptr(bg), W, H, fptr(m3),
-                          fptr(shc), fptr(col), fptr(op), fptr(sc), scale_modifier, fptr(rot), fptr(c3), fptr(vm),
-                          fptr(pm), fptr(cp), tan_fovx, tan_fovy, prefiltered ? 1 : 0, out_color.data_ptr<float>(),
-                          out_depth.data_ptr<float>(), radii.data_ptr<int>(), debug ? 1 : 0, (void *)stream,
-                          &rendered);
+    int st = gs4d_forward_ex(resize_cb, &rg, resize_cb, &rb, resize_cb, &ri, P, degree, M, fptr(bg), W, H, fptr(m3),
+                             fptr(shc), fptr(col), fptr(op), fptr(sc), scale_modifier, fptr(rot), fptr(c3), fptr(vm),
+                             fptr(pm), fptr(cp), tan_fovx, tan_fovy, prefiltered ? 1 : 0, out_color.data_ptr<float>(),
+                             out_depth.data_ptr<float>(), radii.data_ptr<int>(), debug ? 1 : 0, (void *)stream,
+                             &rendered, vt);
     check_status(st, "rasterize_gaussians");
     return std::make_tuple(rendered, out_color, out_depth, radii, geomBuffer, binningBuffer, imgBuffer);
 }
@@ -130,16 +146,18 @@ RasterizeGaussiansBackward(const torch::Tensor &background, const torch::Tensor 
     if (P != 0) {
         auto bg = prep(background, "bg", dev), m3 = prep(means3D, "means3D", dev), col = prep(colors, "colors_precomp", dev),
              sc = prep(scales, "scales", dev), rot = prep(rotations, "rotations", dev),
-             c3 = prep(cov3D_precomp, "cov3D_precomp", dev), vm = prep(viewmatrix, "viewmatrix", dev),
-             pm = prep(projmatrix, "projmatrix", dev), dl = prep(dL_dout_color, "grad_out_color", dev),
-             shc = prep(sh, "sh", dev), cp = prep(campos, "campos", dev);
+             c3 = prep(cov3D_precomp, "cov3D_precomp", dev), pm = prep(projmatrix, "projmatrix", dev),
+             dl = prep(dL_dout_color, "grad_out_color", dev), shc = prep(sh, "sh", dev),
+             cp = prep(campos, "campos", dev);
+        int vt = 0;
+        auto vm = prep_view(viewmatrix, dev, vt);
         torch::Tensor rad = radii.contiguous();
         if (rad.numel() && (rad.scalar_type() != torch::kInt32 || !rad.is_cuda()))
             throw std::runtime_error("radii must be an int32 GPU tensor");
         torch::Tensor scratch = torch::empty({0}, means3D.options().dtype(torch::kByte));
         Resizer rs{&scratch};
         hipStream_t stream = c10::hip::getCurrentHIPStream(dev.index()).stream();
-        int st = gs4d_backward(
+        int st = gs4d_backward_ex(
             P, degree, M, R, fptr(bg), W, H, fptr(m3), fptr(shc), fptr(col), fptr(sc), scale_modifier, fptr(rot),
             fptr(c3), fptr(vm), fptr(pm), fptr(cp), tan_fovx, tan_fovy, rad.numel() ? rad.data_ptr<int>() : nullptr,
             reinterpret_cast<char *>(geomBuffer.data_ptr()),
@@ -147,7 +165,7 @@ RasterizeGaussiansBackward(const torch::Tensor &background, const torch::Tensor 
             reinterpret_cast<char *>(imageBuffer.data_ptr()), fptr(dl), dL_dmeans2D.data_ptr<float>(), nullptr,
             dL_dopacity.data_ptr<float>(), dL_dcolors.data_ptr<float>(), dL_dmeans3D.data_ptr<float>(),
             dL_dcov3D.data_ptr<float>(), M ? dL_dsh.data_ptr<float>() : nullptr, dL_dscales.data_ptr<float>(),
-            dL_drotations.data_ptr<float>(), resize_cb, &rs, debug ? 1 : 0, (void *)stream);
+            dL_drotations.data_ptr<float>(), resize_cb, &rs, debug ? 1 : 0, (void *)stream, vt);
         check_status(st, "rasterize_gaussians_backward");
     }
     return std::make_tuple(dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales,
@@ -162,11 +180,12 @@ torch::Tensor MarkVisible(torch::Tensor &means3D, torch::Tensor &viewmatrix, tor
         if (!means3D.is_cuda()) throw std::runtime_error("means3D must be a HIP (GPU) tensor; the MI355X rasterizer has no CPU path");
         const auto dev = means3D.device();
         c10::hip::HIPGuard guard(dev.index());
-        auto m3 = prep(means3D, "means3D", dev), vm = prep(viewmatrix, "viewmatrix", dev),
-             pm = prep(projmatrix, "projmatrix", dev);
+        auto m3 = prep(means3D, "means3D", dev), pm = prep(projmatrix, "projmatrix", dev);
+        int vt = 0;
+        auto vm = prep_view(viewmatrix, dev, vt);
         hipStream_t stream = c10::hip::getCurrentHIPStream(dev.index()).stream();
-        int st = gs4d_mark_visible(P, fptr(m3), fptr(vm), fptr(pm), reinterpret_cast<uint8_t *>(present.data_ptr<bool>()),
-                                   (void *)stream);
+        int st = gs4d_mark_visible_ex(P, fptr(m3), fptr(vm), fptr(pm),
+                                      reinterpret_cast<uint8_t *>(present.data_ptr<bool>()), (void *)stream, vt);
         check_status(st, "mark_visible");
     }
     return present;

@@ -76,6 +76,30 @@ int gs4d_backward(int P, int D, int M, int R, const float *background, int width
                   float *dL_dcov3D, float *dL_dsh, float *dL_dscale, float *dL_drot, gs4d_alloc_fn scratch_alloc,
                   void *scratch_ctx, int debug, void *stream);
 
+/* The same three entry points for a view matrix handed over transposed (view_transposed = 1: the 16
+ * floats hold the transpose of the column-major matrix, i.e. a (1, 4)-strided 4x4 view such as the
+ * reference callers' world_view_transform.cuda(), gaussian_renderer/__init__.py:45).  Reading it in
+ * place saves the caller a copy per call; view_transposed = 0 is the plain entry point.  projmatrix
+ * is always the column-major flat layout. */
+int gs4d_mark_visible_ex(int P, const float *means3D, const float *viewmatrix, const float *projmatrix,
+                         uint8_t *present, void *stream, int view_transposed);
+int gs4d_forward_ex(gs4d_alloc_fn geometry_alloc, void *geometry_ctx, gs4d_alloc_fn binning_alloc, void *binning_ctx,
+                    gs4d_alloc_fn image_alloc, void *image_ctx, int P, int D, int M, const float *background,
+                    int width, int height, const float *means3D, const float *shs, const float *colors_precomp,
+                    const float *opacities, const float *scales, float scale_modifier, const float *rotations,
+                    const float *cov3D_precomp, const float *viewmatrix, const float *projmatrix,
+                    const float *cam_pos, float tan_fovx, float tan_fovy, int prefiltered, float *out_color,
+                    float *out_depth, int *radii, int debug, void *stream, int *num_rendered, int view_transposed);
+int gs4d_backward_ex(int P, int D, int M, int R, const float *background, int width, int height,
+                     const float *means3D, const float *shs, const float *colors_precomp, const float *scales,
+                     float scale_modifier, const float *rotations, const float *cov3D_precomp,
+                     const float *viewmatrix, const float *projmatrix, const float *campos, float tan_fovx,
+                     float tan_fovy, const int *radii, char *geom_buffer, char *binning_buffer, char *image_buffer,
+                     const float *dL_dpix, float *dL_dmean2D, float *dL_dconic, float *dL_dopacity,
+                     float *dL_dcolor, float *dL_dmean3D, float *dL_dcov3D, float *dL_dsh, float *dL_dscale,
+                     float *dL_drot, gs4d_alloc_fn scratch_alloc, void *scratch_ctx, int debug, void *stream,
+                     int view_transposed);
+
 /* Replaces SimpleKNN::knn (submodules/simple-knn/simple_knn.h:14-20, simple_knn.cu:187-223), the
  * native layer behind simple_knn._C.distCUDA2 (spatial.cu:15-25, ext.cpp:15-16), which
  * scene/gaussian_model.py:148-149 uses to initialise the Gaussian scales.

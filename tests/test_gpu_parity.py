@@ -286,3 +286,23 @@ def test_tile_order_longest_first(C, oracle, dev, W, H):
     assert np.array_equal(np.sort(order), np.arange(T))
     lens = np.minimum(ranges[order, 1] - ranges[order, 0], 1023)
     assert np.all(np.diff(lens.astype(np.int64)) <= 0)
+
+
+def test_view_matrix_layouts_agree(C, dev):
+    """The reference's callers pass world_view_transform as a transposed (1, 4)-strided view, which the
+    kernels read in place (gs4d_*_ex, view_transposed = 1); a contiguous copy of the same matrix takes
+    the plain path.  Both must give bit-identical images, radii, gradients and visibility."""
+    s = make_scene(5000, 200, 136, seed=26)
+    d = to_dev(s, dev)
+    vm_c = d["viewmatrix"].contiguous()
+    vm_t = vm_c.t().contiguous().t()
+    assert vm_t.stride() == (1, 4) and vm_c.stride() == (4, 1) and torch.equal(vm_t, vm_c)
+    outs = []
+    for vm in (vm_c, vm_t):
+        dd = dict(d, viewmatrix=vm)
+        fwd = c_forward(C, s, dd)
+        grads = c_backward(C, s, dd, fwd, torch.sign(fwd[1] - 0.5))
+        vis = C.mark_visible(dd["means3D"], vm, dd["projmatrix"])
+        outs.append([fwd[1], fwd[2], fwd[3], vis] + list(grads))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
