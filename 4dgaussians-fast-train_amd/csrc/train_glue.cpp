@@ -213,6 +213,7 @@ static gs4d_reg_batch reg_batch(const std::vector<torch::Tensor> &planes, const 
     need(w_smooth.size() == planes.size() && w_l1.size() == planes.size(), "hexplane_reg: one weight pair per plane");
     gs4d_reg_batch b;
     b.count = (int)planes.size();
+    b.accumulate = 0;
     int64_t blocks = 0;
     for (size_t i = 0; i < planes.size(); i++) {
         const torch::Tensor &p = planes[i];
@@ -252,6 +253,22 @@ std::vector<torch::Tensor> hexplane_reg_backward(std::vector<torch::Tensor> plan
     auto dloss = dloss_.to(planes[0].device(), torch::kFloat32).contiguous();
     check(gs4d_hexplane_reg_backward(&b, dloss.data_ptr<float>(), (void *)stream_of(planes[0])), "hexplane_reg backward");
     return grads;
+}
+
+// the regulariser's gradient added in place to the planes' existing gradients (one launch for all)
+void hexplane_reg_accumulate(std::vector<torch::Tensor> planes, std::vector<torch::Tensor> grads,
+                             std::vector<double> w_smooth, std::vector<double> w_l1, const torch::Tensor &dloss_) {
+    need(grads.size() == planes.size(), "hexplane_reg_accumulate: one gradient per plane");
+    for (size_t i = 0; i < planes.size(); i++) {
+        gpu_f32(grads[i], "hexplane_reg gradient");
+        need(grads[i].sizes() == planes[i].sizes() && grads[i].is_contiguous(),
+             "hexplane_reg_accumulate: gradients must be contiguous and shaped like their planes");
+    }
+    gs4d_reg_batch b = reg_batch(planes, w_smooth, w_l1, &grads);
+    b.accumulate = 1;
+    c10::hip::HIPGuard guard(planes[0].device().index());
+    auto dloss = dloss_.to(planes[0].device(), torch::kFloat32).contiguous();
+    check(gs4d_hexplane_reg_backward(&b, dloss.data_ptr<float>(), (void *)stream_of(planes[0])), "hexplane_reg accumulate");
 }
 
 // ---- Linear weight gradients: [(dw (n, W), db (n))] for pairs dy (P, n), x (P, W) (row strides kept)
@@ -329,6 +346,7 @@ PYBIND11_MODULE(_C, m) {
     m.def("linear_dw", &linear_dw);
     m.def("hexplane_reg_forward", &hexplane_reg_forward);
     m.def("hexplane_reg_backward", &hexplane_reg_backward);
+    m.def("hexplane_reg_accumulate", &hexplane_reg_accumulate);
     m.def("hexplane_forward", &hexplane_forward, py::arg("pts"), py::arg("planes"), py::arg("order") = py::none());
     m.def("hexplane_backward", &hexplane_backward);
     m.def("l1_forward", &l1_forward);

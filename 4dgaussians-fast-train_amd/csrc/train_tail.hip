@@ -211,7 +211,9 @@ __global__ __launch_bounds__(kTailThreads) void reg_backward_kernel(gs4d_reg_bat
         const float t = d.data[i];
         const float one_m = 1.f - t;
         const float sg = (float)((one_m > 0.f) - (one_m < 0.f));
-        d.grad[i] = (df_prev - df_cur) + (-sg) * gl;
+        const float v = (df_prev - df_cur) + (-sg) * gl;
+        if (b.accumulate) d.grad[i] += v;
+        else d.grad[i] = v;
     }
 }
 

@@ -74,6 +74,10 @@ class _RasterizeGaussians(torch.autograd.Function):
             _C.rasterize_gaussians, args, s.debug, "snapshot_fw.dump", "forward")
         ctx.raster_settings = s
         ctx.num_rendered = num_rendered
+        # radii are integers and the depth image gets no gradient (below): autograd need not build
+        # zero gradients for them before calling backward
+        ctx.mark_non_differentiable(radii)
+        ctx.set_materialize_grads(False)
         ctx.save_for_backward(colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geom_buf,
                               binning_buf, img_buf)
         return color, radii, depth
@@ -83,6 +87,8 @@ class _RasterizeGaussians(torch.autograd.Function):
         # grad_radii and grad_depth are ignored, exactly like the reference (:100-101): no gradient
         # flows from the depth image.
         s = ctx.raster_settings
+        if grad_out_color is None:  # only the depth image was used: nothing flows back (as the reference)
+            return (None,) * 9
         (colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geom_buf, binning_buf,
          img_buf) = ctx.saved_tensors
         # positional order of _C.rasterize_gaussians_backward (rasterize_points.h:40-62)

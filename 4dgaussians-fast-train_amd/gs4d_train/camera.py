@@ -61,6 +61,16 @@ class Camera:
             self.projection_matrix.unsqueeze(0))).squeeze(0)
         self.camera_center = self.world_view_transform.inverse()[3, :3]
 
+    def on_device(self, dev):
+        """(world_view_transform, full_proj_transform, camera_center) on `dev`, copied once per device
+        (render() of the reference copies them host->device on every call, gaussian_renderer:45-51)."""
+        cache = self.__dict__.setdefault("_dev_cache", {})
+        key = str(dev)
+        if key not in cache:
+            cache[key] = (self.world_view_transform.to(dev), self.full_proj_transform.to(dev),
+                          self.camera_center.to(dev))
+        return cache[key]
+
     @property
     def tanfovx(self):
         return math.tan(self.FoVx * 0.5)

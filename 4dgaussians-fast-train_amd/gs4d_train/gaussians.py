@@ -370,6 +370,21 @@ class GaussianModel:
         l1 = sum(torch.abs(1 - g[i]).mean() for g in grids if len(g) != 3 for i in [2, 4, 5])
         return plane_tv_weight * plane + time_smoothness_weight * time + l1_time_planes_weight * l1
 
+    def regulation_value(self, time_smoothness_weight, l1_time_planes_weight, plane_tv_weight):
+        """compute_regulation's value with no autograd graph (fused path; see add_regulation_grad)."""
+        from .kernels import hexplane_regulation_value
+        grids = self._deformation.deformation_net.grid.grids
+        return hexplane_regulation_value([list(g) for g in grids], time_smoothness_weight, l1_time_planes_weight,
+                                         plane_tv_weight)
+
+    def add_regulation_grad(self, time_smoothness_weight, l1_time_planes_weight, plane_tv_weight, scale=1.0):
+        """scale * d(compute_regulation)/d(plane) added to the planes' .grad in one launch: the gradient
+        the loss's regulariser term contributes, applied after the rest of the backward."""
+        from .kernels import hexplane_regulation_accumulate_grad
+        grids = self._deformation.deformation_net.grid.grids
+        hexplane_regulation_accumulate_grad([list(g) for g in grids], time_smoothness_weight, l1_time_planes_weight,
+                                            plane_tv_weight, scale)
+
     # ---- on-disk formats (gaussian_model.py:214-314 and scene/__init__.py:143-150)
     def save_ply(self, path):
         from .ply import save_gaussians

@@ -10,7 +10,8 @@ import torch
 
 from . import _C
 
-__all__ = ["l1_loss", "densify_stats", "FusedAdam", "hexplane", "hexplane_regulation"]
+__all__ = ["l1_loss", "densify_stats", "FusedAdam", "hexplane", "hexplane_regulation", "hexplane_regulation_value",
+           "hexplane_regulation_accumulate_grad"]
 
 
 class _L1Loss(torch.autograd.Function):
@@ -144,6 +145,45 @@ class _HexPlaneReg(torch.autograd.Function):
         planes = ctx.saved_tensors
         grads = _C.hexplane_reg_backward(list(planes), ctx.w[0], ctx.w[1], dloss.reshape(1))
         return (None, None, *grads)
+
+
+def _reg_batch(ms_grids, time_smoothness_weight, l1_time_planes_weight, plane_tv_weight):
+    planes, ws, wl = [], [], []
+    for g in ms_grids:
+        if len(g) == 3:
+            continue
+        for i in range(6):
+            planes.append(g[i])
+            time = i in (2, 4, 5)
+            ws.append(float(time_smoothness_weight if time else plane_tv_weight))
+            wl.append(float(l1_time_planes_weight if time else 0.0))
+    return planes, ws, wl
+
+
+@torch.no_grad()
+def hexplane_regulation_value(ms_grids, time_smoothness_weight, l1_time_planes_weight, plane_tv_weight):
+    """hexplane_regulation's value, outside autograd (its gradient comes from
+    hexplane_regulation_accumulate_grad after the step's backward)."""
+    planes, ws, wl = _reg_batch(ms_grids, time_smoothness_weight, l1_time_planes_weight, plane_tv_weight)
+    if not planes:
+        return torch.zeros((), device=ms_grids[0][0].device)
+    return _C.hexplane_reg_forward([p.detach().contiguous() for p in planes], ws, wl)
+
+
+@torch.no_grad()
+def hexplane_regulation_accumulate_grad(ms_grids, time_smoothness_weight, l1_time_planes_weight, plane_tv_weight,
+                                        scale=1.0):
+    """Adds scale * d(regulariser)/d(plane) to every plane's .grad in one launch: the gradient autograd
+    would add to the field's plane gradients when the regulariser is part of the loss (train.py:251-254),
+    without autograd's separate add per plane.  A plane without a gradient yet gets one."""
+    planes, ws, wl = _reg_batch(ms_grids, time_smoothness_weight, l1_time_planes_weight, plane_tv_weight)
+    if not planes:
+        return
+    for p in planes:
+        if p.grad is None:
+            p.grad = torch.zeros_like(p)
+    dloss = torch.full((1,), float(scale), device=planes[0].device)
+    _C.hexplane_reg_accumulate([p.detach() for p in planes], [p.grad for p in planes], ws, wl, dloss)
 
 
 def hexplane_regulation(ms_grids, time_smoothness_weight, l1_time_planes_weight, plane_tv_weight):

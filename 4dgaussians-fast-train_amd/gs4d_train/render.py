@@ -14,20 +14,22 @@ import diff_gaussian_rasterization as dgr
 
 def render(viewpoint_camera, pc, pipe_debug, bg_color, scaling_modifier=1.0, stage="fine"):
     xyz = pc.get_xyz
-    screenspace_points = torch.zeros_like(xyz, dtype=xyz.dtype, requires_grad=True, device=xyz.device) + 0
-    try:
-        screenspace_points.retain_grad()
-    except Exception:
-        pass
+    # the rasterizer's means2D gradient sink (:24-29 builds zeros + 0 and retains its grad; a zero leaf
+    # holds the same values and receives the same .grad)
+    screenspace_points = torch.zeros_like(xyz, dtype=xyz.dtype, requires_grad=True, device=xyz.device)
     dev = xyz.device
+    if hasattr(viewpoint_camera, "on_device"):
+        view_m, proj_m, cam_c = viewpoint_camera.on_device(dev)
+    else:
+        view_m, proj_m, cam_c = (viewpoint_camera.world_view_transform.to(dev),
+                                 viewpoint_camera.full_proj_transform.to(dev), viewpoint_camera.camera_center.to(dev))
     settings = dgr.GaussianRasterizationSettings(
         image_height=int(viewpoint_camera.image_height), image_width=int(viewpoint_camera.image_width),
         tanfovx=math.tan(viewpoint_camera.FoVx * 0.5), tanfovy=math.tan(viewpoint_camera.FoVy * 0.5),
-        bg=bg_color, scale_modifier=scaling_modifier,
-        viewmatrix=viewpoint_camera.world_view_transform.to(dev),
-        projmatrix=viewpoint_camera.full_proj_transform.to(dev), sh_degree=pc.active_sh_degree,
-        campos=viewpoint_camera.camera_center.to(dev), prefiltered=False, debug=pipe_debug)
-    time = torch.tensor(viewpoint_camera.time).to(dev).repeat(xyz.shape[0], 1)
+        bg=bg_color, scale_modifier=scaling_modifier, viewmatrix=view_m, projmatrix=proj_m,
+        sh_degree=pc.active_sh_degree, campos=cam_c, prefiltered=False, debug=pipe_debug)
+    # torch.tensor(time).to(dev).repeat(P, 1) (:52): the same float32 column, filled on the device
+    time = torch.full((xyz.shape[0], 1), float(torch.tensor(viewpoint_camera.time)), device=dev)
     rasterizer = dgr.GaussianRasterizer(raster_settings=settings)
     opacity, shs, scales, rotations = pc._opacity, pc.get_features, pc._scaling, pc._rotation
     if "coarse" in stage:

@@ -63,9 +63,17 @@ def train_step(gaussians, views, opt, hyper, iteration, background, stage="fine"
         loss = Ll1 * (len(mine) / len(views)) if data_parallel else Ll1
     else:
         loss = torch.zeros((), device=dev)
+    reg_w = (hyper.time_smoothness_weight, hyper.l1_time_planes, hyper.plane_tv_weight)
+    reg_scale = 1.0 / dp.world() if data_parallel else 1.0
+    reg_deferred = None
     if stage == "fine" and hyper.time_smoothness_weight != 0:
-        reg = gaussians.compute_regulation(hyper.time_smoothness_weight, hyper.l1_time_planes, hyper.plane_tv_weight)
-        loss = loss + (reg / dp.world() if data_parallel else reg)
+        if fused:
+            # the regulariser depends only on the planes: its value joins the reported loss and its
+            # gradient is added to the planes' gradients after the backward, in one launch
+            reg_deferred = gaussians.regulation_value(*reg_w) * reg_scale
+        else:
+            reg = gaussians.compute_regulation(*reg_w)
+            loss = loss + reg * reg_scale
     if opt.lambda_dssim != 0 and images:
         from .losses import ssim
         loss = loss + opt.lambda_dssim * (1.0 - ssim(image_tensor, gt_image_tensor)) * (
@@ -74,6 +82,9 @@ def train_step(gaussians, views, opt, hyper, iteration, background, stage="fine"
     # constant loss: nothing to back-propagate, its gradients are the zeros filled in below
     if loss.requires_grad:
         loss.backward()
+    if reg_deferred is not None:
+        gaussians.add_regulation_grad(*reg_w, scale=reg_scale)
+        loss = loss.detach() + reg_deferred
     if len(vs_list) == 1 and vs_list[0].grad is not None:
         viewspace_grad = vs_list[0].grad
     else:

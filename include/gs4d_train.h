@@ -98,8 +98,9 @@ int gs4d_hexplane_backward(int N, const float *pts, const uint32_t *order, const
  * l1_time_planes for the time planes, 0 otherwise).  H >= 3.  forward: *loss = the sum over the
  * batch (fp64 partials summed in a fixed order; scratch of gs4d_reg_scratch_bytes).  backward: grad
  * (1, C, H, W) of each plane = dloss * d(loss)/d(t), the gradient autograd derives from the
- * reference's graph (assigned, not accumulated).  first_block of plane i = the sum of
- * gs4d_reg_blocks over planes 0..i-1. */
+ * reference's graph: assigned, or with accumulate = 1 added to what grad holds (the plane's .grad after
+ * the field's backward: the sum autograd would form, without its extra add per plane).  first_block of
+ * plane i = the sum of gs4d_reg_blocks over planes 0..i-1. */
 #define GS4D_REG_MAX_PLANES 24
 typedef struct {
     const float *data;
@@ -110,6 +111,7 @@ typedef struct {
 } gs4d_reg_plane;
 typedef struct {
     int count;
+    int accumulate;
     gs4d_reg_plane p[GS4D_REG_MAX_PLANES];
 } gs4d_reg_batch;
 int64_t gs4d_reg_blocks(int C, int H, int W);

@@ -65,7 +65,7 @@ def op_profile(cfg="metric", steps=5):
             train_step(g, views, opt, hyper, 3006 + i, bg)
         torch.cuda.synchronize()
     if "--shapes" in sys.argv:
-        print(prof.key_averages(group_by_input_shape=True).table(sort_by="cuda_time_total", row_limit=60,
+        print(prof.key_averages(group_by_input_shape=True).table(sort_by="cuda_time_total", row_limit=400,
                                                                  max_name_column_width=40, max_shapes_column_width=70))
     else:
         print(prof.key_averages().table(sort_by="cuda_time_total", row_limit=45, max_name_column_width=60))
