@@ -206,6 +206,74 @@ std::tuple<torch::Tensor, std::vector<torch::Tensor>> hexplane_backward(const to
     return {dpts, grads};
 }
 
+
+// ---- deformation tail + activations (gs4d_deform_tail_forward / _backward)
+static const float *opt_f32(const c10::optional<torch::Tensor> &t, int64_t numel, const char *name) {
+    if (!t.has_value() || !t->defined()) return nullptr;
+    gpu_f32(*t, name);
+    need(t->is_contiguous() && t->numel() == numel, "deform_tail: optional tensors must be contiguous with the right size");
+    return t->data_ptr<float>();
+}
+
+std::vector<torch::Tensor> deform_tail_forward(const torch::Tensor &xyz, const torch::Tensor &s, const torch::Tensor &r,
+                                               const torch::Tensor &o, const torch::Tensor &f_dc,
+                                               const torch::Tensor &f_rest, const c10::optional<torch::Tensor> &dx,
+                                               const c10::optional<torch::Tensor> &ds,
+                                               const c10::optional<torch::Tensor> &dr,
+                                               const c10::optional<torch::Tensor> &d_o,
+                                               const c10::optional<torch::Tensor> &dshs) {
+    const int64_t P = xyz.size(0);
+    const int K = 1 + (int)f_rest.size(1);
+    for (auto *t : {&xyz, &s, &r, &o, &f_dc, &f_rest}) {
+        gpu_f32(*t, "deform_tail input");
+        need(t->is_contiguous() && t->size(0) == P, "deform_tail: inputs must be contiguous with P rows");
+    }
+    need(xyz.numel() == 3 * P && s.numel() == 3 * P && r.numel() == 4 * P && o.numel() == P && f_dc.numel() == 3 * P &&
+             f_rest.numel() == 3 * (K - 1) * P,
+         "deform_tail: xyz / scales (P, 3), rotations (P, 4), opacity (P, 1), f_dc (P, 1, 3), f_rest (P, K-1, 3)");
+    c10::hip::HIPGuard guard(xyz.device().index());
+    auto means = torch::empty_like(xyz), scales = torch::empty_like(s), rot = torch::empty_like(r),
+         opac = torch::empty_like(o), shs = torch::empty({P, K, 3}, xyz.options());
+    check(gs4d_deform_tail_forward((int)P, K, xyz.data_ptr<float>(), s.data_ptr<float>(), r.data_ptr<float>(),
+                                   o.data_ptr<float>(), f_dc.data_ptr<float>(), K > 1 ? f_rest.data_ptr<float>() : nullptr,
+                                   opt_f32(dx, 3 * P, "dx"), opt_f32(ds, 3 * P, "ds"), opt_f32(dr, 4 * P, "dr"),
+                                   opt_f32(d_o, P, "do"), opt_f32(dshs, 3 * K * P, "dshs"), means.data_ptr<float>(),
+                                   scales.data_ptr<float>(), rot.data_ptr<float>(), opac.data_ptr<float>(),
+                                   shs.data_ptr<float>(), (void *)stream_of(xyz)),
+          "deform_tail forward");
+    return {means, scales, rot, opac, shs};
+}
+
+std::vector<torch::Tensor> deform_tail_backward(const torch::Tensor &scales, const torch::Tensor &r,
+                                                const c10::optional<torch::Tensor> &dr, const torch::Tensor &opac,
+                                                const c10::optional<torch::Tensor> &g_means,
+                                                const c10::optional<torch::Tensor> &g_scales,
+                                                const c10::optional<torch::Tensor> &g_rot,
+                                                const c10::optional<torch::Tensor> &g_opac,
+                                                const c10::optional<torch::Tensor> &g_shs, int64_t K,
+                                                std::vector<bool> has_delta) {
+    need(has_delta.size() == 4, "deform_tail_backward: has_delta = (dx, ds, dr, do)");
+    const int64_t P = scales.size(0);
+    c10::hip::HIPGuard guard(scales.device().index());
+    auto o3 = scales.options();
+    auto d_xyz = torch::empty({P, 3}, o3), d_s = torch::empty({P, 3}, o3), d_r = torch::empty({P, 4}, o3),
+         d_o = torch::empty({P, 1}, o3), d_fdc = torch::empty({P, 1, 3}, o3), d_frest = torch::empty({P, K - 1, 3}, o3);
+    torch::Tensor gd[4];
+    const int64_t w[4] = {3, 3, 4, 1};
+    for (int i = 0; i < 4; i++) gd[i] = has_delta[i] ? torch::empty({P, w[i]}, o3) : torch::Tensor();
+    auto ptr = [](torch::Tensor &t) { return t.defined() ? t.data_ptr<float>() : nullptr; };
+    check(gs4d_deform_tail_backward((int)P, (int)K, scales.data_ptr<float>(), r.data_ptr<float>(),
+                                    opt_f32(dr, 4 * P, "dr"), opac.data_ptr<float>(), opt_f32(g_means, 3 * P, "g_means"),
+                                    opt_f32(g_scales, 3 * P, "g_scales"), opt_f32(g_rot, 4 * P, "g_rot"),
+                                    opt_f32(g_opac, P, "g_opac"), opt_f32(g_shs, 3 * K * P, "g_shs"),
+                                    d_xyz.data_ptr<float>(), d_s.data_ptr<float>(), d_r.data_ptr<float>(),
+                                    d_o.data_ptr<float>(), d_fdc.data_ptr<float>(),
+                                    K > 1 ? d_frest.data_ptr<float>() : nullptr, ptr(gd[0]), ptr(gd[1]), ptr(gd[2]),
+                                    ptr(gd[3]), (void *)stream_of(scales)),
+          "deform_tail backward");
+    return {d_xyz, d_s, d_r, d_o, d_fdc, d_frest, gd[0], gd[1], gd[2], gd[3]};
+}
+
 // ---- HexPlane regularisers ------------------------------------------------------------------------
 static gs4d_reg_batch reg_batch(const std::vector<torch::Tensor> &planes, const std::vector<double> &w_smooth,
                                 const std::vector<double> &w_l1, const std::vector<torch::Tensor> *grads) {
@@ -347,6 +415,8 @@ PYBIND11_MODULE(_C, m) {
     m.def("hexplane_reg_forward", &hexplane_reg_forward);
     m.def("hexplane_reg_backward", &hexplane_reg_backward);
     m.def("hexplane_reg_accumulate", &hexplane_reg_accumulate);
+    m.def("deform_tail_forward", &deform_tail_forward);
+    m.def("deform_tail_backward", &deform_tail_backward);
     m.def("hexplane_forward", &hexplane_forward, py::arg("pts"), py::arg("planes"), py::arg("order") = py::none());
     m.def("hexplane_backward", &hexplane_backward);
     m.def("l1_forward", &l1_forward);

@@ -129,6 +129,100 @@ __global__ __launch_bounds__(kTailThreads) void adam_kernel(gs4d_adam_batch batc
     }
 }
 
+
+// ---- deformation tail + activations (scene/deformation.py:140-146, gaussian_renderer/__init__.py:97-99)
+// Blocks [0, nb_g) take one Gaussian per thread (means, scales, rotation, opacity); blocks [nb_g, ..)
+// take the 3K SH values of the Gaussians as one flat, coalesced range.
+__global__ __launch_bounds__(kTailThreads) void deform_tail_fwd_kernel(
+    int P, int K, int nb_g, const float *__restrict__ xyz, const float *__restrict__ s, const float *__restrict__ r,
+    const float *__restrict__ o, const float *__restrict__ f_dc, const float *__restrict__ f_rest,
+    const float *__restrict__ dx, const float *__restrict__ ds, const float *__restrict__ dr,
+    const float *__restrict__ d_o, const float *__restrict__ dshs, float *__restrict__ means,
+    float *__restrict__ scales, float *__restrict__ rot, float *__restrict__ opac, float *__restrict__ shs) {
+    if ((int)blockIdx.x < nb_g) {
+        const int i = blockIdx.x * kTailThreads + threadIdx.x;
+        if (i >= P) return;
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            const size_t k = 3 * (size_t)i + c;
+            means[k] = dx ? xyz[k] + dx[k] : xyz[k];
+            scales[k] = expf(ds ? s[k] + ds[k] : s[k]);
+        }
+        float q[4];
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const size_t k = 4 * (size_t)i + c;
+            q[c] = dr ? r[k] + dr[k] : r[k];
+        }
+        // F.normalize: x / max(||x||_2, eps)
+        const float nrm = fmaxf(sqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]), 1e-12f);
+#pragma unroll
+        for (int c = 0; c < 4; c++) rot[4 * (size_t)i + c] = q[c] / nrm;
+        const float x = d_o ? o[i] + d_o[i] : o[i];
+        opac[i] = 1.f / (1.f + expf(-x));
+        return;
+    }
+    const int64_t e = (int64_t)(blockIdx.x - nb_g) * kTailThreads + threadIdx.x;
+    const int64_t n = (int64_t)P * 3 * K;
+    if (e >= n) return;
+    const int64_t g = e / (3 * K), k = e - g * 3 * K;
+    const float base = k < 3 ? f_dc[3 * g + k] : f_rest[g * 3 * (K - 1) + (k - 3)];
+    shs[e] = dshs ? base + dshs[e] : base;
+}
+
+__global__ __launch_bounds__(kTailThreads) void deform_tail_bwd_kernel(
+    int P, int K, int nb_g, const float *__restrict__ scales, const float *__restrict__ r,
+    const float *__restrict__ dr, const float *__restrict__ opac, const float *__restrict__ g_means,
+    const float *__restrict__ g_scales, const float *__restrict__ g_rot, const float *__restrict__ g_opac,
+    const float *__restrict__ g_shs, float *__restrict__ d_xyz, float *__restrict__ d_s, float *__restrict__ d_r,
+    float *__restrict__ d_o, float *__restrict__ d_fdc, float *__restrict__ d_frest, float *__restrict__ g_dx,
+    float *__restrict__ g_ds, float *__restrict__ g_dr, float *__restrict__ g_do) {
+    if ((int)blockIdx.x < nb_g) {
+        const int i = blockIdx.x * kTailThreads + threadIdx.x;
+        if (i >= P) return;
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            const size_t k = 3 * (size_t)i + c;
+            const float gm = g_means ? g_means[k] : 0.f;
+            const float gs = g_scales ? g_scales[k] * scales[k] : 0.f;  // d exp(x) = exp(x) dx
+            d_xyz[k] = gm;
+            d_s[k] = gs;
+            if (g_dx) g_dx[k] = gm;
+            if (g_ds) g_ds[k] = gs;
+        }
+        float q[4], g[4];
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const size_t k = 4 * (size_t)i + c;
+            q[c] = dr ? r[k] + dr[k] : r[k];
+            g[c] = g_rot ? g_rot[k] : 0.f;
+        }
+        // autograd of x / clamp_min(||x||, eps): g / n - x (x . g) / n^3 (the second term only when ||x|| > eps)
+        const float n0 = sqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+        const float nrm = fmaxf(n0, 1e-12f);
+        const float xg = q[0] * g[0] + q[1] * g[1] + q[2] * g[2] + q[3] * g[3];
+        const float gn = n0 > 1e-12f ? -xg / (nrm * nrm) : 0.f;
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const float v = g[c] / nrm + gn * (q[c] / n0);
+            d_r[4 * (size_t)i + c] = v;
+            if (g_dr) g_dr[4 * (size_t)i + c] = v;
+        }
+        const float y = opac[i];
+        const float go = g_opac ? g_opac[i] * (y * (1.f - y)) : 0.f;  // sigmoid backward
+        d_o[i] = go;
+        if (g_do) g_do[i] = go;
+        return;
+    }
+    const int64_t e = (int64_t)(blockIdx.x - nb_g) * kTailThreads + threadIdx.x;
+    const int64_t n = (int64_t)P * 3 * K;
+    if (e >= n) return;
+    const int64_t gi = e / (3 * K), k = e - gi * 3 * K;
+    const float v = g_shs ? g_shs[e] : 0.f;
+    if (k < 3) d_fdc[3 * gi + k] = v;
+    else d_frest[gi * 3 * (K - 1) + (k - 3)] = v;
+}
+
 // ---- HexPlane regularisers ------------------------------------------------------------------------
 constexpr int kRegPerThread = 8;
 constexpr int kRegBlock = kTailThreads * kRegPerThread;  // plane elements per workgroup
@@ -822,6 +916,37 @@ int gs4d_l1_loss_backward(int64_t n, const int8_t *sign, const float *dloss, flo
     if (n == 0) return 0;
     const int nblk = (int)std::min<int64_t>((n + kTailThreads - 1) / kTailThreads, 8192);
     hipLaunchKernelGGL(l1_backward_kernel, dim3(nblk), dim3(kTailThreads), 0, (hipStream_t)stream, n, sign, dloss, grad);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+int gs4d_deform_tail_forward(int P, int K, const float *xyz, const float *s, const float *r, const float *o,
+                             const float *f_dc, const float *f_rest, const float *dx, const float *ds, const float *dr,
+                             const float *d_o, const float *dshs, float *means, float *scales, float *rot,
+                             float *opac, float *shs, void *stream) {
+    if (P < 0 || K < 1 || (P > 0 && (!xyz || !s || !r || !o || !f_dc || (K > 1 && !f_rest) || !means || !scales ||
+                                     !rot || !opac || !shs)))
+        return 1;
+    if (P == 0) return 0;
+    const int nb_g = (P + kTailThreads - 1) / kTailThreads;
+    const int64_t nb_s = ((int64_t)P * 3 * K + kTailThreads - 1) / kTailThreads;
+    hipLaunchKernelGGL(deform_tail_fwd_kernel, dim3((unsigned)(nb_g + nb_s)), dim3(kTailThreads), 0, (hipStream_t)stream,
+                       P, K, nb_g, xyz, s, r, o, f_dc, f_rest, dx, ds, dr, d_o, dshs, means, scales, rot, opac, shs);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+int gs4d_deform_tail_backward(int P, int K, const float *scales, const float *r, const float *dr, const float *opac,
+                              const float *g_means, const float *g_scales, const float *g_rot, const float *g_opac,
+                              const float *g_shs, float *d_xyz, float *d_s, float *d_r, float *d_o, float *d_fdc,
+                              float *d_frest, float *g_dx, float *g_ds, float *g_dr, float *g_do, void *stream) {
+    if (P < 0 || K < 1 || (P > 0 && (!scales || !r || !opac || !d_xyz || !d_s || !d_r || !d_o || !d_fdc ||
+                                     (K > 1 && !d_frest))))
+        return 1;
+    if (P == 0) return 0;
+    const int nb_g = (P + kTailThreads - 1) / kTailThreads;
+    const int64_t nb_s = ((int64_t)P * 3 * K + kTailThreads - 1) / kTailThreads;
+    hipLaunchKernelGGL(deform_tail_bwd_kernel, dim3((unsigned)(nb_g + nb_s)), dim3(kTailThreads), 0, (hipStream_t)stream,
+                       P, K, nb_g, scales, r, dr, opac, g_means, g_scales, g_rot, g_opac, g_shs, d_xyz, d_s, d_r, d_o,
+                       d_fdc, d_frest, g_dx, g_ds, g_dr, g_do);
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 

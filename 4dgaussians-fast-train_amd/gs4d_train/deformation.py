@@ -242,6 +242,26 @@ class Deformation(nn.Module):
         self.opacity_deform, self.shs_deform = head(1), head(16 * 3)
         self.fused_heads = False  # True: the heads as one _DeformHeads block (GPU training)
 
+    def deltas(self, xyz, time):
+        """The active heads' outputs {name: (P, n)} of forward_dynamic (scene/deformation.py:97-139),
+        before the residual adds (which gs4d_train.kernels.deform_tail fuses with the activations)."""
+        a = self.args
+        if a.apply_rotation and not a.no_dr:
+            raise NotImplementedError("apply_rotation (documented as unused in arguments/__init__.py:104)")
+        xyz = xyz if xyz.shape[1] == 3 else xyz[:, :3]
+        time = time if time.shape[1] == 1 else time[:, :1]
+        hidden = self.feature_out(self.grid(xyz, time))
+        active = [name for name, flag in (("pos_deform", a.no_dx), ("scales_deform", a.no_ds),
+                                          ("rotations_deform", a.no_dr), ("opacity_deform", a.no_do),
+                                          ("shs_deform", a.no_dshs)) if not flag]
+        if self.fused_heads and hidden.is_cuda and torch.is_grad_enabled() and active:
+            heads = [getattr(self, name) for name in active]
+            w1 = torch.cat([hd[1].weight for hd in heads], 0)
+            b1 = torch.cat([hd[1].bias for hd in heads], 0)
+            second = [t for hd in heads for t in (hd[3].weight, hd[3].bias)]
+            return dict(zip(active, _DeformHeads.apply(hidden, w1, b1, *second)))
+        return {name: getattr(self, name)(hidden) for name in active}
+
     def forward(self, xyz, scales, rotations, opacity, shs, time):
         """forward_dynamic (scene/deformation.py:97-146); mask = 1 (no static_mlp / empty_voxel)."""
         a = self.args
@@ -301,6 +321,9 @@ class DeformNetwork(nn.Module):
 
     def forward(self, point, scales=None, rotations=None, opacity=None, shs=None, times_sel=None):
         return self.deformation_net(point, scales, rotations, opacity, shs, times_sel)
+
+    def deltas(self, point, times_sel):
+        return self.deformation_net.deltas(point, times_sel)
 
     def get_mlp_parameters(self):
         return self.deformation_net.get_mlp_parameters() + list(self.timenet.parameters())

@@ -10,7 +10,7 @@ import torch
 
 from . import _C
 
-__all__ = ["l1_loss", "densify_stats", "FusedAdam", "hexplane", "hexplane_regulation", "hexplane_regulation_value",
+__all__ = ["deform_tail", "l1_loss", "densify_stats", "FusedAdam", "hexplane", "hexplane_regulation", "hexplane_regulation_value",
            "hexplane_regulation_accumulate_grad"]
 
 
@@ -91,6 +91,48 @@ class FusedAdam(torch.optim.Optimizer):
             if ps:
                 _C.adam_step(ps, gs, ms, vs, ss, bs, beta1, beta2, eps)
         return loss
+
+
+class _DeformTail(torch.autograd.Function):
+    """The deformation's residual adds (scene/deformation.py:140-146, on features = cat(f_dc, f_rest),
+    scene/gaussian_model.py:116-118) and render()'s activations exp / normalize / sigmoid
+    (gaussian_renderer/__init__.py:97-99) in one HIP pass each way (gs4d_deform_tail_*).  A delta that
+    is None is a head switched off.  The gradient of each residual input is the gradient of its base."""
+
+    @staticmethod
+    def forward(ctx, xyz, s, r, o, f_dc, f_rest, dx, ds, dr, d_o, dshs):
+        c = lambda t: None if t is None else t.contiguous()
+        dshs_flat = None if dshs is None else dshs.reshape(dshs.shape[0], -1)
+        means, scales, rot, opac, shs = _C.deform_tail_forward(xyz.contiguous(), s.contiguous(), r.contiguous(),
+                                                               o.contiguous(), f_dc.contiguous(), f_rest.contiguous(),
+                                                               c(dx), c(ds), c(dr), c(d_o), c(dshs_flat))
+        ctx.save_for_backward(scales, r, dr, opac)
+        ctx.K = f_rest.shape[1] + 1
+        ctx.has = tuple(t is not None for t in (dx, ds, dr, d_o, dshs))
+        ctx.dshs_shape = None if dshs is None else dshs.shape
+        ctx.set_materialize_grads(False)
+        return means, scales, rot, opac, shs
+
+    @staticmethod
+    def backward(ctx, g_means, g_scales, g_rot, g_opac, g_shs):
+        scales, r, dr, opac = ctx.saved_tensors
+        c = lambda t: None if t is None else t.contiguous()
+        g_shs_flat = None if g_shs is None else g_shs.contiguous().reshape(g_shs.shape[0], -1)
+        has = ctx.has
+        d_xyz, d_s, d_r, d_o, d_fdc, d_frest, g_dx, g_ds, g_dr, g_do = _C.deform_tail_backward(
+            scales, r.contiguous(), c(dr), opac, c(g_means), c(g_scales), c(g_rot), c(g_opac), g_shs_flat, ctx.K,
+            list(has[:4]))
+        d_dshs = None
+        if has[4]:
+            d_dshs = (g_shs_flat if g_shs_flat is not None else torch.zeros(scales.shape[0], 3 * ctx.K,
+                                                                          device=scales.device)).reshape(ctx.dshs_shape)
+        return (d_xyz, d_s, d_r, d_o, d_fdc, d_frest, g_dx if has[0] else None, g_ds if has[1] else None,
+                g_dr if has[2] else None, g_do if has[3] else None, d_dshs)
+
+
+def deform_tail(xyz, scales, rotations, opacity, f_dc, f_rest, dx=None, ds=None, dr=None, d_o=None, dshs=None):
+    """(means3D, exp(scales + ds), normalize(rotations + dr), sigmoid(opacity + do), cat(f_dc, f_rest) + dshs)."""
+    return _DeformTail.apply(xyz, scales, rotations, opacity, f_dc, f_rest, dx, ds, dr, d_o, dshs)
 
 
 class _HexPlane(torch.autograd.Function):

@@ -31,16 +31,24 @@ def render(viewpoint_camera, pc, pipe_debug, bg_color, scaling_modifier=1.0, sta
     # torch.tensor(time).to(dev).repeat(P, 1) (:52): the same float32 column, filled on the device
     time = torch.full((xyz.shape[0], 1), float(torch.tensor(viewpoint_camera.time)), device=dev)
     rasterizer = dgr.GaussianRasterizer(raster_settings=settings)
-    opacity, shs, scales, rotations = pc._opacity, pc.get_features, pc._scaling, pc._rotation
-    if "coarse" in stage:
-        m3, sc, rot, op, sh = xyz, scales, rotations, opacity, shs
-    elif "fine" in stage:
-        m3, sc, rot, op, sh = pc._deformation(xyz, scales, rotations, opacity, shs, time)
-    else:
+    if "coarse" not in stage and "fine" not in stage:
         raise NotImplementedError(stage)
-    sc = pc.scaling_activation(sc)
-    rot = pc.rotation_activation(rot)
-    op = pc.opacity_activation(op)
+    if getattr(pc, "fused", False) and getattr(pc, "fused_tail", True) and xyz.is_cuda:
+        # the heads' residual adds, cat(f_dc, f_rest) and the activations as one HIP pass each way
+        from .kernels import deform_tail
+        d = pc._deformation.deltas(xyz, time) if "fine" in stage else {}
+        m3, sc, rot, op, sh = deform_tail(xyz, pc._scaling, pc._rotation, pc._opacity, pc._features_dc,
+                                          pc._features_rest, d.get("pos_deform"), d.get("scales_deform"),
+                                          d.get("rotations_deform"), d.get("opacity_deform"), d.get("shs_deform"))
+    else:
+        opacity, shs, scales, rotations = pc._opacity, pc.get_features, pc._scaling, pc._rotation
+        if "coarse" in stage:
+            m3, sc, rot, op, sh = xyz, scales, rotations, opacity, shs
+        else:
+            m3, sc, rot, op, sh = pc._deformation(xyz, scales, rotations, opacity, shs, time)
+        sc = pc.scaling_activation(sc)
+        rot = pc.rotation_activation(rot)
+        op = pc.opacity_activation(op)
     image, radii, depth = rasterizer(means3D=m3, means2D=screenspace_points, shs=sh, colors_precomp=None,
                                      opacities=op, scales=sc, rotations=rot, cov3D_precomp=None)
     return {"render": image, "viewspace_points": screenspace_points, "visibility_filter": radii > 0,

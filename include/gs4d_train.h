@@ -23,6 +23,26 @@ int gs4d_l1_loss_forward(int64_t n, const float *x, const float *y, int8_t *sign
                          void *stream);
 int gs4d_l1_loss_backward(int64_t n, const int8_t *sign, const float *dloss, float *grad, void *stream);
 
+/* ---- the deformation's tail and the activations before the rasterizer, in one pass each way:
+ * scene/deformation.py:140-146 (residual adds of the heads' outputs, features = cat(f_dc, f_rest),
+ * scene/gaussian_model.py:116-118) and gaussian_renderer/__init__.py:97-99 (exp, normalize, sigmoid):
+ *   means = xyz + dx, scales = exp(s + ds), rot = (r + dr) / max(|r + dr|, 1e-12), opac = sigmoid(o + do),
+ *   shs[:, 0] = f_dc + dshs[:, 0:3], shs[:, 1:] = f_rest + dshs[:, 3:] (K = 1 + K_rest coefficients).
+ * Any delta may be NULL (that head is off: zero).  xyz, s (P, 3), r (P, 4), o (P, 1), f_dc (P, 1, 3),
+ * f_rest (P, K-1, 3), dshs (P, 3K).  backward: given the gradients of the five outputs (each may be
+ * NULL: zero), writes d xyz, d s, d r, d o, d f_dc and d f_rest (the slices of d shs, whose flat
+ * (P, 3K) form is also the gradient of dshs), and the same values again into the deltas' gradients
+ * g_dx, g_ds, g_dr, g_do where those are not NULL (separate buffers: autograd hands them to other
+ * functions while the bases' gradients may become leaf .grad tensors). */
+int gs4d_deform_tail_forward(int P, int K, const float *xyz, const float *s, const float *r, const float *o,
+                             const float *f_dc, const float *f_rest, const float *dx, const float *ds, const float *dr,
+                             const float *d_o, const float *dshs, float *means, float *scales, float *rot,
+                             float *opac, float *shs, void *stream);
+int gs4d_deform_tail_backward(int P, int K, const float *scales, const float *r, const float *dr, const float *opac,
+                              const float *g_means, const float *g_scales, const float *g_rot, const float *g_opac,
+                              const float *g_shs, float *d_xyz, float *d_s, float *d_r, float *d_o, float *d_fdc,
+                              float *d_frest, float *g_dx, float *g_ds, float *g_dr, float *g_do, void *stream);
+
 /* ---- densification statistics: train.py:346-349 and scene/gaussian_model.py:521-523.
  * For every i with visible[i]: max_radii[i] = max(max_radii[i], radii[i]) (skipped when radii is
  * NULL), grad_accum[i] += |viewspace_grad[i, 0:2]|, denom[i] += 1.  viewspace_grad is (P, 3). */

@@ -268,3 +268,41 @@ def test_train_step_fused_matches_torch_tail():
     torch.testing.assert_close(gb.xyz_gradient_accum, ga.xyz_gradient_accum, rtol=1e-4, atol=1e-4 * acc_scale)
     torch.testing.assert_close(gb.denom, ga.denom, rtol=0, atol=0)
     torch.testing.assert_close(gb.max_radii2D, ga.max_radii2D, rtol=0, atol=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("heads", ["all", "some", "none"])
+def test_deform_tail_matches_torch(heads):
+    """kernels.deform_tail (residual adds + cat(f_dc, f_rest) + exp / normalize / sigmoid in one HIP pass
+    each way) against the reference's torch graph (scene/deformation.py:140-146, gaussian_model.py:116-118,
+    gaussian_renderer/__init__.py:97-99): outputs to 1e-6 relative, every gradient to 1e-5 of its max."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs an MI355X")
+    from gs4d_train.kernels import deform_tail
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device="cpu").manual_seed(3)
+    P = 5003
+    mk = lambda *s: torch.randn(*s, generator=g).to(dev).requires_grad_(True)
+    base = [mk(P, 3), mk(P, 3), mk(P, 4), mk(P, 1), mk(P, 1, 3), mk(P, 15, 3)]
+    deltas = [mk(P, 3), mk(P, 3), mk(P, 4), mk(P, 1), mk(P, 48)]
+    if heads == "some":
+        deltas[1] = deltas[3] = None
+    elif heads == "none":
+        deltas = [None] * 5
+    ups = [torch.randn(P, 3, generator=g).to(dev), torch.randn(P, 3, generator=g).to(dev),
+           torch.randn(P, 4, generator=g).to(dev), torch.randn(P, 1, generator=g).to(dev),
+           torch.randn(P, 16, 3, generator=g).to(dev)]
+    leaves = base + [d for d in deltas if d is not None]
+    out = deform_tail(*base, *deltas)
+    ga = torch.autograd.grad(sum((o * u).sum() for o, u in zip(out, ups)), leaves)
+    xyz, s, r, o, fdc, frest = base
+    add = lambda a, b: a if b is None else a + b
+    sh = torch.cat((fdc, frest), dim=1)
+    ref = (add(xyz, deltas[0]), torch.exp(add(s, deltas[1])), torch.nn.functional.normalize(add(r, deltas[2])),
+           torch.sigmoid(add(o, deltas[3])), sh if deltas[4] is None else sh + deltas[4].reshape(P, 16, 3))
+    gb = torch.autograd.grad(sum((x * u).sum() for x, u in zip(ref, ups)), leaves)
+    for a, b in zip(out, ref):
+        torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-6)
+    for a, b in zip(ga, gb):
+        assert a.shape == b.shape
+        assert float((a - b).abs().max()) <= 1e-5 * max(float(b.abs().max()), 1e-20)
