@@ -504,8 +504,9 @@ __device__ __forceinline__ void half_step(f2 &T, f2 &A, const f2 dp0, const f2 d
     W2 = fma2(w, dp2, W2);
 }
 
-// 3 waves per SIMD (166 VGPRs): the pair walk's four falloff chains need the registers; at 4 waves it spills.
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void render_backward_kernel(Args a, const uint2 *__restrict__ ranges, const uint32_t *__restrict__ order,
+// 4 waves per SIMD (<= 128 VGPRs, no spills): the reach-combo blocks hold at most the four falloff chains
+// of one pair.
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void render_backward_kernel(Args a, const uint2 *__restrict__ ranges, const uint32_t *__restrict__ order,
                             const uint32_t *__restrict__ gid_by_e,
                             const uint32_t *__restrict__ upos, const float2 *__restrict__ xy,
                             const float4 *__restrict__ conic_opacity, const float4 *__restrict__ rgbd,
@@ -676,8 +677,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void
             for (int j = 0; j < n; j += 2) {
                 if (((nonpd | hiop) >> j) & 3) {
                     walk_pair(j, all, std::true_type{}, I3{}, I3{});
-                } else if (!decltype(all)::value) {
-                    walk_pair(j, all, std::false_type{}, I3{}, I3{});
                 } else {
                     const uint32_t combo = (uint32_t)((reach[0] >> j) & 3u) | (uint32_t)(((reach[1] >> j) & 3u) << 2);
                     auto go = [&](auto c) {
