@@ -18,7 +18,7 @@ KEYS = {"render_backward_kernel": "render_backward", "render_forward_kernel": "r
         "onesweep_kernel": "onesweep", "emit_instances_kernel": "emit_instances", "preprocess_kernel": "preprocess",
         "contrib_segments_kernel": "contrib_segments", "gaussian_backward_kernel": "gaussian_backward",
         "visible_scan_kernel": "visible_scan", "tile_ranges_kernel": "tile_ranges",
-        "tile_sort_kernel": "tile_sort",
+        "tile_sort_kernel": "tile_sort", "tile_order_kernel": "tile_order",
         "contrib_finish_kernel": "contrib_finish"}
 
 
