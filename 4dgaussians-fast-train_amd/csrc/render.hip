@@ -269,31 +269,31 @@ __global__ __launch_bounds__(64) void render_forward_kernel(Args a, const uint2 
         }
         ids_left = 4;
     };
-    float2 rp;
-    float4 rco, rcd;
-    uint32_t rge = 0;
+    // the next batch's attributes are gathered into LDS by LDS-DMA loads (as the backward does), only
+    // its lanes' reach bits stay in a register
+    __shared__ RawLDS s_raw;
+    uint32_t rnxt = 0;
     auto fetch = [&](uint32_t first) {
         if (ids_left == 0) refill(first);
-        rge = ug[0];
+        const uint32_t rge = ug[0];
         ev[0] = ev[1]; ev[1] = ev[2]; ev[2] = ev[3];
         ug[0] = ug[1]; ug[1] = ug[2]; ug[2] = ug[3];
         ids_left--;
-        if (first + lane < range.y) {
-            const uint32_t gid = rge & kGidMask;
-            rp = xy[gid];
-            rco = conic_opacity[gid];
-            rcd = rgbd[gid];
-        }
+        rnxt = rge >> kReachShift;
+        issue_raw_lds(s_raw, first + lane < range.y, rge & kGidMask, xy, conic_opacity, rgbd, nullptr);
     };
     if (range.x < range.y) fetch(range.x);
     for (uint32_t base = range.x; base < range.y; base += 64) {
         if ((alive[0] | alive[1] | alive[2] | alive[3]) == 0) break;  // forward.cu:312-314
         SplatRegs nxt;
+        const RawSplat raw = read_raw_lds(s_raw, lane, false);
         if (base + lane < range.y) {  // blend constants (as to_regs)
+            const float2 rp = raw.p;
+            const float4 rco = raw.co;
             nxt.geo = make_float4(rp.x, rp.y - yc, (-0.5f * rco.x) * kLog2e, (-rco.y) * kLog2e);
             nxt.opc = make_float4((-0.5f * rco.z) * kLog2e, rco.w, 0.f, 0.f);
-            nxt.col = rcd;
-            nxt.reach = rge >> kReachShift;
+            nxt.col = make_float4(raw.c.x, raw.c.y, raw.c.z, s_raw.cd[4 * lane + 3]);  // rgb, view depth
+            nxt.reach = rnxt;
         } else {
             nxt.geo = nxt.opc = nxt.col = make_float4(0.f, 0.f, 0.f, 0.f);
             nxt.reach = 0;
@@ -345,6 +345,7 @@ __global__ __launch_bounds__(64) void render_forward_kernel(Args a, const uint2 
             }
         }
     }
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // an early exit may leave the next batch's LDS-DMA loads in flight
     const size_t HW = (size_t)a.W * a.H;
     const V3 bg = load_v3(a.bg);
 #pragma unroll
