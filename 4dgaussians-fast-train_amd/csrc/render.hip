@@ -384,18 +384,6 @@ hipError_t launch_render_forward(const Args &a, GeomState g, BinningState b, Ima
 }
 
 // ---------------------------------------------------------------------------------------------
-// 16-lane DPP row sum: every lane of each row ends with its row's total.
-template <int CTRL>
-__device__ __forceinline__ float dpp_add(float v) {
-    return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
-}
-__device__ __forceinline__ float row_sum(float v) {
-    v = dpp_add<0xB1>(v);   // quad_perm [1,0,3,2]
-    v = dpp_add<0x4E>(v);   // quad_perm [2,3,0,1]
-    v = dpp_add<0x141>(v);  // row_half_mirror
-    v = dpp_add<0x140>(v);  // row_mirror
-    return v;
-}
 // lanes 0-31 of the result hold a's half-wave sums, lanes 32-63 b's (v_permlane32_swap)
 __device__ __forceinline__ float swap32_add(float a, float b) {
     auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
@@ -417,40 +405,55 @@ struct SplatPart {
 // Wave64 totals of two splats' partial sums, left in LDS as their 9 record values:
 //   0 sum u, 1 sum dx u, 2 sum u yl, 3 sum dx^2 u, 4 sum dx u yl, 5 sum u yl^2, 6-8 colour sums
 // (dx = mean.x - pixel x, per lane column).  v_permlane32_swap then v_permlane16_swap sum each value
-// over the 4 lanes of a column (reduce-scatter: row r of r1 ends with (a.u0, a.u1, b.u0, b.u1)[r], of r2
-// (a.u2, a.w0, b.u2, b.w0)[r], of r3 (a.w1, a.w2, b.w1, b.w2)[r]); the dx-weighted moments are formed
-// on those column sums, and a 16-lane DPP tree sums the columns.  The first lane of each row stores.
+// over the 4 lanes of a column (reduce-scatter: row r of x1 ends with (a.u0, a.u1, b.u0, b.u1)[r], of x2
+// (a.u2, a.w0, b.u2, b.w0)[r], of x3 (a.w1, a.w2, b.w1, b.w2)[r]); the dx-weighted moments x4, x5 are
+// formed on those column sums.  The 16 columns of each row are then reduce-scattered too, with DPP:
+// pairs of registers halve at each of the four stages (column c with c ^ 8, the half-row mirror, c ^ 2,
+// c ^ 1), so every lane ends with one finished total (15 DPP-stage instructions for the 5 registers
+// instead of 20 for 5 butterflies) and writes it with ONE ds_write at a lane-constant offset `roff`
+// (red_offset(); -1: nothing to write).
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+// record float offset (from record j's start; record j + 1 follows at +12) of this lane's total
+__device__ __forceinline__ int red_offset(int lane) {
+    const int r = lane >> 4, c = lane & 15, splat = (r >> 1) * 12, odd = r & 1;
+    switch (c) {
+    case 0: return splat + (odd ? 2 : 0);   // x1: S u, S u yl
+    case 4: return splat + (odd ? 8 : 7);   // x3: W1, W2
+    case 8: return splat + (odd ? 6 : 5);   // x2: S u yl^2, W0
+    case 12: return splat + (odd ? 4 : 1);  // x4: S dx u yl, S dx u
+    case 2: return odd ? -1 : splat + 3;    // x5: S dx^2 u (odd rows hold nothing)
+    default: return -1;
+    }
+}
 __device__ __forceinline__ void wave_sum_pair_to_lds(const SplatPart &a, const SplatPart &b, float dxa, float dxb,
-                                                     float *dst0, float *dst1, int lane) {
+                                                     float *rec_pair, int lane, int roff) {
     const float h0 = swap32_add(a.u0, b.u0);  // lanes 0-31: a, 32-63: b
     const float h1 = swap32_add(a.u1, b.u1);
     const float h2 = swap32_add(a.u2, b.u2);
     const float h3 = swap32_add(a.w0, b.w0);
     const float h4 = swap32_add(a.w1, b.w1);
     const float h5 = swap32_add(a.w2, b.w2);
-    const float r1 = swap16_add(h0, h1);
-    const float r2 = swap16_add(h2, h3);
-    const float r3 = swap16_add(h4, h5);
+    const float x1 = swap16_add(h0, h1);
+    const float x2 = swap16_add(h2, h3);
+    const float x3 = swap16_add(h4, h5);
     const float dxs = lane < 32 ? dxa : dxb;  // rows 0-1 hold splat a, rows 2-3 splat b
-    const float r4 = r1 * dxs;                 // (dx a.u0, dx a.u1, dx b.u0, dx b.u1)
-    const float r5 = r4 * dxs;                 // (dx^2 a.u0, -, dx^2 b.u0, -)
-    const float s1 = row_sum(r1), s2 = row_sum(r2), s3 = row_sum(r3), s4 = row_sum(r4), s5 = row_sum(r5);
-    if ((lane & 15) == 0) {
-        const int r = lane >> 4;
-        float *d = r < 2 ? dst0 : dst1;
-        if (r & 1) {
-            d[2] = s1;
-            d[4] = s4;
-            d[6] = s2;
-            d[8] = s3;
-        } else {
-            d[0] = s1;
-            d[1] = s4;
-            d[3] = s5;
-            d[5] = s2;
-            d[7] = s3;
-        }
-    }
+    const float x4 = x1 * dxs;                 // (dx a.u0, dx a.u1, dx b.u0, dx b.u1)
+    const float x5 = x4 * dxs;                 // (dx^2 a.u0, -, dx^2 b.u0, -)
+    const bool c8 = (lane & 8) == 0, c4 = (lane & 4) == 0, c2 = (lane & 2) == 0;
+    // stage A (c, c ^ 8): x1 | x2 -> z12, x3 | x4 -> z34, x5 -> z5
+    const float z12 = (c8 ? x1 : x2) + dpp<0x128>(c8 ? x2 : x1);  // row_ror:8
+    const float z34 = (c8 ? x3 : x4) + dpp<0x128>(c8 ? x4 : x3);
+    const float z5 = x5 + dpp<0x128>(x5);
+    // stage B (half-row mirror): z12 | z34 -> w
+    const float w = (c4 ? z12 : z34) + dpp<0x141>(c4 ? z34 : z12);
+    const float w5 = z5 + dpp<0x141>(z5);
+    // stage C (c ^ 2): w | w5 -> v; stage D (c ^ 1)
+    const float v = (c2 ? w : w5) + dpp<0x4E>(c2 ? w5 : w);  // quad_perm [2, 3, 0, 1]
+    const float u = v + dpp<0xB1>(v);                         // quad_perm [1, 0, 3, 2]
+    if (roff >= 0) rec_pair[roff] = u;
 }
 
 // Per-pixel state of the reverse walk (pairs): T (recovered backwards), A = accum_rec . dL/dpix and
@@ -539,6 +542,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     const f2 yl[2] = {f2{ylane, ylane + 4.f}, f2{ylane + 8.f, ylane + 12.f}};
     const f2 yl2[2] = {yl[0] * yl[0], yl[1] * yl[1]};
     const float yc = (float)(ty * kBlockY) + 7.5f;
+    const int roff = red_offset(lane);
 
     BwdPixels st;
     uint32_t lastc[4];
@@ -676,8 +680,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
             for (int i = 0; i < 2; i++)
                 part[i] = SplatPart{U[i][0].x + U[i][0].y, U[i][1].x + U[i][1].y, U[i][2].x + U[i][2].y,
                                     U[i][3].x + U[i][3].y, U[i][4].x + U[i][4].y, U[i][5].x + U[i][5].y};
-            wave_sum_pair_to_lds(part[0], part[1], dxs[0], dxs[1], reinterpret_cast<float *>(s_rec[j]),
-                                 reinterpret_cast<float *>(s_rec[j + 1]), lane);
+            wave_sum_pair_to_lds(part[0], part[1], dxs[0], dxs[1], reinterpret_cast<float *>(s_rec[j]), lane, roff);
         };
         using I3 = std::integral_constant<int, 3>;
         auto walk_batch = [&](auto all) {
