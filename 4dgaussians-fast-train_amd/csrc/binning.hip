@@ -460,15 +460,20 @@ __global__ __launch_bounds__(1024) void tile_order_kernel(const uint2 *__restric
 }
 
 // Tiles with more than kWaveSortMax instances (shorter runs are sorted in registers by the render
-// forward): one workgroup each.  Up to kSortCap: register + LDS bitonic (block_sort); longer: runs of
-// kSortCap in LDS merged by the network's global steps.  One launch for both (an empty launch costs
-// ~4 us of the timeline).
-__global__ __launch_bounds__(256) void tile_sort_kernel(const uint2 *__restrict__ ranges,
+// forward): one workgroup each (workgroup t + 1 for tile t).  Up to kSortCap: register + LDS bitonic
+// (block_sort); longer: runs of kSortCap in LDS merged by the network's global steps.  Workgroup 0
+// orders the tiles (order_tiles), so one launch does both (a launch costs ~4 us of the timeline).
+__global__ __launch_bounds__(256) void tile_sort_kernel(const uint2 *__restrict__ ranges, int T,
+                                                        uint32_t *__restrict__ order,
                                                         const uint32_t *__restrict__ gid_by_e,
                                                         const float *__restrict__ depths, uint32_t *__restrict__ upos,
                                                         uint32_t *__restrict__ tkey_hi, uint32_t *__restrict__ tkey_lo) {
     __shared__ TileSortLds s;
-    const uint2 r = ranges[blockIdx.x];
+    if (blockIdx.x == 0) {
+        order_tiles(ranges, T, order, reinterpret_cast<uint32_t *>(s.key));
+        return;
+    }
+    const uint2 r = ranges[blockIdx.x - 1];
     const int n = (int)(r.y - r.x);
     if (n <= kWaveSortMax) return;  // the render forward sorts these
     uint32_t *seg = upos + r.x;
@@ -554,9 +559,8 @@ hipError_t launch_binning(const Args &a, GeomState g, const int *radii, BinningS
     onesweep_sort<kSortThreads, kItemsL>(keys, vals, L, n_dev, b.key_bits, b.scratch + kZeroHist,
                                          b.scratch + bin_look_off(L), b.scratch + bin_chain_off() + 1, s);
     hipLaunchKernelGGL(tile_ranges_kernel, dim3((L + 255) / 256), dim3(256), 0, s, b.sorted_keys, n_dev, img.ranges);
-    hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, s, img.ranges, T, img.order);
-    hipLaunchKernelGGL(tile_sort_kernel, dim3(T), dim3(256), 0, s, img.ranges, b.gid_by_e, g.depths, b.upos,
-                       b.tmp_hi, b.tmp_lo);
+    hipLaunchKernelGGL(tile_sort_kernel, dim3(T + 1), dim3(256), 0, s, img.ranges, T, img.order, b.gid_by_e, g.depths,
+                       b.upos, b.tmp_hi, b.tmp_lo);
     return hipGetLastError();
 }
 

@@ -312,7 +312,7 @@ int gs4d_backward_ex(int P, int D, int M, int R, const float *background, int wi
     // segmented-reduction partials
     const size_t rec_bytes = align_up((size_t)R * kContribStride * sizeof(float), 256);
     const size_t dconic_bytes = align_up(16 * (size_t)P, 256);
-    char *scratch = scratch_alloc(scratch_ctx, rec_bytes + dconic_bytes + contrib_scratch_bytes(R) + 256);
+    char *scratch = scratch_alloc(scratch_ctx, rec_bytes + dconic_bytes + contrib_scratch_bytes(R, P) + 256);
     if (!scratch) return fail(GS4D_ERR_ALLOC, "backward: scratch allocation failed");
     float *contrib = (float *)align_up((size_t)scratch, 256);
     char *reduce_scratch = (char *)contrib + rec_bytes + dconic_bytes;
@@ -327,12 +327,13 @@ int gs4d_backward_ex(int P, int D, int M, int R, const float *background, int wi
     }
     GS4D_STAGE("contrib_reduce", launch_contrib_reduce(a, g, b, R, contrib, reduce_scratch, dL_dmean2D, dconic,
                                                        dL_dopacity, dL_dcolor, stream));
-    if (dL_dconic && (float *)dconic != dL_dconic)
-        GS4D_HIP(hipMemcpyAsync(dL_dconic, dconic, 16 * (size_t)P, hipMemcpyDeviceToDevice, stream));
     const float *cov3D_ptr = cov3D_precomp ? cov3D_precomp : g.cov3D;  // rasterizer_impl.cu:414
     GS4D_STAGE("gaussian_backward",
-               launch_gaussian_backward(a, g, radii_ptr, means3D, shs, scales, rotations, cov3D_ptr, dL_dmean2D,
-                                        dconic, dL_dcolor, dL_dmean3D, dL_dcov3D, dL_dsh, dL_dscale, dL_drot, stream));
+               launch_gaussian_backward(a, g, R, reduce_scratch, radii_ptr, means3D, shs, scales, rotations, cov3D_ptr,
+                                        dL_dmean2D, dconic, dL_dopacity, dL_dcolor, dL_dmean3D, dL_dcov3D, dL_dsh,
+                                        dL_dscale, dL_drot, stream));
+    if (dL_dconic && (float *)dconic != dL_dconic)
+        GS4D_HIP(hipMemcpyAsync(dL_dconic, dconic, 16 * (size_t)P, hipMemcpyDeviceToDevice, stream));
     end_marks();
     return GS4D_OK;
 }

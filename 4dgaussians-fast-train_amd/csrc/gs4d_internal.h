@@ -190,15 +190,17 @@ hipError_t launch_render_forward(const Args &a, GeomState g, BinningState b, Ima
                                  float *out_depth, hipStream_t s);  // also sorts runs <= kWaveSortMax
 hipError_t launch_render_backward(const Args &a, GeomState g, const uint32_t *gid_by_e, const uint32_t *upos, ImageState img,
                                   const float *colors, const float *dL_dpix, float *contrib, hipStream_t s);
-size_t contrib_scratch_bytes(int R);
+size_t contrib_scratch_bytes(int R, int P);
 hipError_t launch_contrib_reduce(const Args &a, GeomState g, BinningState b, int R, const float *contrib,
                                  char *scratch, float *dL_dmean2D, float4 *dL_dconic, float *dL_dopacity,
                                  float *dL_dcolor, hipStream_t s);
-hipError_t launch_gaussian_backward(const Args &a, GeomState g, const int *radii, const float *means3D,
-                                    const float *shs, const float *scales, const float *rotations, const float *cov3D,
-                                    const float *dL_dmean2D, const float4 *dL_dconic, const float *dL_dcolor,
-                                    float *dL_dmean3D, float *dL_dcov3D, float *dL_dsh, float *dL_dscale,
-                                    float *dL_drot, hipStream_t s);
+// also finishes the contrib_reduce sums of Gaussians spanning waves (same scratch) and zero-fills the
+// render-level gradients of Gaussians without instances
+hipError_t launch_gaussian_backward(const Args &a, GeomState g, int R, char *scratch, const int *radii,
+                                    const float *means3D, const float *shs, const float *scales, const float *rotations,
+                                    const float *cov3D, float *dL_dmean2D, float4 *dL_dconic, float *dL_dopacity,
+                                    float *dL_dcolor, float *dL_dmean3D, float *dL_dcov3D, float *dL_dsh,
+                                    float *dL_dscale, float *dL_drot, hipStream_t s);
 
 size_t knn_scratch_bytes(int P);
 hipError_t launch_knn(int P, const float *pts, float *mean_dists, char *scratch, hipStream_t s);

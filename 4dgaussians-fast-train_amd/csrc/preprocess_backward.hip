@@ -8,8 +8,9 @@
 //    at its emission slots -- consecutive, in tile-rect order -- with a fixed-order segmented
 //    reduction, which replaces the reference's float atomics (backward.cu:523,545-554): bitwise
 //    deterministic, and balanced (one lane per record, whatever the splat sizes).
-// 2. gaussian_backward: K8 + K9 per Gaussian.  Every output element is written (zeros for culled
-//    Gaussians and for SH coefficients >= (D+1)^2), so no zero-fill pass is needed.
+// 2. gaussian_backward: the sums of the Gaussians whose records span waves, then K8 + K9 per
+//    Gaussian.  Every output element is written (zeros for culled Gaussians and for SH coefficients
+//    >= (D+1)^2), so no zero-fill pass is needed.
 #include <algorithm>
 
 #include "gs4d_internal.h"
@@ -65,13 +66,13 @@ __device__ __forceinline__ void add9(float *acc, const float4 *p) {
 // Pass 1: one lane per emission slot, one wave per 64 slots.  A Gaussian's records occupy consecutive
 // slots, so a segmented inclusive scan (fixed shuffle tree) sums each Gaussian's piece of the wave.
 // Pieces that are a whole Gaussian are written out; a piece continuing from the previous wave goes
-// to part[w][0], a piece that starts a Gaussian and continues into the next wave to part[w][1].
-// flags[w]: bit 0 = the wave's first piece ends its Gaussian, bit 1 = part[w][1] starts a chain.
+// to part[w][0], a piece that starts a Gaussian and continues into the next wave to part[w][1];
+// e_first[g] = the Gaussian's first slot.
 __global__ __launch_bounds__(256) void contrib_segments_kernel(const uint32_t *__restrict__ n_dev,
                                                                const uint32_t *__restrict__ gid_by_e,
                                                                const float4 *__restrict__ rec, GradOut o,
                                                                float4 *__restrict__ part,
-                                                               uint32_t *__restrict__ flags) {
+                                                               uint32_t *__restrict__ e_first) {
     const int n = (int)__builtin_amdgcn_readfirstlane(*n_dev);
     const int lane = threadIdx.x & 63;
     const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -96,6 +97,7 @@ __global__ __launch_bounds__(256) void contrib_segments_kernel(const uint32_t *_
     if (lane == 63) kn = e + 1 < n ? gid_by_e[e + 1] & kGidMask : 0xFFFFFFFFu;
     const bool head = valid && key != kp;  // first slot of its Gaussian
     const bool tail = valid && key != kn;  // last slot of its Gaussian
+    if (head) e_first[key] = (uint32_t)e;  // locates the pieces of a Gaussian spanning waves
     bool f = head || lane == 0;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
@@ -109,54 +111,43 @@ __global__ __launch_bounds__(256) void contrib_segments_kernel(const uint32_t *_
         }
         f = f || (lane >= off && fu);
     }
-    const uint64_t vmask = __ballot(valid), tailm = __ballot(tail), headm = __ballot(head);
     const uint64_t endm = __ballot(valid && (tail || lane == 63));
     const int fe = __ffsll((unsigned long long)endm) - 1;  // end lane of the first piece
-    const int le = 63 - __clzll(vmask);                    // end lane of the last piece
-    const bool head0 = headm & 1ull;
-    const bool pend = valid && (tail || lane == 63);
-    if (pend) {
+    const bool head0 = __ballot(head) & 1ull;
+    if (valid && (tail || lane == 63)) {
         const bool starts = lane != fe || head0;  // the piece starts at its Gaussian's first slot
         if (starts && tail) write_grads(o, key, acc);
         else if (!starts) store9(part + ((size_t)w * 2) * 3, acc);
         else store9(part + ((size_t)w * 2 + 1) * 3, acc);
     }
-    if (lane == 0) {
-        const bool last_starts = le != fe || head0;
-        const bool last_open = !((tailm >> le) & 1ull);
-        flags[w] = (uint32_t)((tailm >> fe) & 1ull) | ((last_starts && last_open) ? 2u : 0u);
-    }
 }
 
-// Pass 2: Gaussians spanning several waves (summed in wave order from their chain start), and zeros
-// for Gaussians without instances.
-__global__ __launch_bounds__(256) void contrib_finish_kernel(int P, const uint32_t *__restrict__ n_dev,
-                                                             const uint32_t *__restrict__ n_inst,
-                                                             const uint32_t *__restrict__ gid_by_e,
-                                                             const float4 *__restrict__ part,
-                                                             const uint32_t *__restrict__ flags, GradOut o) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    const int nw = n_dev ? ((int)*n_dev + 63) / 64 : 0;
-    if (i < nw && (flags[i] & 2u)) {
-        float acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-        add9(acc, part + ((size_t)i * 2 + 1) * 3);
-        for (int w = i + 1; w < nw; w++) {
-            add9(acc, part + ((size_t)w * 2) * 3);
-            if (flags[w] & 1u) break;
-        }
-        write_grads(o, gid_by_e[(size_t)i * 64 + 63] & kGidMask, acc);
-    }
-    if (i < P && n_inst[i] == 0) write_zero_grads(o, (uint32_t)i);
-}
-
+// Pass 2 (at the start of gaussian_backward, one thread per Gaussian): a Gaussian whose slots span
+// several waves sums its pieces in wave order -- part[w0][1] (its head piece) then part[w][0] of each
+// following wave up to the one holding its last slot -- and a Gaussian without instances gets zeros.
 __global__ __launch_bounds__(256) void gaussian_backward_kernel(
     Args a, GeomState g, const int *__restrict__ radii, const float *__restrict__ means3D,
     const float *__restrict__ shs, const float *__restrict__ scales, const float *__restrict__ rotations,
-    const float *__restrict__ cov3Ds, const float *__restrict__ dL_dmean2D, const float4 *__restrict__ dL_dconic,
-    const float *__restrict__ dL_dcolor, float *__restrict__ dL_dmean3D, float *__restrict__ dL_dcov3D,
-    float *__restrict__ dL_dsh, float *__restrict__ dL_dscale, float *__restrict__ dL_drot) {
+    const float *__restrict__ cov3Ds, const float *dL_dmean2D, const float4 *dL_dconic,
+    const float *dL_dcolor, float *__restrict__ dL_dmean3D, float *__restrict__ dL_dcov3D,
+    float *__restrict__ dL_dsh, float *__restrict__ dL_dscale, float *__restrict__ dL_drot,
+    const uint32_t *__restrict__ e_first, const float4 *__restrict__ part, GradOut o) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= a.P) return;
+    {
+        const uint32_t ni = g.n_inst[idx];
+        if (ni == 0) {
+            write_zero_grads(o, (uint32_t)idx);
+        } else {
+            const uint32_t e0 = e_first[idx], w0 = e0 >> 6, w1 = (e0 + ni - 1) >> 6;
+            if (w0 != w1) {
+                float acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+                add9(acc, part + ((size_t)w0 * 2 + 1) * 3);
+                for (uint32_t w = w0 + 1; w <= w1; w++) add9(acc, part + ((size_t)w * 2) * 3);
+                write_grads(o, (uint32_t)idx, acc);
+            }
+        }
+    }
     float dcov[6] = {0, 0, 0, 0, 0, 0};
     V3 dmean = v3(0, 0, 0);
     V3 dscale = v3(0, 0, 0);
@@ -239,36 +230,43 @@ __global__ __launch_bounds__(256) void gaussian_backward_kernel(
     reinterpret_cast<float4 *>(dL_drot)[idx] = drot;
 }
 
-size_t contrib_scratch_bytes(int R) {
+size_t contrib_scratch_bytes(int R, int P) {
     const size_t nw = ((size_t)R + 63) / 64;
-    return align_up(nw * 2 * 3 * sizeof(float4), 256) + 4 * nw + 256;
+    return align_up(nw * 2 * 3 * sizeof(float4), 256) + align_up(4 * (size_t)P, 256) + 256;
+}
+
+static GradOut grad_out(const Args &a, GeomState g, float *dL_dmean2D, float4 *dL_dconic, float *dL_dopacity,
+                        float *dL_dcolor) {
+    return GradOut{dL_dmean2D, dL_dconic, dL_dopacity, dL_dcolor, g.conic_opacity, 0.5f * a.W, 0.5f * a.H};
+}
+static float4 *scratch_part(char *scratch) { return (float4 *)scratch; }
+static uint32_t *scratch_e_first(char *scratch, int R) {
+    const size_t nw = ((size_t)R + 63) / 64;
+    return (uint32_t *)(scratch + align_up(nw * 2 * 3 * sizeof(float4), 256));
 }
 
 hipError_t launch_contrib_reduce(const Args &a, GeomState g, BinningState b, int R, const float *contrib,
                                  char *scratch, float *dL_dmean2D, float4 *dL_dconic, float *dL_dopacity,
                                  float *dL_dcolor, hipStream_t s) {
-    const GradOut o = {dL_dmean2D, dL_dconic, dL_dopacity, dL_dcolor, g.conic_opacity, 0.5f * a.W, 0.5f * a.H};
+    if (R == 0) return hipSuccess;  // every Gaussian has n_inst = 0: gaussian_backward writes the zeros
     const size_t nw = ((size_t)R + 63) / 64;
-    float4 *part = (float4 *)scratch;
-    uint32_t *flags = (uint32_t *)(scratch + align_up(nw * 2 * 3 * sizeof(float4), 256));
-    const uint32_t *n_dev = R > 0 ? b.scratch : nullptr;  // L' (binning.hip)
-    if (R > 0)
-        hipLaunchKernelGGL(contrib_segments_kernel, dim3((unsigned)((nw + 3) / 4)), dim3(256), 0, s, n_dev,
-                           b.gid_by_e, reinterpret_cast<const float4 *>(contrib), o, part, flags);
-    const size_t nthreads = std::max<size_t>((size_t)a.P, R > 0 ? nw : 0);
-    hipLaunchKernelGGL(contrib_finish_kernel, dim3((unsigned)((nthreads + 255) / 256)), dim3(256), 0, s, a.P,
-                       R > 0 ? n_dev : nullptr, g.n_inst, R > 0 ? b.gid_by_e : nullptr, part, flags, o);
+    const uint32_t *n_dev = b.scratch;  // L' (binning.hip)
+    hipLaunchKernelGGL(contrib_segments_kernel, dim3((unsigned)((nw + 3) / 4)), dim3(256), 0, s, n_dev, b.gid_by_e,
+                       reinterpret_cast<const float4 *>(contrib), grad_out(a, g, dL_dmean2D, dL_dconic, dL_dopacity,
+                                                                          dL_dcolor),
+                       scratch_part(scratch), scratch_e_first(scratch, R));
     return hipGetLastError();
 }
 
-hipError_t launch_gaussian_backward(const Args &a, GeomState g, const int *radii, const float *means3D,
-                                    const float *shs, const float *scales, const float *rotations, const float *cov3D,
-                                    const float *dL_dmean2D, const float4 *dL_dconic, const float *dL_dcolor,
-                                    float *dL_dmean3D, float *dL_dcov3D, float *dL_dsh, float *dL_dscale,
-                                    float *dL_drot, hipStream_t s) {
+hipError_t launch_gaussian_backward(const Args &a, GeomState g, int R, char *scratch, const int *radii,
+                                    const float *means3D, const float *shs, const float *scales, const float *rotations,
+                                    const float *cov3D, float *dL_dmean2D, float4 *dL_dconic, float *dL_dopacity,
+                                    float *dL_dcolor, float *dL_dmean3D, float *dL_dcov3D, float *dL_dsh,
+                                    float *dL_dscale, float *dL_drot, hipStream_t s) {
     hipLaunchKernelGGL(gaussian_backward_kernel, dim3((a.P + 255) / 256), dim3(256), 0, s, a, g, radii, means3D, shs,
                        scales, rotations, cov3D, dL_dmean2D, dL_dconic, dL_dcolor, dL_dmean3D, dL_dcov3D, dL_dsh,
-                       dL_dscale, dL_drot);
+                       dL_dscale, dL_drot, scratch_e_first(scratch, R), scratch_part(scratch),
+                       grad_out(a, g, dL_dmean2D, dL_dconic, dL_dopacity, dL_dcolor));
     return hipGetLastError();
 }
 

@@ -103,6 +103,9 @@ __global__ __launch_bounds__(THREADS) void onesweep_kernel(const uint32_t *__res
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int n = count_of(n_host, n_dev);
     const uint32_t b = blockIdx.x;
+    // a chunk past the device count (the grid is sized by the host's upper bound) has no items, and
+    // no chunk with items reads its look-back words (they only read lower chunks)
+    if ((size_t)b * (THREADS * ITEMS) >= (size_t)n && n_dev) return;
     const size_t wbase = (size_t)b * (THREADS * ITEMS) + (size_t)w * (64 * ITEMS);
     uint32_t key[ITEMS], val[ITEMS], lrank[ITEMS];
     // issue every load of the chunk first
