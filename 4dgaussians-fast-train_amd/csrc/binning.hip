@@ -42,17 +42,19 @@ constexpr int kSortCap = 4096;              // tile runs sorted in LDS by one wo
 constexpr int kScanPer = 4;  // Gaussians per thread of the visible scan (1024 per workgroup)
 __host__ __device__ static size_t nchunk_scan(int P) { return ((size_t)P + 256 * kScanPer - 1) / (256 * kScanPer); }
 __host__ __device__ static size_t nchunk_emit(int L) { return ((size_t)L + kEmitChunk - 1) / kEmitChunk; }
-// geometry: counters | visible-count chain (+ err) | area chain (+ err)
+// geometry: counters | visible-count chain (+ err) | area chain (+ err) | the emission's tile-digit
+// histograms (zeroed by the forward's one memset, before the preprocess)
 __host__ __device__ static size_t geom_vis_chain_off() { return 64; }
 __host__ __device__ static size_t geom_area_chain_off(int P) { return 64 + nchunk_scan(P) + 64; }
+__host__ __device__ static size_t geom_hist_off(int P) { return geom_area_chain_off(P) + nchunk_scan(P) + 64; }
 // rounded to 256 B so that one fill clears each region
-size_t geom_zero_words(int P) { return align_up(geom_area_chain_off(P) + nchunk_scan(P) + 64, 64); }
-// binning: counters ([0] = L') | tile-sort digit histograms | emission chain (+ err) | sort look-back
-__host__ __device__ static size_t bin_chain_off() { return kZeroHist + kHistWords; }
-static size_t bin_look_off(int L) { return bin_chain_off() + nchunk_emit(L) + 64; }
+size_t geom_zero_words(int P) { return align_up(geom_hist_off(P) + kHistWords, 64); }
+// binning: counters ([0] = L', written by the last emission chunk) | the tile sort's look-back words
+// (zeroed by the emission kernel, which runs before the sort): the binning buffer needs no memset
+static size_t bin_look_off() { return 64; }
 size_t binning_zero_words(int L, int T) {
     (void)T;
-    return align_up(bin_look_off(L) + (size_t)kMaxPasses * 256 * sort_nblk(L, kSortThreads * kItemsL), 64);
+    return align_up(bin_look_off() + (size_t)kMaxPasses * 256 * sort_nblk(L, kSortThreads * kItemsL), 64);
 }
 size_t max_emit_chunks(int P, int T) {
     // L < 2^30 is enforced by the caller
@@ -123,6 +125,13 @@ __global__ __launch_bounds__(256) void visible_scan_kernel(GeomState g, int P, u
             g.zero[kZeroV] = v;   // V
         }
     }
+    // the last workgroup knows L (its inclusive area prefix): it clears the emission's chunk-prefix
+    // chain for the nchunk_emit(L) chunks of this call (the emission runs after this kernel)
+    if (b == gridDim.x - 1) {
+        const uint32_t L = apre + atot;
+        const uint32_t n = min((uint32_t)((L + kEmitChunk - 1) / kEmitChunk), jmax) + 64;
+        for (uint32_t i = threadIdx.x; i < n; i += 256) g.emit_chain[i] = 0u;
+    }
 }
 
 hipError_t launch_visible_scan(const Args &a, GeomState g, hipStream_t s) {
@@ -143,10 +152,11 @@ __global__ __launch_bounds__(256) void emit_instances_kernel(Args a, GeomState g
                                                              int L, int npass, uint32_t *__restrict__ keys,
                                                              uint32_t *__restrict__ gid_by_e,
                                                              uint32_t *__restrict__ zero, uint2 *__restrict__ ranges,
-                                                             int T) {
-    // the tile ranges start empty (tile_ranges_kernel writes the non-empty ones): zeroed here instead of
-    // by a memset launch of their own
+                                                             int T, uint32_t *__restrict__ look, int nlook) {
+    // the tile ranges start empty (tile_ranges_kernel writes the non-empty ones) and the tile sort's
+    // look-back words start at zero: both cleared here instead of by memset launches of their own
     for (int i = blockIdx.x * 256 + threadIdx.x; i < T; i += gridDim.x * 256) ranges[i] = make_uint2(0u, 0u);
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < nlook; i += gridDim.x * 256) look[i] = 0u;
     __shared__ uint32_t s_own[kEmitChunk];
     __shared__ uint32_t s_off[kEmitChunk + 2];
     __shared__ uint32_t s_n[kEmitChunk + 1];
@@ -244,7 +254,7 @@ __global__ __launch_bounds__(256) void emit_instances_kernel(Args a, GeomState g
         before += q < w ? s_w[q] : 0u;
         total += s_w[q];
     }
-    uint32_t *chain = zero + bin_chain_off();
+    uint32_t *chain = g.emit_chain;  // cleared by visible_scan
     const uint32_t prefix = block_prefix(chain + 64, b, total, chain + 1, s_tmp);
     if (tid == 0 && c1 == (uint32_t)L) zero[0] = prefix + total;  // L'
     uint32_t e = prefix + before + x - cnt;
@@ -258,7 +268,7 @@ __global__ __launch_bounds__(256) void emit_instances_kernel(Args a, GeomState g
     }
     for (int i = tid; i < nr; i += 256)
         if (s_n[i]) atomicAdd(&g.n_inst[g.vis_gid[rlo + i]], s_n[i]);
-    uint32_t *hist = zero + kZeroHist + (b % kHistShards) * (kMaxPasses * 256);
+    uint32_t *hist = g.zero + geom_hist_off(a.P) + (b % kHistShards) * (kMaxPasses * 256);
     for (int p = 0; p < npass; p++)
         if (s_hist[p][tid]) atomicAdd(&hist[p * 256 + tid], s_hist[p][tid]);
 }
@@ -542,22 +552,22 @@ __global__ __launch_bounds__(256) void tile_sort_kernel(const uint2 *__restrict_
 hipError_t launch_binning(const Args &a, GeomState g, const int *radii, BinningState b, int L, ImageState img,
                           hipStream_t s) {
     const int T = a.gx * a.gy;
-    hipError_t e = hipMemsetAsync(b.scratch, 0, 4 * binning_zero_words(L, T), s);
-    if (e != hipSuccess) return e;
     if (L == 0) {
-        e = hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)T, s);
+        hipError_t e = hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)T, s);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, s, img.ranges, T, img.order);
         return hipGetLastError();
     }
     const int npass = (b.key_bits + 7) / 8;
+    uint32_t *look = b.scratch + bin_look_off();
+    const int nlook = npass * 256 * sort_nblk(L, kSortThreads * kItemsL);
     hipLaunchKernelGGL(emit_instances_kernel, dim3((unsigned)nchunk_emit(L)), dim3(256), 0, s, a, g, radii, L, npass,
-                       b.keys[0], b.gid_by_e, b.scratch, img.ranges, T);
+                       b.keys[0], b.gid_by_e, b.scratch, img.ranges, T, look, nlook);
     const uint32_t *n_dev = b.scratch;  // L' <= L reached instances
     uint32_t *keys[2] = {b.keys[0], b.keys[1]};
     uint32_t *vals[2] = {b.vals[0], b.vals[1]};
-    onesweep_sort<kSortThreads, kItemsL>(keys, vals, L, n_dev, b.key_bits, b.scratch + kZeroHist,
-                                         b.scratch + bin_look_off(L), b.scratch + bin_chain_off() + 1, s);
+    onesweep_sort<kSortThreads, kItemsL>(keys, vals, L, n_dev, b.key_bits, g.zero + geom_hist_off(a.P), look,
+                                         g.emit_chain + 1, s);
     hipLaunchKernelGGL(tile_ranges_kernel, dim3((L + 255) / 256), dim3(256), 0, s, b.sorted_keys, n_dev, img.ranges);
     hipLaunchKernelGGL(tile_sort_kernel, dim3(T + 1), dim3(256), 0, s, img.ranges, T, img.order, b.gid_by_e, g.depths,
                        b.upos, b.tmp_hi, b.tmp_lo);

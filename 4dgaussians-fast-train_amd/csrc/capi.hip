@@ -90,6 +90,7 @@ GeomState GeomState::carve(char *base, int P, int T) {
     g.vis_gid = (uint32_t *)gs4d::carve(p, 4 * n);
     g.cand_off = (uint32_t *)gs4d::carve(p, 4 * n + 4);
     g.first_vis = (uint32_t *)gs4d::carve(p, 4 * max_emit_chunks(P, T));
+    g.emit_chain = (uint32_t *)gs4d::carve(p, 4 * (max_emit_chunks(P, T) + 64));
     g.zero = (uint32_t *)gs4d::carve(p, 4 * geom_zero_words(P));
     return g;
 }

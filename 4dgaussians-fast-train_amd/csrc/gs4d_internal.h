@@ -33,14 +33,16 @@ struct GeomState {
     uint32_t *cand_off;       // P+1 exclusive scan of tiles_touched over the visible Gaussians: first
                               //     candidate instance of each (cand_off[V] = num_rendered)
     uint32_t *first_vis;      // nchunk_max: visible index owning candidate j * kEmitChunk
+    uint32_t *emit_chain;     // nchunk_max + 64: the emission's chunk-prefix chain (+ err word), cleared
+                              //     for this call's chunks by visible_scan (no memset)
     uint32_t *zero;           // geom_zero_words(P): counters, histograms, look-back words (one memset)
     static size_t required(int P, int T);
     static GeomState carve(char *base, int P, int T);
 };
 // Zero regions (u32 words) of the geometry and binning states: [0..63] counters, then the per-state
-// regions of binning.hip (chunk-prefix chains, tile counts).
-// geometry: [0] prefiltered flag, [8..23] 8 u64 shards of num_rendered, [24] V (visible Gaussians);
-// binning: [0] = L'.  Radix-sort users (knn.hip) keep digit histograms [kHistShards][kMaxPasses][256]
+// regions of binning.hip (chunk-prefix chains, digit histograms, look-back words).
+// geometry (one memset per forward): [0] prefiltered flag, [8..23] 8 u64 shards of num_rendered,
+// [24] V (visible Gaussians); binning (cleared by the kernels themselves): [0] = L'.  Radix-sort users (knn.hip) keep digit histograms [kHistShards][kMaxPasses][256]
 // of their own: producers add with atomics sharded by workgroup.
 constexpr int kZeroFlag = 0, kZeroL = 8, kZeroV = 24, kZeroHist = 64;
 constexpr int kHistShards = 8, kMaxPasses = 4;
