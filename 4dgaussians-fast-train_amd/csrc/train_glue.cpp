@@ -409,7 +409,32 @@ std::vector<torch::Tensor> heads_backward(const torch::Tensor &a, const std::vec
     return out;
 }
 
+// ---- first deformation layer backward: (dx, dW, db) for g = dL/dh, h = relu(x W^T + b) (P, Fout), x (P, Fin)
+std::vector<torch::Tensor> feature_relu_backward(const torch::Tensor &g_, const torch::Tensor &h, const torch::Tensor &x,
+                                                 const torch::Tensor &w) {
+    auto g = g_.contiguous();
+    for (const torch::Tensor *t : std::initializer_list<const torch::Tensor *>{&g, &h, &x, &w})
+        gpu_f32(*t, "feature_relu_backward operand");
+    need(h.is_contiguous() && x.is_contiguous() && w.is_contiguous(), "feature_relu_backward: contiguous operands");
+    need(g.dim() == 2 && h.sizes() == g.sizes() && x.dim() == 2 && x.size(0) == g.size(0) && w.dim() == 2 &&
+             w.size(0) == g.size(1) && w.size(1) == x.size(1),
+         "feature_relu_backward: g, h (P, Fout), x (P, Fin), W (Fout, Fin)");
+    c10::hip::HIPGuard guard(g.device().index());
+    const int P = (int)g.size(0), Fout = (int)g.size(1), Fin = (int)x.size(1);
+    auto dx = torch::empty_like(x);
+    auto dw = torch::empty_like(w);
+    auto db = torch::empty({Fout}, w.options());
+    auto scratch = torch::empty({(int64_t)gs4d_feature_relu_backward_scratch_bytes(P, Fin, Fout)},
+                                g.options().dtype(torch::kUInt8));
+    check(gs4d_feature_relu_backward(P, Fin, Fout, g.data_ptr<float>(), h.data_ptr<float>(), x.data_ptr<float>(),
+                                     w.data_ptr<float>(), dx.data_ptr<float>(), dw.data_ptr<float>(),
+                                     db.data_ptr<float>(), scratch.data_ptr(), (void *)stream_of(g)),
+          "feature_relu_backward");
+    return {dx, dw, db};
+}
+
 PYBIND11_MODULE(_C, m) {
+    m.def("feature_relu_backward", &feature_relu_backward);
     m.def("heads_backward", &heads_backward);
     m.def("linear_dw", &linear_dw);
     m.def("hexplane_reg_forward", &hexplane_reg_forward);

@@ -732,6 +732,188 @@ static int dw_rows_per_wg(int P, int nmax) {
     return nmax <= 8 ? 256 : 1024;
 }
 
+
+// ---- the deformation field's first layer, backward (scene/deformation.py:51-55 with defor_depth <= 1:
+// hidden = feature_out(x) = x W^T + b; every head starts with ReLU, so the heads read h = relu(hidden)).
+// Given g = dL/dh, ONE pass over the rows forms dz = g * (h > 0) and both GEMMs on the f32 MFMA
+// (v_mfma_f32_16x16x4_f32: exact f32, a k-ordered fma chain):
+//   dx = dz W   (rows x Fin)   and   dW += dz^T x,  db += column sums of dz  (per-wave partials).
+// A wave takes 16-row blocks: g and h rows are read coalesced (lanes along the outputs), dz is staged
+// in an LDS tile, W lives in LDS.  At the end the
+// workgroup's waves add their dW / db partials in wave order and a second launch sums the workgroups'
+// partials in workgroup order (deterministic).
+constexpr int kFbThreads = 256, kFbRows = 16;
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+template <int FIN, int FOUT>
+__global__ __launch_bounds__(kFbThreads) void feature_bwd_kernel(int P, const float *__restrict__ g,
+                                                                 const float *__restrict__ h,
+                                                                 const float *__restrict__ x,
+                                                                 const float *__restrict__ w, float *__restrict__ dx,
+                                                                 float *__restrict__ part) {
+    constexpr int NB = FIN / 16, MB = FOUT / 16, NW = kFbThreads / 64;
+    // tile row stride = 17 (mod 64) words: the 16-row column reads of dx and the 4-row x 16-column reads
+    // of dW both spread over the LDS banks
+    constexpr int TS = FOUT + 17;
+    constexpr int PER = FOUT * FIN + FOUT;  // one partial: dW (row-major) then db
+    __shared__ float s_w[FOUT * FIN + FOUT];
+    __shared__ float s_t[NW][kFbRows * TS];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int i = threadIdx.x; i < FOUT * FIN / 4; i += kFbThreads)
+        reinterpret_cast<float4 *>(s_w)[i] = reinterpret_cast<const float4 *>(w)[i];
+    __syncthreads();
+    float *t = s_t[wv];
+    f4v accw[MB][NB];
+#pragma unroll
+    for (int m = 0; m < MB; m++)
+#pragma unroll
+        for (int n = 0; n < NB; n++) accw[m][n] = f4v{0.f, 0.f, 0.f, 0.f};
+    float db0 = 0.f, db1 = 0.f;                  // this lane's output pair (o, o + 1)
+    const int o = (2 * lane) % FOUT, rofs = (2 * lane) / FOUT;
+    constexpr int RPI = 128 / FOUT;              // rows per coalesced load instruction
+    const int nblk = (P + kFbRows - 1) / kFbRows;
+    // block loads (g, h rows: lanes along the outputs; x rows as the B operand of dW:
+    // B[k = row 4s + (l >> 4)][n = 16 nb + (l & 15)]), issued one block ahead of their use
+    constexpr int NIT = kFbRows / RPI;
+    float2 gv[NIT], hv[NIT];
+    float xb[4][NB];
+    auto load_block = [&](int blk) {
+        const int r0 = blk * kFbRows;
+#pragma unroll
+        for (int it = 0; it < NIT; it++) {
+            const int r = r0 + it * RPI + rofs;
+            gv[it] = hv[it] = make_float2(0.f, 0.f);
+            if (blk < nblk && r < P) {
+                gv[it] = *reinterpret_cast<const float2 *>(g + (size_t)r * FOUT + o);
+                hv[it] = *reinterpret_cast<const float2 *>(h + (size_t)r * FOUT + o);
+            }
+        }
+#pragma unroll
+        for (int st = 0; st < 4; st++) {
+            const int r = r0 + 4 * st + (lane >> 4);
+#pragma unroll
+            for (int n = 0; n < NB; n++)
+                xb[st][n] = (blk < nblk && r < P) ? x[(size_t)r * FIN + 16 * n + (lane & 15)] : 0.f;
+        }
+    };
+    const int stride = gridDim.x * NW;
+    int blk = blockIdx.x * NW + wv;
+    load_block(blk);
+    for (; blk < nblk; blk += stride) {
+        const int r0 = blk * kFbRows;
+        // dz = g * (h > 0) into the tile, column sums into db
+#pragma unroll
+        for (int it = 0; it < NIT; it++) {
+            const int row = it * RPI + rofs;
+            const float d0 = hv[it].x > 0.f ? gv[it].x : 0.f, d1 = hv[it].y > 0.f ? gv[it].y : 0.f;
+            db0 += d0;
+            db1 += d1;
+            t[row * TS + o] = d0;
+            t[row * TS + o + 1] = d1;
+        }
+        float xc[4][NB];
+#pragma unroll
+        for (int st = 0; st < 4; st++)
+#pragma unroll
+            for (int n = 0; n < NB; n++) xc[st][n] = xb[st][n];
+        load_block(blk + stride);  // the next block's loads fly while this one runs on the MFMA
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the tile is written (LDS is in order per wave)
+        __builtin_amdgcn_wave_barrier();
+        // dx = dz W: A[row l & 15][k = o 4s + (l >> 4)], B[k = o][n = 16 nb + (l & 15)]
+        f4v accx[NB];
+#pragma unroll
+        for (int n = 0; n < NB; n++) accx[n] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+        for (int st = 0; st < FOUT / 4; st++) {
+            const int ok = 4 * st + (lane >> 4);
+            const float av = t[(lane & 15) * TS + ok];
+#pragma unroll
+            for (int n = 0; n < NB; n++)
+                accx[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, s_w[ok * FIN + 16 * n + (lane & 15)], accx[n], 0, 0, 0);
+        }
+        // C[row (l >> 4) * 4 + i][col 16 nb + (l & 15)]
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int r = r0 + (lane >> 4) * 4 + i;
+            if (r < P) {
+#pragma unroll
+                for (int n = 0; n < NB; n++) dx[(size_t)r * FIN + 16 * n + (lane & 15)] = accx[n][i];
+            }
+        }
+        // dW += dz^T x: A[m = o 16 mb + (l & 15)][k = row 4s + (l >> 4)], B = xb
+#pragma unroll
+        for (int st = 0; st < 4; st++) {
+#pragma unroll
+            for (int m = 0; m < MB; m++) {
+                const float av = t[(4 * st + (lane >> 4)) * TS + 16 * m + (lane & 15)];
+#pragma unroll
+                for (int n = 0; n < NB; n++)
+                    accw[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, xc[st][n], accw[m][n], 0, 0, 0);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();  // the tile's reads are done before the next block overwrites it
+    }
+    // the waves' partials added in wave order in LDS (W is no longer needed there)
+    for (int q = 0; q < NW; q++) {
+        __syncthreads();
+        if (wv == q) {
+#pragma unroll
+            for (int m = 0; m < MB; m++)
+#pragma unroll
+                for (int n = 0; n < NB; n++)
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        float &dst = s_w[(16 * m + (lane >> 4) * 4 + i) * FIN + 16 * n + (lane & 15)];
+                        dst = q == 0 ? accw[m][n][i] : dst + accw[m][n][i];
+                    }
+            // db: lanes with the same outputs (RPI > 1) add in lane order
+#pragma unroll
+            for (int rr = 0; rr < RPI; rr++) {
+                if (rofs == rr) {
+                    float &d0 = s_w[FOUT * FIN + o], &d1 = s_w[FOUT * FIN + o + 1];
+                    d0 = (q == 0 && rr == 0) ? db0 : d0 + db0;
+                    d1 = (q == 0 && rr == 0) ? db1 : d1 + db1;
+                }
+                __builtin_amdgcn_s_waitcnt(0xc07f);
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+    }
+    __syncthreads();
+    float *dst = part + (size_t)blockIdx.x * PER;
+    for (int i = threadIdx.x; i < PER; i += kFbThreads) dst[i] = s_w[i];
+}
+
+// dW / db = the workgroups' partials summed in workgroup order: 16 outputs per workgroup, 16 threads per
+// output each summing a strided slice of the partials (all loads independent), then the 16 slices
+// added in slice order
+__global__ __launch_bounds__(256) void feature_bwd_reduce_kernel(int nwg, int per, int nwb, const float *__restrict__ part,
+                                                                 float *__restrict__ dw, float *__restrict__ db) {
+    __shared__ float s_sum[16][17];
+    const int oi = threadIdx.x & 15, sl = threadIdx.x >> 4;
+    const int i = blockIdx.x * 16 + oi;
+    float acc = 0.f;
+    if (i < per) {
+        int k = sl;
+        for (; k + 48 < nwg; k += 64) {
+            const float a0 = part[(size_t)k * per + i], a1 = part[(size_t)(k + 16) * per + i];
+            const float a2 = part[(size_t)(k + 32) * per + i], a3 = part[(size_t)(k + 48) * per + i];
+            acc += a0;
+            acc += a1;
+            acc += a2;
+            acc += a3;
+        }
+        for (; k < nwg; k += 16) acc += part[(size_t)k * per + i];
+    }
+    s_sum[sl][oi] = acc;
+    __syncthreads();
+    if (sl == 0 && i < per) {
+        float t = 0.f;
+        for (int q = 0; q < 16; q++) t += s_sum[q][oi];
+        if (i < nwb) dw[i] = t;
+        else db[i - nwb] = t;
+    }
+}
 }  // namespace gs4d
 
 using namespace gs4d;
@@ -970,6 +1152,37 @@ int gs4d_adam_step(const gs4d_adam_batch *batch, void *stream) {
     }
     if (chunks == 0) return 0;
     hipLaunchKernelGGL(adam_kernel, dim3((unsigned)chunks), dim3(kTailThreads), 0, (hipStream_t)stream, *batch);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+static int fb_grid(int P) {
+    const int nblk = (P + kFbRows - 1) / kFbRows;
+    return std::max(1, std::min(512, (nblk + 3) / 4));
+}
+size_t gs4d_feature_relu_backward_scratch_bytes(int P, int Fin, int Fout) {
+    return 4 * (size_t)fb_grid(std::max(P, 0)) * ((size_t)Fout * Fin + Fout) + 256;
+}
+
+int gs4d_feature_relu_backward(int P, int Fin, int Fout, const float *g, const float *h, const float *x,
+                               const float *w, float *dx, float *dw, float *db, void *scratch, void *stream) {
+    if (P < 0 || !w || !dw || !db || !scratch) return 1;
+    if (!((Fin == 32 && Fout == 128) || (Fin == 64 && Fout == 64) || (Fin == 32 && Fout == 64))) return 1;
+    if (P > 0 && (!g || !h || !x || !dx)) return 1;
+    if ((((size_t)g | (size_t)h | (size_t)w) & 15) != 0) return 1;
+    hipStream_t s = (hipStream_t)stream;
+    const int nwg = fb_grid(P), per = Fout * Fin + Fout;
+    float *part = (float *)align_up((size_t)scratch, 256);
+    if (P == 0) {
+        if (hipMemsetAsync(part, 0, 4 * (size_t)per, s) != hipSuccess) return 3;
+    } else if (Fin == 32 && Fout == 128) {
+        hipLaunchKernelGGL((feature_bwd_kernel<32, 128>), dim3(nwg), dim3(kFbThreads), 0, s, P, g, h, x, w, dx, part);
+    } else if (Fin == 64) {
+        hipLaunchKernelGGL((feature_bwd_kernel<64, 64>), dim3(nwg), dim3(kFbThreads), 0, s, P, g, h, x, w, dx, part);
+    } else {
+        hipLaunchKernelGGL((feature_bwd_kernel<32, 64>), dim3(nwg), dim3(kFbThreads), 0, s, P, g, h, x, w, dx, part);
+    }
+    hipLaunchKernelGGL(feature_bwd_reduce_kernel, dim3((per + 15) / 16), dim3(256), 0, s, P == 0 ? 1 : nwg, per,
+                       Fout * Fin, (const float *)part, dw, db);
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 

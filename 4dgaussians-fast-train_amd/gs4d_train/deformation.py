@@ -175,20 +175,28 @@ class _DeformHeads(torch.autograd.Function):
     GEMMs sum in a different order, so results agree to fp32 rounding."""
 
     @staticmethod
-    def forward(ctx, hidden, w1, b1, *second):
+    def forward(ctx, relu_done, hidden, w1, b1, *second):
+        """relu_done: `hidden` is already relu(hidden) (_FeatureReLU); the returned input gradient is
+        then the gradient of that ReLU's output."""
         k = len(second) // 2
         W = hidden.shape[1]
-        h = torch.relu(hidden)
+        h = hidden if relu_done else torch.relu(hidden)
         a = torch._addmm_activation(b1, h, w1.t())  # bias + ReLU in the GEMM epilogue where supported
         outs = [torch.addmm(second[2 * i + 1], a[:, i * W:(i + 1) * W], second[2 * i].t()) for i in range(k)]
         ctx.save_for_backward(h, a, w1, *second[0::2])
         ctx.W = W
+        ctx.relu_done = relu_done
         return tuple(outs)
 
     @staticmethod
     def backward(ctx, *douts):
+        return (None,) + _DeformHeads._backward(ctx, *douts)
+
+    @staticmethod
+    def _backward(ctx, *douts):
         h, a, w1, *w2 = ctx.saved_tensors
         W, k = ctx.W, len(w2)
+        relu_in = (lambda d: d) if ctx.relu_done else (lambda d: torch.ops.aten.threshold_backward(d, h, 0))
         douts = [d if d is not None else torch.zeros(a.shape[0], w2[i].shape[0], device=a.device)
                  for i, d in enumerate(douts)]
         if a.is_cuda and W in (64, 128, 256) and k * W <= 768 and all(x.shape[0] <= 16 or (x.shape[0] == 48 and W <= 128)
@@ -198,7 +206,7 @@ class _DeformHeads(torch.autograd.Function):
             out = _C.heads_backward(a, list(douts), [x.contiguous() for x in w2])
             da, db1 = out[0], out[1]
             dw1 = _splitk_dw(da, h)
-            dh = torch.ops.aten.threshold_backward(da @ w1, h, 0)
+            dh = relu_in(da @ w1)
             return tuple([dh, dw1, db1] + out[2:])
         da = torch.empty_like(a)
         dw2, db2 = [None] * k, [None] * k
@@ -219,11 +227,33 @@ class _DeformHeads(torch.autograd.Function):
         da = torch.ops.aten.threshold_backward(da, a, 0)  # ReLU backward (a = relu(z): a > 0 <=> z > 0)
         dw1 = _splitk_dw(da, h)
         db1 = da.sum(0)
-        dh = torch.ops.aten.threshold_backward(da @ w1, h, 0)  # the heads' first ReLU
+        dh = relu_in(da @ w1)  # the heads' first ReLU
         grads = [dh, dw1, db1]
         for i in range(k):
             grads += [dw2[i], db2[i]]
         return tuple(grads)
+
+
+class _FeatureReLU(torch.autograd.Function):
+    """feature_out with defor_depth <= 1 (scene/deformation.py:51-55: ONE Linear(feat_dim, W)) followed by
+    the ReLU every head starts with (:73-78): h = relu(x W^T + b), bias and ReLU in the GEMM epilogue.
+    Backward in one HIP pass on the f32 MFMA (gs4d_feature_relu_backward): the ReLU mask, dx = dz W,
+    dW = dz^T x and db.  Same function as Linear + ReLU (the sums run in another order: fp32 rounding)."""
+
+    shapes = ((32, 128), (64, 64), (32, 64))  # (feat_dim, W) the HIP backward is built for
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        h = torch._addmm_activation(b, x, w.t())
+        ctx.save_for_backward(x, w, h)
+        return h
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w, h = ctx.saved_tensors
+        from . import _C
+        dx, dw, db = _C.feature_relu_backward(g, h, x, w)
+        return dx, dw, db
 
 
 class Deformation(nn.Module):
@@ -250,16 +280,24 @@ class Deformation(nn.Module):
             raise NotImplementedError("apply_rotation (documented as unused in arguments/__init__.py:104)")
         xyz = xyz if xyz.shape[1] == 3 else xyz[:, :3]
         time = time if time.shape[1] == 1 else time[:, :1]
-        hidden = self.feature_out(self.grid(xyz, time))
         active = [name for name, flag in (("pos_deform", a.no_dx), ("scales_deform", a.no_ds),
                                           ("rotations_deform", a.no_dr), ("opacity_deform", a.no_do),
                                           ("shs_deform", a.no_dshs)) if not flag]
-        if self.fused_heads and hidden.is_cuda and torch.is_grad_enabled() and active:
+        return self._heads(self.grid(xyz, time), active)
+
+    def _heads(self, feat, active):
+        """{name: head output} of the active heads on the field features (feature_out, then the heads)."""
+        if self.fused_heads and feat.is_cuda and torch.is_grad_enabled() and active:
             heads = [getattr(self, name) for name in active]
             w1 = torch.cat([hd[1].weight for hd in heads], 0)
             b1 = torch.cat([hd[1].bias for hd in heads], 0)
             second = [t for hd in heads for t in (hd[3].weight, hd[3].bias)]
-            return dict(zip(active, _DeformHeads.apply(hidden, w1, b1, *second)))
+            lin = self.feature_out[0]
+            if len(self.feature_out) == 1 and (feat.shape[1], self.W) in _FeatureReLU.shapes:
+                h = _FeatureReLU.apply(feat.contiguous(), lin.weight, lin.bias)
+                return dict(zip(active, _DeformHeads.apply(True, h, w1, b1, *second)))
+            return dict(zip(active, _DeformHeads.apply(False, self.feature_out(feat), w1, b1, *second)))
+        hidden = self.feature_out(feat)
         return {name: getattr(self, name)(hidden) for name in active}
 
     def forward(self, xyz, scales, rotations, opacity, shs, time):
@@ -272,18 +310,10 @@ class Deformation(nn.Module):
         xyz, scales, rotations, opacity = (t if t.shape[1] == n else t[:, :n] for t, n in
                                            ((xyz, 3), (scales, 3), (rotations, 4), (opacity, 1)))
         time = time if time.shape[1] == 1 else time[:, :1]
-        hidden = self.feature_out(self.grid(xyz, time))
-        active = [(name, flag) for name, flag in (("pos_deform", a.no_dx), ("scales_deform", a.no_ds),
-                                                  ("rotations_deform", a.no_dr), ("opacity_deform", a.no_do),
-                                                  ("shs_deform", a.no_dshs)) if not flag]
-        if self.fused_heads and hidden.is_cuda and torch.is_grad_enabled() and active:
-            heads = [getattr(self, name) for name, _ in active]
-            w1 = torch.cat([hd[1].weight for hd in heads], 0)
-            b1 = torch.cat([hd[1].bias for hd in heads], 0)
-            second = [t for hd in heads for t in (hd[3].weight, hd[3].bias)]
-            outs = dict(zip([name for name, _ in active], _DeformHeads.apply(hidden, w1, b1, *second)))
-        else:
-            outs = {name: getattr(self, name)(hidden) for name, _ in active}
+        active = [name for name, flag in (("pos_deform", a.no_dx), ("scales_deform", a.no_ds),
+                                          ("rotations_deform", a.no_dr), ("opacity_deform", a.no_do),
+                                          ("shs_deform", a.no_dshs)) if not flag]
+        outs = self._heads(self.grid(xyz, time), active)
         pts = xyz if a.no_dx else xyz + outs["pos_deform"]
         sc = scales if a.no_ds else scales + outs["scales_deform"]
         rot = rotations if a.no_dr else rotations + outs["rotations_deform"]

@@ -178,6 +178,17 @@ typedef struct gs4d_heads_bwd {
 size_t gs4d_heads_backward_scratch_bytes(int P, int W, int k, const int *n);
 int gs4d_heads_backward(const gs4d_heads_bwd *args, void *scratch, void *stream);
 
+/* ---- The deformation field's first layer, backward, when feature_out is ONE Linear (defor_depth <= 1,
+ * scene/deformation.py:51-55: hidden = x W^T + b) and every head begins with ReLU, so the heads read
+ * h = relu(hidden).  Given g = dL/dh (P, Fout), h (P, Fout), x (P, Fin), W (Fout, Fin), one pass over the
+ * rows (f32 MFMA, exact f32 products) writes what autograd forms with threshold_backward, two GEMMs and a
+ * sum: dx = (g * (h > 0)) W (P, Fin), dW = (g * (h > 0))^T x (Fout, Fin), db = column sums of
+ * g * (h > 0) (Fout); partial sums reduced in a fixed order.  (Fin, Fout) in {(32, 128), (64, 64),
+ * (32, 64)}; contiguous; g, h, W 16-byte aligned; scratch of gs4d_feature_relu_backward_scratch_bytes. */
+size_t gs4d_feature_relu_backward_scratch_bytes(int P, int Fin, int Fout);
+int gs4d_feature_relu_backward(int P, int Fin, int Fout, const float *g, const float *h, const float *x,
+                               const float *w, float *dx, float *dw, float *db, void *scratch, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -213,7 +213,7 @@ def test_deform_heads_block_matches_separate_heads():
     b2 = [torch.randn(n, dtype=torch.float64, requires_grad=True) for n in ns]
     ups = [torch.randn(P, n, dtype=torch.float64) for n in ns]
     leaves = [hid] + w1 + b1 + w2 + b2
-    outs = _DeformHeads.apply(hid, torch.cat(w1), torch.cat(b1), *[t for i in range(5) for t in (w2[i], b2[i])])
+    outs = _DeformHeads.apply(False, hid, torch.cat(w1), torch.cat(b1), *[t for i in range(5) for t in (w2[i], b2[i])])
     ga = torch.autograd.grad(sum((o * u).sum() for o, u in zip(outs, ups)), leaves)
     F = torch.nn.functional
     ref = [F.linear(torch.relu(F.linear(torch.relu(hid), w1[i], b1[i])), w2[i], b2[i]) for i in range(5)]

@@ -226,6 +226,43 @@ def test_heads_backward_matches_fp64(P, W, ns):
         assert float((out[3 + 2 * i].double() - rb).abs().max() / sb) <= 1e-5
 
 
+@pytest.mark.parametrize("P,Fin,Fout", [(100_003, 32, 128), (777, 64, 64), (1, 32, 128), (0, 32, 128),
+                                        (333, 32, 64), (16, 64, 64)])
+def test_feature_relu_backward_matches_fp64(P, Fin, Fout):
+    """gs4d_feature_relu_backward (the first deformation layer's ReLU mask, input gradient, weight and
+    bias gradients in one MFMA pass) vs fp64 torch: dx to 1e-5 of its row's |terms| sum, dW / db to
+    1e-5 of their largest |term| sum, rows whose h <= 0 contribute exactly nothing; ragged P, P = 1,
+    P = 0 (zero gradients); then _FeatureReLU end to end through autograd."""
+    from gs4d_train import _C
+    from gs4d_train.deformation import _FeatureReLU
+    torch.manual_seed(P + Fin)
+    x = torch.randn(P, Fin, device="cuda")
+    w = torch.randn(Fout, Fin, device="cuda") * 0.2
+    b = torch.randn(Fout, device="cuda") * 0.1
+    h = torch.relu(x @ w.t() + b)
+    g = torch.randn(P, Fout, device="cuda")
+    dx, dw, db = _C.feature_relu_backward(g, h, x, w)
+    rd = (g * (h > 0)).double()
+    assert dx.shape == x.shape and dw.shape == w.shape and db.shape == (Fout,)
+    if P:
+        ref_dx, scale = rd @ w.double(), rd.abs() @ w.double().abs()
+        assert float(((dx.double() - ref_dx).abs() - 1e-5 * scale).max().clamp_min(0)) == 0.0
+    rw, rb = rd.t() @ x.double(), rd.sum(0)
+    sw = (rd.abs().t() @ x.double().abs()).max().clamp_min(1e-30) if P else torch.tensor(1.0)
+    sb = rd.abs().sum(0).max().clamp_min(1e-30) if P else torch.tensor(1.0)
+    assert float((dw.double() - rw).abs().max() / sw) <= 1e-5
+    assert float((db.double() - rb).abs().max() / sb) <= 1e-5
+    # the autograd Function end to end
+    xa, wa, ba = (t.clone().requires_grad_(True) for t in (x, w, b))
+    ha = _FeatureReLU.apply(xa, wa, ba)
+    torch.testing.assert_close(ha, h, rtol=1e-5, atol=1e-5)
+    ha.backward(g)
+    ex, ew, eb = _C.feature_relu_backward(g, ha.detach(), x, w)  # same mask as the Function's (its own h)
+    torch.testing.assert_close(xa.grad, ex, rtol=0, atol=0)    # deterministic: bitwise
+    torch.testing.assert_close(wa.grad, ew, rtol=0, atol=0)
+    torch.testing.assert_close(ba.grad, eb, rtol=0, atol=0)
+
+
 def test_train_step_fused_matches_torch_tail():
     """One fine-stage step through deformation + rasterizer + loss + densification statistics, fused
     (HexPlane kernel, L1 kernel, stats kernel) vs the reference's torch formulation.  The optimizer is

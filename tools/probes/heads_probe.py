@@ -37,10 +37,10 @@ def main(P=100_000, W=128):
 
     def fwd():
         with torch.no_grad():
-            return _DeformHeads.apply(hid, w1, b1, *second)
+            return _DeformHeads.apply(False, hid, w1, b1, *second)
 
     def fwdbwd():
-        outs = _DeformHeads.apply(hid, w1, b1, *second)
+        outs = _DeformHeads.apply(False, hid, w1, b1, *second)
         torch.autograd.backward(outs, ups)
 
     a = torch.relu(torch.randn(P, 5 * W, device=dev))
