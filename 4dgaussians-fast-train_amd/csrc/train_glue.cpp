@@ -433,7 +433,38 @@ std::vector<torch::Tensor> feature_relu_backward(const torch::Tensor &g_, const 
     return {dx, dw, db};
 }
 
+// ---- heads block forward: [out_i (P, n_i)] for a (P, kW), W2_i (n_i, W), b2_i (n_i)
+std::vector<torch::Tensor> heads_forward(const torch::Tensor &a, const std::vector<torch::Tensor> &w2s,
+                                         const std::vector<torch::Tensor> &b2s) {
+    const int k = (int)w2s.size();
+    need(k >= 1 && k <= GS4D_HEADS_MAX && (int)b2s.size() == k, "heads_forward: 1-8 heads");
+    need(a.is_cuda() && a.scalar_type() == torch::kFloat32 && a.dim() == 2 && a.is_contiguous() && a.size(1) % k == 0,
+         "heads_forward: a contiguous float32 (P, kW) GPU tensor");
+    c10::hip::HIPGuard guard(a.device().index());
+    gs4d_heads_fwd b{};
+    b.P = (int)a.size(0), b.W = (int)(a.size(1) / k), b.k = k, b.a = a.data_ptr<float>();
+    std::vector<torch::Tensor> out, keep;
+    for (int i = 0; i < k; i++) {
+        auto w2 = w2s[i].contiguous();
+        auto b2 = b2s[i].contiguous();
+        need(w2.is_cuda() && w2.scalar_type() == torch::kFloat32 && w2.dim() == 2 && w2.size(1) == b.W &&
+                 b2.scalar_type() == torch::kFloat32 && b2.numel() == w2.size(0),
+             "heads_forward: W2_i (n_i, W), b2_i (n_i) float32");
+        b.n[i] = (int)w2.size(0);
+        b.w2[i] = w2.data_ptr<float>();
+        b.b2[i] = b2.data_ptr<float>();
+        auto o = torch::empty({a.size(0), w2.size(0)}, a.options());
+        b.out[i] = o.data_ptr<float>();
+        out.push_back(o);
+        keep.push_back(w2);
+        keep.push_back(b2);
+    }
+    check(gs4d_heads_forward(&b, (void *)stream_of(a)), "heads_forward");
+    return out;
+}
+
 PYBIND11_MODULE(_C, m) {
+    m.def("heads_forward", &heads_forward);
     m.def("feature_relu_backward", &feature_relu_backward);
     m.def("heads_backward", &heads_backward);
     m.def("linear_dw", &linear_dw);

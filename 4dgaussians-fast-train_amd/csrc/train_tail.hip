@@ -914,6 +914,95 @@ __global__ __launch_bounds__(256) void feature_bwd_reduce_kernel(int nwg, int pe
         else db[i - nwb] = t;
     }
 }
+// ---- the deformation heads' second layers, forward (scene/deformation.py:73-78 as one block: head i =
+// a[:, iW:(i+1)W] W2_i^T + b2_i on a = relu(h W1^T + b1), (P, kW)) in ONE pass over a on the f32 MFMA
+// (v_mfma_f32_16x16x4_f32), where torch runs k small GEMMs on column slices.  A wave takes 16-row
+// blocks; for each head and 16-column K chunk the wave reads a as float4 straight from HBM (lane group
+// q = l >> 4 holds columns 4q..4q+3 of its row l & 15: the MFMA's k index in step s is column 4q + s,
+// so each lane's 4 steps come from one 16-byte load), the matching W2 rows (staged in LDS, row stride
+// W + 4: conflict-free 16-byte reads) are the B operand, one accumulator per 16 outputs of the head.
+struct HfArgs {
+    int P, W, k, kW;  // kW: the row stride of a (floats)
+    int n[kHbMaxHeads];
+    int roff[kHbMaxHeads];  // head i's first row in the LDS copy of the W2s
+    const float *w2[kHbMaxHeads];
+    const float *b2[kHbMaxHeads];
+    float *out[kHbMaxHeads];
+};
+constexpr int kHfThreads = 256, kHfMaxTiles = 4;  // up to 64 outputs per head
+
+// NT...: tiles of 16 outputs per head, compile-time, so that every head's accumulators are registers
+// and ALL heads advance together through each 16-column K chunk (sum NT independent MFMA chains; the
+// next chunk's loads are issued before this chunk's MFMAs).
+template <int W, int... NT>
+__global__ __launch_bounds__(kHfThreads) void heads_fwd_kernel(HfArgs A, const float *__restrict__ a) {
+    constexpr int K = sizeof...(NT);
+    constexpr int nt[K] = {NT...};
+    extern __shared__ float4 s_w2v[];
+    float *s_w2 = reinterpret_cast<float *>(s_w2v);
+    constexpr int WS = W + 4;
+    for (int i = 0; i < K; i++)
+        for (int e = threadIdx.x; e < A.n[i] * (W / 4); e += kHfThreads) {
+            const int row = e / (W / 4), c4 = e % (W / 4);
+            reinterpret_cast<float4 *>(s_w2 + (size_t)(A.roff[i] + row) * WS)[c4] =
+                reinterpret_cast<const float4 *>(A.w2[i] + (size_t)row * W)[c4];
+        }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, q = lane >> 4, c = lane & 15;
+    const int nblk = (A.P + 15) / 16;
+    for (int blk = blockIdx.x * (kHfThreads / 64) + wv; blk < nblk; blk += gridDim.x * (kHfThreads / 64)) {
+        const int r0 = blk * 16, ra = r0 + c;
+        const bool live = ra < A.P;
+        const float *arow = a + (size_t)min(ra, A.P - 1) * A.kW + 4 * q;
+        f4v acc[K][4];
+#pragma unroll
+        for (int i = 0; i < K; i++)
+#pragma unroll
+            for (int t = 0; t < 4; t++) acc[i][t] = f4v{0.f, 0.f, 0.f, 0.f};
+        float4 av[K], an[K];
+#pragma unroll
+        for (int i = 0; i < K; i++) an[i] = *reinterpret_cast<const float4 *>(arow + i * W);
+#pragma unroll 2
+        for (int kc = 0; kc < W / 16; kc++) {
+#pragma unroll
+            for (int i = 0; i < K; i++) av[i] = live ? an[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+            if (kc + 1 < W / 16) {
+#pragma unroll
+                for (int i = 0; i < K; i++) an[i] = *reinterpret_cast<const float4 *>(arow + i * W + 16 * (kc + 1));
+            }
+#pragma unroll
+            for (int i = 0; i < K; i++) {
+#pragma unroll
+                for (int t = 0; t < nt[i]; t++) {
+                    const int nn = 16 * t + c;
+                    const float4 bv = nn < A.n[i] ? *reinterpret_cast<const float4 *>(
+                                                        s_w2 + (size_t)(A.roff[i] + nn) * WS + 16 * kc + 4 * q)
+                                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+                    acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i].x, bv.x, acc[i][t], 0, 0, 0);
+                    acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i].y, bv.y, acc[i][t], 0, 0, 0);
+                    acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i].z, bv.z, acc[i][t], 0, 0, 0);
+                    acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i].w, bv.w, acc[i][t], 0, 0, 0);
+                }
+            }
+        }
+        // C[row 4q + j][col 16 t + c]
+#pragma unroll
+        for (int i = 0; i < K; i++) {
+#pragma unroll
+            for (int t = 0; t < nt[i]; t++) {
+                const int col = 16 * t + c, n = A.n[i];
+                if (col < n) {
+                    const float bias = A.b2[i][col];
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const int r = r0 + 4 * q + j;
+                        if (r < A.P) A.out[i][(size_t)r * n + col] = acc[i][t][j] + bias;
+                    }
+                }
+            }
+        }
+    }
+}
 }  // namespace gs4d
 
 using namespace gs4d;
@@ -1183,6 +1272,65 @@ int gs4d_feature_relu_backward(int P, int Fin, int Fout, const float *g, const f
     }
     hipLaunchKernelGGL(feature_bwd_reduce_kernel, dim3((per + 15) / 16), dim3(256), 0, s, P == 0 ? 1 : nwg, per,
                        Fout * Fin, (const float *)part, dw, db);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+int gs4d_heads_forward(const gs4d_heads_fwd *args, void *stream) {
+    if (!args) return 1;
+    const gs4d_heads_fwd &b = *args;
+    if (b.P < 0 || (b.W != 64 && b.W != 128 && b.W != 256) || b.k < 1 || b.k > kHbMaxHeads) return 1;
+    HfArgs A{};
+    A.P = b.P, A.W = b.W, A.k = b.k, A.kW = b.k * b.W;
+    int rows = 0;
+    for (int i = 0; i < b.k; i++) {
+        if (b.n[i] < 1 || b.n[i] > 16 * kHfMaxTiles || !b.w2[i] || !b.b2[i] || (b.P > 0 && !b.out[i])) return 1;
+        if (((size_t)b.w2[i] & 15) != 0) return 1;
+        A.n[i] = b.n[i], A.w2[i] = b.w2[i], A.b2[i] = b.b2[i], A.out[i] = b.out[i], A.roff[i] = rows;
+        rows += b.n[i];
+    }
+    const size_t lds = 4 * (size_t)rows * (b.W + 4);
+    if (lds > 64 * 1024) return 1;
+    if (b.P == 0) return 0;
+    if (!b.a || ((size_t)b.a & 15) != 0) return 1;
+    const int nblk = (b.P + 15) / 16;
+    const int nwg = std::max(1, std::min(1024, (nblk + 3) / 4));
+    hipStream_t s = (hipStream_t)stream;
+    int tiles[kHbMaxHeads];
+    for (int i = 0; i < b.k; i++) tiles[i] = (b.n[i] + 15) / 16;
+    auto is = [&](std::initializer_list<int> cfg) {
+        if ((int)cfg.size() != b.k) return false;
+        int i = 0;
+        for (int t : cfg) if (tiles[i++] != t) return false;
+        return true;
+    };
+    auto launch = [&](auto kernel, const HfArgs &args, const float *ap) {
+        hipLaunchKernelGGL(kernel, dim3(nwg), dim3(kHfThreads), lds, s, args, ap);
+    };
+    // the reference's head sets: arguments/dynerf (pos, scales, rotations, opacity, shs: 3,3,4,1,48 outputs)
+    // and the defaults (pos, scales, rotations); any other set runs head by head
+    if (b.W == 128 && is({1, 1, 1, 1, 3})) launch(heads_fwd_kernel<128, 1, 1, 1, 1, 3>, A, b.a);
+    else if (b.W == 64 && is({1, 1, 1, 1, 3})) launch(heads_fwd_kernel<64, 1, 1, 1, 1, 3>, A, b.a);
+    else if (b.W == 64 && is({1, 1, 1})) launch(heads_fwd_kernel<64, 1, 1, 1>, A, b.a);
+    else if (b.W == 128 && is({1, 1, 1})) launch(heads_fwd_kernel<128, 1, 1, 1>, A, b.a);
+    else {
+        for (int i = 0; i < b.k; i++) {  // one head per launch: a's row stride stays k W
+            HfArgs H{};
+            H.P = b.P, H.W = b.W, H.k = 1, H.n[0] = b.n[i], H.roff[0] = 0, H.w2[0] = b.w2[i], H.b2[0] = b.b2[i];
+            H.out[0] = b.out[i];
+            const float *ap = b.a + (size_t)i * b.W;
+            const int t = tiles[i];
+            H.kW = b.k * b.W;
+            auto one = [&](auto k64, auto k128, auto k256) {
+                if (b.W == 64) launch(k64, H, ap);
+                else if (b.W == 128) launch(k128, H, ap);
+                else launch(k256, H, ap);
+            };
+            if (t == 1) one(heads_fwd_kernel<64, 1>, heads_fwd_kernel<128, 1>, heads_fwd_kernel<256, 1>);
+            else if (t == 2) one(heads_fwd_kernel<64, 2>, heads_fwd_kernel<128, 2>, heads_fwd_kernel<256, 2>);
+            else if (t == 3) one(heads_fwd_kernel<64, 3>, heads_fwd_kernel<128, 3>, heads_fwd_kernel<256, 3>);
+            else one(heads_fwd_kernel<64, 4>, heads_fwd_kernel<128, 4>, heads_fwd_kernel<256, 4>);
+        }
+    }
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 

@@ -182,7 +182,13 @@ class _DeformHeads(torch.autograd.Function):
         W = hidden.shape[1]
         h = hidden if relu_done else torch.relu(hidden)
         a = torch._addmm_activation(b1, h, w1.t())  # bias + ReLU in the GEMM epilogue where supported
-        outs = [torch.addmm(second[2 * i + 1], a[:, i * W:(i + 1) * W], second[2 * i].t()) for i in range(k)]
+        if a.is_cuda and W in (64, 128, 256) and k <= 8 and all(t.shape[0] <= 64 for t in second[0::2]) and \
+                sum(t.shape[0] for t in second[0::2]) * (W + 4) * 4 <= 64 * 1024:
+            # the k second layers in one MFMA pass over a (gs4d_heads_forward)
+            from . import _C
+            outs = _C.heads_forward(a, list(second[0::2]), list(second[1::2]))
+        else:
+            outs = [torch.addmm(second[2 * i + 1], a[:, i * W:(i + 1) * W], second[2 * i].t()) for i in range(k)]
         ctx.save_for_backward(h, a, w1, *second[0::2])
         ctx.W = W
         ctx.relu_done = relu_done

@@ -189,6 +189,21 @@ size_t gs4d_feature_relu_backward_scratch_bytes(int P, int Fin, int Fout);
 int gs4d_feature_relu_backward(int P, int Fin, int Fout, const float *g, const float *h, const float *x,
                                const float *w, float *dx, float *dw, float *db, void *scratch, void *stream);
 
+/* ---- The deformation heads' second layers, forward (scene/deformation.py:73-78 as one block): given
+ * a = relu(h W1^T + b1) (P, kW), out_i = a[:, iW:(i+1)W] W2_i^T + b2_i (P, n_i) for every head in one pass
+ * over a (f32 MFMA, exact f32 products), where torch runs k GEMMs on column slices.  W in {64, 128, 256},
+ * 1 <= k <= 8, 1 <= n_i <= 64, the W2s (n_i, W) 16-byte aligned and at most 64 KiB together; a contiguous,
+ * 16-byte aligned; out_i (P, n_i) contiguous. */
+typedef struct gs4d_heads_fwd {
+    int P, W, k;
+    const float *a;
+    int n[GS4D_HEADS_MAX];
+    const float *w2[GS4D_HEADS_MAX];
+    const float *b2[GS4D_HEADS_MAX];
+    float *out[GS4D_HEADS_MAX];
+} gs4d_heads_fwd;
+int gs4d_heads_forward(const gs4d_heads_fwd *args, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

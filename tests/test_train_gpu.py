@@ -226,6 +226,29 @@ def test_heads_backward_matches_fp64(P, W, ns):
         assert float((out[3 + 2 * i].double() - rb).abs().max() / sb) <= 1e-5
 
 
+@pytest.mark.parametrize("P,W,ns", [(100_003, 128, [3, 3, 4, 1, 48]), (777, 64, [2, 16, 5]), (1, 128, [1, 48]),
+                                     (0, 128, [3, 4]), (1001, 256, [17, 40]), (40, 128, [33, 64])])
+def test_heads_forward_matches_fp64(P, W, ns):
+    """gs4d_heads_forward (the heads block's second layers in one MFMA pass over a) vs the same products
+    in fp64 torch: every output to 1e-5 of its |terms| sum (+ |bias|); ragged P, P = 1, P = 0, n_i from 1
+    to 64 (partial 16-output tiles)."""
+    from gs4d_train import _C
+    torch.manual_seed(P + W + len(ns))
+    k = len(ns)
+    a = torch.relu(torch.randn(P, k * W, device="cuda"))
+    w2 = [torch.randn(n, W, device="cuda") for n in ns]
+    b2 = [torch.randn(n, device="cuda") for n in ns]
+    out = _C.heads_forward(a, w2, b2)
+    assert len(out) == k
+    for i, (w, b) in enumerate(zip(w2, b2)):
+        x = a[:, i * W:(i + 1) * W].double()
+        ref = x @ w.double().t() + b.double()
+        scale = x.abs() @ w.double().abs().t() + b.double().abs()
+        assert out[i].shape == (P, ns[i])
+        if P:
+            assert float(((out[i].double() - ref).abs() - 1e-5 * scale).max().clamp_min(0)) == 0.0
+
+
 @pytest.mark.parametrize("P,Fin,Fout", [(100_003, 32, 128), (777, 64, 64), (1, 32, 128), (0, 32, 128),
                                         (333, 32, 64), (16, 64, 64)])
 def test_feature_relu_backward_matches_fp64(P, Fin, Fout):
@@ -267,7 +290,8 @@ def test_train_step_fused_matches_torch_tail():
     """One fine-stage step through deformation + rasterizer + loss + densification statistics, fused
     (HexPlane kernel, L1 kernel, stats kernel) vs the reference's torch formulation.  The optimizer is
     held back (iteration >= opt.iterations) so the parameter gradients themselves are compared; the
-    optimizer has its own test above.  Tolerance: 1e-4 relative to each gradient tensor's max."""
+    optimizer has its own test above.  Tolerance: 1e-3 of each gradient tensor's max (2e-5 at the 99.9th
+    percentile)."""
     from gs4d_train import config
     from gs4d_train.gaussians import GaussianModel
     from gs4d_train.synthetic import make_point_cloud, make_training_views
@@ -297,8 +321,13 @@ def test_train_step_fused_matches_torch_tail():
     for k in gra:
         a, b = gra[k], grb[k]
         scale = max(a.abs().max().item(), 1e-30)
-        err = (a - b).abs().max().item() / scale
-        assert err < 1e-4, (k, err)
+        d = (a - b).abs().flatten() / scale
+        # fp32 summation order differs (MFMA heads / feature layer vs hipBLASLt, fused field vs
+        # grid_sample); the step amplifies ~1e-7 output differences through the L1 sign and the blend
+        # thresholds into isolated gradient elements (measured <= 1.3e-4: tools/probes/heads_fwd_delta.py),
+        # so the bar is the north star's 1e-3 on the max and 2e-5 on the 99.9th percentile
+        assert d.max().item() < 1e-3, (k, d.max().item())
+        assert d.kthvalue(max(1, int(0.999 * d.numel()))).values.item() < 2e-5, k
     # the statistic sums |d loss / d mean2D| per point: fp32 rounding of the deformation MLP moves it by
     # ~1e-9 absolute (1e-4 of the tensor's max, the same bar as the gradients above)
     acc_scale = max(ga.xyz_gradient_accum.abs().max().item(), 1e-30)
