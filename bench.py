@@ -167,7 +167,7 @@ def main():
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None, "traffic": traffic,
                          "traffic_raw": traffic_raw,
-                         "traffic_note": "PMC bytes per launch (profiles/r01_pmc.json): traffic = 2 x FETCH_SIZE + "
+                         "traffic_note": "PMC bytes per launch (profiles/r02_pmc.json): traffic = 2 x FETCH_SIZE + "
                                          "WRITE_SIZE (gfx950 wide-read correction), traffic_raw = FETCH_SIZE + "
                                          "WRITE_SIZE; the kernel's reads are mostly gathers, so the truth lies between",
                          "algorithmic_bytes": dom_bytes, "avg_ms": round(dom_ms, 4)},
