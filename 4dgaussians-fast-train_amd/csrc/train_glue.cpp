@@ -463,7 +463,23 @@ std::vector<torch::Tensor> heads_forward(const torch::Tensor &a, const std::vect
     return out;
 }
 
+// ---- first deformation layer forward: h = relu(x W^T + b)
+torch::Tensor feature_relu_forward(const torch::Tensor &x, const torch::Tensor &w, const torch::Tensor &b) {
+    for (const torch::Tensor *t : std::initializer_list<const torch::Tensor *>{&x, &w, &b})
+        gpu_f32(*t, "feature_relu_forward operand");
+    need(x.is_contiguous() && w.is_contiguous() && b.is_contiguous() && x.dim() == 2 && w.dim() == 2 &&
+             w.size(1) == x.size(1) && b.numel() == w.size(0),
+         "feature_relu_forward: x (P, Fin), W (Fout, Fin), b (Fout), contiguous");
+    c10::hip::HIPGuard guard(x.device().index());
+    auto h = torch::empty({x.size(0), w.size(0)}, x.options());
+    check(gs4d_feature_relu_forward((int)x.size(0), (int)x.size(1), (int)w.size(0), x.data_ptr<float>(),
+                                    w.data_ptr<float>(), b.data_ptr<float>(), h.data_ptr<float>(), (void *)stream_of(x)),
+          "feature_relu_forward");
+    return h;
+}
+
 PYBIND11_MODULE(_C, m) {
+    m.def("feature_relu_forward", &feature_relu_forward);
     m.def("heads_forward", &heads_forward);
     m.def("feature_relu_backward", &feature_relu_backward);
     m.def("heads_backward", &heads_backward);

@@ -1003,6 +1003,59 @@ __global__ __launch_bounds__(kHfThreads) void heads_fwd_kernel(HfArgs A, const f
         }
     }
 }
+// ---- the deformation field's first layer, forward: h = relu(x W^T + b) (P, FOUT) from x (P, FIN) on the
+// f32 MFMA.  Per 16-row block: lane group q = l >> 4 reads columns 4q..4q+3 of its row l & 15 of a 16-column
+// K chunk as one float4 (the MFMA's k index in step s is column 4q + s), the matching W rows (LDS, row stride
+// FIN + 4) are the B operand, FOUT / 16 accumulators; bias and ReLU on the way out.
+template <int FIN, int FOUT>
+__global__ __launch_bounds__(kFbThreads) void feature_fwd_kernel(int P, const float *__restrict__ x,
+                                                                 const float *__restrict__ w,
+                                                                 const float *__restrict__ b, float *__restrict__ h) {
+    constexpr int WS = FIN + 4, NT = FOUT / 16, NW = kFbThreads / 64;
+    __shared__ float s_w[FOUT * WS];
+    for (int e = threadIdx.x; e < FOUT * FIN / 4; e += kFbThreads) {
+        const int row = e / (FIN / 4), c4 = e % (FIN / 4);
+        reinterpret_cast<float4 *>(s_w + row * WS)[c4] = reinterpret_cast<const float4 *>(w + (size_t)row * FIN)[c4];
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, q = lane >> 4, c = lane & 15;
+    float bias[NT];
+#pragma unroll
+    for (int t = 0; t < NT; t++) bias[t] = b[16 * t + c];
+    const int nblk = (P + 15) / 16;
+    for (int blk = blockIdx.x * NW + wv; blk < nblk; blk += gridDim.x * NW) {
+        const int r0 = blk * 16, ra = r0 + c;
+        float4 xv[FIN / 16];
+#pragma unroll
+        for (int kc = 0; kc < FIN / 16; kc++)
+            xv[kc] = ra < P ? *reinterpret_cast<const float4 *>(x + (size_t)ra * FIN + 16 * kc + 4 * q)
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
+        f4v acc[NT];
+#pragma unroll
+        for (int t = 0; t < NT; t++) acc[t] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kc = 0; kc < FIN / 16; kc++) {
+#pragma unroll
+            for (int t = 0; t < NT; t++) {
+                const float4 bv = *reinterpret_cast<const float4 *>(s_w + (16 * t + c) * WS + 16 * kc + 4 * q);
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[kc].x, bv.x, acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[kc].y, bv.y, acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[kc].z, bv.z, acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[kc].w, bv.w, acc[t], 0, 0, 0);
+            }
+        }
+        // C[row 4q + j][col 16 t + c]
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int r = r0 + 4 * q + j;
+            if (r < P) {
+#pragma unroll
+                for (int t = 0; t < NT; t++) h[(size_t)r * FOUT + 16 * t + c] = fmaxf(acc[t][j] + bias[t], 0.f);
+            }
+        }
+    }
+}
+
 }  // namespace gs4d
 
 using namespace gs4d;
@@ -1331,6 +1384,23 @@ int gs4d_heads_forward(const gs4d_heads_fwd *args, void *stream) {
             else one(heads_fwd_kernel<64, 4>, heads_fwd_kernel<128, 4>, heads_fwd_kernel<256, 4>);
         }
     }
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+int gs4d_feature_relu_forward(int P, int Fin, int Fout, const float *x, const float *w, const float *b, float *h,
+                              void *stream) {
+    if (P < 0 || !w || !b) return 1;
+    if (!((Fin == 32 && Fout == 128) || (Fin == 64 && Fout == 64) || (Fin == 32 && Fout == 64))) return 1;
+    if (P == 0) return 0;
+    if (!x || !h || (((size_t)x | (size_t)w) & 15) != 0) return 1;
+    hipStream_t s = (hipStream_t)stream;
+    const int nwg = std::max(1, std::min(1024, ((P + 15) / 16 + 3) / 4));
+    if (Fin == 32 && Fout == 128)
+        hipLaunchKernelGGL((feature_fwd_kernel<32, 128>), dim3(nwg), dim3(kFbThreads), 0, s, P, x, w, b, h);
+    else if (Fin == 64)
+        hipLaunchKernelGGL((feature_fwd_kernel<64, 64>), dim3(nwg), dim3(kFbThreads), 0, s, P, x, w, b, h);
+    else
+        hipLaunchKernelGGL((feature_fwd_kernel<32, 64>), dim3(nwg), dim3(kFbThreads), 0, s, P, x, w, b, h);
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 

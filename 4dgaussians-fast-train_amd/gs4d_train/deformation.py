@@ -242,7 +242,7 @@ class _DeformHeads(torch.autograd.Function):
 
 class _FeatureReLU(torch.autograd.Function):
     """feature_out with defor_depth <= 1 (scene/deformation.py:51-55: ONE Linear(feat_dim, W)) followed by
-    the ReLU every head starts with (:73-78): h = relu(x W^T + b), bias and ReLU in the GEMM epilogue.
+    the ReLU every head starts with (:73-78): h = relu(x W^T + b) in one f32-MFMA pass (gs4d_feature_relu_forward).
     Backward in one HIP pass on the f32 MFMA (gs4d_feature_relu_backward): the ReLU mask, dx = dz W,
     dW = dz^T x and db.  Same function as Linear + ReLU (the sums run in another order: fp32 rounding)."""
 
@@ -250,7 +250,8 @@ class _FeatureReLU(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, b):
-        h = torch._addmm_activation(b, x, w.t())
+        from . import _C
+        h = _C.feature_relu_forward(x, w.contiguous(), b.contiguous())  # one f32-MFMA pass, bias + ReLU fused
         ctx.save_for_backward(x, w, h)
         return h
 

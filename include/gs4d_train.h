@@ -185,6 +185,8 @@ int gs4d_heads_backward(const gs4d_heads_bwd *args, void *scratch, void *stream)
  * sum: dx = (g * (h > 0)) W (P, Fin), dW = (g * (h > 0))^T x (Fout, Fin), db = column sums of
  * g * (h > 0) (Fout); partial sums reduced in a fixed order.  (Fin, Fout) in {(32, 128), (64, 64),
  * (32, 64)}; contiguous; g, h, W 16-byte aligned; scratch of gs4d_feature_relu_backward_scratch_bytes. */
+int gs4d_feature_relu_forward(int P, int Fin, int Fout, const float *x, const float *w, const float *b, float *h,
+                              void *stream);  /* h = relu(x W^T + b), f32 MFMA; same shapes; x, W 16-byte aligned */
 size_t gs4d_feature_relu_backward_scratch_bytes(int P, int Fin, int Fout);
 int gs4d_feature_relu_backward(int P, int Fin, int Fout, const float *g, const float *h, const float *x,
                                const float *w, float *dx, float *dw, float *db, void *scratch, void *stream);
