@@ -484,21 +484,50 @@ static size_t hex_order_zero_words(int N) {
     return 64 + (size_t)kHistWords + 4 * 256 * (size_t)sort_nblk(N, kHexSortThreads * kHexSortItems);
 }
 
-// (1, F, H, W) planes <-> the packed channels-last buffer.  One thread per packed element.
-template <bool PACK>
-__global__ __launch_bounds__(kHexThreads) void hexplane_repack_kernel(gs4d_hexplane_layout lay,
-                                                                      float *__restrict__ packed) {
-    const int64_t i = (int64_t)blockIdx.x * kHexThreads + threadIdx.x;
-    if (i >= lay.total) return;
+// (1, F, H, W) planes <-> the packed channels-last buffer: a transpose per plane, tiled through LDS so that
+// both sides are coalesced.  Workgroup = TC consecutive cells of one plane (all F features; TC = 256 for
+// F <= 32, fewer for wider planes: the tile stays <= 33 KiB): the planar side is F rows of TC contiguous
+// floats, the packed side TC F contiguous floats (tile row stride TC + 1: the column reads spread over the
+// banks).
+constexpr int kRepackThreads = 256;
+__host__ __device__ inline int repack_cells(int F) { return F <= 32 ? 256 : 8192 / F; }
+__device__ __forceinline__ int repack_plane(const gs4d_hexplane_layout &lay, int64_t &tile) {
+    const int TC = repack_cells(lay.F);
     int p = 0;
-    while (p + 1 < 6 * lay.levels && lay.plane[p + 1].offset <= i) p++;
+    for (; p < 6 * lay.levels; p++) {
+        const int64_t nt = ((int64_t)lay.plane[p].W * lay.plane[p].H + TC - 1) / TC;
+        if (tile < nt) break;
+        tile -= nt;
+    }
+    return p;
+}
+template <bool PACK>
+__global__ __launch_bounds__(kRepackThreads) void hexplane_repack_kernel(gs4d_hexplane_layout lay,
+                                                                         float *__restrict__ packed) {
+    extern __shared__ float s_tile[];  // F x (TC + 1)
+    int64_t tile = blockIdx.x;
+    const int p = repack_plane(lay, tile);
+    if (p >= 6 * lay.levels) return;
     const gs4d_hexplane_plane pl = lay.plane[p];
-    const int64_t local = i - pl.offset;  // = cell * F + f
-    const int f = (int)(local % lay.F);
-    const int64_t cell = local / lay.F;
-    const int64_t planar = (int64_t)f * pl.H * pl.W + cell;  // (F, H, W) index
-    if (PACK) packed[i] = pl.param[planar];
-    else pl.grad[planar] = packed[i];
+    const int F = lay.F, TC = repack_cells(F), TS = TC + 1, t = threadIdx.x;
+    const int64_t HW = (int64_t)pl.W * pl.H, c0 = tile * TC;
+    const int nc = (int)min((int64_t)TC, HW - c0);
+    float *dst = packed + pl.offset + c0 * F;
+    if (PACK) {
+        for (int e = t; e < F * nc; e += kRepackThreads) {
+            const int f = e / nc, c = e % nc;
+            s_tile[f * TS + c] = pl.param[f * HW + c0 + c];
+        }
+        __syncthreads();
+        for (int k = t; k < nc * F; k += kRepackThreads) dst[k] = s_tile[(k % F) * TS + k / F];
+    } else {
+        for (int k = t; k < nc * F; k += kRepackThreads) s_tile[(k % F) * TS + k / F] = dst[k];
+        __syncthreads();
+        for (int e = t; e < F * nc; e += kRepackThreads) {
+            const int f = e / nc, c = e % nc;
+            pl.grad[f * HW + c0 + c] = s_tile[f * TS + c];
+        }
+    }
 }
 
 }  // namespace gs4d
@@ -526,13 +555,19 @@ int gs4d_hexplane_layout_init(gs4d_hexplane_layout *lay, int levels, int F, cons
     return 0;
 }
 
+static int64_t repack_tiles(const gs4d_hexplane_layout &lay) {
+    int64_t n = 0;
+    const int TC = repack_cells(lay.F);
+    for (int p = 0; p < 6 * lay.levels; p++) n += ((int64_t)lay.plane[p].W * lay.plane[p].H + TC - 1) / TC;
+    return n;
+}
+
 int gs4d_hexplane_pack(const gs4d_hexplane_layout *lay, float *packed, void *stream) {
     if (!lay || !packed) return 1;
     for (int p = 0; p < 6 * lay->levels; p++)
         if (!lay->plane[p].param) return 1;
-    const int64_t nb = (lay->total + kHexThreads - 1) / kHexThreads;
-    hipLaunchKernelGGL(hexplane_repack_kernel<true>, dim3((unsigned)nb), dim3(kHexThreads), 0, (hipStream_t)stream,
-                       *lay, packed);
+    hipLaunchKernelGGL(hexplane_repack_kernel<true>, dim3((unsigned)repack_tiles(*lay)), dim3(kRepackThreads),
+                       4 * (size_t)lay->F * (repack_cells(lay->F) + 1), (hipStream_t)stream, *lay, packed);
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
@@ -540,9 +575,8 @@ int gs4d_hexplane_unpack(const gs4d_hexplane_layout *lay, const float *packed, v
     if (!lay || !packed) return 1;
     for (int p = 0; p < 6 * lay->levels; p++)
         if (!lay->plane[p].grad) return 1;
-    const int64_t nb = (lay->total + kHexThreads - 1) / kHexThreads;
-    hipLaunchKernelGGL(hexplane_repack_kernel<false>, dim3((unsigned)nb), dim3(kHexThreads), 0, (hipStream_t)stream,
-                       *lay, (float *)packed);
+    hipLaunchKernelGGL(hexplane_repack_kernel<false>, dim3((unsigned)repack_tiles(*lay)), dim3(kRepackThreads),
+                       4 * (size_t)lay->F * (repack_cells(lay->F) + 1), (hipStream_t)stream, *lay, (float *)packed);
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
