@@ -449,6 +449,7 @@ __global__ __launch_bounds__(256) void linear_dw_reduce_kernel(DwBatch b, int W,
 // wave-uniform): its W2_i column and dW2_i accumulators stay in registers, the g_i row is wave-uniform
 // (scalar loads).  Per-workgroup partials are summed in a fixed order by a second launch.
 constexpr int kHbMaxHeads = 8;
+typedef float f4v __attribute__((ext_vector_type(4)));  // an MFMA 16x16 accumulator (4 per lane)
 // One launch serves the heads [h0, h0 + hk) (columns h0 W .. (h0 + hk) W of a): the narrow heads and
 // the 48-wide one go in separate launches, each with its own row blocking, so no workgroup waits on a
 // few compute-heavy waves.
@@ -685,6 +686,160 @@ __global__ __launch_bounds__(512) void heads_bwd_wide_kernel(HbArgs A, const flo
     if (c < N) ph[c * (W + 1) + W] = bsum;
 }
 
+// The wide head on the f32 MFMA (v_mfma_f32_16x16x4_f32), for W in {64, 128} and N a multiple of 16:
+// a wave takes 16-row blocks and forms
+//   da (16 x W) = (a > 0) * (g (16 x N) W2 (N x W)):  lane group q = l >> 4 reads columns 4q..4q+3 of its
+//       g row l & 15 per 16-column K chunk as one float4 (k index of step s = column 4q + s); W2^T in LDS
+//       (row stride N + 4) is the B operand;
+//   dW2 (N x W) += g^T a:  K = the 16 rows, lane group q takes rows 4q..4q+3 (k index of step s = row
+//       4q + s), so the a values it needs are exactly the ones the da mask reads at the C positions
+//       (rows 4q + j, columns 16t + c): loaded once, used twice;
+//   db1 (column sums of da) and db2 (column sums of g) on the way.
+// The waves' partials are added in wave order in LDS, the workgroups' by heads_bwd_reduce_kernel (the
+// same partial layout as heads_bwd_wide_kernel).
+template <int W, int N>
+__global__ __launch_bounds__(256) void heads_bwd_wide_mfma_kernel(HbArgs A, const float *__restrict__ a,
+                                                                   float *__restrict__ da,
+                                                                   const float *__restrict__ g,
+                                                                   float *__restrict__ part) {
+    // each wave takes half of the head's W columns (CT tiles of 16) of a row block: waves 2i and 2i + 1
+    // share block i's rows; only the first half accumulates db2 (g's column sums)
+    constexpr int CT = W / 32, MT = N / 16, NKC = N / 16, WS = N + 4, NWV = 4;
+    constexpr int PER = W + N * (W + 1);  // partial: db1 (W) then for each output r: dW2[r][0..W), db2[r]
+    __shared__ float s_w2t[W * WS];
+    __shared__ float s_red[PER];
+    const int ld = A.k * W, h = A.h0;
+    const float *__restrict__ w2 = A.w2[h];
+    for (int e = threadIdx.x; e < N * W; e += 256) {  // W2 (N x W) -> W2^T rows
+        const int r = e / W, col = e % W;
+        s_w2t[col * WS + r] = w2[e];
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, q = lane >> 4, c = lane & 15;
+    const int half = wv & 1, cb = half * (W / 2);  // this wave's first column
+    f4v accw[MT][CT];
+#pragma unroll
+    for (int m = 0; m < MT; m++)
+#pragma unroll
+        for (int t = 0; t < CT; t++) accw[m][t] = f4v{0.f, 0.f, 0.f, 0.f};
+    float csum[CT], bsum[MT];
+#pragma unroll
+    for (int t = 0; t < CT; t++) csum[t] = 0.f;
+#pragma unroll
+    for (int m = 0; m < MT; m++) bsum[m] = 0.f;
+    const int P = A.P, nblk = (P + 15) / 16;
+    const float *acol = a + h * W + cb;
+    float *dacol = da + h * W + cb;
+    // a block's loads: g rows as the da A operand, g at (row 4q + s, output 16m + c) as the dW2 A operand,
+    // a at the C positions (row 4q + j, column 16t + c); issued one block ahead of their use
+    float4 gA[NKC];
+    float gT[MT][4], av[CT][4];
+    auto load_block = [&](int blk) {
+        const int r0 = blk * 16, rg = r0 + c;
+#pragma unroll
+        for (int kc = 0; kc < NKC; kc++)
+            gA[kc] = (blk < nblk && rg < P) ? *reinterpret_cast<const float4 *>(g + (size_t)rg * N + 16 * kc + 4 * q)
+                                            : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int r = r0 + 4 * q + j;
+            const bool ok = blk < nblk && r < P;
+#pragma unroll
+            for (int m = 0; m < MT; m++) gT[m][j] = ok ? g[(size_t)r * N + 16 * m + c] : 0.f;
+#pragma unroll
+            for (int t = 0; t < CT; t++) av[t][j] = ok ? acol[(size_t)r * ld + 16 * t + c] : 0.f;
+        }
+    };
+    const int stride = gridDim.x * (NWV / 2);
+    int blk = blockIdx.x * (NWV / 2) + (wv >> 1);
+    load_block(blk);
+    for (; blk < nblk; blk += stride) {
+        const int r0 = blk * 16;
+        float4 gAc[NKC];
+        float gTc[MT][4], avc[CT][4];
+#pragma unroll
+        for (int kc = 0; kc < NKC; kc++) gAc[kc] = gA[kc];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+#pragma unroll
+            for (int m = 0; m < MT; m++) gTc[m][j] = gT[m][j];
+#pragma unroll
+            for (int t = 0; t < CT; t++) avc[t][j] = av[t][j];
+        }
+        load_block(blk + stride);
+        // da
+#pragma unroll
+        for (int t = 0; t < CT; t++) {
+            f4v acc = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kc = 0; kc < NKC; kc++) {
+                const float4 bv = *reinterpret_cast<const float4 *>(s_w2t + (cb + 16 * t + c) * WS + 16 * kc + 4 * q);
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(gAc[kc].x, bv.x, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(gAc[kc].y, bv.y, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(gAc[kc].z, bv.z, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(gAc[kc].w, bv.w, acc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int r = r0 + 4 * q + j;
+                const float v = avc[t][j] > 0.f ? acc[j] : 0.f;
+                if (r < P) dacol[(size_t)r * ld + 16 * t + c] = v;
+                csum[t] += v;
+            }
+        }
+        // dW2 += g^T a, db2
+#pragma unroll
+        for (int m = 0; m < MT; m++) {
+#pragma unroll
+            for (int j = 0; j < 4; j++) bsum[m] += gTc[m][j];
+#pragma unroll
+            for (int t = 0; t < CT; t++)
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    accw[m][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(gTc[m][j], avc[t][j], accw[m][t], 0, 0, 0);
+        }
+    }
+    // wave partials -> LDS: the two halves' column ranges are disjoint; waves of the same half are
+    // added in wave order (accw C layout: row = output 16m + 4q + j, column cb + 16t + c); db1 / db2: the
+    // 4 lane groups (q) of a column added in q order; db2 from the first half only
+    for (int qw = 0; qw < NWV; qw++) {
+        __syncthreads();
+        if (wv == qw) {
+            const bool first = qw < 2;  // the first wave of this half
+#pragma unroll
+            for (int m = 0; m < MT; m++)
+#pragma unroll
+                for (int t = 0; t < CT; t++)
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        float &d = s_red[W + (16 * m + 4 * q + j) * (W + 1) + cb + 16 * t + c];
+                        d = first ? accw[m][t][j] : d + accw[m][t][j];
+                    }
+            for (int qq = 0; qq < 4; qq++) {
+                if (q == qq) {
+#pragma unroll
+                    for (int t = 0; t < CT; t++) {
+                        float &d = s_red[cb + 16 * t + c];
+                        d = (first && qq == 0) ? csum[t] : d + csum[t];
+                    }
+                    if (half == 0) {
+#pragma unroll
+                        for (int m = 0; m < MT; m++) {
+                            float &d = s_red[W + (16 * m + c) * (W + 1) + W];
+                            d = (first && qq == 0) ? bsum[m] : d + bsum[m];
+                        }
+                    }
+                }
+                __builtin_amdgcn_s_waitcnt(0xc07f);
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+    }
+    __syncthreads();
+    float *pw = part + (size_t)blockIdx.x * PER;
+    for (int i = threadIdx.x; i < PER; i += 256) pw[i] = s_red[i];
+}
+
 // the partials summed over the workgroups (32 record entries per workgroup, 8 eighths in a fixed
 // order) and routed to db1 / dW2_i / db2_i
 struct HbOut {
@@ -743,7 +898,6 @@ static int dw_rows_per_wg(int P, int nmax) {
 // workgroup's waves add their dW / db partials in wave order and a second launch sums the workgroups'
 // partials in workgroup order (deterministic).
 constexpr int kFbThreads = 256, kFbRows = 16;
-typedef float f4v __attribute__((ext_vector_type(4)));
 
 template <int FIN, int FOUT>
 __global__ __launch_bounds__(kFbThreads) void feature_bwd_kernel(int P, const float *__restrict__ g,
@@ -1064,6 +1218,7 @@ extern "C" {
 
 // the launches: maximal runs of heads of one class (narrow: n <= 16; wide: n = 48)
 static bool hb_wide(int n) { return n > 16; }  // n = 48 (validated), one head per launch
+static bool hb_mfma(int W, int n) { return (W == 64 || W == 128) && n == 48; }  // heads_bwd_wide_mfma_kernel
 static int hb_rows_per_wg(int P, bool wide) {
     // narrow heads stream a: about two workgroups per CU; the wide head's waves are compute-heavy and
     // its per-workgroup partials large: 256-row blocks
@@ -1127,7 +1282,14 @@ int gs4d_heads_backward(const gs4d_heads_bwd *args, void *scratch, void *stream)
         if (b.P == 0) {  // empty sums: the partials of one empty workgroup
             if (hipMemsetAsync(part, 0, 4 * (size_t)A.poff[hk], s) != hipSuccess) err = 3;
         } else {
-            if (hb_wide(b.n[h0]))
+            if (hb_wide(b.n[h0]) && hb_mfma(b.W, b.n[h0])) {
+                if (b.W == 128)
+                    hipLaunchKernelGGL((heads_bwd_wide_mfma_kernel<128, 48>), dim3(nwg), dim3(256), 0, s, A, b.a, b.da,
+                                       g[h0], part);
+                else
+                    hipLaunchKernelGGL((heads_bwd_wide_mfma_kernel<64, 48>), dim3(nwg), dim3(256), 0, s, A, b.a, b.da,
+                                       g[h0], part);
+            } else if (hb_wide(b.n[h0]))
                 hipLaunchKernelGGL(heads_bwd_wide_kernel<48>, dim3(nwg), dim3(kWideGroups * b.W), 0, s, A, b.a, b.da,
                                    g[h0], part);
             else
