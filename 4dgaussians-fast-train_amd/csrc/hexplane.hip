@@ -501,7 +501,7 @@ __device__ __forceinline__ int repack_plane(const gs4d_hexplane_layout &lay, int
     }
     return p;
 }
-template <bool PACK>
+template <bool PACK, int FC>  // FC: the feature count when known at compile time (all loads in flight), else 0
 __global__ __launch_bounds__(kRepackThreads) void hexplane_repack_kernel(gs4d_hexplane_layout lay,
                                                                          float *__restrict__ packed) {
     extern __shared__ float s_tile[];  // F x (TC + 1)
@@ -509,10 +509,44 @@ __global__ __launch_bounds__(kRepackThreads) void hexplane_repack_kernel(gs4d_he
     const int p = repack_plane(lay, tile);
     if (p >= 6 * lay.levels) return;
     const gs4d_hexplane_plane pl = lay.plane[p];
-    const int F = lay.F, TC = repack_cells(F), TS = TC + 1, t = threadIdx.x;
+    const int F = FC ? FC : lay.F, TC = repack_cells(F), TS = TC + 1, t = threadIdx.x;
     const int64_t HW = (int64_t)pl.W * pl.H, c0 = tile * TC;
     const int nc = (int)min((int64_t)TC, HW - c0);
     float *dst = packed + pl.offset + c0 * F;
+    if (FC && TC == kRepackThreads) {
+        // one cell per thread on the planar side, F values in flight
+        if (PACK) {
+            float v[FC > 0 ? FC : 1];
+#pragma unroll
+            for (int f = 0; f < FC; f++) v[f] = t < nc ? pl.param[f * HW + c0 + t] : 0.f;
+#pragma unroll
+            for (int f = 0; f < FC; f++) s_tile[f * TS + t] = v[f];
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < FC; j++) {
+                const int k = t + j * kRepackThreads;
+                if (k < nc * FC) dst[k] = s_tile[(k % FC) * TS + k / FC];
+            }
+        } else {
+            float v[FC > 0 ? FC : 1];
+#pragma unroll
+            for (int j = 0; j < FC; j++) {
+                const int k = t + j * kRepackThreads;
+                v[j] = k < nc * FC ? dst[k] : 0.f;
+            }
+#pragma unroll
+            for (int j = 0; j < FC; j++) {
+                const int k = t + j * kRepackThreads;
+                s_tile[(k % FC) * TS + k / FC] = v[j];
+            }
+            __syncthreads();
+            if (t < nc) {
+#pragma unroll
+                for (int f = 0; f < FC; f++) pl.grad[f * HW + c0 + t] = s_tile[f * TS + t];
+            }
+        }
+        return;
+    }
     if (PACK) {
         for (int e = t; e < F * nc; e += kRepackThreads) {
             const int f = e / nc, c = e % nc;
@@ -566,8 +600,14 @@ int gs4d_hexplane_pack(const gs4d_hexplane_layout *lay, float *packed, void *str
     if (!lay || !packed) return 1;
     for (int p = 0; p < 6 * lay->levels; p++)
         if (!lay->plane[p].param) return 1;
-    hipLaunchKernelGGL(hexplane_repack_kernel<true>, dim3((unsigned)repack_tiles(*lay)), dim3(kRepackThreads),
-                       4 * (size_t)lay->F * (repack_cells(lay->F) + 1), (hipStream_t)stream, *lay, packed);
+    const dim3 grid((unsigned)repack_tiles(*lay));
+    const size_t lds = 4 * (size_t)lay->F * (repack_cells(lay->F) + 1);
+    if (lay->F == 16)
+        hipLaunchKernelGGL((hexplane_repack_kernel<true, 16>), grid, dim3(kRepackThreads), lds, (hipStream_t)stream, *lay, packed);
+    else if (lay->F == 32)
+        hipLaunchKernelGGL((hexplane_repack_kernel<true, 32>), grid, dim3(kRepackThreads), lds, (hipStream_t)stream, *lay, packed);
+    else
+        hipLaunchKernelGGL((hexplane_repack_kernel<true, 0>), grid, dim3(kRepackThreads), lds, (hipStream_t)stream, *lay, packed);
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
@@ -575,8 +615,15 @@ int gs4d_hexplane_unpack(const gs4d_hexplane_layout *lay, const float *packed, v
     if (!lay || !packed) return 1;
     for (int p = 0; p < 6 * lay->levels; p++)
         if (!lay->plane[p].grad) return 1;
-    hipLaunchKernelGGL(hexplane_repack_kernel<false>, dim3((unsigned)repack_tiles(*lay)), dim3(kRepackThreads),
-                       4 * (size_t)lay->F * (repack_cells(lay->F) + 1), (hipStream_t)stream, *lay, (float *)packed);
+    const dim3 grid((unsigned)repack_tiles(*lay));
+    const size_t lds = 4 * (size_t)lay->F * (repack_cells(lay->F) + 1);
+    float *pk = (float *)packed;
+    if (lay->F == 16)
+        hipLaunchKernelGGL((hexplane_repack_kernel<false, 16>), grid, dim3(kRepackThreads), lds, (hipStream_t)stream, *lay, pk);
+    else if (lay->F == 32)
+        hipLaunchKernelGGL((hexplane_repack_kernel<false, 32>), grid, dim3(kRepackThreads), lds, (hipStream_t)stream, *lay, pk);
+    else
+        hipLaunchKernelGGL((hexplane_repack_kernel<false, 0>), grid, dim3(kRepackThreads), lds, (hipStream_t)stream, *lay, pk);
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
