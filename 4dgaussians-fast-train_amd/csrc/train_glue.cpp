@@ -478,7 +478,37 @@ torch::Tensor feature_relu_forward(const torch::Tensor &x, const torch::Tensor &
     return h;
 }
 
+// ---- the field's input points: (pts (N, 4)) from xyz (N, 3+), t (N, 1+), aabb (2, 3); backward dxyz
+torch::Tensor hexplane_points(const torch::Tensor &xyz, const torch::Tensor &t, const torch::Tensor &aabb_) {
+    gpu_f32(xyz, "xyz");
+    gpu_f32(t, "timestamps");
+    need(xyz.dim() == 2 && xyz.size(1) >= 3 && xyz.stride(1) == 1 && t.dim() == 2 && t.size(0) == xyz.size(0),
+         "hexplane_points: xyz (N, 3) with unit column stride, t (N, 1)");
+    c10::hip::HIPGuard guard(xyz.device().index());
+    auto aabb = aabb_.to(xyz.device(), torch::kFloat32).contiguous();
+    need(aabb.numel() == 6, "hexplane_points: aabb (2, 3)");
+    auto pts = torch::empty({xyz.size(0), 4}, xyz.options());
+    check(gs4d_hexplane_points((int)xyz.size(0), xyz.data_ptr<float>(), xyz.stride(0), t.data_ptr<float>(), t.stride(0),
+                               aabb.data_ptr<float>(), pts.data_ptr<float>(), (void *)stream_of(xyz)),
+          "hexplane_points");
+    return pts;
+}
+torch::Tensor hexplane_points_backward(const torch::Tensor &dpts_, const torch::Tensor &aabb_) {
+    auto dpts = dpts_.contiguous();
+    gpu_f32(dpts, "dpts");
+    need(dpts.dim() == 2 && dpts.size(1) == 4, "hexplane_points_backward: dpts (N, 4)");
+    c10::hip::HIPGuard guard(dpts.device().index());
+    auto aabb = aabb_.to(dpts.device(), torch::kFloat32).contiguous();
+    auto dxyz = torch::empty({dpts.size(0), 3}, dpts.options());
+    check(gs4d_hexplane_points_backward((int)dpts.size(0), dpts.data_ptr<float>(), aabb.data_ptr<float>(),
+                                        dxyz.data_ptr<float>(), (void *)stream_of(dpts)),
+          "hexplane_points_backward");
+    return dxyz;
+}
+
 PYBIND11_MODULE(_C, m) {
+    m.def("hexplane_points", &hexplane_points);
+    m.def("hexplane_points_backward", &hexplane_points_backward);
     m.def("feature_relu_forward", &feature_relu_forward);
     m.def("heads_forward", &heads_forward);
     m.def("feature_relu_backward", &feature_relu_backward);

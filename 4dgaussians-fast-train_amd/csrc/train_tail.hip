@@ -1210,6 +1210,35 @@ __global__ __launch_bounds__(kFbThreads) void feature_fwd_kernel(int P, const fl
     }
 }
 
+// ---- the HexPlane field's input points: scene/hexplane.py:20-21 normalize_aabb + :166 torch.cat((pts, t)) in
+// one pass, pts4[n] = ((xyz[n] - aabb[0]) * s - 1, t[n]) with s = (1 / (aabb[1] - aabb[0])) * 2 (torch's
+// 2.0 / tensor is reciprocal-then-multiply), the same float operations as the reference's graph; backward:
+// dxyz = dpts[:, 0:3] * s (the mul's gradient; the time column takes none).
+__device__ __forceinline__ float3 hex_scale(const float *aabb) {
+    return make_float3((1.0f / (aabb[3] - aabb[0])) * 2.0f, (1.0f / (aabb[4] - aabb[1])) * 2.0f,
+                       (1.0f / (aabb[5] - aabb[2])) * 2.0f);
+}
+__global__ __launch_bounds__(256) void hex_points_kernel(int N, const float *__restrict__ xyz, int64_t ld_xyz,
+                                                         const float *__restrict__ t, int64_t ld_t,
+                                                         const float *__restrict__ aabb, float4 *__restrict__ pts) {
+    const int n = blockIdx.x * 256 + threadIdx.x;
+    if (n >= N) return;
+    const float3 sc = hex_scale(aabb);
+    const float *x = xyz + (size_t)n * ld_xyz;
+    pts[n] = make_float4((x[0] - aabb[0]) * sc.x - 1.0f, (x[1] - aabb[1]) * sc.y - 1.0f, (x[2] - aabb[2]) * sc.z - 1.0f,
+                         t[(size_t)n * ld_t]);
+}
+__global__ __launch_bounds__(256) void hex_points_bwd_kernel(int N, const float4 *__restrict__ dpts,
+                                                             const float *__restrict__ aabb, float *__restrict__ dxyz) {
+    const int n = blockIdx.x * 256 + threadIdx.x;
+    if (n >= N) return;
+    const float3 sc = hex_scale(aabb);
+    const float4 d = dpts[n];
+    dxyz[3 * (size_t)n] = d.x * sc.x;
+    dxyz[3 * (size_t)n + 1] = d.y * sc.y;
+    dxyz[3 * (size_t)n + 2] = d.z * sc.z;
+}
+
 }  // namespace gs4d
 
 using namespace gs4d;
@@ -1563,6 +1592,25 @@ int gs4d_feature_relu_forward(int P, int Fin, int Fout, const float *x, const fl
         hipLaunchKernelGGL((feature_fwd_kernel<64, 64>), dim3(nwg), dim3(kFbThreads), 0, s, P, x, w, b, h);
     else
         hipLaunchKernelGGL((feature_fwd_kernel<32, 64>), dim3(nwg), dim3(kFbThreads), 0, s, P, x, w, b, h);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+int gs4d_hexplane_points(int N, const float *xyz, int64_t ld_xyz, const float *t, int64_t ld_t, const float *aabb,
+                         float *pts, void *stream) {
+    if (N < 0 || !aabb) return 1;
+    if (N == 0) return 0;
+    if (!xyz || !t || !pts || ((size_t)pts & 15) != 0 || ld_xyz < 3 || ld_t < 1) return 1;
+    hipLaunchKernelGGL(hex_points_kernel, dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream, N, xyz, ld_xyz, t,
+                       ld_t, aabb, (float4 *)pts);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+int gs4d_hexplane_points_backward(int N, const float *dpts, const float *aabb, float *dxyz, void *stream) {
+    if (N < 0 || !aabb) return 1;
+    if (N == 0) return 0;
+    if (!dpts || !dxyz || ((size_t)dpts & 15) != 0) return 1;
+    hipLaunchKernelGGL(hex_points_bwd_kernel, dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream, N,
+                       (const float4 *)dpts, aabb, dxyz);
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 

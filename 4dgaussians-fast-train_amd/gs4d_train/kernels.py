@@ -10,7 +10,7 @@ import torch
 
 from . import _C
 
-__all__ = ["deform_tail", "l1_loss", "densify_stats", "FusedAdam", "hexplane", "hexplane_regulation", "hexplane_regulation_value",
+__all__ = ["deform_tail", "l1_loss", "densify_stats", "FusedAdam", "hexplane", "hexplane_points", "hexplane_regulation", "hexplane_regulation_value",
            "hexplane_regulation_accumulate_grad"]
 
 
@@ -165,6 +165,27 @@ class _HexPlane(torch.autograd.Function):
         pts, packed, order, *planes = ctx.saved_tensors
         dpts, dplanes = _C.hexplane_backward(pts, planes, packed, dfeat, order)
         return (dpts, *dplanes)
+
+
+class _HexPoints(torch.autograd.Function):
+    """scene/hexplane.py:20-21 normalize_aabb + :166 torch.cat((pts, timestamps), -1) in one HIP pass each
+    way (gs4d_hexplane_points): the reference's float operations, so the result is bitwise its graph's.
+    The time column takes no gradient (as the reference's timestamps, which never require one here)."""
+
+    @staticmethod
+    def forward(ctx, xyz, t, aabb):
+        ctx.save_for_backward(aabb)
+        return _C.hexplane_points(xyz, t, aabb)
+
+    @staticmethod
+    def backward(ctx, dpts):
+        (aabb,) = ctx.saved_tensors
+        return _C.hexplane_points_backward(dpts, aabb), None, None
+
+
+def hexplane_points(xyz, t, aabb):
+    """(N, 4) = (normalize_aabb(xyz, aabb), t) for the field (gradient to xyz only)."""
+    return _HexPoints.apply(xyz, t.detach(), aabb.detach())
 
 
 def hexplane(pts, ms_grids):

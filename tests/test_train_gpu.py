@@ -226,6 +226,26 @@ def test_heads_backward_matches_fp64(P, W, ns):
         assert float((out[3 + 2 * i].double() - rb).abs().max() / sb) <= 1e-5
 
 
+def test_hexplane_points_match_reference_graph():
+    """gs4d_hexplane_points (normalize_aabb + cat with the time column, scene/hexplane.py:20-21, 166) and its
+    backward vs the reference's torch graph: bitwise equal both ways (the same float operations)."""
+    from gs4d_train.deformation import normalize_aabb
+    from gs4d_train.kernels import hexplane_points
+    torch.manual_seed(3)
+    N = 10007
+    xyz = (torch.randn(N, 3, device="cuda") * 2).requires_grad_(True)
+    t = torch.rand(N, 1, device="cuda")
+    aabb = torch.tensor([[1.3, 1.7, 2.1], [-1.1, -1.9, -0.7]], device="cuda")
+    x2 = xyz.detach().clone().requires_grad_(True)
+    ref = torch.cat((normalize_aabb(x2, aabb), t), dim=-1)
+    out = hexplane_points(xyz, t, aabb)
+    torch.testing.assert_close(out, ref, rtol=0, atol=0)
+    g = torch.randn(N, 4, device="cuda")
+    ref.backward(g)
+    out.backward(g)
+    torch.testing.assert_close(xyz.grad, x2.grad, rtol=0, atol=0)
+
+
 @pytest.mark.parametrize("P,W,ns", [(100_003, 128, [3, 3, 4, 1, 48]), (777, 64, [2, 16, 5]), (1, 128, [1, 48]),
                                      (0, 128, [3, 4]), (1001, 256, [17, 40]), (40, 128, [33, 64])])
 def test_heads_forward_matches_fp64(P, W, ns):
