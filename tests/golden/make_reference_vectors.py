@@ -6,10 +6,15 @@ the path that exist as runnable reference Python pin the oracle:
                                                    polynomial; the rasterizer adds +0.5 and clamps)
   * utils/graphics_utils.py:38-71 getWorld2View2 / getProjectionMatrix, composed as
     scene/cameras.py:61-66 does  -> viewmatrix / projmatrix / campos handed to the rasterizer.
+  * utils/general_utils.py:70-116 build_scaling_rotation / strip_symmetric, composed as
+    scene/gaussian_model.py:30-34 build_covariance_from_scaling_rotation does -> the 3D covariance the
+    rasterizer's computeCov3D (forward.cu:118-152) forms, for unit quaternions.  These helpers allocate
+    with a hard-coded device="cuda"; the script runs them with that allocation redirected to the CPU
+    (the only change: the arithmetic is the reference's own).
 
 Usage (from the repo root, in the build container where /root/reference exists):
     python tests/golden/make_reference_vectors.py
-Writes tests/golden/ref_sh_vectors.npz and tests/golden/ref_camera_vectors.npz (inputs + outputs).
+Writes tests/golden/ref_sh_vectors.npz, ref_camera_vectors.npz and ref_cov3d_vectors.npz (inputs + outputs).
 """
 import math
 import os
@@ -69,7 +74,30 @@ def main():
     np.savez_compressed(os.path.join(OUT, "ref_camera_vectors.npz"),
                         **{f"{k}_{i}": np.asarray(v) for i, c in enumerate(cams) for k, v in c.items()},
                         n=np.array(len(cams)))
-    print("wrote ref_sh_vectors.npz, ref_camera_vectors.npz")
+    # --- 3D covariance vectors: scene/gaussian_model.py:30-34 -------------------------------------
+    import utils.general_utils as gu  # noqa: E402  (reference code)
+
+    class _CpuTorch:
+        """torch with zeros(..., device=...) allocating on the CPU (general_utils hard-codes "cuda")."""
+
+        def __getattr__(self, name):
+            return getattr(torch, name)
+
+        @staticmethod
+        def zeros(*args, device=None, **kw):
+            return torch.zeros(*args, **kw)
+
+    gu.torch = _CpuTorch()
+    P = 1024
+    scales = np.exp(rng.normal(np.log(0.05), 0.7, (P, 3))).astype(np.float32)
+    rots = rng.normal(0, 1, (P, 4))
+    rots = (rots / np.linalg.norm(rots, axis=1, keepdims=True)).astype(np.float32)
+    cov = {}
+    for tag, mod in (("mod1", 1.0), ("mod07", 0.7)):
+        L = gu.build_scaling_rotation(mod * torch.from_numpy(scales), torch.from_numpy(rots))
+        cov[tag] = gu.strip_symmetric(L @ L.transpose(1, 2)).numpy().astype(np.float32)
+    np.savez_compressed(os.path.join(OUT, "ref_cov3d_vectors.npz"), scales=scales, rotations=rots, **cov)
+    print("wrote ref_sh_vectors.npz, ref_camera_vectors.npz, ref_cov3d_vectors.npz")
 
 
 if __name__ == "__main__":

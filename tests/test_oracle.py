@@ -50,6 +50,24 @@ def test_sh_matches_reference_eval_sh(oracle):
         assert np.array_equal(((cl[:, None] >> np.arange(3)) & 1).astype(bool)[safe], (raw < 0)[safe])
 
 
+def test_cov3d_matches_reference_build_covariance(oracle):
+    """computeCov3D (forward.cu:118-152, the oracle's cov3d_forward) against the reference's own Python
+    covariance (scene/gaussian_model.py:30-34 over utils/general_utils.py build_scaling_rotation /
+    strip_symmetric, run by tests/golden/make_reference_vectors.py) for unit quaternions, scale_modifier 1
+    and 0.7: the same matrix R S S^T R^T, formed in another order (fp32 rounding)."""
+    v = np.load(os.path.join(GOLD, "ref_cov3d_vectors.npz"))
+    P = v["scales"].shape[0]
+    s = make_scene(P, 64, 48, seed=9)
+    s["scales"], s["rotations"] = v["scales"], v["rotations"]
+    for tag, mod in (("mod1", 1.0), ("mod07", 0.7)):
+        s["scale_modifier"] = mod
+        *_, st = _fwd(oracle, s)
+        cov = st.export()["cov3D"]  # every Gaussian passes the near-plane test (z in [2, 10])
+        ref = v[tag]
+        scale = np.abs(ref).max(axis=1, keepdims=True)
+        assert np.all(np.abs(cov - ref) <= 2e-6 * scale), float((np.abs(cov - ref) / scale).max())
+
+
 def test_camera_matches_reference_graphics_utils():
     v = np.load(os.path.join(GOLD, "ref_camera_vectors.npz"))
     for i in range(int(v["n"])):
