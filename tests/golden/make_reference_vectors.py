@@ -11,10 +11,14 @@ the path that exist as runnable reference Python pin the oracle:
     rasterizer's computeCov3D (forward.cu:118-152) forms, for unit quaternions.  These helpers allocate
     with a hard-coded device="cuda"; the script runs them with that allocation redirected to the CPU
     (the only change: the arithmetic is the reference's own).
+  * scene/hexplane.py (loaded from its file and run as-is: HexPlaneField, init_grid_param,
+    grid_sample_wrapper, interpolate_ms_features) -> the deformation field's features and, through
+    autograd, the gradients of the planes and of the points (SURVEY §8f row 2);
+  * scene/regulation.py:22-28 compute_plane_smoothness -> the planes' smoothness regulariser.
 
 Usage (from the repo root, in the build container where /root/reference exists):
     python tests/golden/make_reference_vectors.py
-Writes tests/golden/ref_sh_vectors.npz, ref_camera_vectors.npz and ref_cov3d_vectors.npz (inputs + outputs).
+Writes tests/golden/ref_{sh,camera,cov3d,hexplane}_vectors.npz (inputs + outputs).
 """
 import math
 import os
@@ -97,7 +101,39 @@ def main():
         L = gu.build_scaling_rotation(mod * torch.from_numpy(scales), torch.from_numpy(rots))
         cov[tag] = gu.strip_symmetric(L @ L.transpose(1, 2)).numpy().astype(np.float32)
     np.savez_compressed(os.path.join(OUT, "ref_cov3d_vectors.npz"), scales=scales, rotations=rots, **cov)
-    print("wrote ref_sh_vectors.npz, ref_camera_vectors.npz, ref_cov3d_vectors.npz")
+    # --- HexPlane field and smoothness: scene/hexplane.py, scene/regulation.py -------------------------
+    import importlib.util
+
+    def load(name, rel):
+        spec = importlib.util.spec_from_file_location(name, os.path.join(REF, rel))
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        return mod
+
+    hp = load("ref_hexplane", "scene/hexplane.py")
+    rg = load("ref_regulation", "scene/regulation.py")
+    torch.manual_seed(5)
+    cfg = {"grid_dimensions": 2, "input_coordinate_dim": 4, "output_coordinate_dim": 4, "resolution": [8, 6, 10, 5]}
+    field = hp.HexPlaneField(1.6, cfg, [1, 2])
+    with torch.no_grad():  # move the planes off their initial values (the time planes start at exactly 1)
+        for level in field.grids:
+            for pl in level:
+                pl.add_(0.2 * torch.randn_like(pl))
+    N = 300
+    pts = torch.from_numpy(rng.uniform(-1.9, 1.9, (N, 3)).astype(np.float32)).requires_grad_(True)
+    tms = torch.from_numpy(rng.uniform(-1.2, 1.2, (N, 1)).astype(np.float32))  # beyond [-1, 1]: border clip
+    feat = field(pts, tms)
+    G = torch.from_numpy(rng.normal(0, 1, tuple(feat.shape)).astype(np.float32))
+    (feat * G).sum().backward()
+    hx = dict(pts=pts.detach().numpy(), times=tms.numpy(), G=G.numpy(), feat=feat.detach().numpy(),
+              gpts=pts.grad.numpy(), levels=np.array(len(field.grids)))
+    for li, level in enumerate(field.grids):
+        for pi, pl in enumerate(level):
+            hx[f"plane_{li}_{pi}"] = pl.detach().numpy()
+            hx[f"gplane_{li}_{pi}"] = pl.grad.numpy()
+            hx[f"smooth_{li}_{pi}"] = np.array(float(rg.compute_plane_smoothness(pl.detach())), np.float32)
+    np.savez_compressed(os.path.join(OUT, "ref_hexplane_vectors.npz"), **hx)
+    print("wrote ref_sh_vectors.npz, ref_camera_vectors.npz, ref_cov3d_vectors.npz, ref_hexplane_vectors.npz")
 
 
 if __name__ == "__main__":

@@ -317,3 +317,38 @@ def test_ssim_restatement():
     assert abs(float(ssim(torch.tensor(a), torch.tensor(b))) - ref) < 1e-5
     per_image = ssim(torch.tensor(a), torch.tensor(b), size_average=False)
     assert per_image.shape == (1,)
+
+
+def _ref_hexplane_field(device="cpu"):
+    """Our HexPlaneField (gs4d_train/deformation.py) holding the planes of tests/golden/ref_hexplane_vectors.npz,
+    which the reference's own scene/hexplane.py produced (tests/golden/make_reference_vectors.py)."""
+    import numpy as np
+    import torch
+    from gs4d_train.deformation import HexPlaneField
+    v = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ref_hexplane_vectors.npz"))
+    cfg = {"grid_dimensions": 2, "input_coordinate_dim": 4, "output_coordinate_dim": 4, "resolution": [8, 6, 10, 5]}
+    field = HexPlaneField(1.6, cfg, [1, 2]).to(device)
+    with torch.no_grad():
+        for li, level in enumerate(field.grids):
+            for pi, pl in enumerate(level):
+                pl.copy_(torch.from_numpy(v[f"plane_{li}_{pi}"]))
+    return field, v
+
+
+def test_hexplane_field_matches_reference_module():
+    """The restated HexPlane field (scene/hexplane.py restated in gs4d_train/deformation.py) against vectors
+    made by RUNNING the reference's scene/hexplane.py: features, point gradients and plane gradients bitwise
+    (the same grid_sample graph), and scene/regulation.py's compute_plane_smoothness per plane."""
+    import numpy as np
+    import torch
+    from gs4d_train.gaussians import compute_plane_smoothness
+    field, v = _ref_hexplane_field()
+    pts = torch.from_numpy(v["pts"]).requires_grad_(True)
+    feat = field(pts, torch.from_numpy(v["times"]))
+    np.testing.assert_array_equal(feat.detach().numpy(), v["feat"])
+    (feat * torch.from_numpy(v["G"])).sum().backward()
+    np.testing.assert_array_equal(pts.grad.numpy(), v["gpts"])
+    for li, level in enumerate(field.grids):
+        for pi, pl in enumerate(level):
+            np.testing.assert_array_equal(pl.grad.numpy(), v[f"gplane_{li}_{pi}"])
+            assert float(compute_plane_smoothness(pl.detach())) == float(v[f"smooth_{li}_{pi}"])

@@ -226,6 +226,29 @@ def test_heads_backward_matches_fp64(P, W, ns):
         assert float((out[3 + 2 * i].double() - rb).abs().max() / sb) <= 1e-5
 
 
+def test_hexplane_fused_matches_reference_module():
+    """The fused HexPlane kernels (the field's input points, forward and backward in HIP) against vectors made
+    by RUNNING the reference's scene/hexplane.py (tests/golden/ref_hexplane_vectors.npz; F = 4, two levels,
+    points beyond the bounds and times beyond [-1, 1]: border clipping): features to 1e-5 relative, the point
+    and plane gradients to 1e-4 of each tensor's maximum (summation order)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from test_harness_cpu import _ref_hexplane_field
+    field, v = _ref_hexplane_field("cuda")
+    field.fused = True
+    pts = torch.from_numpy(v["pts"]).cuda().requires_grad_(True)
+    feat = field(pts, torch.from_numpy(v["times"]).cuda())
+    ref = torch.from_numpy(v["feat"]).cuda()
+    assert float((feat.detach() - ref).abs().max()) <= 1e-5 * float(ref.abs().max())
+    (feat * torch.from_numpy(v["G"]).cuda()).sum().backward()
+    pairs = [(pts.grad, v["gpts"])] + [(pl.grad, v[f"gplane_{li}_{pi}"]) for li, level in enumerate(field.grids)
+                                       for pi, pl in enumerate(level)]
+    for got, exp in pairs:
+        exp = torch.from_numpy(exp).cuda()
+        assert float((got - exp).abs().max()) <= 1e-4 * max(float(exp.abs().max()), 1e-30)
+
+
 def test_hexplane_points_match_reference_graph():
     """gs4d_hexplane_points (normalize_aabb + cat with the time column, scene/hexplane.py:20-21, 166) and its
     backward vs the reference's torch graph: bitwise equal both ways (the same float operations)."""
