@@ -14,11 +14,13 @@ the path that exist as runnable reference Python pin the oracle:
   * scene/hexplane.py (loaded from its file and run as-is: HexPlaneField, init_grid_param,
     grid_sample_wrapper, interpolate_ms_features) -> the deformation field's features and, through
     autograd, the gradients of the planes and of the points (SURVEY §8f row 2);
-  * scene/regulation.py:22-28 compute_plane_smoothness -> the planes' smoothness regulariser.
+  * scene/regulation.py:22-28 compute_plane_smoothness -> the planes' smoothness regulariser;
+  * utils/general_utils.py:35-68 get_expon_lr_func -> the learning-rate schedules GaussianModel builds
+    (scene/gaussian_model.py training_setup) with the DyNeRF / default hyper-parameters.
 
 Usage (from the repo root, in the build container where /root/reference exists):
     python tests/golden/make_reference_vectors.py
-Writes tests/golden/ref_{sh,camera,cov3d,hexplane}_vectors.npz (inputs + outputs).
+Writes tests/golden/ref_{sh,camera,cov3d,hexplane,lr}_vectors.npz (inputs + outputs).
 """
 import math
 import os
@@ -133,7 +135,22 @@ def main():
             hx[f"gplane_{li}_{pi}"] = pl.grad.numpy()
             hx[f"smooth_{li}_{pi}"] = np.array(float(rg.compute_plane_smoothness(pl.detach())), np.float32)
     np.savez_compressed(os.path.join(OUT, "ref_hexplane_vectors.npz"), **hx)
-    print("wrote ref_sh_vectors.npz, ref_camera_vectors.npz, ref_cov3d_vectors.npz, ref_hexplane_vectors.npz")
+
+    # --- learning-rate schedules: utils/general_utils.py:35-68 -------------------------------------------
+    steps = np.array([-1, 0, 1, 2, 7, 100, 499, 500, 1000, 3000, 3001, 9999, 14000, 20000, 30000, 10 ** 6])
+    lr = dict(steps=steps)
+    # (lr_init, lr_final, lr_delay_mult, max_steps): position / deformation / grid of arguments/__init__.py
+    # defaults and arguments/dynerf/default.py (spatial_lr_scale folded into the first two as the model does)
+    for i, (a0, a1, dm, ms) in enumerate([(0.00016 * 5.0, 0.0000016 * 5.0, 0.01, 20000),
+                                          (0.00016 * 5.0, 0.000016 * 5.0, 0.01, 20000),
+                                          (0.0016 * 5.0, 0.00016 * 5.0, 0.01, 20000),
+                                          (0.0016, 0.000016, 0.01, 14000),
+                                          (1e-3, 1e-3, 1.0, 1000)]):
+        f = gu.get_expon_lr_func(a0, a1, lr_delay_mult=dm, max_steps=ms)
+        lr[f"args_{i}"] = np.array([a0, a1, dm, ms], np.float64)
+        lr[f"lr_{i}"] = np.array([f(int(k)) for k in steps], np.float64)
+    np.savez_compressed(os.path.join(OUT, "ref_lr_vectors.npz"), **lr)
+    print("wrote ref_{sh,camera,cov3d,hexplane,lr}_vectors.npz")
 
 
 if __name__ == "__main__":

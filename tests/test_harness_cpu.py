@@ -352,3 +352,19 @@ def test_hexplane_field_matches_reference_module():
         for pi, pl in enumerate(level):
             np.testing.assert_array_equal(pl.grad.numpy(), v[f"gplane_{li}_{pi}"])
             assert float(compute_plane_smoothness(pl.detach())) == float(v[f"smooth_{li}_{pi}"])
+
+
+def test_lr_schedule_matches_reference():
+    """gs4d_train.gaussians.get_expon_lr_func against utils/general_utils.py:35-68 run by
+    tests/golden/make_reference_vectors.py: the same float64 values at every step (warm-up, decay, clamp)."""
+    import numpy as np
+    from gs4d_train.gaussians import get_expon_lr_func
+    v = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ref_lr_vectors.npz"))
+    i = 0
+    while f"lr_{i}" in v:
+        a0, a1, dm, ms = v[f"args_{i}"]
+        f = get_expon_lr_func(float(a0), float(a1), lr_delay_mult=float(dm), max_steps=int(ms))
+        got = np.array([f(int(k)) for k in v["steps"]], np.float64)
+        np.testing.assert_array_equal(got, v[f"lr_{i}"])
+        i += 1
+    assert i == 5
