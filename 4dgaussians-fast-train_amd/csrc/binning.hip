@@ -14,9 +14,13 @@
 //      the splat sizes) keeps only the (tile, splat) pairs the splat reaches (half_reach,
 //      gs4d_internal.h) and compacts them in candidate order (so a Gaussian's instances are
 //      consecutive: the backward reduces its gradient records by segment);
-//   3. a STABLE LSD radix sort of the emitted instances by tile id alone (ceil(msb(T)/8) passes over
-//      u32 keys; digit histograms built by the emission, no atomics on contended counters): each
-//      tile's run is left in Gaussian-id order; tile ranges follow from the sorted keys;
+//   3. a counting sort of the emitted instances by tile id alone (tile_count / tile_scan /
+//      tile_scatter: per-chunk tile counts in LDS, their (tile, chunk) exclusive offsets, an LDS
+//      fetch-add per instance; the tile ranges fall out of the offsets).  The order inside a tile's
+//      run is left arbitrary: step 4 sorts every run by a key unique in the tile, so the result is the
+//      same whatever it was.  Tile grids beyond kCountMaxT tiles, or more chunks than the column scan
+//      holds, take a STABLE LSD radix sort by tile id instead (ceil(msb(T)/8) passes over u32 keys,
+//      digit histograms built by the emission) and tile ranges from the sorted keys;
 //   4. tile_sort: each tile's run is sorted by the 64-bit key (depth bits, Gaussian id) -- exactly the
 //      reference's within-tile order (the key is unique inside a tile).  Runs of up to kWaveSortMax
 //      (256) are sorted by the render forward itself, in registers, before it blends them
@@ -27,6 +31,8 @@
 // 32-bit status+count word per chunk, agent-scope relaxed atomics) and sum the lower chunks' words
 // directly (radix_sort.h).
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 
 #include "radix_sort.h"
 
@@ -60,6 +66,25 @@ size_t max_emit_chunks(int P, int T) {
     // L < 2^30 is enforced by the caller
     const size_t bound = ((size_t)P * (size_t)T + kEmitChunk - 1) / kEmitChunk;
     return std::min<size_t>(bound, ((size_t)1 << 30) / kEmitChunk) + 1;
+}
+
+// Counting binning (see the header): chunks of kCountThreads * ITEMS emission slots.
+constexpr int kCountThreads = 1024;
+constexpr int kCountMaxT = 16384;  // LDS bins of one chunk (64 KiB)
+constexpr int kColWaves = 16, kColPer = 32;  // column scan: 16 waves x 32 chunks per lane
+int count_items(int L, int T) {
+    // GS4D_BINNING=radix: the radix-sort binning everywhere (A/B diagnostics; read once per process,
+    // so a forward and its backward always agree on the buffer layout)
+    static const char *force = getenv("GS4D_BINNING");
+    if (force && strcmp(force, "radix") == 0) return 0;
+    if (T > kCountMaxT || L <= 0) return 0;
+    for (int items = 8; items <= 16; items *= 2)
+        if (sort_nblk(L, kCountThreads * items) <= kColWaves * kColPer) return items;
+    return 0;
+}
+size_t tile_hist_words(int L, int T) {
+    const int items = count_items(L, T);
+    return items ? (size_t)sort_nblk(L, kCountThreads * items) * (size_t)T : 0;
 }
 
 // Exclusive 256-thread workgroup scan: returns this thread's exclusive prefix inside the workgroup
@@ -291,6 +316,137 @@ __global__ void tile_ranges_kernel(const uint32_t *__restrict__ keys, const uint
         }
     }
     if (idx == L - 1) ranges[cur].y = L;
+}
+
+// ---- Counting binning ---------------------------------------------------------------------------
+// tile_count: chunk c's tile histogram, hist[c][t] (chunks past L' exit at once).
+template <int ITEMS>
+__global__ __launch_bounds__(kCountThreads) void tile_count_kernel(const uint32_t *__restrict__ keys,
+                                                                   const uint32_t *__restrict__ n_dev, int T,
+                                                                   uint32_t *__restrict__ hist) {
+    extern __shared__ uint32_t s_bin[];
+    const int n = count_of(0, n_dev), tid = threadIdx.x;
+    const size_t c0 = (size_t)blockIdx.x * (kCountThreads * ITEMS);
+    if (c0 >= (size_t)n) return;
+    uint32_t key[ITEMS];
+#pragma unroll
+    for (int r = 0; r < ITEMS; r++) {
+        const size_t i = c0 + (size_t)r * kCountThreads + tid;
+        key[r] = i < (size_t)n ? keys[i] : ~0u;
+    }
+    for (int t = tid; t < T; t += kCountThreads) s_bin[t] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < ITEMS; r++)
+        if (key[r] != ~0u) atomicAdd(&s_bin[key[r]], 1u);
+    __syncthreads();
+    uint32_t *h = hist + (size_t)blockIdx.x * T;
+    for (int t = tid; t < T; t += kCountThreads) h[t] = s_bin[t];
+}
+
+// tile_scan: workgroup g owns tiles [64 g, 64 g + 64), lane l tile 64 g + l; wave w the chunks
+// [w per, (w + 1) per).  Rewrites hist[c][t] in place as the exclusive offset of (t, c) in
+// tile-major order -- the global start of chunk c's share of tile t -- and writes ranges[t]
+// (rasterizer_impl.cu:116-138's result; empty tiles (0, 0)).  The tile groups' totals are chained
+// by the published-count prefix of radix_sort.h (look: zeroed words, one per group).
+__global__ __launch_bounds__(kCountThreads) void tile_scan_kernel(uint32_t *__restrict__ hist,
+                                                                  const uint32_t *__restrict__ n_dev, int T, int chunk,
+                                                                  uint2 *__restrict__ ranges,
+                                                                  uint32_t *__restrict__ look, uint32_t *__restrict__ err) {
+    __shared__ uint32_t s_col[kColWaves][64];
+    __shared__ uint32_t s_base[64];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int n = count_of(0, n_dev);
+    const int nc = (n + chunk - 1) / chunk;
+    const int t = blockIdx.x * 64 + lane;
+    const bool tv = t < T;
+    const int per = (nc + kColWaves - 1) / kColWaves;
+    const int cb = w * per;
+    uint32_t v[kColPer];
+#pragma unroll
+    for (int k = 0; k < kColPer; k++) {
+        const int c = cb + k;
+        v[k] = (k < per && c < nc && tv) ? hist[(size_t)c * T + t] : 0u;
+    }
+    uint32_t run = 0;
+#pragma unroll
+    for (int k = 0; k < kColPer; k++) {
+        const uint32_t x = v[k];
+        v[k] = run;
+        run += x;
+    }
+    s_col[w][lane] = run;
+    __syncthreads();
+    uint32_t before = 0, tot = 0;
+#pragma unroll
+    for (int q = 0; q < kColWaves; q++) {
+        const uint32_t x = s_col[q][lane];
+        before += q < w ? x : 0u;
+        tot += x;
+    }
+    if (w == 0) {
+        uint32_t x = tot;  // inclusive scan of the group's tile totals
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(x, off);
+            if (lane >= off) x += y;
+        }
+        const uint32_t gsum = __shfl(x, 63);
+        if (lane == 0) store_word(look + blockIdx.x, kAgg | gsum);
+        uint32_t lower = sum_published(look, 1, (int)blockIdx.x, lane, 64, err);
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) lower += __shfl_xor(lower, off);
+        const uint32_t base = lower + x - tot;
+        s_base[lane] = base;
+        if (tv) ranges[t] = tot ? make_uint2(base, base + tot) : make_uint2(0u, 0u);
+    }
+    __syncthreads();
+    const uint32_t base = s_base[lane] + before;
+#pragma unroll
+    for (int k = 0; k < kColPer; k++) {
+        const int c = cb + k;
+        if (k < per && c < nc && tv) hist[(size_t)c * T + t] = base + v[k];
+    }
+}
+
+// tile_scatter: chunk c's offsets into LDS, one fetch-add per instance places its emission slot in
+// its tile's run (the order inside the run is the arbitrary order of the LDS atomics: see the header).
+template <int ITEMS>
+__global__ __launch_bounds__(kCountThreads) void tile_scatter_kernel(const uint32_t *__restrict__ keys,
+                                                                     const uint32_t *__restrict__ n_dev, int T,
+                                                                     const uint32_t *__restrict__ offs,
+                                                                     uint32_t *__restrict__ upos) {
+    extern __shared__ uint32_t s_off[];
+    const int n = count_of(0, n_dev), tid = threadIdx.x;
+    const size_t c0 = (size_t)blockIdx.x * (kCountThreads * ITEMS);
+    if (c0 >= (size_t)n) return;
+    uint32_t key[ITEMS];
+#pragma unroll
+    for (int r = 0; r < ITEMS; r++) {
+        const size_t i = c0 + (size_t)r * kCountThreads + tid;
+        key[r] = i < (size_t)n ? keys[i] : ~0u;
+    }
+    const uint32_t *h = offs + (size_t)blockIdx.x * T;
+    for (int t = tid; t < T; t += kCountThreads) s_off[t] = h[t];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < ITEMS; r++)
+        if (key[r] != ~0u) upos[atomicAdd(&s_off[key[r]], 1u)] = (uint32_t)(c0 + (size_t)r * kCountThreads + tid);
+}
+
+template <int ITEMS>
+static void launch_counting(const BinningState &b, int L, int T, ImageState img, uint32_t *look, uint32_t *err,
+                            hipStream_t s) {
+    constexpr int C = kCountThreads * ITEMS;
+    const int nblk = sort_nblk(L, C);
+    const uint32_t *n_dev = b.scratch;
+    const size_t lds = 4 * (size_t)T;
+    hipLaunchKernelGGL(tile_count_kernel<ITEMS>, dim3(nblk), dim3(kCountThreads), lds, s, b.keys[0], n_dev, T,
+                       b.tile_hist);
+    hipLaunchKernelGGL(tile_scan_kernel, dim3((T + 63) / 64), dim3(kCountThreads), 0, s, b.tile_hist, n_dev, T, C,
+                       img.ranges, look, err);
+    hipLaunchKernelGGL(tile_scatter_kernel<ITEMS>, dim3(nblk), dim3(kCountThreads), lds, s, b.keys[0], n_dev, T,
+                       b.tile_hist, b.upos);
 }
 
 // ---- K4: per-tile sort by (depth bits, Gaussian id) -------------------------------------------------
@@ -558,17 +714,28 @@ hipError_t launch_binning(const Args &a, GeomState g, const int *radii, BinningS
         hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, s, img.ranges, T, img.order);
         return hipGetLastError();
     }
-    const int npass = (b.key_bits + 7) / 8;
     uint32_t *look = b.scratch + bin_look_off();
-    const int nlook = npass * 256 * sort_nblk(L, kSortThreads * kItemsL);
-    hipLaunchKernelGGL(emit_instances_kernel, dim3((unsigned)nchunk_emit(L)), dim3(256), 0, s, a, g, radii, L, npass,
-                       b.keys[0], b.gid_by_e, b.scratch, img.ranges, T, look, nlook);
-    const uint32_t *n_dev = b.scratch;  // L' <= L reached instances
-    uint32_t *keys[2] = {b.keys[0], b.keys[1]};
-    uint32_t *vals[2] = {b.vals[0], b.vals[1]};
-    onesweep_sort<kSortThreads, kItemsL>(keys, vals, L, n_dev, b.key_bits, g.zero + geom_hist_off(a.P), look,
-                                         g.emit_chain + 1, s);
-    hipLaunchKernelGGL(tile_ranges_kernel, dim3((L + 255) / 256), dim3(256), 0, s, b.sorted_keys, n_dev, img.ranges);
+    uint32_t *err = g.emit_chain + 1;
+    if (b.count_items) {
+        // counting binning: no digit histograms, the tile scan writes every range and uses (T + 63) / 64
+        // look-back words
+        hipLaunchKernelGGL(emit_instances_kernel, dim3((unsigned)nchunk_emit(L)), dim3(256), 0, s, a, g, radii, L, 0,
+                           b.keys[0], b.gid_by_e, b.scratch, img.ranges, 0, look, (T + 63) / 64);
+        if (b.count_items == 8) launch_counting<8>(b, L, T, img, look, err, s);
+        else launch_counting<16>(b, L, T, img, look, err, s);
+    } else {
+        const int npass = (b.key_bits + 7) / 8;
+        const int nlook = npass * 256 * sort_nblk(L, kSortThreads * kItemsL);
+        hipLaunchKernelGGL(emit_instances_kernel, dim3((unsigned)nchunk_emit(L)), dim3(256), 0, s, a, g, radii, L,
+                           npass, b.keys[0], b.gid_by_e, b.scratch, img.ranges, T, look, nlook);
+        const uint32_t *n_dev = b.scratch;  // L' <= L reached instances
+        uint32_t *keys[2] = {b.keys[0], b.keys[1]};
+        uint32_t *vals[2] = {b.vals[0], b.vals[1]};
+        onesweep_sort<kSortThreads, kItemsL>(keys, vals, L, n_dev, b.key_bits, g.zero + geom_hist_off(a.P), look, err,
+                                             s);
+        hipLaunchKernelGGL(tile_ranges_kernel, dim3((L + 255) / 256), dim3(256), 0, s, b.sorted_keys, n_dev,
+                           img.ranges);
+    }
     hipLaunchKernelGGL(tile_sort_kernel, dim3(T + 1), dim3(256), 0, s, img.ranges, T, img.order, b.gid_by_e, g.depths,
                        b.upos, b.tmp_hi, b.tmp_lo);
     return hipGetLastError();

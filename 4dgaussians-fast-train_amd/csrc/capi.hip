@@ -143,6 +143,8 @@ BinningState BinningState::carve(char *base, int L, int T) {
     b.sorted_keys = b.keys[final_buf];
     b.tmp_hi = b.keys[final_buf ^ 1];
     b.tmp_lo = b.vals[final_buf ^ 1];
+    b.count_items = gs4d::count_items(L, T);
+    b.tile_hist = b.count_items ? (uint32_t *)gs4d::carve(p, 4 * tile_hist_words(L, T)) : nullptr;
     b.scratch = (uint32_t *)gs4d::carve(p, 4 * binning_zero_words(L, T));
     return b;
 }

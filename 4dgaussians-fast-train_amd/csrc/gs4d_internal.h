@@ -70,8 +70,11 @@ struct BinningState {
                             //     gradient record goes to slot upos[i]
     uint32_t *sorted_keys;  // = the keys buffer holding the sorted tile ids
     uint32_t *tmp_hi, *tmp_lo;  // = the other ping-pong pair: long-tile sort keys
+    uint32_t *tile_hist;    // counting binning: chunks x T per-chunk tile counts, then their (tile, chunk)
+                            //     exclusive offsets (binning.hip); nullptr when the radix sort bins
     uint32_t *scratch;      // binning_zero_words(L, T), zeroed by one memset; word 0 = L' (emitted instances)
     int key_bits;           // msb(T) (rasterizer_impl.cu:301)
+    int count_items;        // keys per lane of the counting binning (8 or 16), 0 = radix-sort binning
     static size_t required(int L, int T);
     static BinningState carve(char *base, int L, int T);
 };
@@ -97,6 +100,8 @@ __device__ __forceinline__ V3 load_v3(const float *__restrict__ p) { return v3(p
 
 size_t geom_zero_words(int P);
 size_t binning_zero_words(int L, int T);
+int count_items(int L, int T);          // binning.hip: the counting binning's keys per lane, 0 = radix sort
+size_t tile_hist_words(int L, int T);   // binning.hip: chunks x T (counting binning)
 
 // ---- exact tile culling ------------------------------------------------------------------------
 // The reference bins a splat into every tile of its 3-sigma rectangle (forward.cu:232-237), but a

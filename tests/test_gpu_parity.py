@@ -271,11 +271,14 @@ def _image_buffer_views(ib, W, H):
     return ranges, order
 
 
-@pytest.mark.parametrize("W,H", [(1352, 1014), (2304, 1296)])
+@pytest.mark.parametrize("W,H", [(1352, 1014), (2304, 1296), (2400, 2000)])
 def test_tile_order_longest_first(C, oracle, dev, W, H):
     """The blend kernels take tiles longest run first (tile_order_kernel): the order is a permutation
     of the tiles with non-increasing run lengths (capped at 1023).  2304x1296 has 11,664 tiles, more than
-    the order kernel keeps in registers (8192), and is checked against the oracle as well."""
+    the order kernel keeps in registers (8192), and is checked against the oracle as well; 2400x2000 has
+    18,750, more than the counting binning's LDS bins (binning.hip kCountMaxT): the radix-sort binning.
+    The tile ranges partition the emitted instances in tile order, empty tiles (0, 0) as
+    identifyTileRanges leaves them (rasterizer_impl.cu:116-138)."""
     s = make_scene(100_000 if W == 1352 else 3000, W, H, seed=25)
     if W == 1352:
         fwd = c_forward(C, s, to_dev(s, dev))
@@ -286,6 +289,11 @@ def test_tile_order_longest_first(C, oracle, dev, W, H):
     assert np.array_equal(np.sort(order), np.arange(T))
     lens = np.minimum(ranges[order, 1] - ranges[order, 0], 1023)
     assert np.all(np.diff(lens.astype(np.int64)) <= 0)
+    ne = ranges[:, 1] > ranges[:, 0]
+    assert np.all(ranges[~ne] == 0)
+    r = ranges[ne].astype(np.int64)
+    assert r[0, 0] == 0 and np.array_equal(r[1:, 0], r[:-1, 1])
+    assert r[-1, 1] <= fwd[0]  # L' <= num_rendered
 
 
 def test_view_matrix_layouts_agree(C, dev):
