@@ -76,9 +76,11 @@ int count_items(int L, int T) {
     // GS4D_BINNING=radix: the radix-sort binning everywhere (A/B diagnostics; read once per process,
     // so a forward and its backward always agree on the buffer layout)
     static const char *force = getenv("GS4D_BINNING");
+    static const char *min_items = getenv("GS4D_COUNT_MIN_ITEMS");  // A/B diagnostics: 4, 8 (default), 16
     if (force && strcmp(force, "radix") == 0) return 0;
+    if (min_items && atoi(min_items) != 4 && atoi(min_items) != 8 && atoi(min_items) != 16) return 0;
     if (T > kCountMaxT || L <= 0) return 0;
-    for (int items = 8; items <= 16; items *= 2)
+    for (int items = min_items ? atoi(min_items) : 8; items <= 16; items *= 2)
         if (sort_nblk(L, kCountThreads * items) <= kColWaves * kColPer) return items;
     return 0;
 }
@@ -193,7 +195,10 @@ __global__ __launch_bounds__(256) void emit_instances_kernel(Args a, GeomState g
     const uint32_t c1 = min((uint32_t)L, c0 + kEmitChunk);
     const int V = (int)(g.zero[kZeroV]);
     const int rlo = (int)g.first_vis[b];
-    const int nr = min(V - rlo, kEmitChunk + 1);  // visible Gaussians starting at or after c1 are ignored
+    // the chunk's Gaussians: first_vis[b] .. first_vis[b + 1] (the owner of candidate c1); the last
+    // chunk's run to V.  Visible Gaussians starting at or after c1 are ignored.
+    const int rhi = c1 < (uint32_t)L ? (int)g.first_vis[b + 1] + 1 : V;
+    const int nr = min(rhi - rlo, kEmitChunk + 1);
     for (int i = tid; i < kEmitChunk; i += 256) s_own[i] = 0;
     for (int i = tid; i < kMaxPasses * 256; i += 256) (&s_hist[0][0])[i] = 0;
     __syncthreads();
@@ -721,7 +726,8 @@ hipError_t launch_binning(const Args &a, GeomState g, const int *radii, BinningS
         // look-back words
         hipLaunchKernelGGL(emit_instances_kernel, dim3((unsigned)nchunk_emit(L)), dim3(256), 0, s, a, g, radii, L, 0,
                            b.keys[0], b.gid_by_e, b.scratch, img.ranges, 0, look, (T + 63) / 64);
-        if (b.count_items == 8) launch_counting<8>(b, L, T, img, look, err, s);
+        if (b.count_items == 4) launch_counting<4>(b, L, T, img, look, err, s);
+        else if (b.count_items == 8) launch_counting<8>(b, L, T, img, look, err, s);
         else launch_counting<16>(b, L, T, img, look, err, s);
     } else {
         const int npass = (b.key_bits + 7) / 8;

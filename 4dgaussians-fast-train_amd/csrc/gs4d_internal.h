@@ -74,7 +74,7 @@ struct BinningState {
                             //     exclusive offsets (binning.hip); nullptr when the radix sort bins
     uint32_t *scratch;      // binning_zero_words(L, T), zeroed by one memset; word 0 = L' (emitted instances)
     int key_bits;           // msb(T) (rasterizer_impl.cu:301)
-    int count_items;        // keys per lane of the counting binning (8 or 16), 0 = radix-sort binning
+    int count_items;        // keys per lane of the counting binning (4, 8 or 16), 0 = radix-sort binning
     static size_t required(int L, int T);
     static BinningState carve(char *base, int L, int T);
 };
