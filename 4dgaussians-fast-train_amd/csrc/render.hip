@@ -133,6 +133,9 @@ __device__ __forceinline__ RawSplat read_raw_lds(const RawLDS &r, int lane, bool
 
 // Falloff of one splat at a pixel pair: exponent (base 2) and G = 2^power2.  Forward and backward use
 // this one sequence, so they take identical blend decisions.
+// alpha = min(0.99, o G) caps nothing for opacities at or below kCapFree: G = 2^power <= 1 wherever the
+// power test passes (up to an ulp), so o G <= 0.98 (1 + ulp) < 0.99.
+constexpr float kCapFree = 0.98f;
 struct Falloff {
     f2 dy, pw, G, alpha;
 };
@@ -472,7 +475,7 @@ struct BwdPixels {
 //   ALL: the splat lies below every pixel's n_contrib (the contributor test passes; pixels outside
 //        the image have T = dL/dpix = 0 and contribute exact zeros).
 //   GEN: the general splat: `chk` = its conic is not positive definite (power > 0 skips, forward.cu:341),
-//        and the 0.99 cap applies; without GEN the opacity is <= 0.9, so o * G never reaches the cap.
+//        and the 0.99 cap applies; without GEN the opacity is <= kCapFree, so o * G never reaches the cap.
 template <bool ALL, bool GEN>
 __device__ __forceinline__ void half_step(f2 &T, f2 &A, const f2 dp0, const f2 dp1, const f2 dp2,
                                           const f2 Y2, const f2 C2, const f2 O2, const f2 R2, const f2 G2,
@@ -634,7 +637,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
         nxt.geo.y -= yc;                    // my - yc, as the forward stages it
         // per-splat wave masks (the staged zero splats past n are neither)
         const uint64_t nonpd = ballot(lane < n && !conic_pd(nxt.geo, nxt.opc));
-        const uint64_t hiop = ballot(nxt.opc.y > 0.9f);
+        const uint64_t hiop = ballot(nxt.opc.y > kCapFree);
         __syncthreads();
         s_sp[lane].geo = nxt.geo;
         s_sp[lane].opc = nxt.opc;
