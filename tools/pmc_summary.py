@@ -19,7 +19,8 @@ KEYS = {"render_backward_kernel": "render_backward", "render_forward_kernel": "r
         "contrib_segments_kernel": "contrib_segments", "gaussian_backward_kernel": "gaussian_backward",
         "visible_scan_kernel": "visible_scan", "tile_ranges_kernel": "tile_ranges",
         "tile_sort_kernel": "tile_sort", "tile_order_kernel": "tile_order",
-        "contrib_finish_kernel": "contrib_finish"}
+        "contrib_finish_kernel": "contrib_finish", "tile_count_kernel": "tile_count",
+        "tile_scan_kernel": "tile_scan", "tile_scatter_kernel": "tile_scatter"}
 
 
 def short(name):
