@@ -106,48 +106,46 @@ size_t tile_hist_words(int L, int T);   // binning.hip: chunks x T (counting bin
 // ---- exact tile culling ------------------------------------------------------------------------
 // The reference bins a splat into every tile of its 3-sigma rectangle (forward.cu:232-237), but a
 // pixel only blends a splat when alpha = min(0.99, o * exp(power)) >= 1/255 (forward.cu:346-348).
-// rect_reached() is false only when NO pixel centre of the rectangle [x0,x1] x [y0,y1] can reach that
-// threshold: the minimum of the quadratic form q = a dx^2 + 2b dx dy + c dy^2 (power = -q/2) over
-// the rectangle is taken in closed form (convex q: interior minimum or clamped stationary point on
-// an edge) and compared with a 0.1% margin.  Dropping such (tile, splat) pairs -- or such half tiles
-// in the blend kernels -- changes no output bit: the reference skips every one of their pixel
-// evaluations.  A conic that is not positive definite is never culled.
-__device__ __forceinline__ bool rect_reached(float mx, float my, float4 co, int x0, int x1, int y0, int y1) {
-    // evaluated identically wherever it is inlined (emission and blend passes)
-#pragma clang fp contract(off)
-    const float a = co.x, b = co.y, c = co.z, o = co.w;
-    if (!(a > 0.f && c > 0.f && a * c - b * b > 0.f)) return true;
-    // d = mean - pixel centre over the rectangle
-    const float X0 = mx - (float)x1, X1 = mx - (float)x0;
-    const float Y0 = my - (float)y1, Y1 = my - (float)y0;
-    float q = 0.f;
-    if (!(X0 <= 0.f && X1 >= 0.f && Y0 <= 0.f && Y1 >= 0.f)) {
-        const float ia = 1.f / a, ic = 1.f / c;
-        float y = fminf(fmaxf(-b * X0 * ic, Y0), Y1);
-        float q0 = a * X0 * X0 + 2.f * b * X0 * y + c * y * y;
-        y = fminf(fmaxf(-b * X1 * ic, Y0), Y1);
-        float q1 = a * X1 * X1 + 2.f * b * X1 * y + c * y * y;
-        float x = fminf(fmaxf(-b * Y0 * ia, X0), X1);
-        float q2 = a * x * x + 2.f * b * x * Y0 + c * Y0 * Y0;
-        x = fminf(fmaxf(-b * Y1 * ia, X0), X1);
-        float q3 = a * x * x + 2.f * b * x * Y1 + c * Y1 * Y1;
-        q = fminf(fminf(q0, q1), fminf(q2, q3));
-    }
-    return !(o * __expf(-0.5f * q) * 1.001f < 1.0f / 255.0f);
+// A half tile is reached when SOME pixel centre of its rectangle [x0,x1] x [y0,y1] can reach the
+// threshold: the minimum of the quadratic form q = a dx^2 + 2b dx dy + c dy^2 (power = -q/2) over the
+// rectangle (d = mean - pixel centre) is taken in closed form -- 0 when the mean lies inside, else the
+// least of the four edges' minima (convex q: the edge's stationary point, clamped to the edge) -- and
+// compared with q_thr = 2 ln(255 * 1.001 o), i.e. o exp(-q/2) >= (1/255) / 1.001: a 0.1% margin that
+// dwarfs the rounding of this evaluation (fast reciprocals and log, fused multiply-adds).  Dropping
+// an unreached (tile, splat) pair -- or half tile in the blend kernels -- changes no output bit: the
+// reference skips every one of their pixel evaluations.  A conic that is not positive definite is
+// never culled.
+__device__ __forceinline__ float edge_q(float a, float b2, float c, float X, float y) {
+    return __builtin_fmaf(X, __builtin_fmaf(b2, y, a * X), c * y * y);  // a X^2 + 2b X y + c y^2
 }
+__device__ __forceinline__ float clampf(float v, float lo, float hi) { return fminf(fmaxf(v, lo), hi); }
 // Rows [8h, 8h+7] of a tile are blended by the pixel pair h of every lane (render.hip), so the
 // emission records, per instance, which half tiles the splat reaches (bit h; pixel centres inside the
 // image) and the blend kernels skip a half it cannot reach.  An instance reaching neither half is
 // not emitted.
 __device__ __forceinline__ uint32_t half_reach(float mx, float my, float4 co, int tx, int ty, int W, int H) {
-    const int x0 = tx * kBlockX, x1 = min(x0 + kBlockX - 1, W - 1);
+    const float a = co.x, b = co.y, c = co.z, o = co.w;
+    const int px0 = tx * kBlockX, px1 = min(px0 + kBlockX - 1, W - 1);
+    const int y00 = ty * kBlockY, y01 = min(y00 + 7, H - 1), y10 = y00 + 8, y11 = min(y00 + 15, H - 1);
+    const uint32_t exists = 1u | (y10 <= y11 ? 2u : 0u);
+    if (!(a > 0.f && c > 0.f && a * c - b * b > 0.f)) return exists;
+    const float thr = (2.f * 0.693147181f) * __log2f(o * (255.f * 1.001f));  // -inf / NaN: never reached
+    const float b2 = 2.f * b, ia = __builtin_amdgcn_rcpf(a), ic = __builtin_amdgcn_rcpf(c);
+    const float X0 = mx - (float)px1, X1 = mx - (float)px0;
+    const float ys0 = -b * X0 * ic, ys1 = -b * X1 * ic;  // stationary y of the x edges (unclamped)
+    const bool xin = X0 <= 0.f && X1 >= 0.f;
     uint32_t r = 0;
 #pragma unroll
     for (int h = 0; h < 2; h++) {
-        const int y0 = ty * kBlockY + 8 * h, y1 = min(y0 + 7, H - 1);
-        if (y0 <= y1 && rect_reached(mx, my, co, x0, x1, y0, y1)) r |= 1u << h;
+        const float Y0 = my - (float)(h ? y11 : y01), Y1 = my - (float)(h ? y10 : y00);
+        const float q0 = edge_q(a, b2, c, X0, clampf(ys0, Y0, Y1));
+        const float q1 = edge_q(a, b2, c, X1, clampf(ys1, Y0, Y1));
+        const float q2 = edge_q(c, b2, a, Y0, clampf(-b * Y0 * ia, X0, X1));  // q symmetric in (x, a) <-> (y, c)
+        const float q3 = edge_q(c, b2, a, Y1, clampf(-b * Y1 * ia, X0, X1));
+        const float qmin = (xin && Y0 <= 0.f && Y1 >= 0.f) ? 0.f : fminf(fminf(q0, q1), fminf(q2, q3));
+        if (qmin <= thr) r |= 1u << h;
     }
-    return r;
+    return r & exists;
 }
 // Tile runs of up to kWaveSortMax instances are depth-sorted by the render forward (render.hip), longer
 // ones by tile_sort_kernel (binning.hip) before it.
