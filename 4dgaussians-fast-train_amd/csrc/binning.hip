@@ -186,7 +186,7 @@ __global__ __launch_bounds__(256) void emit_instances_kernel(Args a, GeomState g
     for (int i = blockIdx.x * 256 + threadIdx.x; i < nlook; i += gridDim.x * 256) look[i] = 0u;
     __shared__ uint32_t s_own[kEmitChunk];
     __shared__ uint32_t s_off[kEmitChunk + 2];
-    __shared__ uint32_t s_n[kEmitChunk + 1];
+    __shared__ uint32_t s_n[kEmitChunk + 1];  // kept candidates before each candidate of the chunk
     __shared__ uint32_t s_hist[kMaxPasses][256];
     __shared__ uint32_t s_w[4], s_tmp[4];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -205,7 +205,6 @@ __global__ __launch_bounds__(256) void emit_instances_kernel(Args a, GeomState g
     for (int i = tid; i < nr; i += 256) {
         const uint32_t st = g.cand_off[rlo + i];
         s_off[i] = st;
-        s_n[i] = 0;
         if (st > c0 && st < c1) s_own[st - c0] = (uint32_t)i;
     }
     if (tid == 0) s_off[nr] = g.cand_off[rlo + nr];
@@ -256,13 +255,18 @@ __global__ __launch_bounds__(256) void emit_instances_kernel(Args a, GeomState g
             const int i = (int)own[k];
             int x0, y0, x1, y1;
             getRect(xy[k].x, xy[k].y, rad[k], a.gx, a.gy, x0, y0, x1, y1);
-            const uint32_t local = c - s_off[i], wdt = (uint32_t)(x1 - x0);
-            const int ty = y0 + (int)(local / wdt), tx = x0 + (int)(local % wdt);
+            // row-major position in the rect: local = qd * wdt + rm by a float reciprocal and one
+            // correction step (exact for local < 2^20: the forward rejects grids of 2^20 tiles or more)
+            const int local = (int)(c - s_off[i]), wdt = x1 - x0;
+            int qd = (int)((float)local * __builtin_amdgcn_rcpf((float)wdt));
+            int rm = local - qd * wdt;
+            if (rm < 0) { qd--; rm += wdt; }
+            else if (rm >= wdt) { qd++; rm -= wdt; }
+            const int ty = y0 + qd, tx = x0 + rm;
             reach[k] = half_reach(xy[k].x, xy[k].y, co[k], tx, ty, a.W, a.H);
             if (reach[k] != 0) {
                 keep |= 1u << k;
                 tile[k] = (uint32_t)(ty * a.gx + tx);
-                atomicAdd(&s_n[i], 1u);
                 for (int p = 0; p < npass; p++) atomicAdd(&s_hist[p][(tile[k] >> (8 * p)) & 0xFFu], 1u);
             }
         }
@@ -296,8 +300,23 @@ __global__ __launch_bounds__(256) void emit_instances_kernel(Args a, GeomState g
             e++;
         }
     }
-    for (int i = tid; i < nr; i += 256)
-        if (s_n[i]) atomicAdd(&g.n_inst[g.vis_gid[rlo + i]], s_n[i]);
+    // n_inst: a Gaussian's candidates are consecutive, so its kept count in this chunk is a difference
+    // of the chunk-local kept prefix at the ends of its candidate range (no per-candidate atomics)
+    {
+        uint32_t run = before + x - cnt;
+#pragma unroll
+        for (int k = 0; k < kEmitPer; k++) {
+            s_n[tid * kEmitPer + k] = run;
+            run += (keep >> k) & 1u;
+        }
+        if (tid == 255) s_n[kEmitChunk] = run;  // the chunk total
+    }
+    __syncthreads();
+    for (int i = tid; i < nr; i += 256) {
+        const uint32_t lo = max(s_off[i], c0) - c0, hi = min(s_off[i + 1], c1) - c0;
+        const uint32_t n = hi > lo ? s_n[hi] - s_n[lo] : 0u;
+        if (n) atomicAdd(&g.n_inst[g.vis_gid[rlo + i]], n);
+    }
     uint32_t *hist = g.zero + geom_hist_off(a.P) + (b % kHistShards) * (kMaxPasses * 256);
     for (int p = 0; p < npass; p++)
         if (s_hist[p][tid]) atomicAdd(&hist[p * 256 + tid], s_hist[p][tid]);

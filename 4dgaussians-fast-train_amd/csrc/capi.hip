@@ -228,6 +228,7 @@ int gs4d_forward_ex(gs4d_alloc_fn geometry_alloc, void *geometry_ctx, gs4d_alloc
     begin_marks(stream);
 
     const int T = a.gx * a.gy;
+    if (T >= (1 << 20)) return fail(GS4D_ERR_ARG, "forward: at most 2^20 - 1 tiles (16x16 pixels each)");
     char *gbuf = geometry_alloc(geometry_ctx, GeomState::required(P, T) + 16);
     if (!gbuf) return fail(GS4D_ERR_ALLOC, "forward: geometry buffer allocation failed");
     GeomState g = GeomState::carve(gbuf, P, T);
