@@ -271,12 +271,13 @@ def _image_buffer_views(ib, W, H):
     return ranges, order
 
 
-@pytest.mark.parametrize("W,H", [(1352, 1014), (2304, 1296), (2400, 2000)])
+@pytest.mark.parametrize("W,H", [(1352, 1014), (2304, 1296), (2048, 2048), (2400, 2000)])
 def test_tile_order_longest_first(C, oracle, dev, W, H):
     """The blend kernels take tiles longest run first (tile_order_kernel): the order is a permutation
     of the tiles with non-increasing run lengths (capped at 1023).  2304x1296 has 11,664 tiles, more than
-    the order kernel keeps in registers (8192), and is checked against the oracle as well; 2400x2000 has
-    18,750, more than the counting binning's LDS bins (binning.hip kCountMaxT): the radix-sort binning.
+    the order kernel keeps in registers (8192), and is checked against the oracle as well; 2048x2048 has
+    16,384, the counting binning's largest grid (64 KiB of LDS bins, binning.hip kCountMaxT); 2400x2000 has
+    18,750, more than that: the radix-sort binning.
     The tile ranges partition the emitted instances in tile order, empty tiles (0, 0) as
     identifyTileRanges leaves them (rasterizer_impl.cu:116-138)."""
     s = make_scene(100_000 if W == 1352 else 3000, W, H, seed=25)
