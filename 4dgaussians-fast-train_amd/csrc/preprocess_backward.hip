@@ -63,6 +63,24 @@ __device__ __forceinline__ void add9(float *acc, const float4 *p) {
     acc[8] += c.x;
 }
 
+// One step of the wave's segmented inclusive scan by DPP moves (no LDS): lane l takes the (sums, flag) of
+// the lane CTRL names (row_shr:n inside rows of 16, row_bcast:15 / :31 across rows, only the rows RM
+// enables; lanes without a source read zeros, the identity) and adds its sums unless a segment head
+// lies between them.
+template <int CTRL, int RM>
+__device__ __forceinline__ void seg_scan_step(float acc[9], bool &f) {
+    const bool fu = __builtin_amdgcn_update_dpp(0, (int)f, CTRL, RM, 0xF, false) != 0;
+    float up[9];
+#pragma unroll
+    for (int q = 0; q < 9; q++)
+        up[q] = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(acc[q]), CTRL, RM, 0xF, false));
+    if (!f) {
+#pragma unroll
+        for (int q = 0; q < 9; q++) acc[q] += up[q];
+    }
+    f = f || fu;
+}
+
 // Pass 1: one lane per emission slot, one wave per 64 slots.  A Gaussian's records occupy consecutive
 // slots, so a segmented inclusive scan (fixed shuffle tree) sums each Gaussian's piece of the wave.
 // Pieces that are a whole Gaussian are written out; a piece continuing from the previous wave goes
@@ -99,18 +117,12 @@ __global__ __launch_bounds__(256) void contrib_segments_kernel(const uint32_t *_
     const bool tail = valid && key != kn;  // last slot of its Gaussian
     if (head) e_first[key] = (uint32_t)e;  // locates the pieces of a Gaussian spanning waves
     bool f = head || lane == 0;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        float up[9];
-#pragma unroll
-        for (int q = 0; q < 9; q++) up[q] = __shfl_up(acc[q], off);
-        const bool fu = __shfl_up((int)f, off) != 0;
-        if (lane >= off && !f) {
-#pragma unroll
-            for (int q = 0; q < 9; q++) acc[q] += up[q];
-        }
-        f = f || (lane >= off && fu);
-    }
+    seg_scan_step<0x111, 0xF>(acc, f);  // row_shr:1
+    seg_scan_step<0x112, 0xF>(acc, f);  // row_shr:2
+    seg_scan_step<0x114, 0xF>(acc, f);  // row_shr:4
+    seg_scan_step<0x118, 0xF>(acc, f);  // row_shr:8
+    seg_scan_step<0x142, 0xA>(acc, f);  // row_bcast:15 -> rows 1, 3
+    seg_scan_step<0x143, 0xC>(acc, f);  // row_bcast:31 -> rows 2, 3
     const uint64_t endm = __ballot(valid && (tail || lane == 63));
     const int fe = __ffsll((unsigned long long)endm) - 1;  // end lane of the first piece
     const bool head0 = __ballot(head) & 1ull;
