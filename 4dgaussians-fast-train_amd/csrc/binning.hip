@@ -93,12 +93,7 @@ size_t tile_hist_words(int L, int T) {
 // and (in *total) the workgroup sum.
 __device__ __forceinline__ uint32_t wg_exclusive(uint32_t v, uint32_t *s_w, uint32_t *total) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    uint32_t x = v;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t y = __shfl_up(x, off);
-        if (lane >= off) x += y;
-    }
+    const uint32_t x = wave_incl_sum(v);
     __syncthreads();
     if (lane == 63) s_w[w] = x;
     __syncthreads();
@@ -218,16 +213,10 @@ __global__ __launch_bounds__(256) void emit_instances_kernel(Args a, GeomState g
         own[k] = mx;
     }
     {
-        uint32_t x = mx;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t y = __shfl_up(x, off);
-            if (lane >= off) x = max(x, y);
-        }
+        const uint32_t x = wave_incl_max(mx);
         if (lane == 63) s_w[w] = x;
         __syncthreads();
-        uint32_t carry = __shfl_up(x, 1);
-        if (lane == 0) carry = 0;
+        uint32_t carry = dpp_src<0x138, 0xF>(x);  // wave_shr:1 (lane 0 reads 0)
         for (int q = 0; q < w; q++) carry = max(carry, s_w[q]);
 #pragma unroll
         for (int k = 0; k < kEmitPer; k++) own[k] = max(own[k], carry);
@@ -273,12 +262,7 @@ __global__ __launch_bounds__(256) void emit_instances_kernel(Args a, GeomState g
     }
     // compaction offsets: exclusive scan of the per-lane counts, chunk total chained by look-back
     const uint32_t cnt = __popc(keep);
-    uint32_t x = cnt;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t y = __shfl_up(x, off);
-        if (lane >= off) x += y;
-    }
+    const uint32_t x = wave_incl_sum(cnt);
     __syncthreads();
     if (lane == 63) s_w[w] = x;
     __syncthreads();
@@ -409,12 +393,7 @@ __global__ __launch_bounds__(kCountThreads) void tile_scan_kernel(uint32_t *__re
         tot += x;
     }
     if (w == 0) {
-        uint32_t x = tot;  // inclusive scan of the group's tile totals
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t y = __shfl_up(x, off);
-            if (lane >= off) x += y;
-        }
+        const uint32_t x = wave_incl_sum(tot);  // inclusive scan of the group's tile totals
         const uint32_t gsum = __shfl(x, 63);
         if (lane == 0) store_word(look + blockIdx.x, kAgg | gsum);
         uint32_t lower = sum_published(look, 1, (int)blockIdx.x, lane, 64, err);

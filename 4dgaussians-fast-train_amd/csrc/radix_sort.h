@@ -8,6 +8,32 @@
 namespace gs4d {
 
 constexpr uint32_t kAgg = 1u << 30, kValMask = (1u << 30) - 1;
+
+// Wave-wide inclusive scans by DPP moves (row_shr 1/2/4/8 inside rows of 16, then row_bcast:15 into rows
+// 1 and 3 and row_bcast:31 into rows 2 and 3): plain VALU, no LDS round trips as __shfl_up's bpermutes.
+// Lanes without a source read 0, the identity of both operations (unsigned values).
+template <int CTRL, int RM>
+__device__ __forceinline__ uint32_t dpp_src(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, RM, 0xF, false);
+}
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
+    x += dpp_src<0x111, 0xF>(x);
+    x += dpp_src<0x112, 0xF>(x);
+    x += dpp_src<0x114, 0xF>(x);
+    x += dpp_src<0x118, 0xF>(x);
+    x += dpp_src<0x142, 0xA>(x);
+    x += dpp_src<0x143, 0xC>(x);
+    return x;
+}
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
+    x = max(x, dpp_src<0x111, 0xF>(x));
+    x = max(x, dpp_src<0x112, 0xF>(x));
+    x = max(x, dpp_src<0x114, 0xF>(x));
+    x = max(x, dpp_src<0x118, 0xF>(x));
+    x = max(x, dpp_src<0x142, 0xA>(x));
+    x = max(x, dpp_src<0x143, 0xC>(x));
+    return x;
+}
 constexpr uint32_t kSpinLimit = 1u << 20;
 
 __device__ __forceinline__ void store_word(uint32_t *p, uint32_t v) {
