@@ -12,12 +12,13 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def test_l1_loss_matches_torch():
+@pytest.mark.parametrize("H,W", [(101, 77), (100, 76)])  # n % 4 != 0: scalar kernels; n % 4 == 0: float4 / char4
+def test_l1_loss_matches_torch(H, W):
     from gs4d_train.kernels import l1_loss
     from gs4d_train.losses import l1_loss_torch
     g = torch.Generator(device="cuda").manual_seed(0)
-    x = torch.rand(2, 3, 101, 77, device="cuda", generator=g).requires_grad_(True)
-    y = torch.rand(2, 3, 101, 77, device="cuda", generator=g)
+    x = torch.rand(2, 3, H, W, device="cuda", generator=g).requires_grad_(True)
+    y = torch.rand(2, 3, H, W, device="cuda", generator=g)
     y[0, 0, 0, :5] = x.detach()[0, 0, 0, :5]  # exact ties: subgradient 0
     x2 = x.detach().clone().requires_grad_(True)
     l_f = l1_loss(x, y)
