@@ -115,7 +115,9 @@ __global__ __launch_bounds__(kTailThreads) void l1_final_kernel(int nblk, int64_
 __global__ __launch_bounds__(kTailThreads) void l1_backward_kernel(int64_t n, const int8_t *__restrict__ sign,
                                                                    const float *__restrict__ dloss,
                                                                    float *__restrict__ grad) {
-    const float scale = *dloss / (float)n;  // d mean / dx = sign / N, times the upstream gradient
+    // d mean / dx = sign / N, times the upstream gradient, rounded as torch's MeanBackward does it
+    // (grad / numel with a scalar divisor: grad * (1 / numel))
+    const float scale = *dloss * (1.0f / (float)n);
     for (int64_t i = (int64_t)blockIdx.x * kTailThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kTailThreads)
         grad[i] = (float)sign[i] * scale;
 }
@@ -123,7 +125,7 @@ __global__ __launch_bounds__(kTailThreads) void l1_backward_kernel(int64_t n, co
 __global__ __launch_bounds__(kTailThreads) void l1_backward_v4_kernel(int64_t n4, const char4 *__restrict__ sign,
                                                                       const float *__restrict__ dloss,
                                                                       float4 *__restrict__ grad, int64_t n) {
-    const float scale = *dloss / (float)n;
+    const float scale = *dloss * (1.0f / (float)n);  // as l1_backward_kernel
     for (int64_t i = (int64_t)blockIdx.x * kTailThreads + threadIdx.x; i < n4; i += (int64_t)gridDim.x * kTailThreads) {
         const char4 c = sign[i];
         grad[i] = make_float4((float)c.x * scale, (float)c.y * scale, (float)c.z * scale, (float)c.w * scale);
