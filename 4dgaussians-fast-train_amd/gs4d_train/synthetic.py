@@ -87,6 +87,34 @@ def make_training_views(n_views, W, H, seed=0, time_range=(0.0, 1.0), radius=4.0
     return views
 
 
+def make_train_like_scene(P, W, H, seed=0, extent=1.2, radius=4.0):
+    """The rasterizer's input at the start of a training run (a bench workload next to the metric
+    scene): `make_point_cloud` initialised as `GaussianModel.create_from_pcd` does
+    (scene/gaussian_model.py:134-163) -- scales sqrt(3-NN mean squared distance) on every axis (the
+    simple_knn value, here from a k-d tree), identity rotations, opacity 0.1, SH DC from the colours,
+    the rest zero -- seen by view 0 of `make_training_views` (radius 4, looking at the origin).
+    Its splats are larger than the metric scene's: ~1,200 instances per touched tile."""
+    from scipy.spatial import cKDTree
+    pts, cols = make_point_cloud(P, seed=seed, extent=extent)
+    d, _ = cKDTree(pts.astype(np.float64)).query(pts.astype(np.float64), k=4)
+    dist2 = np.maximum((d[:, 1:] ** 2).mean(1), 1e-7)
+    scales = np.repeat(np.sqrt(dist2)[:, None], 3, 1).astype(np.float32)
+    rotations = np.zeros((P, 4), np.float32)
+    rotations[:, 0] = 1.0
+    opacities = np.full((P, 1), 0.1, np.float32)
+    shs = np.zeros((P, 16, 3), np.float32)
+    shs[:, 0, :] = (cols - 0.5) / SH_C0
+    c = np.array([0.0, 0.0, -radius])
+    Rw2c = np.eye(3)          # view 0 of make_training_views: camera axes = world axes
+    cam = make_camera(W, H, R=Rw2c.T, T=-Rw2c @ c)
+    return dict(
+        means3D=pts, scales=scales, rotations=rotations, opacities=opacities, shs=shs,
+        bg=np.ones(3, np.float32), viewmatrix=cam.world_view_transform.numpy().astype(np.float32),
+        projmatrix=cam.full_proj_transform.numpy().astype(np.float32),
+        campos=cam.camera_center.numpy().astype(np.float32), tanfovx=cam.tanfovx, tanfovy=cam.tanfovy,
+        W=W, H=H, sh_degree=3, scale_modifier=1.0, camera=cam)
+
+
 def make_point_cloud(P, seed=0, extent=1.2):
     """Random initial point cloud inside the deformation field's bounds, with random colours."""
     rng = np.random.default_rng(seed)

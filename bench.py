@@ -7,15 +7,22 @@ rank renders its own view (independent views/timesteps shard across GPUs, SURVEY
 work is fixed as N grows ("weak" scaling).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config metric] [--no-cpu-baseline]
-  multi-GPU: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py launches its own N ranks
+(`torch.distributed.run`, 127.0.0.1) as a child process before anything touches the GPU, and exits
+with the child's status; under a launcher (WORLD_SIZE set) it refuses to run unless WORLD_SIZE == N,
+so a multi-GPU run can never silently measure one rank.  `--dry-run` goes through the same launcher
+and rendezvous over gloo on the CPU, with a stand-in step instead of the HIP calls (the CPU test of the
+launcher path, tests/test_bench_launcher.py).
 
 Rank 0 prints ONE JSON line (see the contract in the task statement): value = whole-job
 MGaussians/s = N * P * K / max-over-ranks(timed seconds) / 1e6.
 """
 import argparse
 import json
-import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -27,11 +34,8 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 # BASELINE.json's metric; value = the rasterizer fwd+bwd MGaussians/s, train_step.ms = the train-step ms
-BASELINE_METRIC = "train-step ms + rasterizer fwd+bwd MGaussians/s @100k pts, 1352\u00d71014"
+BASELINE_METRIC = "train-step ms + rasterizer fwd+bwd MGaussians/s @100k pts, 1352×1014"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: 8.0 TB/s spec
-# VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 4 cycles per SIMD at 2.4 GHz
-# (MI355X_MICROARCH.md: v_fma_f32 issue cost 4 cycles)
-VALU_PEAK_GINST = 256 * 4 * 2.4 / 4
 
 
 def algorithmic_bytes(P, L, W, H, K=16):
@@ -45,7 +49,7 @@ def algorithmic_bytes(P, L, W, H, K=16):
                 step=b_fwd + b_bwd)
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -54,84 +58,74 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-train-step", action="store_true", help="skip the full train-step timing")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the autograd-wrapper and training-like-scene timings")
     ap.add_argument("--train-steps", type=int, default=20)
-    args = ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher/rendezvous check on the CPU (gloo, no HIP call); not a measurement")
+    return ap.parse_args(argv)
 
-    from gs4d_train.synthetic import CONFIGS, make_scene, make_upstream_grad
-    import diff_gaussian_rasterization as dgr
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args, argv):
+    """Start N ranks of this script under torch.distributed.run (a child process: nothing in this
+    process has touched the GPU) and return the child's exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__), *argv]
+    return subprocess.call(cmd, cwd=ROOT)
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    if args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args, argv))
+    world = int(env_world or "1")
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to measure a different "
+                 f"number of ranks than asked for")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        return dry_run(args, world, rank)
+
+    from gs4d_train.synthetic import CONFIGS, make_scene
+    import diff_gaussian_rasterization as dgr
+    import torch.distributed as tdist
+
     dist = world > 1
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if dist:
-        import torch.distributed as tdist
         tdist.init_process_group("nccl", device_id=dev)
+        assert tdist.get_world_size() == args.gpus, (tdist.get_world_size(), args.gpus)
 
     P, W, H = CONFIGS[args.config]
     # rank r renders its own view: same scene statistics, per-rank seed
     s = make_scene(P, W, H, seed=rank)
-    t = lambda a: torch.tensor(np.asarray(a), device=dev)
-    bg, vm, pm, cp = t(s["bg"]), t(s["viewmatrix"]), t(s["projmatrix"]), t(s["campos"])
-    means3D, opac, scales, rots, shs = (t(s[k]) for k in ("means3D", "opacities", "scales", "rotations", "shs"))
-    e = torch.empty(0, device=dev)
-    C = dgr._C
-    from gs4d_train import _C as TC
-    one = torch.ones(1, device=dev)
-    gt = t(np.random.default_rng(rank + 1).uniform(0, 1, (3, H, W)).astype(np.float32))
-
-    def step():
-        fwd = C.rasterize_gaussians(bg, means3D, e, opac, scales, rots, 1.0, e, vm, pm, s["tanfovx"], s["tanfovy"],
-                                    H, W, shs, 3, cp, False, False)
-        nr, color, depth, radii, gb, bb, ib = fwd
-        # train.py:244 L1 loss and its gradient sign(color - gt) / N (fused kernels, csrc/train_tail.hip)
-        loss, sgn = TC.l1_forward(color, gt)
-        grad = TC.l1_backward(sgn, one)
-        grads = C.rasterize_gaussians_backward(bg, means3D, radii, e, scales, rots, 1.0, e, vm, pm, s["tanfovx"],
-                                               s["tanfovy"], grad, shs, 3, cp, gb, nr, bb, ib, False)
-        if dist:
-            tdist.all_reduce(loss)                    # the harness's loss all-reduce over RCCL
-        return nr, loss, grads
-
-    for _ in range(args.warmup):
-        nr, loss, grads = step()
-    torch.cuda.synchronize()
-    if dist:
-        tdist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        nr, loss, grads = step()
-    torch.cuda.synchronize()
-    if dist:
-        tdist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if dist:
-        et = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        tdist.all_reduce(et, op=tdist.ReduceOp.MAX)
-        elapsed = float(et.item())
+    scene = upload_scene(s, dev)
+    step = make_step(scene, dev, rank, dgr._C, dist)
+    elapsed, nr = timed_steps(step, args.steps, args.warmup, dist)
+    my_ms = elapsed / args.steps * 1e3
+    per_rank = gather_per_rank([float(nr), my_ms], world, dev, dist)
+    elapsed = max(r[1] for r in per_rank) * args.steps / 1e3   # max over ranks
     ms_per_step = elapsed / args.steps * 1e3
     value = world * P * args.steps / elapsed / 1e6
 
-    # ---- per-kernel timing with hipEvents on the launch stream (same workload, K more steps) ----
-    C.set_profiling(True)
-    stage_ms = {}
-    for _ in range(max(5, min(args.steps, 20))):
-        nr, color, depth, radii, gb, bb, ib = C.rasterize_gaussians(bg, means3D, e, opac, scales, rots, 1.0, e, vm, pm,
-                                                                    s["tanfovx"], s["tanfovy"], H, W, shs, 3, cp,
-                                                                    False, False)
-        for name, ms in C.last_timings():
-            stage_ms.setdefault("fwd." + name, []).append(ms)
-        grad = torch.sign(color - gt) / color.numel()
-        C.rasterize_gaussians_backward(bg, means3D, radii, e, scales, rots, 1.0, e, vm, pm, s["tanfovx"], s["tanfovy"],
-                                       grad, shs, 3, cp, gb, nr, bb, ib, False)
-        for name, ms in C.last_timings():
-            stage_ms.setdefault("bwd." + name, []).append(ms)
-    C.set_profiling(False)
-    stage_avg = {k: float(np.mean(v)) for k, v in stage_ms.items()}
+    stage_avg = stage_timings(scene, dgr._C, args.steps)
+
+    extras = {}
+    if not args.no_extras:
+        extras["autograd_wrapper"] = autograd_timing(scene, dgr, args.steps, args.warmup, P)
+        extras["train_like_scene"] = train_like_timing(P, W, H, dev, args.steps, args.warmup, dgr._C, rank)
 
     # ---- the full fine-stage train step (the metric's "train-step ms") ----
     train = None if args.no_train_step else train_step_timing(P, W, H, dev, world, rank, args.train_steps,
@@ -145,15 +139,7 @@ def main():
         dom_bytes = ab["render_backward"] if dom == "bwd.render_backward" else (
             ab["render"] if dom == "fwd.render" else None)
         achieved = dom_bytes / (dom_ms * 1e-3) / 1e9 if dom_bytes else None
-        def pmc(name):
-            path = os.path.join(ROOT, "profiles", name)
-            try:
-                return json.load(open(path)).get(dom.split(".", 1)[1], None)
-            except Exception:
-                return None
-        traffic = pmc("pmc_traffic.json")
-        traffic_raw = pmc("pmc_traffic_raw.json")
-        valu = pmc("pmc_valu.json")
+        prof = load_profile_summary(dom.split(".", 1)[1])
         out = {
             "metric": BASELINE_METRIC,
             "value": round(value, 3), "unit": "MGaussians/s", "n_gpus": world, "steps": args.steps,
@@ -162,30 +148,213 @@ def main():
             "config": {"workload": f"{args.config}: P={P} Gaussians, {W}x{H}, SH deg 3, 1 view/GPU/step, fwd+bwd",
                        "global_batch": world, "parallelism": f"views x{world} (independent views + RCCL loss all-reduce)"},
             "num_rendered": L,
+            "per_rank": [{"rank": i, "num_rendered": int(r[0]), "ms_per_step": round(r[1], 4)}
+                         for i, r in enumerate(per_rank)],
             "stage_ms": {k: round(v, 4) for k, v in stage_avg.items()},
             "roofline": {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 2) if achieved else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None, "traffic": traffic,
-                         "traffic_raw": traffic_raw,
-                         "traffic_note": "PMC bytes per launch (profiles/r02_pmc.json): traffic = 2 x FETCH_SIZE + "
+                         "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None,
+                         "traffic": prof.get("traffic"), "traffic_raw": prof.get("traffic_raw"),
+                         "traffic_note": "PMC bytes per launch (profiles/pmc_traffic.json): traffic = 2 x FETCH_SIZE + "
                                          "WRITE_SIZE (gfx950 wide-read correction), traffic_raw = FETCH_SIZE + "
                                          "WRITE_SIZE; the kernel's reads are mostly gathers, so the truth lies between",
                          "algorithmic_bytes": dom_bytes, "avg_ms": round(dom_ms, 4)},
-            # the blend kernels are VALU-issue bound, not HBM bound: instruction rate vs the issue peak
-            "valu_issue": {"kernel": dom, "insts_per_launch": valu,
-                           "achieved_Ginst_s": round(valu / (dom_ms * 1e-3) / 1e9, 1) if valu else None,
-                           "peak_Ginst_s": VALU_PEAK_GINST,
-                           "frac": round(valu / (dom_ms * 1e-3) / 1e9 / VALU_PEAK_GINST, 4) if valu else None,
-                           "source": "SQ_INSTS_VALU per launch, profiles/pmc_valu.json (rocprofv3 --pmc)"},
             "step_roofline": {"algorithmic_bytes": ab["step"],
                               "achieved_GBs": round(ab["step"] / (ms_per_step * 1e-3) / 1e9, 2),
                               "frac": round(ab["step"] / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)},
         }
+        if prof.get("valu") is not None:
+            # the blend kernels are VALU-issue bound, not HBM bound: measured VALU busy fraction
+            out["valu_utilisation"] = prof["valu"]
+        out.update(extras)
         if train is not None:
             out["train_step"] = train
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(s, args.cpu_seconds)
         print(json.dumps(out), flush=True)
+    if dist:
+        tdist.destroy_process_group()
+
+
+def upload_scene(s, dev):
+    t = lambda a: torch.tensor(np.asarray(a), device=dev)
+    d = {k: t(s[k]) for k in ("bg", "viewmatrix", "projmatrix", "campos", "means3D", "opacities", "scales",
+                              "rotations", "shs")}
+    d.update(W=s["W"], H=s["H"], tanfovx=s["tanfovx"], tanfovy=s["tanfovy"], e=torch.empty(0, device=dev))
+    return d
+
+
+def _fwd(C, d):
+    return C.rasterize_gaussians(d["bg"], d["means3D"], d["e"], d["opacities"], d["scales"], d["rotations"], 1.0,
+                                 d["e"], d["viewmatrix"], d["projmatrix"], d["tanfovx"], d["tanfovy"], d["H"], d["W"],
+                                 d["shs"], 3, d["campos"], False, False)
+
+
+def _bwd(C, d, radii, grad, gb, nr, bb, ib):
+    return C.rasterize_gaussians_backward(d["bg"], d["means3D"], radii, d["e"], d["scales"], d["rotations"], 1.0,
+                                          d["e"], d["viewmatrix"], d["projmatrix"], d["tanfovx"], d["tanfovy"], grad,
+                                          d["shs"], 3, d["campos"], gb, nr, bb, ib, False)
+
+
+def make_step(d, dev, seed, C, dist):
+    from gs4d_train import _C as TC
+    one = torch.ones(1, device=dev)
+    gt = torch.tensor(np.random.default_rng(seed + 1).uniform(0, 1, (3, d["H"], d["W"])).astype(np.float32),
+                      device=dev)
+
+    def step():
+        nr, color, depth, radii, gb, bb, ib = _fwd(C, d)
+        # train.py:244 L1 loss and its gradient sign(color - gt) / N (fused kernels, csrc/train_tail.hip)
+        loss, sgn = TC.l1_forward(color, gt)
+        grad = TC.l1_backward(sgn, one)
+        _bwd(C, d, radii, grad, gb, nr, bb, ib)
+        if dist:
+            import torch.distributed as tdist
+            tdist.all_reduce(loss)                    # the harness's loss all-reduce over RCCL
+        return nr
+    return step
+
+
+def timed_steps(step, steps, warmup, dist, sync=True):
+    """W untimed steps, then K steps bracketed by barrier + synchronize on both sides."""
+    import torch.distributed as tdist
+    cuda = sync and torch.cuda.is_available()
+    nr = 0
+    for _ in range(warmup):
+        nr = step()
+    if cuda:
+        torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    if cuda:
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        nr = step()
+    if cuda:
+        torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    if cuda:
+        torch.cuda.synchronize()
+    return time.perf_counter() - t0, nr
+
+
+def gather_per_rank(row, world, dev, dist):
+    """[[num_rendered, ms_per_step] of every rank] (one all-reduce of a world x 2 table)."""
+    if not dist:
+        return [row]
+    import torch.distributed as tdist
+    tab = torch.zeros(world, len(row), dtype=torch.float64, device=dev)
+    tab[tdist.get_rank()] = torch.tensor(row, dtype=torch.float64)
+    tdist.all_reduce(tab)
+    return tab.cpu().tolist()
+
+
+def stage_timings(d, C, steps):
+    """Per-kernel hipEvent timings on the launch stream (same workload, a few more steps)."""
+    C.set_profiling(True)
+    stage_ms = {}
+    gt = torch.tensor(np.random.default_rng(1).uniform(0, 1, (3, d["H"], d["W"])).astype(np.float32),
+                      device=d["bg"].device)
+    for _ in range(max(5, min(steps, 20))):
+        nr, color, depth, radii, gb, bb, ib = _fwd(C, d)
+        for name, ms in C.last_timings():
+            stage_ms.setdefault("fwd." + name, []).append(ms)
+        grad = torch.sign(color - gt) / color.numel()
+        _bwd(C, d, radii, grad, gb, nr, bb, ib)
+        for name, ms in C.last_timings():
+            stage_ms.setdefault("bwd." + name, []).append(ms)
+    C.set_profiling(False)
+    return {k: float(np.mean(v)) for k, v in stage_ms.items()}
+
+
+def autograd_timing(d, dgr, steps, warmup, P):
+    """The same fwd+bwd through the Python API (GaussianRasterizer + torch.autograd), as
+    gaussian_renderer/__init__.py drives it (report it with and without the wrapper)."""
+    settings = dgr.GaussianRasterizationSettings(
+        image_height=d["H"], image_width=d["W"], tanfovx=d["tanfovx"], tanfovy=d["tanfovy"], bg=d["bg"],
+        scale_modifier=1.0, viewmatrix=d["viewmatrix"], projmatrix=d["projmatrix"], sh_degree=3,
+        campos=d["campos"], prefiltered=False, debug=False)
+    rast = dgr.GaussianRasterizer(settings)
+    leaves = {k: d[k].clone().requires_grad_(True) for k in ("means3D", "shs", "opacities", "scales", "rotations")}
+    means2D = torch.zeros_like(leaves["means3D"], requires_grad=True)
+    gt = torch.tensor(np.random.default_rng(1).uniform(0, 1, (3, d["H"], d["W"])).astype(np.float32),
+                      device=d["bg"].device)
+
+    def step():
+        for v in list(leaves.values()) + [means2D]:
+            v.grad = None
+        color, radii, depth = rast(means3D=leaves["means3D"], means2D=means2D, shs=leaves["shs"],
+                                   opacities=leaves["opacities"], scales=leaves["scales"],
+                                   rotations=leaves["rotations"])
+        loss = torch.abs(color - gt).mean()          # train.py:244 l1_loss
+        loss.backward()
+        return 0
+    el, _ = timed_steps(step, steps, warmup, False)
+    ms = el / steps * 1e3
+    return {"ms_per_step": round(ms, 4), "MGaussians_s": round(P / (ms * 1e-3) / 1e6, 3),
+            "note": "GaussianRasterizer + torch L1 + loss.backward() (torch's own L1 kernels, not the fused "
+                    "ones of the headline step)"}
+
+
+def train_like_timing(P, W, H, dev, steps, warmup, C, seed):
+    """A second named workload: the metric-size rasterizer fwd+bwd on the scene a training run starts
+    from (gs4d_train.synthetic.make_train_like_scene: k-NN scales, larger splats, ~1,200 instances per
+    touched tile), where the blend kernels weigh more than in the metric scene."""
+    from gs4d_train.synthetic import make_train_like_scene
+    s = make_train_like_scene(P, W, H, seed=0)
+    d = upload_scene(s, dev)
+    step = make_step(d, dev, seed, C, False)
+    el, nr = timed_steps(step, steps, warmup, False)
+    ms = el / steps * 1e3
+    stages = stage_timings(d, C, steps)
+    T = ((W + 15) // 16) * ((H + 15) // 16)
+    return {"workload": f"train_like: P={P}, {W}x{H}, k-NN-initialised point cloud (create_from_pcd), view 0",
+            "ms_per_step": round(ms, 4), "MGaussians_s": round(P / (ms * 1e-3) / 1e6, 3),
+            "num_rendered": int(nr), "tiles": T,
+            "stage_ms": {k: round(v, 4) for k, v in sorted(stages.items(), key=lambda kv: -kv[1])[:6]}}
+
+
+def load_profile_summary(kernel):
+    """The rocprofv3 PMC evidence for the dominant kernel, committed under profiles/ by
+    tools/profile.sh + tools/pmc_summary.py (bytes per launch; VALU busy from SQ counters)."""
+    out = {}
+    for key, name in (("traffic", "pmc_traffic.json"), ("traffic_raw", "pmc_traffic_raw.json"),
+                      ("valu", "pmc_valu.json")):
+        try:
+            with open(os.path.join(ROOT, "profiles", name)) as f:
+                out[key] = json.load(f).get(kernel)
+        except (OSError, ValueError):
+            out[key] = None
+    return out
+
+
+def dry_run(args, world, rank):
+    """The launcher path without the GPU: gloo rendezvous, a CPU stand-in step, the same per-rank
+    gather and max-over-ranks timing, and a JSON line marked as not a measurement."""
+    import torch.distributed as tdist
+    dist = world > 1
+    if dist:
+        tdist.init_process_group("gloo")
+        assert tdist.get_world_size() == args.gpus, (tdist.get_world_size(), args.gpus)
+    x = torch.randn(256, 256, generator=torch.Generator().manual_seed(rank))
+
+    def step():
+        y = x @ x
+        if dist:
+            v = y.sum().reshape(1)
+            tdist.all_reduce(v)
+        return 1000 + rank
+    el, nr = timed_steps(step, args.steps, args.warmup, dist, sync=False)
+    per_rank = gather_per_rank([float(nr), el / args.steps * 1e3], world, torch.device("cpu"), dist)
+    if rank == 0:
+        ms = max(r[1] for r in per_rank)
+        print(json.dumps({"metric": BASELINE_METRIC, "value": None, "unit": "MGaussians/s", "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),
+                          "dry_run": True, "per_rank": [{"rank": i, "num_rendered": int(r[0]),
+                                                         "ms_per_step": round(r[1], 4)}
+                                                        for i, r in enumerate(per_rank)]}), flush=True)
     if dist:
         tdist.destroy_process_group()
 
@@ -216,20 +385,13 @@ def train_step_timing(P, W, H, dev, world, rank, steps, warmup, dist, unfused=Tr
         views = make_training_views(world, W, H, seed=1, device=dev)
         bg = torch.ones(3, device=dev)
         it0 = 3001  # fine stage, densification statistics on, no densify/prune/reset iteration in range
-        for i in range(n_warm):
-            train_step(g, views, opt, hyper, it0 + i, bg, data_parallel=dist)
-        torch.cuda.synchronize()
-        if dist:
-            tdist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for i in range(n_steps):
-            loss = train_step(g, views, opt, hyper, it0 + n_warm + i, bg, data_parallel=dist)
-        torch.cuda.synchronize()
-        if dist:
-            tdist.barrier()
-        torch.cuda.synchronize()
-        el = time.perf_counter() - t0
+        state = {"i": it0}
+
+        def one():
+            loss = train_step(g, views, opt, hyper, state["i"], bg, data_parallel=dist)
+            state["i"] += 1
+            return loss
+        el, loss = timed_steps(one, n_steps, n_warm, dist)
         if dist:
             et = torch.tensor([el], device=dev, dtype=torch.float64)
             tdist.all_reduce(et, op=tdist.ReduceOp.MAX)
@@ -247,16 +409,10 @@ def train_step_timing(P, W, H, dev, world, rank, steps, warmup, dist, unfused=Tr
     return res
 
 
-def cpu_baseline(s, budget_s):
-    """The oracle (C restatement, OpenMP) on the host cores: same scene, full fwd+bwd per sample."""
+def _cpu_sample(s, threads, budget_s, max_samples):
     from oracle import oracle as O
     from gs4d_train.synthetic import make_upstream_grad
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except Exception:
-        cores = os.cpu_count() or 1
-    cores = min(cores, 16)   # the GPU box gives this job a 16-CPU share
-    O.set_threads(cores)
+    O.set_threads(threads)
     P, W, H = s["means3D"].shape[0], s["W"], s["H"]
     times = []
     t_start = time.perf_counter()
@@ -269,12 +425,27 @@ def cpu_baseline(s, budget_s):
         O.rasterize_backward(st, s["bg"], s["means3D"], radii, None, s["scales"], s["rotations"], 1.0, None,
                              s["viewmatrix"], s["projmatrix"], s["tanfovx"], s["tanfovy"], g, s["shs"], 3, s["campos"])
         times.append(time.perf_counter() - t0)
-        if time.perf_counter() - t_start > budget_s or len(times) >= 20:
+        if time.perf_counter() - t_start > budget_s or len(times) >= max_samples:
             break
-    med = float(np.median(times))
+    return float(np.median(times)), len(times)
+
+
+def cpu_baseline(s, budget_s):
+    """The oracle (C restatement, OpenMP) on the host cores: same scene, full fwd+bwd per sample, with
+    the box's CPU share (<= 16 threads) and with one thread."""
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except Exception:
+        cores = os.cpu_count() or 1
+    cores = min(cores, 16)   # the GPU box gives this job a 16-CPU share
+    P, W, H = s["means3D"].shape[0], s["W"], s["H"]
+    med, n = _cpu_sample(s, cores, budget_s, 20)
+    med1, n1 = _cpu_sample(s, 1, 0.0, 1)     # one sample: a full view takes seconds on one thread
     return {"value": round(P / med / 1e6, 4), "unit": "MGaussians/s", "cores": cores, "kind": "port",
-            "sample": f"{len(times)} full fwd+bwd of the same metric view (P={P}, {W}x{H}) by the OpenMP C oracle, "
-                      f"median {med * 1e3:.1f} ms"}
+            "sample": f"{n} full fwd+bwd of the same metric view (P={P}, {W}x{H}) by the OpenMP C oracle, "
+                      f"median {med * 1e3:.1f} ms",
+            "one_thread": {"value": round(P / med1 / 1e6, 5), "cores": 1,
+                           "sample": f"{n1} full fwd+bwd of the same view, {med1 * 1e3:.0f} ms"}}
 
 
 if __name__ == "__main__":

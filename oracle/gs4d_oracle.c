@@ -450,6 +450,64 @@ gs4d_oracle_state *gs4d_oracle_forward(int P, int D, int M, const float *backgro
     return s;
 }
 
+/* Near-threshold flags for the parity tests.  The blend's two discrete decisions, alpha >= 1/255
+ * (forward.cu:346-348, backward.cu:486-490) and T(1 - alpha) >= 1e-4 (forward.cu:350-354), flip
+ * between two correct float implementations when their operand lies within rounding of the
+ * threshold.  This replays the K6 walk of every pixel and flags:
+ *   pix_flag bit 0   some splat before the pixel's termination has |255 alpha - 1| <= band_alpha
+ *   pix_flag bit 1   some blended splat has |test_T / 1e-4 - 1| <= band_T (termination may flip)
+ *   gauss_flag bit 0 the Gaussian is such a near-1/255 splat at some pixel
+ *   gauss_flag bit 1 the Gaussian is such a near-termination splat at some pixel
+ * A flip moves the flipping splat's own term of that pixel by O(1) of the term; every other splat of
+ * the pixel moves by at most alpha_flip * T_flip (<= 1/255 resp. ~1e-2) of one pixel's term, far below
+ * the gradient tolerance, and an implementation that walks past a flipped termination adds terms of
+ * T < 1e-4.  Every element outside the flagged sets must agree to the north star's tolerance; the flagged ones
+ * are bounded by the size a single flip can have.  Returns the number of flagged pixels. */
+int gs4d_oracle_flip_flags(const gs4d_oracle_state *s, float band_alpha, float band_T, uint8_t *pix_flag,
+                           uint8_t *gauss_flag) {
+    const int W = s->W, H = s->H, gx = s->gx, T = s->gx * s->gy;
+    const float a_thr = 1.0f / 255.0f;
+    int nflag = 0;
+    memset(gauss_flag, 0, (size_t)(s->P > 0 ? s->P : 0));
+#pragma omp parallel for schedule(dynamic, 1) reduction(+ : nflag)
+    for (int tile = 0; tile < T; tile++) {
+        const int bx = tile % gx, by = tile / gx;
+        const uint32_t rs = s->ranges[2 * tile], re = s->ranges[2 * tile + 1];
+        for (int ty = 0; ty < BLOCK_Y; ty++)
+            for (int tx = 0; tx < BLOCK_X; tx++) {
+                const int pxi = bx * BLOCK_X + tx, pyi = by * BLOCK_Y + ty;
+                if (!(pxi < W && pyi < H)) continue;
+                const float pfx = (float)pxi, pfy = (float)pyi;
+                float Tr = 1.0f;
+                int done = 0;
+                uint8_t f = 0;
+                for (uint32_t k = rs; k < re && !done; k++) {
+                    const uint32_t g = s->point_list[k];
+                    const float dx = s->means2D[2 * g] - pfx, dy = s->means2D[2 * g + 1] - pfy;
+                    const float *co = s->conic_opacity + 4 * (size_t)g;
+                    float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+                    if (power > 0.0f) continue;
+                    float alpha = fminf_(0.99f, co[3] * expf(power));
+                    if (fabsf(alpha * 255.0f - 1.0f) <= band_alpha) {
+                        f |= 1;
+                        __atomic_fetch_or(&gauss_flag[g], (uint8_t)1, __ATOMIC_RELAXED);
+                    }
+                    if (alpha < a_thr) continue;
+                    float test_T = Tr * (1 - alpha);
+                    if (fabsf(test_T * 1e4f - 1.0f) <= band_T) {
+                        f |= 2;
+                        __atomic_fetch_or(&gauss_flag[g], (uint8_t)2, __ATOMIC_RELAXED);
+                    }
+                    if (test_T < 0.0001f) done = 1;
+                    else Tr = test_T;
+                }
+                pix_flag[(size_t)W * pyi + pxi] = f;
+                nflag += f != 0;
+            }
+    }
+    return nflag;
+}
+
 /* ---------------------------------------------------------------------------------------------- */
 /* backward.cu:20-139 */
 static void sh_backward(int idx, int deg, int max_coeffs, const float *means, const float *campos, const float *shs,

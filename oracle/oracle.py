@@ -57,6 +57,8 @@ def _load():
     lib.gs4d_oracle_mark_visible.argtypes = [ctypes.c_int, _f32p, _f32p, _f32p, _u8p]
     lib.gs4d_oracle_sh_forward.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _f32p, _f32p, _f32p, _f32p, _u8p]
     lib.gs4d_oracle_knn.argtypes = [ctypes.c_int, _f32p, _f32p]
+    lib.gs4d_oracle_flip_flags.argtypes = [ctypes.c_void_p, ctypes.c_float, ctypes.c_float, _u8p, _u8p]
+    lib.gs4d_oracle_flip_flags.restype = ctypes.c_int
     lib.gs4d_oracle_set_threads.argtypes = [ctypes.c_int]
     lib.gs4d_oracle_get_threads.restype = ctypes.c_int
     _lib = lib
@@ -179,6 +181,19 @@ def rasterize_backward(state, bg, means3D, radii, colors_precomp, scales, rotati
             g["dL_dsh"].ctypes.data_as(_f32p) if M > 0 else None, q("dL_dscales"), q("dL_drotations"))
     return (g["dL_dmeans2D"], g["dL_dcolors"], g["dL_dopacity"], g["dL_dmeans3D"], g["dL_dcov3D"], g["dL_dsh"],
             g["dL_dscales"], g["dL_drotations"]), g["dL_dconic"]
+
+
+def flip_flags(state, band_alpha, band_T):
+    """Near-threshold flags of the forward's two discrete decisions (gs4d_oracle_flip_flags): returns
+    (pix_flag (H, W) uint8, gauss_flag (P,) uint8); bit 0 = alpha within band_alpha (relative) of
+    1/255, bit 1 = T(1 - alpha) within band_T (relative) of 1e-4."""
+    lib = _load()
+    pix = np.zeros((state.H, state.W), np.uint8)
+    gau = np.zeros(max(state.P, 1), np.uint8)
+    if state.handle:
+        lib.gs4d_oracle_flip_flags(state.handle, float(band_alpha), float(band_T), pix.ctypes.data_as(_u8p),
+                                   gau.ctypes.data_as(_u8p))
+    return pix, gau[:state.P]
 
 
 def sh_forward(degree, means, campos, shs):

@@ -52,6 +52,23 @@ def image_parity(a, b, atol=1e-4):
     return float(err.max()) if err.size else 0.0, float((err > atol).mean()) if err.size else 0.0
 
 
+def grad_errors(a, b):
+    """Per-Gaussian max error normalised by the oracle tensor's max magnitude, shape (P,)."""
+    a = np.asarray(a, np.float64).reshape(a.shape[0], -1)
+    b = np.asarray(b, np.float64).reshape(b.shape[0], -1)
+    if a.size == 0:
+        return np.zeros(a.shape[0])
+    return np.abs(a - b).max(1) / max(np.abs(b).max(), 1e-30)
+
+
+def split_max(err, flagged):
+    """(max of err over unflagged elements, max over flagged ones); 0 for an empty set."""
+    err = np.asarray(err).reshape(-1)
+    flagged = np.asarray(flagged).reshape(-1)
+    unf, fl = err[~flagged], err[flagged]
+    return (float(unf.max()) if unf.size else 0.0), (float(fl.max()) if fl.size else 0.0)
+
+
 def grad_parity(a, b, rtol=1e-3):
     """Per-Gaussian relative error normalised by the tensor's max magnitude.
 

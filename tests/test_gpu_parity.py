@@ -1,11 +1,17 @@
 """GPU parity: the HIP path (through the `_C` binding over the C ABI) against the CPU oracle.
 
-Tolerances (north_star): RGB/depth within 1e-4, gradients within 1e-3.  Images are compared per
-element; a pixel may exceed 1e-4 only through a discrete threshold flip (alpha vs 1/255, T vs 1e-4,
-forward.cu:347,350) caused by last-ulp differences between __expf/FMA on gfx950 and the oracle's
-libm/no-FMA arithmetic, so the tests bound the FRACTION of such elements (<= 1e-4 of the image) and
-their size.  Gradients are compared per Gaussian relative to the tensor's largest magnitude; at most
-0.5% of Gaussians (those touched by a flip) may exceed 1e-3.
+Tolerances (north_star): RGB within 1e-4, depth within 1e-4 of the depth range (max(1, max depth)),
+gradients within 1e-3 per Gaussian, normalised by the tensor's largest magnitude.
+
+Every element must meet them except where the oracle itself says a discrete decision may flip.  The
+blend has two thresholds, alpha >= 1/255 and T(1 - alpha) >= 1e-4 (forward.cu:346-354,
+backward.cu:486-503); two correct float implementations (here exp2/FMA on gfx950 against the oracle's
+libm/no-FMA arithmetic) can land on either side when the operand lies within rounding of the
+threshold.  `oracle.flip_flags` replays the walk and flags the pixels with an operand within
+FLIP_BAND_ALPHA / FLIP_BAND_T (relative) of a threshold, and the Gaussians that are those near-threshold
+splats.  Unflagged elements: the tolerances above, no exception.  Flagged elements: a hard bound on the
+size one flip can have (a termination flip adds or removes one splat of weight alpha*T <= 0.99 * 1e-2;
+an alpha flip one of weight 1/255), and the flagged pixels must stay a small fraction of the image.
 """
 import math
 
@@ -13,15 +19,21 @@ import numpy as np
 import pytest
 import torch
 
-from gpu_helpers import c_backward, c_forward, grad_parity, image_parity, o_backward, o_forward, to_dev
+from gpu_helpers import (c_backward, c_forward, grad_errors, grad_parity, o_backward, o_forward, split_max,
+                         to_dev)
 from gs4d_train.synthetic import make_scene, make_upstream_grad
 
 pytestmark = pytest.mark.gpu
 
 IMG_ATOL = 1e-4
-IMG_FRAC = 1e-4
 GRAD_RTOL = 1e-3
-GRAD_FRAC = 5e-3
+GRAD_FRAC = 5e-3          # test_autograd_api only (no oracle state at hand there)
+FLIP_BAND_ALPHA = 3e-5    # |255 alpha - 1| within which the alpha test may flip
+FLIP_BAND_T = 3e-4        # |T(1 - alpha) / 1e-4 - 1| within which the termination may flip
+FLIP_COLOR_MAX = 0.03     # one splat of weight <= 0.99e-2 times |colour - bg| <= ~3
+FLIP_DEPTH_REL = 0.012    # one splat of weight <= 0.99e-2 times its depth (<= max depth)
+FLIP_GRAD_MAX = 2e-2      # a flipping splat's own gradient term at one pixel, normalised
+FLIP_PIX_FRAC = 2e-2      # the flagged pixels stay a small fraction of the image (measured <= 1.0 %)
 
 
 @pytest.fixture(scope="module")
@@ -37,7 +49,7 @@ def dev():
     return torch.device("cuda:0")
 
 
-def _check(C, O, s, dev, colors=None, cov3D=None, use_sh=True, degree=None, report=None):
+def _check(C, O, s, dev, colors=None, cov3D=None, use_sh=True, degree=None, report=None, pix_frac=FLIP_PIX_FRAC):
     d = to_dev(s, dev)
     col_t = None if colors is None else torch.tensor(colors, device=dev)
     cov_t = None if cov3D is None else torch.tensor(cov3D, device=dev)
@@ -46,8 +58,11 @@ def _check(C, O, s, dev, colors=None, cov3D=None, use_sh=True, degree=None, repo
     nr, color, depth, radii, st = o_forward(O, s, colors=colors, cov3D=cov3D, use_sh=use_sh, degree=degree)
     assert fwd[0] == nr, f"num_rendered {fwd[0]} != oracle {nr}"
     assert np.array_equal(fwd[3].cpu().numpy(), radii), "radii differ"
-    cmax, cfrac = image_parity(fwd[1].cpu().numpy(), color)
-    dmax, dfrac = image_parity(fwd[2].cpu().numpy(), depth, atol=IMG_ATOL * max(1.0, float(np.abs(depth).max())))
+    pflag, gflag = O.flip_flags(st, FLIP_BAND_ALPHA, FLIP_BAND_T) if st is not None else (
+        np.zeros((s["H"], s["W"]), np.uint8), np.zeros(len(radii), np.uint8))
+    cerr = np.abs(fwd[1].cpu().numpy().astype(np.float64) - color).max(0)
+    derr = np.abs(fwd[2].cpu().numpy().astype(np.float64) - depth)[0]
+    dscale = max(1.0, float(np.abs(depth).max()))
     g, _ = make_upstream_grad(color)
     g = g * (3 * s["W"] * s["H"])
     grads_c = c_backward(C, s, d, fwd, torch.tensor(g, device=dev), colors=col_t, cov3D=cov_t, use_sh=use_sh,
@@ -56,21 +71,30 @@ def _check(C, O, s, dev, colors=None, cov3D=None, use_sh=True, degree=None, repo
     grads_o = o_backward(O, s, st, radii, g, colors=colors, cov3D=cov3D, use_sh=use_sh, degree=degree)
     names = ["dL_dmeans2D", "dL_dcolors", "dL_dopacity", "dL_dmeans3D", "dL_dcov3D", "dL_dsh", "dL_dscales",
              "dL_drotations"]
-    res = {"L": nr, "color": (cmax, cfrac), "depth": (dmax, dfrac)}
+    flagged = pflag != 0
+    res = {"L": nr, "flagged_pix": int(flagged.sum()), "flagged_gauss": int((gflag != 0).sum()),
+           "color": split_max(cerr, flagged), "depth": split_max(derr, flagged)}
     for n, a, b in zip(names, grads_c, grads_o):
         a = a.cpu().numpy()
         assert a.shape == b.shape, f"{n} shape {a.shape} != {b.shape}"
         if a.size:
             assert np.isfinite(a).all(), f"{n} has non-finite values"
-        res[n] = grad_parity(a, b)
+        res[n] = split_max(grad_errors(a, b), gflag != 0)
     if report is not None:
         report.append(res)
     print(res)
-    assert cfrac <= IMG_FRAC and cmax < 0.05, f"color parity {cmax:.3e} / {cfrac:.2e}"
-    assert dfrac <= IMG_FRAC, f"depth parity {dmax:.3e} / {dfrac:.2e}"
+    # (max over unflagged, max over flagged) for every quantity
+    assert flagged.mean() <= pix_frac, f"{flagged.mean():.2e} of the pixels flagged"
+    assert res["color"][0] <= IMG_ATOL, f"colour: unflagged pixel off by {res['color'][0]:.3e} at " \
+                                         f"{np.unravel_index(np.argmax(np.where(flagged, 0, cerr)), cerr.shape)}"
+    assert res["color"][1] <= FLIP_COLOR_MAX, f"colour: flagged pixel off by {res['color'][1]:.3e}"
+    assert res["depth"][0] <= IMG_ATOL * dscale, f"depth: unflagged pixel off by {res['depth'][0]:.3e} at " \
+                                                  f"{np.unravel_index(np.argmax(np.where(flagged, 0, derr)), derr.shape)}"
+    assert res["depth"][1] <= FLIP_DEPTH_REL * dscale, f"depth: flagged pixel off by {res['depth'][1]:.3e}"
     for n in names:
-        emax, efrac = res[n]
-        assert efrac <= GRAD_FRAC, f"{n}: {efrac:.3e} of Gaussians beyond {GRAD_RTOL} (max {emax:.3e})"
+        unf, fl = res[n]
+        assert unf <= GRAD_RTOL, f"{n}: an unflagged Gaussian off by {unf:.3e} of the tensor's max"
+        assert fl <= FLIP_GRAD_MAX, f"{n}: a flagged Gaussian off by {fl:.3e} of the tensor's max"
     return fwd, grads_c
 
 
@@ -130,7 +154,8 @@ def test_parity_long_tiles(C, oracle, dev):
     over a 12-tile image (9k-16k instances per tile) exercise the per-tile sort's global merge steps."""
     s = make_scene(30000, 64, 48, seed=19, log_scale=math.log(0.3))
     s["opacities"] = np.full_like(s["opacities"], 0.03)
-    fwd, _ = _check(C, oracle, s, dev)
+    # thousands of faint splats per pixel: ~6 % of the pixels hold a near-1/255 splat
+    fwd, _ = _check(C, oracle, s, dev, pix_frac=0.1)
     assert fwd[0] > 12 * 4096
 
 
@@ -194,13 +219,21 @@ def test_metric_config_properties(C, oracle, dev):
     _check(C, oracle, s, dev)
 
 
-@pytest.mark.parametrize("cfg", ["c4_per_view", "c5_broom"])
+@pytest.mark.parametrize("cfg", ["c2_800", "c4_per_view", "c5_broom"])
 def test_large_configs(C, oracle, dev, cfg):
-    """BASELINE configs C4 (300k Gaussians, 1352x1014, one view of the 8-GPU run) and C5 (1M Gaussians,
-    960x536): full parity with the oracle at those sizes."""
+    """BASELINE configs C2 (100k Gaussians, 800x800), C4 (300k Gaussians, 1352x1014, one view of the
+    8-GPU run) and C5 (1M Gaussians, 960x536): full parity with the oracle at those sizes."""
     from gs4d_train.synthetic import CONFIGS
     P, W, H = CONFIGS[cfg]
     s = make_scene(P, W, H, seed=21)
+    _check(C, oracle, s, dev)
+
+
+def test_train_like_scene(C, oracle, dev):
+    """The bench's second workload (make_train_like_scene: a k-NN-initialised point cloud as
+    create_from_pcd leaves it, ~1,200 instances per touched tile, runs sorted by tile_sort_kernel)."""
+    from gs4d_train.synthetic import make_train_like_scene
+    s = make_train_like_scene(100_000, 1352, 1014, seed=0)
     _check(C, oracle, s, dev)
 
 
@@ -214,10 +247,11 @@ def test_parity_mid_tiles(C, oracle, dev):
 
 
 def test_capacity_prediction_both_ways(C, oracle, dev):
-    """The forward launches the binning against a capacity predicted from the previous call: a scene
-    with ~20x more instances than its predecessor overflows it (relaunch at the exact size), and the
-    small scene after it runs in an oversized buffer; both must match the oracle, backward included
-    (the backward re-carves the buffer with the forward's capacity)."""
+    """Scenes of very different sizes back to back through the same caller-owned buffers: the binning
+    buffer is resized from the host's exact num_rendered on every call (the Resizer of torch_glue.cpp, as
+    rasterizer_impl.cu:283-290 does), so a scene with ~20x more instances than its predecessor grows it
+    and the small scene after it runs in a buffer carved for its own size; all three must match the
+    oracle, backward included (the backward re-carves the buffers from num_rendered)."""
     small = make_scene(2000, 256, 192, seed=23)
     big = make_scene(40000, 512, 384, seed=24, log_scale=math.log(0.05))
     _check(C, oracle, small, dev)
