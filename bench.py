@@ -55,6 +55,9 @@ def parse_args(argv=None):
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="metric")
+    ap.add_argument("--scene", default="synthetic", choices=["synthetic", "train_like"],
+                    help="synthetic: the SURVEY §8d scene (the metric); train_like: make_train_like_scene "
+                         "(profiling of the second workload)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-train-step", action="store_true", help="skip the full train-step timing")
@@ -110,7 +113,11 @@ def main(argv=None):
 
     P, W, H = CONFIGS[args.config]
     # rank r renders its own view: same scene statistics, per-rank seed
-    s = make_scene(P, W, H, seed=rank)
+    if args.scene == "train_like":
+        from gs4d_train.synthetic import make_train_like_scene
+        s = make_train_like_scene(P, W, H, seed=rank)
+    else:
+        s = make_scene(P, W, H, seed=rank)
     scene = upload_scene(s, dev)
     step = make_step(scene, dev, rank, dgr._C, dist)
     elapsed, nr = timed_steps(step, args.steps, args.warmup, dist)
