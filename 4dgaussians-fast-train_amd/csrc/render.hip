@@ -72,21 +72,21 @@ __device__ __forceinline__ void issue_raw(RawSplat &r, bool valid, uint32_t ge, 
         }
     }
 }
-// The alpha test of forward.cu:346-348, alpha = min(0.99, o G) >= 1/255, taken on G against the splat's
-// gate (1/255) / o: one compare per pixel and no product before it (the backward needs o G only for the
-// pixels that pass).  Both kernels use this same test, so their decisions agree; against o G >= 1/255
-// it can differ only where o G rounds to within an ulp of 1/255 (a threshold flip).
-__device__ __forceinline__ float alpha_gate(float o) { return (1.0f / 255.0f) / o; }
+// The alpha test of forward.cu:346-348 / backward.cu:486-490 is taken exactly as the reference states
+// it: alpha = min(0.99, o G) >= 1/255, i.e. the rounded product o G >= 1/255 (the cap is above the
+// threshold).  opc.z holds 1/o (0 for o = 0): the backward accumulates its moments on o G dL/dalpha and
+// divides by o once per splat record.
+constexpr float kAlphaMin = 1.0f / 255.0f;
+__device__ __forceinline__ float inv_opacity(float o) { return o > 0.f ? 1.0f / o : 0.f; }
 
 __device__ __forceinline__ void to_regs(SplatRegs &s, bool valid, const RawSplat &r) {
     if (valid) {
         s.geo = make_float4(r.p.x, r.p.y, (-0.5f * r.co.x) * kLog2e, (-r.co.y) * kLog2e);
-        s.opc = make_float4((-0.5f * r.co.z) * kLog2e, r.co.w, alpha_gate(r.co.w), 0.f);
+        s.opc = make_float4((-0.5f * r.co.z) * kLog2e, r.co.w, inv_opacity(r.co.w), 0.f);
         s.col = make_float4(r.c.x, r.c.y, r.c.z, 0.f);
         s.reach = r.ge >> kReachShift;
     } else {
-        s.geo = s.opc = s.col = make_float4(0.f, 0.f, 0.f, 0.f);
-        s.opc.z = __builtin_inff();  // the zero splat passes no pixel
+        s.geo = s.opc = s.col = make_float4(0.f, 0.f, 0.f, 0.f);  // opacity 0: the zero splat passes no pixel
         s.reach = 0;
     }
 }
@@ -301,12 +301,11 @@ __global__ __launch_bounds__(64) void render_forward_kernel(Args a, const uint2 
             const float2 rp = raw.p;
             const float4 rco = raw.co;
             nxt.geo = make_float4(rp.x, rp.y - yc, (-0.5f * rco.x) * kLog2e, (-rco.y) * kLog2e);
-            nxt.opc = make_float4((-0.5f * rco.z) * kLog2e, rco.w, alpha_gate(rco.w), 0.f);
+            nxt.opc = make_float4((-0.5f * rco.z) * kLog2e, rco.w, 0.f, 0.f);
             nxt.col = make_float4(raw.c.x, raw.c.y, raw.c.z, s_raw.cd[4 * lane + 3]);  // rgb, view depth
             nxt.reach = rnxt;
         } else {
-            nxt.geo = nxt.opc = nxt.col = make_float4(0.f, 0.f, 0.f, 0.f);
-            nxt.opc.z = __builtin_inff();
+            nxt.geo = nxt.opc = nxt.col = make_float4(0.f, 0.f, 0.f, 0.f);  // opacity 0: passes no pixel
             nxt.reach = 0;
         }
         const uint64_t reach[2] = {ballot(nxt.reach & 1u), ballot(nxt.reach & 2u)};
@@ -327,8 +326,8 @@ __global__ __launch_bounds__(64) void render_forward_kernel(Args a, const uint2 
                 const float dx = geo.x - pfx;
                 const float pa = geo.z * dx * dx, pb = geo.w * dx;
                 const Falloff f = falloff(geo, opc, pa, pb, yl[h]);
-                uint64_t m0 = ballot(f.G.x >= opc.z) & alive[2 * h];  // alpha >= 1/255 (alpha_gate)
-                uint64_t m1 = ballot(f.G.y >= opc.z) & alive[2 * h + 1];
+                uint64_t m0 = ballot(f.alpha.x >= kAlphaMin) & alive[2 * h];  // forward.cu:346-348
+                uint64_t m1 = ballot(f.alpha.y >= kAlphaMin) & alive[2 * h + 1];
                 if ((nonpd >> j) & 1) {  // forward.cu:341-342
                     m0 &= ballot(f.pw.x <= 0.0f);
                     m1 &= ballot(f.pw.y <= 0.0f);
@@ -469,9 +468,10 @@ struct BwdPixels {
 };
 
 // One half tile of one splat of the reverse walk: updates the half's pixel state and adds its
-// per-lane partial sums (moments of u = G dL/dalpha in the tile-centred row coordinate yl, and the
-// colour sums) to U0..U2 / W0..W2.  The falloff is the forward's sequence (falloff()) on operand pairs:
-// identical blend decisions.  Branch-free, so that the pair walk below is one basic block.
+// per-lane partial sums (moments of u' = o G dL/dalpha in the tile-centred row coordinate yl -- the
+// record divides them by o once -- and the colour sums) to U0..U2 / W0..W2.  The falloff is the
+// forward's sequence (falloff()) on operand pairs: identical blend decisions.  Branch-free, so that the
+// pair walk below is one basic block.
 //   ALL: the splat lies below every pixel's n_contrib (the contributor test passes; pixels outside
 //        the image have T = dL/dpix = 0 and contribute exact zeros).
 //   GEN: the general splat: `chk` = its conic is not positive definite (power > 0 skips, forward.cu:341),
@@ -479,15 +479,15 @@ struct BwdPixels {
 template <bool ALL, bool GEN>
 __device__ __forceinline__ void half_step(f2 &T, f2 &A, const f2 dp0, const f2 dp1, const f2 dp2,
                                           const f2 Y2, const f2 C2, const f2 O2, const f2 R2, const f2 G2,
-                                          const f2 B2, const f2 pa2, const f2 pb2, f2 yl, f2 yl2, float gate, bool chk,
+                                          const f2 B2, const f2 pa2, const f2 pb2, f2 yl, f2 yl2, bool chk,
                                           uint32_t contributor, uint32_t last0, uint32_t last1, f2 &U0, f2 &U1,
                                           f2 &U2, f2 &W0, f2 &W1, f2 &W2) {
     const f2 dy = Y2 - yl;  // Y2 = my - yc
     const f2 pw = fma2(dy, fma2(C2, dy, pb2), pa2);
     const f2 G = f2{__builtin_amdgcn_exp2f(pw.x), __builtin_amdgcn_exp2f(pw.y)};
-    // backward.cu:486-497: contributor test, alpha < 1/255 (on G against the splat's gate, as the
-    // forward) and power > 0 skips -- the forward's decisions
-    bool k0 = G.x >= gate, k1 = G.y >= gate;
+    const f2 al = O2 * G;  // o G: min(0.99, o G) >= 1/255 iff o G >= 1/255
+    // backward.cu:486-497: contributor test, alpha < 1/255 and power > 0 skip -- the forward's decisions
+    bool k0 = al.x >= kAlphaMin, k1 = al.y >= kAlphaMin;
     if (!ALL) {
         k0 = k0 && contributor < last0;
         k1 = k1 && contributor < last1;
@@ -496,19 +496,19 @@ __device__ __forceinline__ void half_step(f2 &T, f2 &A, const f2 dp0, const f2 d
         k0 = k0 && (!chk || pw.x <= 0.0f);
         k1 = k1 && (!chk || pw.y <= 0.0f);
     }
-    // the skip applied to G; alpha of a skipped pixel is then min(0.99, o * 0) = 0 exactly
-    const f2 Ge = f2{k0 ? G.x : 0.f, k1 ? G.y : 0.f};
-    f2 ae = O2 * Ge;
-    if (GEN) ae = f2{fminf(0.99f, ae.x), fminf(0.99f, ae.y)};
+    // the skip applied to o G: a skipped pixel has alpha 0 exactly
+    const f2 ale = f2{k0 ? al.x : 0.f, k1 ? al.y : 0.f};
+    const f2 ae = GEN ? f2{fminf(0.99f, ale.x), fminf(0.99f, ale.y)} : ale;
     const f2 om = bc2(1.f) - ae;
     const f2 inv = f2{__builtin_amdgcn_rcpf(om.x), __builtin_amdgcn_rcpf(om.y)};
     const f2 Tn = T * inv;  // backward.cu:503
     T = Tn;
     const f2 diff = fma2(B2, dp2, fma2(G2, dp1, fma2(R2, dp0, -A)));  // c . dL/dpix - accum_rec . dL/dpix
-    const f2 dLda = diff * Tn;                  // backward.cu:519-534 (bg term in A's start value)
     A = fma2(ae, diff, A);                      // accum_rec for the next splat in front
-    const f2 u = Ge * dLda;
     const f2 w = ae * Tn;                       // dchannel_dcolor (backward.cu:521)
+    // u' = o G dL/dalpha = o G T diff (backward.cu:519-534, bg term in A's start value); without the
+    // cap o G T = w
+    const f2 u = (GEN ? ale * Tn : w) * diff;
     U0 += u;
     U1 = fma2(u, yl, U1);
     U2 = fma2(u, yl2, U2);
@@ -676,7 +676,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
                     if ((M[h] >> i) & 1)
                     half_step<ALL, GEN>(st.T[h], st.A[h], st.dp0[h], st.dp1[h], st.dp2[h], bc2(geo[i].y),
                                         bc2(opc[i].x), bc2(opc[i].y), bc2(col[i].x), bc2(col[i].y), bc2(col[i].z),
-                                        bc2(pa[i]), bc2(pb[i]), yl[h], yl2[h], opc[i].z, (nonpd >> (j + i)) & 1,
+                                        bc2(pa[i]), bc2(pb[i]), yl[h], yl2[h], (nonpd >> (j + i)) & 1,
                                         (uint32_t)(end - 1 - (j + i)), lastc[2 * h], lastc[2 * h + 1], U[i][0],
                                         U[i][1], U[i][2], U[i][3], U[i][4], U[i][5]);
 #pragma unroll
@@ -726,14 +726,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
             // centre row: dy = my_l - yl (backward.cu:545-551 moments of dy)
             const float4 r0 = s_rec[lane][0], r1 = s_rec[lane][1], r2 = s_rec[lane][2];
             const float my_l = s_sp[lane].geo.y;  // this lane's splat, my - yc
+            const float io = s_sp[lane].opc.z;    // 1 / o: the moments were taken on u' = o u
             // r0 = (S u, S dx u, S u yl, S dx^2 u), r1 = (S dx u yl, S u yl^2, W0, W1), r2 = (W2, -, -, -)
             const float s_u = r0.x, s_uyl = r0.z;
             const float v2 = my_l * s_u - s_uyl;                 // S u dy
             const float v4 = my_l * r0.y - r1.x;                 // S dx u dy
             const float v5 = my_l * v2 - (my_l * s_uyl - r1.y);  // S u dy^2
             float4 *rec = reinterpret_cast<float4 *>(contrib + (size_t)ucur * kContribStride);
-            rec[0] = make_float4(s_u, r0.y, v2, r0.w);
-            rec[1] = make_float4(v4, v5, r1.z, r1.w);
+            rec[0] = make_float4(s_u * io, r0.y * io, v2 * io, r0.w * io);
+            rec[1] = make_float4(v4 * io, v5 * io, r1.z, r1.w);
             rec[2] = r2;
         }
     }
