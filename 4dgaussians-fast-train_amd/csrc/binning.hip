@@ -245,12 +245,19 @@ __global__ __launch_bounds__(256) void emit_instances_kernel(Args a, GeomState g
             int x0, y0, x1, y1;
             getRect(xy[k].x, xy[k].y, rad[k], a.gx, a.gy, x0, y0, x1, y1);
             // row-major position in the rect: local = qd * wdt + rm by a float reciprocal and one
-            // correction step (exact for local < 2^20: the forward rejects grids of 2^20 tiles or more)
+            // correction step (exact for local < 2^20, i.e. for grids of fewer than 2^20 tiles; larger
+            // grids take the integer division)
             const int local = (int)(c - s_off[i]), wdt = x1 - x0;
-            int qd = (int)((float)local * __builtin_amdgcn_rcpf((float)wdt));
-            int rm = local - qd * wdt;
-            if (rm < 0) { qd--; rm += wdt; }
-            else if (rm >= wdt) { qd++; rm -= wdt; }
+            int qd, rm;
+            if (a.exact_div) {
+                qd = local / wdt;
+                rm = local - qd * wdt;
+            } else {
+                qd = (int)((float)local * __builtin_amdgcn_rcpf((float)wdt));
+                rm = local - qd * wdt;
+                if (rm < 0) { qd--; rm += wdt; }
+                else if (rm >= wdt) { qd++; rm -= wdt; }
+            }
             const int ty = y0 + qd, tx = x0 + rm;
             reach[k] = half_reach(xy[k].x, xy[k].y, co[k], tx, ty, a.W, a.H);
             if (reach[k] != 0) {

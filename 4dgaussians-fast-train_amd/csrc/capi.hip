@@ -227,8 +227,9 @@ int gs4d_forward_ex(gs4d_alloc_fn geometry_alloc, void *geometry_ctx, gs4d_alloc
     a.view_transposed = view_transposed ? 1 : 0;
     begin_marks(stream);
 
+    if ((int64_t)a.gx * a.gy >= (int64_t)1 << 30) return fail(GS4D_ERR_ARG, "forward: at most 2^30 - 1 tiles");
     const int T = a.gx * a.gy;
-    if (T >= (1 << 20)) return fail(GS4D_ERR_ARG, "forward: at most 2^20 - 1 tiles (16x16 pixels each)");
+    a.exact_div = T >= (1 << 20);  // the emission's float-reciprocal rect division is exact below 2^20 tiles
     char *gbuf = geometry_alloc(geometry_ctx, GeomState::required(P, T) + 16);
     if (!gbuf) return fail(GS4D_ERR_ALLOC, "forward: geometry buffer allocation failed");
     GeomState g = GeomState::carve(gbuf, P, T);

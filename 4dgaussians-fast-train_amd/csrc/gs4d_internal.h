@@ -87,6 +87,7 @@ struct Args {
     const float *viewmatrix, *projmatrix, *campos, *bg;
     int prefiltered;
     int view_transposed;  // the 16 view-matrix floats are stored transposed (a (1, 4)-strided 4x4 view)
+    int exact_div;        // grids of 2^20 tiles or more: the emission's rect position by integer div/mod
 };
 // The 4x4 column-major flat matrix m[0..15]; `transposed`: p holds its transpose (p[4 r + c] = m[4 c + r]),
 // which is how the reference's callers hand over world_view_transform (a transposed torch view).

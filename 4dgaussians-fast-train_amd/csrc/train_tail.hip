@@ -258,7 +258,7 @@ __global__ __launch_bounds__(kTailThreads) void deform_tail_bwd_kernel(
             if (g_dr) g_dr[4 * (size_t)i + c] = v;
         }
         const float y = opac[i];
-        const float go = g_opac ? g_opac[i] * (y * (1.f - y)) : 0.f;  // sigmoid backward
+        const float go = g_opac ? (g_opac[i] * (1.f - y)) * y : 0.f;  // sigmoid backward, torch's order
         d_o[i] = go;
         if (g_do) g_do[i] = go;
         return;

@@ -83,7 +83,10 @@ class HexPlaneField(nn.Module):
 
     def forward(self, pts, timestamps=None):
         """get_density (scene/hexplane.py:160-177): normalised (x, y, z, t) -> per-level plane products."""
-        if self.fused and pts.is_cuda and pts.dim() == 2 and timestamps is not None and timestamps.dim() == 2:
+        # the fused field differentiates w.r.t. the points only: timestamps that need a gradient take
+        # the grid_sample graph
+        if (self.fused and pts.is_cuda and pts.dim() == 2 and timestamps is not None and timestamps.dim() == 2
+                and not timestamps.requires_grad):
             from .kernels import hexplane, hexplane_points
             return hexplane(hexplane_points(pts, timestamps, self.aabb), [list(g) for g in self.grids])
         pts = normalize_aabb(pts, self.aabb)

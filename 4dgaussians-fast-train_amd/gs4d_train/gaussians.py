@@ -318,7 +318,7 @@ class GaussianModel:
         # data-parallel replicas select the same Gaussians (their statistics are all-reduced) but draw
         # from their own RNGs: rank 0's draws are the ones every replica uses
         from . import dp
-        if dp.world() > 1:
+        if getattr(self, "data_parallel_step", False) and dp.world() > 1:
             torch.distributed.broadcast(samples, src=0)
         rots = build_rotation(self._rotation[sel]).repeat(N, 1, 1)
         new_xyz = torch.bmm(rots, samples.unsqueeze(-1)).squeeze(-1) + self.get_xyz[sel].repeat(N, 1)

@@ -97,7 +97,10 @@ class _DeformTail(torch.autograd.Function):
     """The deformation's residual adds (scene/deformation.py:140-146, on features = cat(f_dc, f_rest),
     scene/gaussian_model.py:116-118) and render()'s activations exp / normalize / sigmoid
     (gaussian_renderer/__init__.py:97-99) in one HIP pass each way (gs4d_deform_tail_*).  A delta that
-    is None is a head switched off.  The gradient of each residual input is the gradient of its base."""
+    is None is a head switched off.  The gradient of each residual input is the gradient of its base.
+    Forward values match the torch graph bitwise; the backward follows torch's operation order for exp
+    and sigmoid (grad * (1 - y) * y) but restates normalize's backward in closed form, so it agrees
+    with autograd to fp32 rounding rather than bitwise (test_deform_tail_matches_torch: 1e-5)."""
 
     @staticmethod
     def forward(ctx, xyz, s, r, o, f_dc, f_rest, dx, ds, dr, d_o, dshs):

@@ -52,3 +52,9 @@ def ssim(img1, img2, window_size=11, size_average=True):
     if size_average:
         return ssim_map.mean()
     return ssim_map.mean(1).mean(1).mean(1)
+
+
+def psnr(img1, img2):
+    """utils/image_utils.py:17-30 without a mask: per-image 20 log10(1 / sqrt(MSE)), shape (B, 1)."""
+    mse = ((img1 - img2) ** 2).view(img1.shape[0], -1).mean(1, keepdim=True)
+    return 20 * torch.log10(1.0 / torch.sqrt(mse))

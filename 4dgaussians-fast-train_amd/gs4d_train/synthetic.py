@@ -121,3 +121,50 @@ def make_point_cloud(P, seed=0, extent=1.2):
     pts = rng.uniform(-extent, extent, (P, 3)).astype(np.float32)
     cols = rng.uniform(0, 1, (P, 3)).astype(np.float32)
     return pts, cols
+
+
+# ---- a synthetic dynamic scene (the stand-in for D-NeRF bouncingballs in the convergence test) ----------
+def look_at_camera(W, H, center, target=(0.0, 0.0, 0.0), time=0.0, fovx_deg=60.0):
+    """A Camera at `center` looking at `target` (world y up), in the reference's R/T convention
+    (R = world->camera rotation transposed, T = translation; scene/cameras.py, getWorld2View2)."""
+    c = np.asarray(center, np.float64)
+    fwd = np.asarray(target, np.float64) - c
+    fwd /= np.linalg.norm(fwd)
+    right = np.cross(np.array([0.0, 1.0, 0.0]), fwd)
+    right /= np.linalg.norm(right)
+    up = np.cross(fwd, right)
+    Rw2c = np.stack([right, up, fwd], 0)
+    return make_camera(W, H, fovx_deg=fovx_deg, R=Rw2c.T, T=-Rw2c @ c, time=time)
+
+
+def bouncing_balls(n_per_ball=1000, seed=0):
+    """Three coloured balls of Gaussians (sphere shells, isotropic splats) and their motion: ball k at
+    time t in [0, 1] is centred at base_k + (dx_k sin(2 pi t), h_k |sin(pi (t + phase_k))|, 0).
+    Returns (canonical dict of float32 arrays, a function t -> means3D at time t)."""
+    rng = np.random.default_rng(seed)
+    bases = np.array([[-0.6, -0.5, 0.0], [0.5, -0.5, 0.3], [0.0, -0.5, -0.5]])
+    amp = np.array([[0.3, 0.8], [0.25, 0.6], [0.35, 0.9]])
+    phase = np.array([0.0, 0.33, 0.66])
+    colors = np.array([[0.9, 0.15, 0.1], [0.1, 0.7, 0.2], [0.15, 0.3, 0.9]])
+    radius = 0.3
+    pts, cols, owner = [], [], []
+    for k in range(3):
+        d = rng.normal(size=(n_per_ball, 3))
+        d /= np.linalg.norm(d, axis=1, keepdims=True)
+        pts.append(d * radius)
+        cols.append(np.clip(colors[k] + rng.normal(0, 0.05, (n_per_ball, 3)), 0, 1))
+        owner.append(np.full(n_per_ball, k))
+    local, cols, owner = np.concatenate(pts), np.concatenate(cols), np.concatenate(owner)
+    P = local.shape[0]
+    shs = np.zeros((P, 16, 3), np.float32)
+    shs[:, 0, :] = (cols - 0.5) / SH_C0
+    rot = np.zeros((P, 4), np.float32)
+    rot[:, 0] = 1.0
+    canon = dict(scales=np.full((P, 3), 0.045, np.float32), rotations=rot,
+                 opacities=np.full((P, 1), 0.95, np.float32), shs=shs)
+
+    def means_at(t):
+        off = np.stack([amp[:, 0] * np.sin(2 * np.pi * t), amp[:, 1] * np.abs(np.sin(np.pi * (t + phase))),
+                        np.zeros(3)], 1)
+        return (local + bases[owner] + off[owner]).astype(np.float32)
+    return canon, means_at

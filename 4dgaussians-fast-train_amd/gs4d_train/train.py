@@ -123,7 +123,12 @@ def train_step(gaussians, views, opt, hyper, iteration, background, stage="fine"
             extent = getattr(gaussians, "cameras_extent", 1.0)
             if iteration > opt.densify_from_iter and iteration % opt.densification_interval == 0 and P < 360000:
                 size_threshold = 20 if iteration > opt.opacity_reset_interval else None
-                gaussians.densify(densify_threshold, opacity_threshold, extent, size_threshold)
+                # the split's random offsets are rank 0's on every replica only in a data-parallel step
+                gaussians.data_parallel_step = bool(data_parallel)
+                try:
+                    gaussians.densify(densify_threshold, opacity_threshold, extent, size_threshold)
+                finally:
+                    gaussians.data_parallel_step = False
             if iteration > opt.pruning_from_iter and iteration % opt.pruning_interval == 0 and \
                     gaussians.get_xyz.shape[0] > 200000:
                 size_threshold = 20 if iteration > opt.opacity_reset_interval else None

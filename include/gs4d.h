@@ -53,7 +53,7 @@ int gs4d_mark_visible(int P, const float *means3D, const float *viewmatrix, cons
 /* Replaces CudaRasterizer::Rasterizer::forward (rasterizer.h:31-57, rasterizer_impl.cu:198-339).
  * radii may be NULL (internal radii are then used).  *num_rendered receives the number of
  * (tile, Gaussian) instances L.  Limits (GS4D_ERR_ARG beyond them): P < 2^30, L < 2^30, fewer than
- * 2^20 16x16 tiles (images up to 16384 x 16368 pixels). */
+ * 2^30 16x16 tiles. */
 int gs4d_forward(gs4d_alloc_fn geometry_alloc, void *geometry_ctx, gs4d_alloc_fn binning_alloc, void *binning_ctx,
                  gs4d_alloc_fn image_alloc, void *image_ctx, int P, int D, int M, const float *background, int width,
                  int height, const float *means3D, const float *shs, const float *colors_precomp,

@@ -349,3 +349,26 @@ def test_view_matrix_layouts_agree(C, dev):
         outs.append([fwd[1], fwd[2], fwd[3], vis] + list(grads))
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+def test_grid_of_2pow20_tiles(C, oracle, dev):
+    """A grid of 2^20 tiles or more (16400 x 16400: 1,050,625 tiles): the emission locates a candidate in
+    its rectangle by exact integer division there (Args.exact_div) instead of the float reciprocal, and
+    the radix-sort binning takes 3 passes over the 21 tile bits.  num_rendered and radii exact, images
+    and gradients against the oracle (a few hundred splats: the image is mostly background)."""
+    s = make_scene(300, 16400, 16400, seed=27)
+    d = to_dev(s, dev)
+    fwd = c_forward(C, s, d)
+    torch.cuda.synchronize()
+    nr, color, depth, radii, st = o_forward(oracle, s)
+    assert fwd[0] == nr and np.array_equal(fwd[3].cpu().numpy(), radii)
+    pflag, gflag = oracle.flip_flags(st, FLIP_BAND_ALPHA, FLIP_BAND_T)
+    cerr = np.abs(fwd[1].cpu().numpy() - color).max(0)
+    assert split_max(cerr, pflag != 0)[0] <= IMG_ATOL
+    del cerr
+    g = np.sign(color - 0.5).astype(np.float32)
+    grads_c = c_backward(C, s, d, fwd, torch.tensor(g, device=dev))
+    torch.cuda.synchronize()
+    grads_o = o_backward(oracle, s, st, radii, g)
+    for a, b in zip(grads_c, grads_o):
+        assert split_max(grad_errors(a.cpu().numpy(), b), gflag != 0)[0] <= GRAD_RTOL
