@@ -17,7 +17,8 @@
 // sort's sharded digit histograms (no separate histogram pass); the sort is the library's onesweep
 // LSD sort (radix_sort.h); the box pass also lays the points out in sorted order (float4) so the
 // distance pass reads them contiguously; the distance pass keeps all box corners of its workgroup's
-// slice in LDS.  Distances are evaluated as (dx*dx + dy*dy) + dz*dz without contraction (compiled
+// slice in LDS and prunes inside a passing box by sub-boxes of 32 points (the same test one level
+// finer: it skips only points that cannot enter the 3 best, so the result is unchanged).  Distances are evaluated as (dx*dx + dy*dy) + dz*dz without contraction (compiled
 // with -ffp-contract=off), identically in the oracle.
 #include <algorithm>
 #include <cfloat>
@@ -31,6 +32,7 @@ constexpr int kKnnThreads = 256;
 constexpr int kKnnSortThreads = 1024;  // Morton-sort workgroup
 constexpr int kKnnSortItems = 4;       // keys per lane of the Morton sort (4096 per workgroup)
 constexpr int kKnnLdsBoxes = 2048;  // box corners staged in LDS per slice (64 KiB)
+constexpr int kKnnSub = 32;         // points per sub-box: the distance pass prunes inside a passing box by these
 
 // order-preserving float <-> u32 map for integer atomic min/max
 __device__ __forceinline__ uint32_t f2ord(float f) {
@@ -204,9 +206,35 @@ __device__ __forceinline__ void update3(float best[3], float d) {
     }
 }
 
+// Corners of every run of kKnnSub consecutive sorted points (a second, finer level of the reference's
+// boxes: a box that passes the distance test is scanned sub-box by sub-box, each with the same test).
+__global__ __launch_bounds__(kKnnThreads) void knn_subboxes_kernel(int P, const float4 *__restrict__ sorted,
+                                                                   KnnBox *__restrict__ sub) {
+    const int i = blockIdx.x * kKnnThreads + threadIdx.x;
+    const bool valid = i < P;
+    const float4 p = valid ? sorted[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    float mn[3] = {valid ? p.x : FLT_MAX, valid ? p.y : FLT_MAX, valid ? p.z : FLT_MAX};
+    float mx[3] = {valid ? p.x : -FLT_MAX, valid ? p.y : -FLT_MAX, valid ? p.z : -FLT_MAX};
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+#pragma unroll
+        for (int off = kKnnSub / 2; off > 0; off >>= 1) {  // inside 32-lane groups
+            mn[c] = fminf(mn[c], __shfl_xor(mn[c], off));
+            mx[c] = fmaxf(mx[c], __shfl_xor(mx[c], off));
+        }
+    }
+    if (valid && (i % kKnnSub) == 0) {
+        KnnBox b;
+        b.mn = make_float4(mn[0], mn[1], mn[2], 0.f);
+        b.mx = make_float4(mx[0], mx[1], mx[2], 0.f);
+        sub[i / kKnnSub] = b;
+    }
+}
+
 __global__ __launch_bounds__(kKnnThreads) void knn_dist_kernel(int P, const float4 *__restrict__ sorted,
                                                                const uint32_t *__restrict__ order,
                                                                const KnnBox *__restrict__ boxes, int nbox,
+                                                               const KnnBox *__restrict__ sub,
                                                                float *__restrict__ mean_dists) {
     __shared__ KnnBox s_box[kKnnLdsBoxes];
     const int idx = blockIdx.x * kKnnThreads + threadIdx.x;
@@ -228,9 +256,17 @@ __global__ __launch_bounds__(kKnnThreads) void knn_dist_kernel(int P, const floa
         for (int k = 0; k < nb; k++) {
             const float d = box_dist(s_box[k].mn, s_box[k].mx, p);
             if (d > reject || d > best[2]) continue;
+            // the box's points, sub-box by sub-box (simple_knn.cu:177-184 scans all 1024; the finer test
+            // only skips points that cannot enter the 3 best)
             const int lo = (b0 + k) * kKnnBox, hi = min(P, lo + kKnnBox);
-            for (int i = lo; i < hi; i++)
-                if (i != idx) update3(best, sqdist(p, sorted[i]));
+            for (int s0 = lo; s0 < hi; s0 += kKnnSub) {
+                const KnnBox sb = sub[s0 / kKnnSub];
+                const float ds = box_dist(sb.mn, sb.mx, p);
+                if (ds > reject || ds > best[2]) continue;
+                const int s1 = min(hi, s0 + kKnnSub);
+                for (int i = s0; i < s1; i++)
+                    if (i != idx) update3(best, sqdist(p, sorted[i]));
+            }
         }
     }
     if (live) mean_dists[order[idx]] = (best[0] + best[1] + best[2]) / 3.0f;
@@ -244,6 +280,7 @@ size_t knn_scratch_bytes(int P) {
     b += 4 * align_up(4 * (size_t)P, 256);                               // codes x2, order x2
     b += align_up(16 * (size_t)P, 256);                                  // sorted points
     b += align_up(sizeof(KnnBox) * nbox, 256);
+    b += align_up(sizeof(KnnBox) * (((size_t)P + kKnnSub - 1) / kKnnSub), 256);
     return b + 256;
 }
 
@@ -262,6 +299,7 @@ hipError_t launch_knn(int P, const float *pts, float *mean_dists, char *scratch,
     uint32_t *order[2] = {(uint32_t *)take(4 * (size_t)P), (uint32_t *)take(4 * (size_t)P)};
     float4 *sorted = (float4 *)take(16 * (size_t)P);
     KnnBox *boxes = (KnnBox *)take(sizeof(KnnBox) * nbox);
+    KnnBox *sub = (KnnBox *)take(sizeof(KnnBox) * (((size_t)P + kKnnSub - 1) / kKnnSub));
     uint32_t *bounds = zero, *err = zero + 8, *hist = zero + 64, *look = zero + 64 + kHistWords;
 
     hipError_t e = hipMemsetAsync(zero, 0, 4 * zero_words, s);
@@ -274,8 +312,10 @@ hipError_t launch_knn(int P, const float *pts, float *mean_dists, char *scratch,
                        bounds, codes[0], hist);
     const int cur = onesweep_sort<kKnnSortThreads, kKnnSortItems>(codes, order, P, nullptr, 30, hist, look, err, s);
     hipLaunchKernelGGL(knn_boxes_kernel, dim3(nbox), dim3(kKnnThreads), 0, s, P, pts, order[cur], sorted, boxes);
+    hipLaunchKernelGGL(knn_subboxes_kernel, dim3((P + kKnnThreads - 1) / kKnnThreads), dim3(kKnnThreads), 0, s, P,
+                       sorted, sub);
     hipLaunchKernelGGL(knn_dist_kernel, dim3((P + kKnnThreads - 1) / kKnnThreads), dim3(kKnnThreads), 0, s, P, sorted,
-                       order[cur], boxes, nbox, mean_dists);
+                       order[cur], boxes, nbox, sub, mean_dists);
     return hipGetLastError();
 }
 

@@ -102,3 +102,11 @@ def test_gpu_refuses_bad_input():
         distCUDA2(torch.zeros(4, 2, device="cuda"))
     with pytest.raises(RuntimeError):
         distCUDA2(torch.zeros(4, 3))  # CPU tensor: no CPU path
+
+
+@pytest.mark.gpu
+def test_gpu_uniform_cube(oracle):
+    # the train step's initial cloud (gs4d_train.synthetic.make_point_cloud: 100k points uniform in a cube)
+    from gs4d_train.synthetic import make_point_cloud
+    x, _ = make_point_cloud(100_000, seed=0)
+    np.testing.assert_array_equal(_dist_gpu(x), oracle.knn_mean_dist(x))
