@@ -15,7 +15,8 @@ def model_hidden_params(**over):
              kplanes_config={"grid_dimensions": 2, "input_coordinate_dim": 4, "output_coordinate_dim": 32,
                              "resolution": [64, 64, 64, 25]},
              multires=[1, 2, 4, 8], no_dx=False, no_grid=False, no_ds=False, no_dr=False, no_do=True, no_dshs=True,
-             empty_voxel=False, grid_pe=0, static_mlp=False, apply_rotation=False)
+             empty_voxel=False, grid_pe=0, static_mlp=False, apply_rotation=False,
+             mlp_dtype="fp32")  # this build's opt-in: "bf16" deformation MLP GEMMs (deformation.py)
     d.update(over)
     return SimpleNamespace(**d)
 

@@ -246,6 +246,89 @@ class _DeformHeads(torch.autograd.Function):
         return tuple(grads)
 
 
+def _sum0_f32(parts):
+    """parts (S, ...) -> their sum over S in fp32, as a (1 x S) @ (S x N) GEMM (torch's reduction over
+    a leading dimension of a few dozen rows is far slower here)."""
+    S = parts.shape[0]
+    flat = parts.reshape(S, -1).float()
+    return (torch.ones(1, S, device=parts.device) @ flat).view(parts.shape[1:])
+
+
+def _splitk_dw_bf16(dy, x):
+    """dy^T x over the P rows on bf16 operands (fp32 accumulate inside each chunk): split-K batched
+    GEMM (see _LinearSplitK for why), the chunk partials summed in fp32."""
+    P, c = x.shape[0], _LinearSplitK.kChunk
+    S = P // c
+    if S < 2:
+        return (dy.t() @ x).float()
+    dw = _sum0_f32(torch.bmm(dy[:S * c].unflatten(0, (S, c)).transpose(1, 2), x[:S * c].unflatten(0, (S, c))))
+    if P > S * c:
+        dw = dw + (dy[S * c:].t() @ x[S * c:]).float()
+    return dw
+
+
+def _colsum(x):
+    """x (P, n) -> its column sums (n,) in fp32: chunks of kChunk rows reduced over their middle dimension
+    (a contiguous-inner reduction), then the chunk partials (no N = 1 GEMM: hipBLASLt's host-side
+    heuristics for that shape cost milliseconds per call)."""
+    P, c = x.shape[0], _LinearSplitK.kChunk
+    S = P // c
+    out = x[:S * c].unflatten(0, (S, c)).sum(1, dtype=torch.float32).sum(0) if S else 0
+    if P > S * c:
+        out = out + x[S * c:].sum(0, dtype=torch.float32)
+    return out
+
+
+class _DeformHeadsBF16(torch.autograd.Function):
+    """The opt-in bf16 form of _DeformHeads (hyper.mlp_dtype = "bf16"): the same block -- ONE first-layer
+    GEMM for the k heads, bias + ReLU in its epilogue, the k second layers -- on bf16 operands with fp32
+    accumulation (hipBLASLt).  The first-layer output a is kept in bf16 (half the bytes of the fp32
+    block); the second layers write fp32 (aten addmm.dtype).  Backward: the k second layers' input
+    gradients as ONE GEMM against the block-diagonal second-layer weights, their weight gradients as
+    one split-K GEMM of the concatenated output gradients against a (the diagonal blocks kept), the
+    ReLU mask in bf16, then the first layer's split-K weight gradient and input gradient (fp32 out).
+    Parameters and their gradients stay fp32."""
+
+    @staticmethod
+    def forward(ctx, h, w1, b1, *second):
+        bf = torch.bfloat16
+        k = len(second) // 2
+        W = h.shape[1]
+        hb = h.to(bf)
+        w1b = w1.to(bf)
+        a = torch._addmm_activation(b1.to(bf), hb, w1b.t())  # (P, kW) bf16, relu(h w1^T + b1)
+        w2b = [second[2 * i].to(bf) for i in range(k)]
+        outs = [torch.addmm(second[2 * i + 1].to(bf), a[:, i * W:(i + 1) * W], w2b[i].t()).float() for i in range(k)]
+        ctx.save_for_backward(hb, a, w1b, *w2b)
+        ctx.W = W
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *douts):
+        bf = torch.bfloat16
+        hb, a, w1b, *w2b = ctx.saved_tensors
+        W, k = ctx.W, len(w2b)
+        P = a.shape[0]
+        ns = [x.shape[0] for x in w2b]
+        pad = -sum(ns) % 64  # GEMM dimensions in multiples of 64 (hipBLASLt's fast paths, host and device)
+        do32 = torch.cat([d if d is not None else torch.zeros(P, n, device=a.device) for d, n in zip(douts, ns)] +
+                         [torch.zeros(P, pad, device=a.device)], 1)
+        do = do32.to(bf)
+        # block-diagonal second-layer weights: row block i (head i's n_i outputs) x column block i (W)
+        w2bd = torch.cat([torch.block_diag(*w2b), torch.zeros(pad, k * W, dtype=bf, device=a.device)], 0)
+        da = torch.ops.aten.threshold_backward(do @ w2bd, a, 0)  # (P, kW) bf16, masked by the first ReLU
+        dw2full = _splitk_dw_bf16(do, a)                           # (sum n, kW): keep the diagonal blocks
+        db2full = _colsum(do32)
+        grads2, o = [], 0
+        for i in range(k):
+            grads2 += [dw2full[o:o + ns[i], i * W:(i + 1) * W].contiguous(), db2full[o:o + ns[i]]]
+            o += ns[i]
+        dw1 = _splitk_dw_bf16(da, hb)
+        db1 = _colsum(da)
+        dh = (da @ w1b).float()
+        return tuple([dh, dw1, db1] + grads2)
+
+
 class _FeatureReLU(torch.autograd.Function):
     """feature_out with defor_depth <= 1 (scene/deformation.py:51-55: ONE Linear(feat_dim, W)) followed by
     the ReLU every head starts with (:73-78): h = relu(x W^T + b) in one f32-MFMA pass (gs4d_feature_relu_forward).
@@ -284,6 +367,10 @@ class Deformation(nn.Module):
         self.pos_deform, self.scales_deform, self.rotations_deform = head(3), head(3), head(4)
         self.opacity_deform, self.shs_deform = head(1), head(16 * 3)
         self.fused_heads = False  # True: the heads as one _DeformHeads block (GPU training)
+        # "bf16" (opt-in, GPU): feature_out and the heads run their GEMMs on bf16 operands with fp32
+        # accumulation; parameters, their gradients and the heads' outputs stay fp32 (BASELINE C3's
+        # "bf16/fp32" train loop).  "fp32" (default) is the reference's precision.
+        self.mlp_dtype = getattr(args, "mlp_dtype", "fp32")
 
     def deltas(self, xyz, time):
         """The active heads' outputs {name: (P, n)} of forward_dynamic (scene/deformation.py:97-139),
@@ -298,8 +385,25 @@ class Deformation(nn.Module):
                                           ("shs_deform", a.no_dshs)) if not flag]
         return self._heads(self.grid(xyz, time), active)
 
+    def _heads_bf16(self, feat, active):
+        """The bf16 form of _heads: feature_out and its ReLU as on the fp32 path (a K = feat_dim layer,
+        cheap), then the heads block on bf16 operands (_DeformHeadsBF16).  The heads' outputs (the
+        deltas) are fp32, as are all parameters and gradients."""
+        lin = self.feature_out[0]
+        if len(self.feature_out) == 1 and (feat.shape[1], self.W) in _FeatureReLU.shapes and torch.is_grad_enabled():
+            h = _FeatureReLU.apply(feat.contiguous(), lin.weight, lin.bias)
+        else:
+            h = torch.relu(self.feature_out(feat))  # every head starts with ReLU (scene/deformation.py:73-78)
+        heads = [getattr(self, name) for name in active]
+        w1 = torch.cat([hd[1].weight for hd in heads], 0)
+        b1 = torch.cat([hd[1].bias for hd in heads], 0)
+        second = [t for hd in heads for t in (hd[3].weight, hd[3].bias)]
+        return dict(zip(active, _DeformHeadsBF16.apply(h.contiguous(), w1, b1, *second)))
+
     def _heads(self, feat, active):
         """{name: head output} of the active heads on the field features (feature_out, then the heads)."""
+        if self.mlp_dtype == "bf16" and feat.is_cuda and active:
+            return self._heads_bf16(feat, active)
         if self.fused_heads and feat.is_cuda and torch.is_grad_enabled() and active:
             heads = [getattr(self, name) for name in active]
             w1 = torch.cat([hd[1].weight for hd in heads], 0)

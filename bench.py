@@ -379,8 +379,9 @@ def train_step_timing(P, W, H, dev, world, rank, steps, warmup, dist, unfused=Tr
     from gs4d_train.synthetic import make_point_cloud, make_training_views
     from gs4d_train.train import train_step
 
-    def run(fused, n_steps, n_warm):
+    def run(fused, n_steps, n_warm, mlp_dtype="fp32"):
         hyper, opt = config.dynerf()
+        hyper.mlp_dtype = mlp_dtype
         torch.manual_seed(0)
         g = GaussianModel(3, hyper, fused=fused)
         pts, cols = make_point_cloud(P, seed=0)
@@ -410,6 +411,10 @@ def train_step_timing(P, W, H, dev, world, rank, steps, warmup, dist, unfused=Tr
            "image": f"{W}x{H}", "loss": round(loss, 6),
            "config": "arguments/dynerf/default.py (HexPlane 16 x [64,64,64,150], multires [1,2], MLP width 128, "
                      "opacity+SH deform), fused libgs4d HexPlane field + regularisers / L1 / densification stats / Adam kernels, deformation heads as one GEMM block with their second-layer backward in HIP (gs4d_heads_backward)"}
+    # BASELINE C3's "bf16/fp32": the same step with the deformation MLP's GEMMs on bf16 operands (opt-in,
+    # deformation.py _heads_bf16; the rasterizer and everything else stay fp32)
+    bms, bloss = run(True, steps, warmup, mlp_dtype="bf16")
+    res["bf16_mlp"] = {"ms": round(bms, 3), "loss": round(bloss, 6)}
     if unfused and world == 1:
         ums, _ = run(False, max(3, steps // 4), 2)
         res["reference_torch_tail_ms"] = round(ums, 3)

@@ -27,7 +27,8 @@ runs already differ by ~0.1 dB.  Hence two tests:
   * short horizon (no densification, 200 + 200 iterations): the two runs' held-out PSNR within 0.1 dB
     and their last-50-iteration mean losses within 1 %;
   * long horizon (the full miniature schedule, 3 seeds each): every run above PSNR_FLOOR, the mean
-    fused PSNR within PSNR_DELTA of the mean unfused PSNR.
+    fused PSNR within PSNR_DELTA of the mean unfused PSNR, and the same for the fused run with the
+    opt-in bf16 deformation MLP.
 """
 import copy
 import math
@@ -99,12 +100,13 @@ def _evaluate(g, views, bg):
     return float(np.mean(vals))
 
 
-def _train(dataset, fused, seed=0, k_coarse=K_COARSE, k_fine=K_FINE, densify=True, losses=None):
+def _train(dataset, fused, seed=0, k_coarse=K_COARSE, k_fine=K_FINE, densify=True, losses=None, mlp_dtype="fp32"):
     from gs4d_train import config
     from gs4d_train.gaussians import GaussianModel
     from gs4d_train.train import train_step
     train_views, test_views = dataset
     hyper, opt = config.dnerf()
+    hyper.mlp_dtype = mlp_dtype
     opt_c, opt_f = copy.copy(opt), copy.copy(opt)
     opt_c.iterations, opt_f.iterations = k_coarse, k_fine
     if not densify:
@@ -161,5 +163,10 @@ def test_long_horizon_psnr(dataset):
             assert test >= init + PSNR_GAIN, (fused, init, test)
     mf = float(np.mean([r[1] for r in res[True]]))
     mu = float(np.mean([r[1] for r in res[False]]))
-    print(f"mean test PSNR: fused {mf:.2f} dB, unfused {mu:.2f} dB")
+    # the opt-in bf16 deformation MLP (BASELINE C3's "bf16/fp32") trains the same scene as well
+    rb = [_train(dataset, True, seed=seed, mlp_dtype="bf16") for seed in range(3)]
+    mb = float(np.mean([r[1] for r in rb]))
+    print(f"mean test PSNR: fused {mf:.2f} dB, unfused {mu:.2f} dB, fused + bf16 MLP {mb:.2f} dB "
+          f"({', '.join(f'{r[1]:.2f}' for r in rb)})")
     assert abs(mf - mu) <= PSNR_DELTA, (mf, mu)
+    assert min(r[1] for r in rb) >= PSNR_FLOOR and abs(mb - mf) <= PSNR_DELTA, (mb, mf)

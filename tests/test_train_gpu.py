@@ -427,3 +427,42 @@ def test_deform_tail_matches_torch(heads):
     for a, b in zip(ga, gb):
         assert a.shape == b.shape
         assert float((a - b).abs().max()) <= 1e-5 * max(float(b.abs().max()), 1e-20)
+
+
+def test_train_step_bf16_mlp_tracks_fp32():
+    """The opt-in bf16 deformation MLP (hyper.mlp_dtype = "bf16", BASELINE C3's "bf16/fp32"): one fused
+    fine-stage step at C3's shape against the fp32 step from the same state.  bf16 operands carry 8
+    mantissa bits, so the bar is statistical: loss within 1 %, every parameter-gradient tensor within 5 %
+    of its norm (relative L2; measured <= 2.4 %, the means' gradient, which also flows through the
+    deformation)."""
+    from gs4d_train import config
+    from gs4d_train.gaussians import GaussianModel
+    from gs4d_train.synthetic import make_point_cloud, make_training_views
+    from gs4d_train.train import train_step
+    pts, cols = make_point_cloud(25000, seed=5)
+    views = make_training_views(2, 800, 800, seed=6)
+    bg = torch.ones(3, device="cuda")
+    runs = []
+    for dtype in ("fp32", "bf16"):
+        hyper, opt = config.dynerf()
+        hyper.mlp_dtype = dtype
+        opt.iterations = 0
+        torch.manual_seed(7)
+        g = GaussianModel(3, hyper, fused=True)
+        g.create_from_pcd(pts, cols, 1.0)
+        g._deformation.deformation_net.grid.fused = True
+        g._deformation.deformation_net.fused_heads = True
+        g.training_setup(opt)
+        g.active_sh_degree = 3
+        loss = float(train_step(g, views, opt, hyper, 3001, bg))
+        grads = {n: p.grad.detach().clone() for n, p in g._deformation.named_parameters() if p.grad is not None}
+        for name in ("_xyz", "_features_dc", "_features_rest", "_opacity", "_scaling", "_rotation"):
+            grads[name] = getattr(g, name).grad.detach().clone()
+        runs.append((loss, grads))
+    (la, ga), (lb, gb) = runs
+    assert abs(lb - la) <= 1e-2 * abs(la), (la, lb)
+    assert ga.keys() == gb.keys()
+    for k in ga:
+        assert gb[k].dtype == torch.float32, k
+        rel = float((gb[k] - ga[k]).norm() / ga[k].norm().clamp_min(1e-30))
+        assert rel <= 5e-2, (k, rel)
