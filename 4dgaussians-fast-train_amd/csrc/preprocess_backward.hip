@@ -9,8 +9,9 @@
 //    reduction, which replaces the reference's float atomics (backward.cu:523,545-554): bitwise
 //    deterministic, and balanced (one lane per record, whatever the splat sizes).
 // 2. gaussian_backward: the sums of the Gaussians whose records span waves, then K8 + K9 per
-//    Gaussian.  Every output element is written (zeros for culled Gaussians and for SH coefficients
-//    >= (D+1)^2), so no zero-fill pass is needed.
+//    Gaussian except K9's SH part, which sh_backward runs after it with the block's coefficient
+//    rows staged through LDS (coalesced loads and stores).  Every output element is written (zeros for culled Gaussians and for
+//    SH coefficients >= (D+1)^2), so no zero-fill pass is needed.
 #include <algorithm>
 
 #include "gs4d_internal.h"
@@ -139,10 +140,9 @@ __global__ __launch_bounds__(256) void contrib_segments_kernel(const uint32_t *_
 // following wave up to the one holding its last slot -- and a Gaussian without instances gets zeros.
 __global__ __launch_bounds__(256) void gaussian_backward_kernel(
     Args a, GeomState g, const int *__restrict__ radii, const float *__restrict__ means3D,
-    const float *__restrict__ shs, const float *__restrict__ scales, const float *__restrict__ rotations,
-    const float *__restrict__ cov3Ds, const float *dL_dmean2D, const float4 *dL_dconic,
-    const float *dL_dcolor, float *__restrict__ dL_dmean3D, float *__restrict__ dL_dcov3D,
-    float *__restrict__ dL_dsh, float *__restrict__ dL_dscale, float *__restrict__ dL_drot,
+    const float *__restrict__ scales, const float *__restrict__ rotations, const float *__restrict__ cov3Ds,
+    const float *dL_dmean2D, const float4 *dL_dconic, float *__restrict__ dL_dmean3D,
+    float *__restrict__ dL_dcov3D, float *__restrict__ dL_dscale, float *__restrict__ dL_drot,
     const uint32_t *__restrict__ e_first, const float4 *__restrict__ part, GradOut o) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= a.P) return;
@@ -164,8 +164,6 @@ __global__ __launch_bounds__(256) void gaussian_backward_kernel(
     V3 dmean = v3(0, 0, 0);
     V3 dscale = v3(0, 0, 0);
     float4 drot = make_float4(0, 0, 0, 0);
-    float *dsh = shs ? dL_dsh + (size_t)idx * a.M * 3 : nullptr;
-    int nsh_written = 0;
     if (radii[idx] > 0) {
         const Mat4 view = load_mat4(a.viewmatrix, a.view_transposed), projm = load_mat4(a.projmatrix);
         const V3 m = v3(means3D[3 * idx], means3D[3 * idx + 1], means3D[3 * idx + 2]);
@@ -188,47 +186,12 @@ __global__ __launch_bounds__(256) void gaussian_backward_kernel(
         dm2.y = (proj[4] * m_w - proj[7] * mul1) * g2x + (proj[5] * m_w - proj[7] * mul2) * g2y;
         dm2.z = (proj[8] * m_w - proj[11] * mul1) * g2x + (proj[9] * m_w - proj[11] * mul2) * g2y;
         dmean = dmean + dm2;
-        // SH part (backward.cu:390-391)
-        if (shs) {
-            const float *sh = shs + (size_t)idx * a.M * 3;
-            const uint8_t cl = g.clamped[idx];
-            V3 dRGB = v3(dL_dcolor[3 * idx] * ((cl & 1) ? 0.f : 1.f), dL_dcolor[3 * idx + 1] * ((cl & 2) ? 0.f : 1.f),
-                         dL_dcolor[3 * idx + 2] * ((cl & 4) ? 0.f : 1.f));
-            V3 dir_orig = m - load_v3(a.campos);
-            if (a.M == 16 && (((size_t)shs | (size_t)dL_dsh) & 15) == 0) {
-                // degree-3 layout (192 B per Gaussian, 16-byte aligned): the coefficients in and their
-                // gradients out as 12 float4 each instead of 48 scalar accesses strided 192 B over the lanes
-                float shl[48], dl[48];
-                const float4 *s4 = reinterpret_cast<const float4 *>(sh);
-#pragma unroll
-                for (int q = 0; q < 12; q++) {
-                    const float4 v = s4[q];
-                    shl[4 * q] = v.x, shl[4 * q + 1] = v.y, shl[4 * q + 2] = v.z, shl[4 * q + 3] = v.w;
-                }
-#pragma unroll
-                for (int q = 0; q < 48; q++) dl[q] = 0.f;
-                dmean = dmean + sh_backward(a.D, shl, dir_orig, dRGB, dl);
-                float4 *d4 = reinterpret_cast<float4 *>(dsh);
-#pragma unroll
-                for (int q = 0; q < 12; q++) d4[q] = make_float4(dl[4 * q], dl[4 * q + 1], dl[4 * q + 2], dl[4 * q + 3]);
-                nsh_written = 16;  // zeros included
-            } else {
-                dmean = dmean + sh_backward(a.D, sh, dir_orig, dRGB, dsh);
-                nsh_written = (a.D + 1) * (a.D + 1);
-            }
-        }
+        // SH part (backward.cu:390-391): sh_backward_kernel, launched next
         // cov3D part (backward.cu:394-395)
         if (scales) {
             V3 sc = v3(scales[3 * idx], scales[3 * idx + 1], scales[3 * idx + 2]);
             float4 rot = reinterpret_cast<const float4 *>(rotations)[idx];
             cov3D_backward(sc, a.scale_modifier, rot, dcov, dscale, drot);
-        }
-    }
-    if (dsh) {
-        for (int k = nsh_written; k < a.M; k++) {
-            dsh[3 * k + 0] = 0.f;
-            dsh[3 * k + 1] = 0.f;
-            dsh[3 * k + 2] = 0.f;
         }
     }
     dL_dmean3D[3 * idx + 0] = dmean.x;
@@ -240,6 +203,82 @@ __global__ __launch_bounds__(256) void gaussian_backward_kernel(
     dL_dscale[3 * idx + 1] = dscale.y;
     dL_dscale[3 * idx + 2] = dscale.z;
     reinterpret_cast<float4 *>(dL_drot)[idx] = drot;
+}
+
+// K9's SH part (backward.cu:390-391 -> computeColorFromSH backward, :20-139), one thread per Gaussian
+// with the block's coefficient rows staged through LDS: the block reads its 128 rows of 3M floats
+// (one contiguous span, float4 when M = 16 and aligned) into a 49-float-stride tile (odd stride: a
+// wave's rows hit distinct banks), each thread takes its row into registers, writes its gradients back
+// into the same row (zeros past (D + 1)^2 and for culled Gaussians) and adds the view-direction term to
+// dL/dmean3D after gaussian_backward's covariance + projection terms (the reference's order, :390), and
+// the block stores the tile as one contiguous span.  A thread per Gaussian straight from global memory
+// (192-byte strided rows) took 12.6 us of gaussian_backward's 26 at P = 100k.
+constexpr int kShThreads = 128, kShRow = 49;
+
+template <bool kVec4>
+__global__ __launch_bounds__(kShThreads) void sh_backward_kernel(Args a, const int *__restrict__ radii,
+                                                                 const float *__restrict__ means3D,
+                                                                 const float *__restrict__ shs,
+                                                                 const uint8_t *__restrict__ clamped,
+                                                                 const float *__restrict__ dL_dcolor,
+                                                                 float *__restrict__ dL_dmean3D,
+                                                                 float *__restrict__ dL_dsh) {
+    __shared__ float tile[kShThreads * kShRow];
+    const int g0 = blockIdx.x * kShThreads;
+    // rows of M > 16 coefficients: only the first 16 can be used (D <= 3); the rest get zeros
+    const int n = min(kShThreads, a.P - g0), row = 3 * a.M, rowl = min(row, 48);
+    const size_t base = (size_t)g0 * row;
+    const int total = n * row;
+    if (kVec4) {  // row = 48 = 12 float4
+        const float4 *s4 = reinterpret_cast<const float4 *>(shs + base);
+        for (int i = threadIdx.x; i < total / 4; i += kShThreads) {
+            const int r = i / 12, c = (i - r * 12) * 4;
+            const float4 v = s4[i];
+            float *t = tile + r * kShRow + c;
+            t[0] = v.x, t[1] = v.y, t[2] = v.z, t[3] = v.w;
+        }
+    } else {
+        for (int i = threadIdx.x; i < total; i += kShThreads) {
+            const int r = i / row, c = i - r * row;
+            if (c < 48) tile[r * kShRow + c] = shs[base + i];
+        }
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < n) {
+        const int idx = g0 + threadIdx.x;
+        float *trow = tile + threadIdx.x * kShRow;
+        float shl[48];
+#pragma unroll
+        for (int k = 0; k < 48; k++) {
+            shl[k] = k < rowl ? trow[k] : 0.f;
+            if (k < rowl) trow[k] = 0.f;
+        }
+        if (radii[idx] > 0) {
+            const uint8_t cl = clamped[idx];
+            const V3 dRGB = v3(dL_dcolor[3 * idx] * ((cl & 1) ? 0.f : 1.f),
+                               dL_dcolor[3 * idx + 1] * ((cl & 2) ? 0.f : 1.f),
+                               dL_dcolor[3 * idx + 2] * ((cl & 4) ? 0.f : 1.f));
+            const V3 m = v3(means3D[3 * idx], means3D[3 * idx + 1], means3D[3 * idx + 2]);
+            const V3 dm = sh_backward(a.D, shl, m - load_v3(a.campos), dRGB, trow);
+            dL_dmean3D[3 * idx + 0] += dm.x;
+            dL_dmean3D[3 * idx + 1] += dm.y;
+            dL_dmean3D[3 * idx + 2] += dm.z;
+        }
+    }
+    __syncthreads();
+    if (kVec4) {
+        float4 *d4 = reinterpret_cast<float4 *>(dL_dsh + base);
+        for (int i = threadIdx.x; i < total / 4; i += kShThreads) {
+            const int r = i / 12, c = (i - r * 12) * 4;
+            const float *t = tile + r * kShRow + c;
+            d4[i] = make_float4(t[0], t[1], t[2], t[3]);
+        }
+    } else {
+        for (int i = threadIdx.x; i < total; i += kShThreads) {
+            const int r = i / row, c = i - r * row;
+            dL_dsh[base + i] = c < 48 ? tile[r * kShRow + c] : 0.f;
+        }
+    }
 }
 
 size_t contrib_scratch_bytes(int R, int P) {
@@ -275,10 +314,16 @@ hipError_t launch_gaussian_backward(const Args &a, GeomState g, int R, char *scr
                                     const float *cov3D, float *dL_dmean2D, float4 *dL_dconic, float *dL_dopacity,
                                     float *dL_dcolor, float *dL_dmean3D, float *dL_dcov3D, float *dL_dsh,
                                     float *dL_dscale, float *dL_drot, hipStream_t s) {
-    hipLaunchKernelGGL(gaussian_backward_kernel, dim3((a.P + 255) / 256), dim3(256), 0, s, a, g, radii, means3D, shs,
-                       scales, rotations, cov3D, dL_dmean2D, dL_dconic, dL_dcolor, dL_dmean3D, dL_dcov3D, dL_dsh,
+    hipLaunchKernelGGL(gaussian_backward_kernel, dim3((a.P + 255) / 256), dim3(256), 0, s, a, g, radii, means3D,
+                       scales, rotations, cov3D, dL_dmean2D, dL_dconic, dL_dmean3D, dL_dcov3D,
                        dL_dscale, dL_drot, scratch_e_first(scratch, R), scratch_part(scratch),
                        grad_out(a, g, dL_dmean2D, dL_dconic, dL_dopacity, dL_dcolor));
+    if (shs) {
+        const bool vec4 = a.M == 16 && (((size_t)shs | (size_t)dL_dsh) & 15) == 0;
+        hipLaunchKernelGGL(vec4 ? sh_backward_kernel<true> : sh_backward_kernel<false>,
+                           dim3((a.P + kShThreads - 1) / kShThreads), dim3(kShThreads), 0, s, a, radii, means3D, shs,
+                           g.clamped, dL_dcolor, dL_dmean3D, dL_dsh);
+    }
     return hipGetLastError();
 }
 

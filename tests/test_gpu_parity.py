@@ -111,6 +111,24 @@ def test_parity_sh(C, oracle, dev, P, W, H, seed, deg):
     _check(C, oracle, s, dev)
 
 
+@pytest.mark.parametrize("M,deg", [(4, 1), (9, 2), (25, 3)])
+def test_parity_sh_row_widths(C, oracle, dev, M, deg):
+    """Coefficient rows other than the 16 of degree 3 (the SH backward's scalar staging path): rows of
+    exactly (D+1)^2, and 25 > 16 coefficients whose tail gets zero gradients (backward.cu:20-139 writes
+    only the (D+1)^2 it uses; the dL_dsh tensor starts zeroed, rasterize_points.cu)."""
+    s = make_scene(2000, 160, 96, seed=30 + M, sh_degree=deg)
+    sh = np.zeros((2000, M, 3), np.float32)
+    k = min(M, 16)
+    sh[:, :k] = s["shs"][:, :k]
+    if M > 16:
+        sh[:, 16:] = np.random.default_rng(M).normal(0, 0.1, (2000, M - 16, 3))
+    s["shs"] = sh
+    _, grads = _check(C, oracle, s, dev)
+    dsh = grads[5]  # (dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, ...)
+    assert tuple(dsh.shape) == (2000, M, 3)
+    assert not bool(dsh[:, (deg + 1) ** 2:].any())
+
+
 def test_parity_bg_black(C, oracle, dev):
     s = make_scene(3000, 160, 96, seed=7)
     s["bg"] = np.zeros(3, np.float32)
