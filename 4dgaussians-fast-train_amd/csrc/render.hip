@@ -130,6 +130,18 @@ __device__ __forceinline__ RawSplat read_raw_lds(const RawLDS &r, int lane, bool
     w.ge = 0;
     return w;
 }
+// the same for a wave that stages its own batch (no workgroup barrier: the other wave of the tile may
+// have retired)
+__device__ __forceinline__ RawSplat read_raw_lds_wave(const RawLDS &r, int lane) {
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
+    __builtin_amdgcn_wave_barrier();
+    RawSplat w;
+    w.co = r.co[lane];
+    w.c = make_float3(r.cd[4 * lane], r.cd[4 * lane + 1], r.cd[4 * lane + 2]);
+    w.p = make_float2(r.x[lane], r.y[lane]);
+    w.ge = 0;
+    return w;
+}
 
 // Falloff of one splat at a pixel pair: exponent (base 2) and G = 2^power2.  Forward and backward use
 // this one sequence, so they take identical blend decisions.
@@ -214,50 +226,74 @@ __device__ __forceinline__ void sort_run(uint32_t *__restrict__ seg, int n, cons
     }
 }
 
-__global__ __launch_bounds__(64) void render_forward_kernel(Args a, const uint2 *__restrict__ ranges,
-                                                            const uint32_t *__restrict__ order,
-                                                            uint32_t *__restrict__ upos,
-                                                            const float *__restrict__ depths,
-                                                            const uint32_t *__restrict__ gid_by_e,
-                                                            const float2 *__restrict__ xy,
-                                                            const float4 *__restrict__ conic_opacity,
-                                                            const float4 *__restrict__ rgbd,
-                                                            float *__restrict__ final_T,
-                                                            uint32_t *__restrict__ n_contrib,
-                                                            float *__restrict__ out_color,
-                                                            float *__restrict__ out_depth) {
-    __shared__ SplatLDS s_sp[64];
+// TWO waves per tile: wave h blends half tile h (rows 8h .. 8h + 7; lane l holds the pixel pair at rows
+// 8h + l/16 and 8h + l/16 + 4 of column l % 16), so a long tile's serial blend walk is split over two
+// waves.  With one wave per tile every tile of the metric scene was resident at once and the kernel's end
+// was set by the longest tiles walking alone on their SIMDs (a launch repeating every tile took only
+// 0.67 of the first pass's time per extra pass).  The short run's sort is done once, by wave 0, and
+// handed to wave 1 through LDS (the only cross-wave step, one barrier); each wave then stages and walks
+// the splats that reach its half on its own (LDS-DMA gathers, no barriers), and retires when its half's
+// pixels are all done.
+__global__ __launch_bounds__(128) void render_forward_kernel(Args a, const uint2 *__restrict__ ranges,
+                                                             const uint32_t *__restrict__ order,
+                                                             uint32_t *__restrict__ upos,
+                                                             const float *__restrict__ depths,
+                                                             const uint32_t *__restrict__ gid_by_e,
+                                                             const float2 *__restrict__ xy,
+                                                             const float4 *__restrict__ conic_opacity,
+                                                             const float4 *__restrict__ rgbd,
+                                                             float *__restrict__ final_T,
+                                                             uint32_t *__restrict__ n_contrib,
+                                                             float *__restrict__ out_color,
+                                                             float *__restrict__ out_depth) {
+    __shared__ SplatLDS s_sp_all[2][64];
+    __shared__ RawLDS s_raw_all[2];
+    __shared__ uint32_t s_ev[kWaveSortMax];
     const int tile = (int)__builtin_amdgcn_readfirstlane(order[blockIdx.x]);  // longest runs first
     const int tx = tile % a.gx, ty = tile / a.gx;
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const int h = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // this wave's half tile
+    SplatLDS *s_sp = s_sp_all[h];
+    RawLDS &s_raw = s_raw_all[h];
     const int px = tx * kBlockX + (lane & 15);
-    const int py0 = ty * kBlockY + (lane >> 4);
+    const int py0 = ty * kBlockY + 8 * h + (lane >> 4);
     const float pfx = (float)px;
     const float yc = (float)(ty * kBlockY) + 7.5f;
-    const float ylane = (float)(lane >> 4) - 7.5f;
-    const f2 yl[2] = {f2{ylane, ylane + 4.f}, f2{ylane + 8.f, ylane + 12.f}};
+    const float ylane = (float)(8 * h + (lane >> 4)) - 7.5f;
+    const f2 yl = f2{ylane, ylane + 4.f};
     // live pixels (forward.cu:287-289: pixels outside the image never blend)
-    uint64_t alive[4];
+    uint64_t alive[2];
 #pragma unroll
-    for (int k = 0; k < 4; k++) alive[k] = ballot(px < a.W && py0 + 4 * k < a.H);
-    f2 T[2] = {bc2(1.f), bc2(1.f)};
-    f2 C0[2] = {bc2(0.f), bc2(0.f)}, C1[2] = {bc2(0.f), bc2(0.f)}, C2[2] = {bc2(0.f), bc2(0.f)},
-       Dp[2] = {bc2(0.f), bc2(0.f)};
-    uint32_t stop[4] = {0, 0, 0, 0};  // list position of the terminating splat (retired pixels)
+    for (int k = 0; k < 2; k++) alive[k] = ballot(px < a.W && py0 + 4 * k < a.H);
+    f2 T = bc2(1.f), C0 = bc2(0.f), C1 = bc2(0.f), C2 = bc2(0.f), Dp = bc2(0.f);
+    uint32_t stop[2] = {0, 0};  // list position of the terminating splat (retired pixels)
     uint2 range = ranges[tile];
     range.x = __builtin_amdgcn_readfirstlane(range.x);
     range.y = __builtin_amdgcn_readfirstlane(range.y);
-    // short runs: sorted here, their emission slots kept in registers (batch b in ev[0] after b shifts)
+    // short runs: sorted here (wave 0), their emission slots kept in registers (batch b in ev[0] after
+    // b shifts)
     const int n_run = (int)(range.y - range.x);
     const bool in_regs = n_run <= kWaveSortMax;
     uint32_t ev[4] = {0u, 0u, 0u, 0u};
-    if (n_run > 1 && in_regs) {
-        uint32_t *seg = upos + range.x;
-        if (n_run <= 64) sort_run<1>(seg, n_run, gid_by_e, depths, lane, ev);
-        else if (n_run <= 128) sort_run<2>(seg, n_run, gid_by_e, depths, lane, ev);
-        else sort_run<4>(seg, n_run, gid_by_e, depths, lane, ev);
-    } else if (n_run == 1 && lane == 0) {
-        ev[0] = upos[range.x];
+    if (in_regs) {
+        if (h == 0) {
+            if (n_run > 1) {
+                uint32_t *seg = upos + range.x;
+                if (n_run <= 64) sort_run<1>(seg, n_run, gid_by_e, depths, lane, ev);
+                else if (n_run <= 128) sort_run<2>(seg, n_run, gid_by_e, depths, lane, ev);
+                else sort_run<4>(seg, n_run, gid_by_e, depths, lane, ev);
+            } else if (n_run == 1 && lane == 0) {
+                ev[0] = upos[range.x];
+            }
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+                if (r * 64 < n_run) s_ev[r * 64 + lane] = ev[r];
+        }
+        __syncthreads();
+        if (h == 1) {
+#pragma unroll
+            for (int r = 0; r < 4; r++) ev[r] = r * 64 + lane < n_run ? s_ev[r * 64 + lane] : 0u;
+        }
     }
     // gid_by_e of each batch's instances, 4 batches at a time (the short run's are all loaded here);
     // the next batch's attributes are issued before the current one is blended and only turned into
@@ -279,9 +315,8 @@ __global__ __launch_bounds__(64) void render_forward_kernel(Args a, const uint2 
         }
         ids_left = 4;
     };
-    // the next batch's attributes are gathered into LDS by LDS-DMA loads (as the backward does), only
-    // its lanes' reach bits stay in a register
-    __shared__ RawLDS s_raw;
+    // the next batch's attributes are gathered into this wave's LDS by LDS-DMA loads (as the backward
+    // does), only its lanes' reach bits stay in a register
     uint32_t rnxt = 0;
     auto fetch = [&](uint32_t first) {
         if (ids_left == 0) refill(first);
@@ -294,9 +329,9 @@ __global__ __launch_bounds__(64) void render_forward_kernel(Args a, const uint2 
     };
     if (range.x < range.y) fetch(range.x);
     for (uint32_t base = range.x; base < range.y; base += 64) {
-        if ((alive[0] | alive[1] | alive[2] | alive[3]) == 0) break;  // forward.cu:312-314
+        if ((alive[0] | alive[1]) == 0) break;  // forward.cu:312-314 (this half)
         SplatRegs nxt;
-        const RawSplat raw = read_raw_lds(s_raw, lane, false);
+        const RawSplat raw = read_raw_lds_wave(s_raw, lane);
         if (base + lane < range.y) {  // blend constants (as to_regs)
             const float2 rp = raw.p;
             const float4 rco = raw.co;
@@ -308,71 +343,78 @@ __global__ __launch_bounds__(64) void render_forward_kernel(Args a, const uint2 
             nxt.geo = nxt.opc = nxt.col = make_float4(0.f, 0.f, 0.f, 0.f);  // opacity 0: passes no pixel
             nxt.reach = 0;
         }
-        const uint64_t reach[2] = {ballot(nxt.reach & 1u), ballot(nxt.reach & 2u)};
+        const uint64_t reach = ballot((nxt.reach >> h) & 1u);
         const uint64_t nonpd = ballot(!conic_pd(nxt.geo, nxt.opc));
-        __syncthreads();
+        // one wave writes and reads its own staging area: LDS operations of a wave complete in order
+        __builtin_amdgcn_wave_barrier();
         s_sp[lane].geo = nxt.geo;
         s_sp[lane].opc = nxt.opc;
         s_sp[lane].col = nxt.col;
-        __syncthreads();
+        __builtin_amdgcn_wave_barrier();
         if (base + 64 < range.y) fetch(base + 64);
         const uint32_t pos0 = base - range.x;
-        // The two half tiles blend independently: each walks only the batch's splats that reach it.
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-            for (uint64_t todo = reach[h]; todo != 0; todo &= todo - 1) {
-                const uint32_t j = (uint32_t)__builtin_ctzll(todo);
-                const float4 geo = s_sp[j].geo, opc = s_sp[j].opc, col = s_sp[j].col;
-                const float dx = geo.x - pfx;
-                const float pa = geo.z * dx * dx, pb = geo.w * dx;
-                const Falloff f = falloff(geo, opc, pa, pb, yl[h]);
-                uint64_t m0 = ballot(f.alpha.x >= kAlphaMin) & alive[2 * h];  // forward.cu:346-348
-                uint64_t m1 = ballot(f.alpha.y >= kAlphaMin) & alive[2 * h + 1];
-                if ((nonpd >> j) & 1) {  // forward.cu:341-342
-                    m0 &= ballot(f.pw.x <= 0.0f);
-                    m1 &= ballot(f.pw.y <= 0.0f);
-                }
-                f2 ae = f2{lane_bit(m0) ? f.alpha.x : 0.f, lane_bit(m1) ? f.alpha.y : 0.f};
-                f2 tT = T[h] * (bc2(1.f) - ae);  // forward.cu:349
-                const uint64_t t0m = ballot(tT.x < 0.0001f), t1m = ballot(tT.y < 0.0001f);
-                if ((t0m | t1m) != 0) {
-                    // forward.cu:350-354: the splat that would drop T below 1e-4 is not blended; the pixel retires
-                    const bool t0 = lane_bit(t0m), t1 = lane_bit(t1m);
-                    ae = f2{t0 ? 0.f : ae.x, t1 ? 0.f : ae.y};
-                    tT = f2{t0 ? T[h].x : tT.x, t1 ? T[h].y : tT.y};
-                    stop[2 * h] = t0 ? pos0 + j : stop[2 * h];
-                    stop[2 * h + 1] = t1 ? pos0 + j : stop[2 * h + 1];
-                    alive[2 * h] &= ~t0m;
-                    alive[2 * h + 1] &= ~t1m;
-                }
-                // every live pixel takes the update; pixels the splat does not touch have ae = 0
-                const f2 w = ae * T[h];  // forward.cu:357-358
-                C0[h] = fma2(bc2(col.x), w, C0[h]);
-                C1[h] = fma2(bc2(col.y), w, C1[h]);
-                C2[h] = fma2(bc2(col.z), w, C2[h]);
-                Dp[h] = fma2(bc2(col.w), w, Dp[h]);
-                T[h] = tT;
+        // the batch's splats that reach this half, two at a time: both falloffs are independent, only
+        // the blend updates chain (a lone last splat runs alone)
+        auto blend = [&](const Falloff &f, const float4 &col, uint32_t j) {
+            uint64_t m0 = ballot(f.alpha.x >= kAlphaMin) & alive[0];  // forward.cu:346-348
+            uint64_t m1 = ballot(f.alpha.y >= kAlphaMin) & alive[1];
+            if ((nonpd >> j) & 1) {  // forward.cu:341-342
+                m0 &= ballot(f.pw.x <= 0.0f);
+                m1 &= ballot(f.pw.y <= 0.0f);
             }
+            f2 ae = f2{lane_bit(m0) ? f.alpha.x : 0.f, lane_bit(m1) ? f.alpha.y : 0.f};
+            f2 tT = T * (bc2(1.f) - ae);  // forward.cu:349
+            const uint64_t t0m = ballot(tT.x < 0.0001f), t1m = ballot(tT.y < 0.0001f);
+            if ((t0m | t1m) != 0) {
+                // forward.cu:350-354: the splat that would drop T below 1e-4 is not blended; the pixel retires
+                const bool t0 = lane_bit(t0m), t1 = lane_bit(t1m);
+                ae = f2{t0 ? 0.f : ae.x, t1 ? 0.f : ae.y};
+                tT = f2{t0 ? T.x : tT.x, t1 ? T.y : tT.y};
+                stop[0] = t0 ? pos0 + j : stop[0];
+                stop[1] = t1 ? pos0 + j : stop[1];
+                alive[0] &= ~t0m;
+                alive[1] &= ~t1m;
+            }
+            // every live pixel takes the update; pixels the splat does not touch have ae = 0
+            const f2 w = ae * T;  // forward.cu:357-358
+            C0 = fma2(bc2(col.x), w, C0);
+            C1 = fma2(bc2(col.y), w, C1);
+            C2 = fma2(bc2(col.z), w, C2);
+            Dp = fma2(bc2(col.w), w, Dp);
+            T = tT;
+        };
+        for (uint64_t todo = reach; todo != 0;) {
+            const uint32_t j0 = (uint32_t)__builtin_ctzll(todo);
+            todo &= todo - 1;
+            const bool two = todo != 0;
+            const uint32_t j1 = two ? (uint32_t)__builtin_ctzll(todo) : j0;
+            todo &= todo - (two ? 1 : 0);
+            const float4 geo0 = s_sp[j0].geo, opc0 = s_sp[j0].opc, col0 = s_sp[j0].col;
+            const float4 geo1 = s_sp[j1].geo, opc1 = s_sp[j1].opc, col1 = s_sp[j1].col;
+            const float dx0 = geo0.x - pfx, dx1 = geo1.x - pfx;
+            const Falloff f0 = falloff(geo0, opc0, geo0.z * dx0 * dx0, geo0.w * dx0, yl);
+            const Falloff f1 = falloff(geo1, opc1, geo1.z * dx1 * dx1, geo1.w * dx1, yl);
+            blend(f0, col0, j0);
+            if (two) blend(f1, col1, j1);
         }
     }
     __builtin_amdgcn_s_waitcnt(0x0f70);  // an early exit may leave the next batch's LDS-DMA loads in flight
     const size_t HW = (size_t)a.W * a.H;
     const V3 bg = load_v3(a.bg);
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
+    for (int k = 0; k < 2; k++) {
         const int py = py0 + 4 * k;
         if (px < a.W && py < a.H) {
-            const int h = k >> 1;
-            const float t = (k & 1) ? T[h].y : T[h].x;
+            const float t = k ? T.y : T.x;
             const size_t pix = (size_t)py * a.W + px;
             final_T[pix] = t;
             // splats at positions >= n_contrib never blended into this pixel (the backward's bound):
             // the terminating splat's position, or the list length for pixels that never terminated
             n_contrib[pix] = lane_bit(alive[k]) ? range.y - range.x : stop[k];
-            out_color[pix] = ((k & 1) ? C0[h].y : C0[h].x) + t * bg.x;
-            out_color[HW + pix] = ((k & 1) ? C1[h].y : C1[h].x) + t * bg.y;
-            out_color[2 * HW + pix] = ((k & 1) ? C2[h].y : C2[h].x) + t * bg.z;
-            out_depth[pix] = (k & 1) ? Dp[h].y : Dp[h].x;
+            out_color[pix] = (k ? C0.y : C0.x) + t * bg.x;
+            out_color[HW + pix] = (k ? C1.y : C1.x) + t * bg.y;
+            out_color[2 * HW + pix] = (k ? C2.y : C2.x) + t * bg.z;
+            out_depth[pix] = k ? Dp.y : Dp.x;
         }
     }
 }
@@ -380,7 +422,7 @@ __global__ __launch_bounds__(64) void render_forward_kernel(Args a, const uint2 
 hipError_t launch_render_forward(const Args &a, GeomState g, BinningState b, ImageState img, float *out_color,
                                  float *out_depth, hipStream_t s) {
     const int T = a.gx * a.gy;
-    hipLaunchKernelGGL(render_forward_kernel, dim3(T), dim3(64), 0, s, a, img.ranges, img.order, b.upos, g.depths, b.gid_by_e, g.xy,
+    hipLaunchKernelGGL(render_forward_kernel, dim3(T), dim3(128), 0, s, a, img.ranges, img.order, b.upos, g.depths, b.gid_by_e, g.xy,
                        g.conic_opacity, g.rgbd, img.final_T, img.n_contrib, out_color, out_depth);
     return hipGetLastError();
 }
