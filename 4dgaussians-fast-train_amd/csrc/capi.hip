@@ -82,7 +82,7 @@ GeomState GeomState::carve(char *base, int P, int T) {
     g.radii = (int *)gs4d::carve(p, 4 * n);
     g.xy = (float2 *)gs4d::carve(p, 8 * n);
     g.conic_opacity = (float4 *)gs4d::carve(p, 16 * n);
-    g.rgbd = (float4 *)gs4d::carve(p, 16 * n);
+    g.splat = (float4 *)gs4d::carve(p, 48 * n);
     g.cov3D = (float *)gs4d::carve(p, 24 * n);
     g.clamped = (uint8_t *)gs4d::carve(p, n);
     g.tiles_touched = (uint32_t *)gs4d::carve(p, 4 * n);

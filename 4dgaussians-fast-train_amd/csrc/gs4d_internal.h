@@ -9,6 +9,7 @@
 namespace gs4d {
 
 constexpr int kTilePixels = kBlockX * kBlockY;  // 256 pixels per 16x16 tile
+constexpr float kLog2e = 1.4426950408889634f;    // the blend kernels evaluate the falloff in base 2
 constexpr int kPreprocessBlock = 256;           // Gaussians per preprocess / duplicate workgroup
 constexpr int kMaxDevices = 64;                 // per-device host state (the forward's readback word)
 // Per-instance gradient record written by the render backward at the instance's emission slot:
@@ -24,7 +25,8 @@ struct GeomState {
     int *radii;               // P   internal radii (used when the caller passes none)
     float2 *xy;               // P   pixel-space centre (forward.cu:233)
     float4 *conic_opacity;    // P   (conic.a, conic.b, conic.c, opacity) (forward.cu:254)
-    float4 *rgbd;             // P   (r, g, b, depth) render attributes
+    float4 *splat;            // 3P  packed blend record per Gaussian (render.hip): (x, y, -a/2 log2e, -b log2e),
+                              //     (-c/2 log2e, opacity, 1/opacity, depth), (r, g, b, 0)
     float *cov3D;             // 6P  world covariance (forward.cu:211)
     uint8_t *clamped;         // P   bit c set when channel c was clamped (forward.cu:67-69)
     uint32_t *tiles_touched;  // P   3-sigma rect area (the reference's tiles_touched, forward.cu:255)

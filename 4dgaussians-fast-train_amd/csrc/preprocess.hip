@@ -88,7 +88,12 @@ __global__ __launch_bounds__(kPreprocessBlock) void preprocess_kernel(
                     g.depths[idx] = p_view.z;
                     g.xy[idx] = point_image;
                     g.conic_opacity[idx] = co;
-                    g.rgbd[idx] = make_float4(rgb.x, rgb.y, rgb.z, p_view.z);
+                    // the blend kernels' packed record: log2(e) folded into the conic (forward.cu:340-342 in
+                    // base 2), 1/o for the backward's per-record division, colour and view depth
+                    float4 *rec = g.splat + 3 * (size_t)idx;
+                    rec[0] = make_float4(point_image.x, point_image.y, (-0.5f * co.x) * kLog2e, (-co.y) * kLog2e);
+                    rec[1] = make_float4((-0.5f * co.z) * kLog2e, co.w, co.w > 0.f ? 1.0f / co.w : 0.f, p_view.z);
+                    rec[2] = make_float4(rgb.x, rgb.y, rgb.z, 0.f);
                     my_r = (int)my_radius;
                     touched = area;
                 }

@@ -33,7 +33,6 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 __device__ __forceinline__ f2 bc2(float x) { return f2{x, x}; }
 
-constexpr float kLog2e = 1.4426950408889634f;
 
 // Blend-ready splat constants.  geo = (x, y - yc, -a/2 log2e, -b log2e), opc = (-c/2 log2e, opacity, -, -),
 // col = (r, g, b, depth).  power2 = log2(e) * power (forward.cu:340-342) at offset d = mean - pixel.
@@ -47,100 +46,46 @@ struct SplatRegs {
     uint32_t reach;  // bit h: the splat reaches some pixel centre of half tile h (rows 8h..8h+7)
 };
 
-// A splat's attributes as loaded (no arithmetic on them), so that the loads of the next batch stay in
-// flight while the current batch is blended; to_regs() forms the blend constants
-// when the batch comes up.
-struct RawSplat {
-    float2 p;
-    float4 co;
-    float3 c;
-    uint32_t ge;  // gid_by_e entry: Gaussian id | half-reach bits
-};
-__device__ __forceinline__ void issue_raw(RawSplat &r, bool valid, uint32_t ge, const float2 *__restrict__ xy,
-                                          const float4 *__restrict__ conic_opacity, const float4 *__restrict__ rgbd,
-                                          const float *__restrict__ colors) {
-    r.ge = valid ? ge : 0u;
-    if (valid) {
-        const uint32_t gid = ge & kGidMask;
-        r.p = xy[gid];
-        r.co = conic_opacity[gid];
-        if (colors) {
-            r.c = make_float3(colors[3 * gid], colors[3 * gid + 1], colors[3 * gid + 2]);
-        } else {
-            const float4 c4 = rgbd[gid];
-            r.c = make_float3(c4.x, c4.y, c4.z);
-        }
-    }
-}
 // The alpha test of forward.cu:346-348 / backward.cu:486-490 is taken exactly as the reference states
 // it: alpha = min(0.99, o G) >= 1/255, i.e. the rounded product o G >= 1/255 (the cap is above the
-// threshold).  opc.z holds 1/o (0 for o = 0): the backward accumulates its moments on o G dL/dalpha and
-// divides by o once per splat record.
+// threshold).  The splat record's 1/o (0 for o = 0) lets the backward accumulate its moments on
+// o G dL/dalpha and divide by o once per splat record.
 constexpr float kAlphaMin = 1.0f / 255.0f;
-__device__ __forceinline__ float inv_opacity(float o) { return o > 0.f ? 1.0f / o : 0.f; }
 
-__device__ __forceinline__ void to_regs(SplatRegs &s, bool valid, const RawSplat &r) {
-    if (valid) {
-        s.geo = make_float4(r.p.x, r.p.y, (-0.5f * r.co.x) * kLog2e, (-r.co.y) * kLog2e);
-        s.opc = make_float4((-0.5f * r.co.z) * kLog2e, r.co.w, inv_opacity(r.co.w), 0.f);
-        s.col = make_float4(r.c.x, r.c.y, r.c.z, 0.f);
-        s.reach = r.ge >> kReachShift;
-    } else {
-        s.geo = s.opc = s.col = make_float4(0.f, 0.f, 0.f, 0.f);  // opacity 0: the zero splat passes no pixel
-        s.reach = 0;
-    }
-}
-
-// The backward's next batch of raw splat attributes, gathered straight into LDS by LDS-DMA loads
-// (global_load_lds: per-lane global address, destination base + lane * size), so the prefetch spans
-// the current batch's walk without holding registers.  cd holds rgbd (16 B per lane) or the caller's
-// colors (three 4-B loads into cd[0..63], cd[64..127], cd[128..191]).
+// A batch of 64 splats, each the Gaussian's packed 48-byte blend record (GeomState::splat, written by
+// preprocess: s0 = (x, y, -a/2 log2e, -b log2e), s1 = (-c/2 log2e, o, 1/o, depth), s2 = (r, g, b, 0)),
+// gathered straight into LDS by LDS-DMA loads (global_load_lds: per-lane global address, destination
+// base + lane * 16): three 16-byte pieces of ONE contiguous record per splat, so the prefetch of the
+// next batch spans the current batch's walk without holding registers.
 struct RawLDS {
-    float4 co[64];
-    float cd[64 * 4];
-    float x[64], y[64];
+    float4 s0[64], s1[64], s2[64];
 };
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) const void gbl_void_t;
-__device__ __forceinline__ void issue_raw_lds(RawLDS &r, bool valid, uint32_t gid, const float2 *__restrict__ xy,
-                                              const float4 *__restrict__ conic_opacity,
-                                              const float4 *__restrict__ rgbd, const float *__restrict__ colors) {
+__device__ __forceinline__ void issue_raw_lds(RawLDS &r, bool valid, uint32_t gid, const float4 *__restrict__ splat) {
     if (valid) {
-        __builtin_amdgcn_global_load_lds((gbl_void_t *)(conic_opacity + gid), (lds_void_t *)r.co, 16, 0, 0);
-        if (colors) {
-            const float *c = colors + 3 * (size_t)gid;
-            __builtin_amdgcn_global_load_lds((gbl_void_t *)c, (lds_void_t *)r.cd, 4, 0, 0);
-            __builtin_amdgcn_global_load_lds((gbl_void_t *)(c + 1), (lds_void_t *)(r.cd + 64), 4, 0, 0);
-            __builtin_amdgcn_global_load_lds((gbl_void_t *)(c + 2), (lds_void_t *)(r.cd + 128), 4, 0, 0);
-        } else
-            __builtin_amdgcn_global_load_lds((gbl_void_t *)(rgbd + gid), (lds_void_t *)r.cd, 16, 0, 0);
-        __builtin_amdgcn_global_load_lds((gbl_void_t *)&xy[gid].x, (lds_void_t *)r.x, 4, 0, 0);
-        __builtin_amdgcn_global_load_lds((gbl_void_t *)&xy[gid].y, (lds_void_t *)r.y, 4, 0, 0);
+        const float4 *rec = splat + 3 * (size_t)gid;
+        __builtin_amdgcn_global_load_lds((gbl_void_t *)rec, (lds_void_t *)r.s0, 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((gbl_void_t *)(rec + 1), (lds_void_t *)r.s1, 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((gbl_void_t *)(rec + 2), (lds_void_t *)r.s2, 16, 0, 0);
     }
 }
-// waits for the LDS-DMA loads, then lane l reads its splat of the staged batch
-__device__ __forceinline__ RawSplat read_raw_lds(const RawLDS &r, int lane, bool colors) {
+// waits for this wave's LDS-DMA loads, then lane l reads its splat of the staged batch: blend constants
+// with rows measured from the tile's centre row (geo.y = my - yc), zeros for lanes past the batch
+// (opacity 0: the zero splat passes no pixel)
+__device__ __forceinline__ void read_raw_lds(SplatRegs &s, const RawLDS &r, int lane, bool valid, float yc,
+                                             bool block_barrier) {
     __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): the LDS-DMA writes have landed (lgkm/exp counters not waited)
-    __builtin_amdgcn_s_barrier();
-    RawSplat w;
-    w.co = r.co[lane];
-    w.c = colors ? make_float3(r.cd[lane], r.cd[64 + lane], r.cd[128 + lane])
-                 : make_float3(r.cd[4 * lane], r.cd[4 * lane + 1], r.cd[4 * lane + 2]);
-    w.p = make_float2(r.x[lane], r.y[lane]);
-    w.ge = 0;
-    return w;
-}
-// the same for a wave that stages its own batch (no workgroup barrier: the other wave of the tile may
-// have retired)
-__device__ __forceinline__ RawSplat read_raw_lds_wave(const RawLDS &r, int lane) {
-    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
-    __builtin_amdgcn_wave_barrier();
-    RawSplat w;
-    w.co = r.co[lane];
-    w.c = make_float3(r.cd[4 * lane], r.cd[4 * lane + 1], r.cd[4 * lane + 2]);
-    w.p = make_float2(r.x[lane], r.y[lane]);
-    w.ge = 0;
-    return w;
+    if (block_barrier) __builtin_amdgcn_s_barrier();
+    else __builtin_amdgcn_wave_barrier();
+    if (valid) {
+        const float4 s0 = r.s0[lane], s1 = r.s1[lane], s2 = r.s2[lane];
+        s.geo = make_float4(s0.x, s0.y - yc, s0.z, s0.w);
+        s.opc = make_float4(s1.x, s1.y, s1.z, 0.f);
+        s.col = make_float4(s2.x, s2.y, s2.z, s1.w);  // rgb, view depth
+    } else {
+        s.geo = s.opc = s.col = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
 }
 
 // Falloff of one splat at a pixel pair: exponent (base 2) and G = 2^power2.  Forward and backward use
@@ -239,9 +184,7 @@ __global__ __launch_bounds__(128) void render_forward_kernel(Args a, const uint2
                                                              uint32_t *__restrict__ upos,
                                                              const float *__restrict__ depths,
                                                              const uint32_t *__restrict__ gid_by_e,
-                                                             const float2 *__restrict__ xy,
-                                                             const float4 *__restrict__ conic_opacity,
-                                                             const float4 *__restrict__ rgbd,
+                                                             const float4 *__restrict__ splat,
                                                              float *__restrict__ final_T,
                                                              uint32_t *__restrict__ n_contrib,
                                                              float *__restrict__ out_color,
@@ -325,24 +268,15 @@ __global__ __launch_bounds__(128) void render_forward_kernel(Args a, const uint2
         ug[0] = ug[1]; ug[1] = ug[2]; ug[2] = ug[3];
         ids_left--;
         rnxt = rge >> kReachShift;
-        issue_raw_lds(s_raw, first + lane < range.y, rge & kGidMask, xy, conic_opacity, rgbd, nullptr);
+        issue_raw_lds(s_raw, first + lane < range.y, rge & kGidMask, splat);
     };
     if (range.x < range.y) fetch(range.x);
     for (uint32_t base = range.x; base < range.y; base += 64) {
         if ((alive[0] | alive[1]) == 0) break;  // forward.cu:312-314 (this half)
         SplatRegs nxt;
-        const RawSplat raw = read_raw_lds_wave(s_raw, lane);
-        if (base + lane < range.y) {  // blend constants (as to_regs)
-            const float2 rp = raw.p;
-            const float4 rco = raw.co;
-            nxt.geo = make_float4(rp.x, rp.y - yc, (-0.5f * rco.x) * kLog2e, (-rco.y) * kLog2e);
-            nxt.opc = make_float4((-0.5f * rco.z) * kLog2e, rco.w, 0.f, 0.f);
-            nxt.col = make_float4(raw.c.x, raw.c.y, raw.c.z, s_raw.cd[4 * lane + 3]);  // rgb, view depth
-            nxt.reach = rnxt;
-        } else {
-            nxt.geo = nxt.opc = nxt.col = make_float4(0.f, 0.f, 0.f, 0.f);  // opacity 0: passes no pixel
-            nxt.reach = 0;
-        }
+        const bool valid = base + lane < range.y;
+        read_raw_lds(nxt, s_raw, lane, valid, yc, false);  // this wave's own staging: no block barrier
+        nxt.reach = valid ? rnxt : 0u;
         const uint64_t reach = ballot((nxt.reach >> h) & 1u);
         const uint64_t nonpd = ballot(!conic_pd(nxt.geo, nxt.opc));
         // one wave writes and reads its own staging area: LDS operations of a wave complete in order
@@ -422,8 +356,8 @@ __global__ __launch_bounds__(128) void render_forward_kernel(Args a, const uint2
 hipError_t launch_render_forward(const Args &a, GeomState g, BinningState b, ImageState img, float *out_color,
                                  float *out_depth, hipStream_t s) {
     const int T = a.gx * a.gy;
-    hipLaunchKernelGGL(render_forward_kernel, dim3(T), dim3(128), 0, s, a, img.ranges, img.order, b.upos, g.depths, b.gid_by_e, g.xy,
-                       g.conic_opacity, g.rgbd, img.final_T, img.n_contrib, out_color, out_depth);
+    hipLaunchKernelGGL(render_forward_kernel, dim3(T), dim3(128), 0, s, a, img.ranges, img.order, b.upos, g.depths,
+                       b.gid_by_e, g.splat, img.final_T, img.n_contrib, out_color, out_depth);
     return hipGetLastError();
 }
 
@@ -563,9 +497,8 @@ __device__ __forceinline__ void half_step(f2 &T, f2 &A, const f2 dp0, const f2 d
 // of one pair.
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void render_backward_kernel(Args a, const uint2 *__restrict__ ranges, const uint32_t *__restrict__ order,
                             const uint32_t *__restrict__ gid_by_e,
-                            const uint32_t *__restrict__ upos, const float2 *__restrict__ xy,
-                            const float4 *__restrict__ conic_opacity, const float4 *__restrict__ rgbd,
-                            const float *__restrict__ colors, const float *__restrict__ final_Ts,
+                            const uint32_t *__restrict__ upos, const float4 *__restrict__ splat,
+                            const float *__restrict__ final_Ts,
                             const uint32_t *__restrict__ n_contrib, const float *__restrict__ dL_dpixels,
                             float *__restrict__ contrib) {
     __shared__ SplatLDS s_sp[64];
@@ -667,7 +600,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
             ug[r] = ug[r + 1];
         }
         ids_left--;
-        issue_raw_lds(s_raw, lane < min(64, end), ge & kGidMask, xy, conic_opacity, rgbd, colors);  // colors_precomp or rgb
+        issue_raw_lds(s_raw, lane < min(64, end), ge & kGidMask, splat);
     };
     if (max_last > 0) fetch((int)max_last);
     for (int end = (int)max_last; end > 0; end -= 64) {
@@ -675,8 +608,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
         const uint32_t ucur = unxt;
         const uint64_t reach[2] = {ballot(lane < n && (rnxt & 1u)), ballot(lane < n && (rnxt & 2u))};
         SplatRegs nxt;
-        to_regs(nxt, lane < n, read_raw_lds(s_raw, lane, colors != nullptr));
-        nxt.geo.y -= yc;                    // my - yc, as the forward stages it
+        read_raw_lds(nxt, s_raw, lane, lane < n, yc, true);  // my - yc, as the forward stages it
         // per-splat wave masks (the staged zero splats past n are neither)
         const uint64_t nonpd = ballot(lane < n && !conic_pd(nxt.geo, nxt.opc));
         const uint64_t hiop = ballot(nxt.opc.y > kCapFree);
@@ -786,8 +718,9 @@ hipError_t launch_render_backward(const Args &a, GeomState g, const uint32_t *gi
                                   ImageState img, const float *colors, const float *dL_dpix, float *contrib,
                                   hipStream_t s) {
     const int T = a.gx * a.gy;
-    hipLaunchKernelGGL(render_backward_kernel, dim3(T), dim3(64), 0, s, a, img.ranges, img.order, gid_by_e, upos, g.xy,
-                       g.conic_opacity, g.rgbd, colors, img.final_T, img.n_contrib, dL_dpix, contrib);
+    (void)colors;  // the splat records hold the colours the forward blended (colors_precomp or SH)
+    hipLaunchKernelGGL(render_backward_kernel, dim3(T), dim3(64), 0, s, a, img.ranges, img.order, gid_by_e, upos,
+                       g.splat, img.final_T, img.n_contrib, dL_dpix, contrib);
     return hipGetLastError();
 }
 

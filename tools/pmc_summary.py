@@ -20,7 +20,8 @@ KEYS = {"render_backward_kernel": "render_backward", "render_forward_kernel": "r
         "visible_scan_kernel": "visible_scan", "tile_ranges_kernel": "tile_ranges",
         "tile_sort_kernel": "tile_sort", "tile_order_kernel": "tile_order",
         "contrib_finish_kernel": "contrib_finish", "tile_count_kernel": "tile_count",
-        "tile_scan_kernel": "tile_scan", "tile_scatter_kernel": "tile_scatter"}
+        "tile_scan_kernel": "tile_scan", "tile_scatter_kernel": "tile_scatter",
+        "sh_backward_kernel": "sh_backward"}
 
 
 def short(name):
@@ -46,7 +47,9 @@ def main():
     shutil.copy(stats, prefix + "kernel_stats.csv")
     res = {}
     per_kernel = defaultdict(dict)
-    for part in ("fetch", "write", "sq"):
+    for part in ("fetch", "write", "sq", "derived", "grbm"):
+        if not os.path.isdir(os.path.join(src, part)):
+            continue
         c = counters(os.path.join(src, part))
         for k, d in c.items():
             for name, vals in d.items():
@@ -69,7 +72,17 @@ def main():
     json.dump(res, open(prefix + "pmc.json", "w"), indent=1)
     json.dump(traffic, open(os.path.join(os.path.dirname(prefix) or ".", "pmc_traffic.json"), "w"), indent=1)
     json.dump(raw, open(os.path.join(os.path.dirname(prefix) or ".", "pmc_traffic_raw.json"), "w"), indent=1)
-    valu = {k: round(d["SQ_INSTS_VALU"]) for k, d in per_kernel.items() if "SQ_INSTS_VALU" in d}
+    # measured VALU utilisation (tools/prof_valu.sh): rocprof's derived VALUBusy (100 x SQ_ACTIVE_INST_VALU /
+    # CU_NUM / GRBM_GUI_ACTIVE: the share of the kernel's time the CUs issue vector ALU instructions) and
+    # VALUUtilization (active lanes per VALU instruction), with the raw counters
+    valu = {}
+    for k, d in per_kernel.items():
+        if "VALUBusy" in d or "SQ_INSTS_VALU" in d:
+            valu[k] = {n: round(d[n], 3) for n in ("VALUBusy", "VALUUtilization", "SQ_INSTS_VALU",
+                                                    "SQ_INSTS_VALU_TRANS_F32", "SQ_ACTIVE_INST_VALU",
+                                                    "SQ_WAIT_INST_ANY", "SQ_WAVE_CYCLES", "GRBM_GUI_ACTIVE")
+                       if n in d}
+            valu[k]["source"] = "rocprofv3 --pmc VALUBusy VALUUtilization / SQ counters, tools/prof_valu.sh"
     json.dump(valu, open(os.path.join(os.path.dirname(prefix) or ".", "pmc_valu.json"), "w"), indent=1)
     print(json.dumps(traffic, indent=1))
 
