@@ -562,6 +562,99 @@ __device__ __forceinline__ void block_sort(uint32_t *__restrict__ seg, int n, co
     }
 }
 
+// Runs of kWaveSortMax < n <= 2048 instances (one 256-thread workgroup): each wave sorts 256-key chunks
+// in registers (the bitonic network of the forward's short-run sort, lane l holding chunk positions
+// l, 64 + l, ..), then merge-path rounds in LDS double the sorted runs up to the power of two >= n:
+// every thread emits total / 256 consecutive outputs of its pair of runs, its start found by a binary
+// search on its diagonal, the last round straight into the segment.  Chunks past n are +inf keys
+// (already in order).  O(n log n) compare-selects against the bitonic network's O(n log^2 n): block_sort
+// at n = 2048 spent 66 network steps of 8 registers per thread.
+__device__ __forceinline__ void wave_sort256(uint64_t key[4], int lane) {
+#pragma unroll
+    for (int k = 2; k <= 256; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j >= 1; j >>= 1) {
+            const int mask = j == (k >> 1) ? k - 1 : j;  // flip, then half-cleaners
+            const int lx = mask & 63, rx = mask >> 6;
+            uint64_t pk[4];
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int rq = r ^ rx;
+                if (lx == 0) {
+                    pk[r] = key[rq];
+                } else {
+                    const uint32_t hi = xor_lane((uint32_t)(key[rq] >> 32), lx);
+                    const uint32_t lo = xor_lane((uint32_t)key[rq], lx);
+                    pk[r] = ((uint64_t)hi << 32) | lo;
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const bool lower = ((r * 64 + lane) & j) == 0;
+                const uint64_t kr = key[r];
+                key[r] = lower ? (pk[r] < kr ? pk[r] : kr) : (pk[r] > kr ? pk[r] : kr);
+            }
+        }
+    }
+}
+
+__device__ void merge_sort_run(uint32_t *__restrict__ seg, int n, const uint32_t *__restrict__ gid_by_e,
+                               const float *__restrict__ depths, uint64_t *__restrict__ s_x) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int total = 512;
+    while (total < n) total <<= 1;  // 512, 1024 or 2048
+    uint64_t *src = s_x, *dst = s_x + 2048;
+    for (int c = w; c < total / 256; c += 4) {
+        uint64_t key[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int i = c * 256 + r * 64 + lane;
+            const uint32_t e = i < n ? seg[i] : 0u;
+            const uint32_t gid = i < n ? gid_by_e[e] & kGidMask : 0u;
+            key[r] = i < n ? ((uint64_t)__float_as_uint(depths[gid]) << 32) | e : ~0ull;  // depths > 0.2
+        }
+        if (c * 256 < n) wave_sort256(key, lane);
+#pragma unroll
+        for (int r = 0; r < 4; r++) src[c * 256 + r * 64 + lane] = key[r];
+    }
+    __syncthreads();
+    const int per = total >> 8;  // outputs per thread
+    const int o0 = threadIdx.x * per;
+    for (int wd = 256; wd < total; wd <<= 1) {
+        const bool last = 2 * wd == total;
+        const int p0 = o0 & ~(2 * wd - 1), d = o0 - p0;  // this thread's pair of runs, its diagonal
+        const uint64_t *r1 = src + p0, *r2 = src + p0 + wd;
+        int lo = max(0, d - wd), hi = min(d, wd);
+        while (lo < hi) {  // ties (the +inf padding only) go to the first run, as below
+            const int mid = (lo + hi) >> 1;
+            if (r1[mid] > r2[d - 1 - mid]) hi = mid;
+            else lo = mid + 1;
+        }
+        int i = lo, j = d - lo;
+        uint64_t x = i < wd ? r1[i] : ~0ull, y = j < wd ? r2[j] : ~0ull;
+        for (int k = 0; k < per; k++) {
+            const bool first = x <= y;
+            const uint64_t v = first ? x : y;
+            if (last) {
+                if (o0 + k < n) seg[o0 + k] = (uint32_t)v;
+            } else {
+                dst[o0 + k] = v;
+            }
+            if (first) {
+                i++;
+                x = i < wd ? r1[i] : ~0ull;
+            } else {
+                j++;
+                y = j < wd ? r2[j] : ~0ull;
+            }
+        }
+        __syncthreads();
+        uint64_t *t = src;
+        src = dst;
+        dst = t;
+    }
+}
+
 // The blend kernels run one wave per tile, more waves than fit on the chip at once: the last ones to
 // start run at low occupancy, so a long tile started late ends the kernel late.  tile_order_kernel
 // (one workgroup) orders the tiles longest run first (a counting sort on min(run, 1023), the order
@@ -636,8 +729,8 @@ __global__ __launch_bounds__(1024) void tile_order_kernel(const uint2 *__restric
 }
 
 // Tiles with more than kWaveSortMax instances (shorter runs are sorted in registers by the render
-// forward): one workgroup each (workgroup t + 1 for tile t).  Up to kSortCap: register + LDS bitonic
-// (block_sort); longer: runs of kSortCap in LDS merged by the network's global steps.  Workgroup 0
+// forward): one workgroup each (workgroup t + 1 for tile t).  Up to 2048: wave sorts + merge path
+// (merge_sort_run); up to kSortCap: register + LDS bitonic (block_sort); longer: runs of kSortCap in LDS merged by the network's global steps.  Workgroup 0
 // orders the tiles (order_tiles), so one launch does both (a launch costs ~4 us of the timeline).
 __global__ __launch_bounds__(256) void tile_sort_kernel(const uint2 *__restrict__ ranges, int T,
                                                         uint32_t *__restrict__ order,
@@ -654,9 +747,7 @@ __global__ __launch_bounds__(256) void tile_sort_kernel(const uint2 *__restrict_
     if (n <= kWaveSortMax) return;  // the render forward sorts these
     uint32_t *seg = upos + r.x;
     if (n <= kSortCap) {
-        if (n <= 512) block_sort<2>(seg, n, gid_by_e, depths, s.key);
-        else if (n <= 1024) block_sort<4>(seg, n, gid_by_e, depths, s.key);
-        else if (n <= 2048) block_sort<8>(seg, n, gid_by_e, depths, s.key);
+        if (n <= 2048) merge_sort_run(seg, n, gid_by_e, depths, s.key);
         else block_sort<16>(seg, n, gid_by_e, depths, s.key);
         return;
     }
