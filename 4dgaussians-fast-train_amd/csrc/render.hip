@@ -127,16 +127,7 @@ __device__ __forceinline__ bool conic_pd(const float4 &geo, const float4 &opc) {
 // shuffles and cross-register steps plain selects; a length that is not a power of two is padded
 // with +inf keys.  The sorted slots are written back for the backward and returned in ev[].
 template <int R>
-__device__ __forceinline__ void sort_run(uint32_t *__restrict__ seg, int n, const uint32_t *__restrict__ gid_by_e,
-                                         const float *__restrict__ depths, int lane, uint32_t ev[4]) {
-    uint64_t key[R];
-#pragma unroll
-    for (int r = 0; r < R; r++) {
-        const int i = r * 64 + lane;
-        const uint32_t e = i < n ? seg[i] : 0u;
-        const uint32_t gid = i < n ? gid_by_e[e] & kGidMask : 0u;
-        key[r] = i < n ? ((uint64_t)__float_as_uint(depths[gid]) << 32) | e : ~0ull;  // depths > 0.2
-    }
+__device__ __forceinline__ void sort_keys(uint64_t key[R], int lane) {
 #pragma unroll
     for (int k = 2; k <= 64 * R; k <<= 1) {
 #pragma unroll
@@ -163,6 +154,26 @@ __device__ __forceinline__ void sort_run(uint32_t *__restrict__ seg, int n, cons
             }
         }
     }
+}
+// the sort keys of run positions base + r * 64 + lane (+inf past n)
+template <int R>
+__device__ __forceinline__ void load_keys(uint64_t key[R], const uint32_t *__restrict__ seg, int base, int n,
+                                          const uint32_t *__restrict__ gid_by_e, const float *__restrict__ depths,
+                                          int lane) {
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const int i = base + r * 64 + lane;
+        const uint32_t e = i < n ? seg[i] : 0u;
+        const uint32_t gid = i < n ? gid_by_e[e] & kGidMask : 0u;
+        key[r] = i < n ? ((uint64_t)__float_as_uint(depths[gid]) << 32) | e : ~0ull;  // depths > 0.2
+    }
+}
+template <int R>
+__device__ __forceinline__ void sort_run(uint32_t *__restrict__ seg, int n, const uint32_t *__restrict__ gid_by_e,
+                                         const float *__restrict__ depths, int lane, uint32_t ev[4]) {
+    uint64_t key[R];
+    load_keys<R>(key, seg, 0, n, gid_by_e, depths, lane);
+    sort_keys<R>(key, lane);
 #pragma unroll
     for (int r = 0; r < 4; r++) {
         const int i = r * 64 + lane;
@@ -218,13 +229,55 @@ __global__ __launch_bounds__(128) void render_forward_kernel(Args a, const uint2
     const int n_run = (int)(range.y - range.x);
     const bool in_regs = n_run <= kWaveSortMax;
     uint32_t ev[4] = {0u, 0u, 0u, 0u};
-    if (in_regs) {
+    if (in_regs && n_run > 128) {
+        // 129..256: each wave sorts 128 keys in registers, then one merge-path step over the two sorted
+        // halves (thread t emits positions 2t, 2t + 1, its start found by a binary search on its
+        // diagonal) -- half the network depth of one wave sorting all 256 (the sort is the walk's
+        // start-up latency).  The keys go through the splat staging area, unused until the walk.
+        uint32_t *seg = upos + range.x;
+        uint64_t *s_key = reinterpret_cast<uint64_t *>(&s_sp_all[0][0]);
+        uint64_t key[2];
+        load_keys<2>(key, seg, 128 * h, n_run, gid_by_e, depths, lane);
+        sort_keys<2>(key, lane);
+        s_key[128 * h + lane] = key[0];
+        s_key[128 * h + 64 + lane] = key[1];
+        __syncthreads();
+        const int t = threadIdx.x, d = 2 * t;
+        int lo = max(0, d - 128), hi = min(d, 128);
+        while (lo < hi) {  // ties (the +inf padding only) go to the first half, as below
+            const int mid = (lo + hi) >> 1;
+            if (s_key[mid] > s_key[128 + d - 1 - mid]) hi = mid;
+            else lo = mid + 1;
+        }
+        int i = lo, j = d - lo;
+        uint64_t xk = i < 128 ? s_key[i] : ~0ull, yk = j < 128 ? s_key[128 + j] : ~0ull;
+        uint32_t outv[2];
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const bool first = xk <= yk;
+            outv[k] = (uint32_t)(first ? xk : yk);
+            if (first) {
+                i++;
+                xk = i < 128 ? s_key[i] : ~0ull;
+            } else {
+                j++;
+                yk = j < 128 ? s_key[128 + j] : ~0ull;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            s_ev[d + k] = outv[k];
+            if (d + k < n_run) seg[d + k] = outv[k];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 4; r++) ev[r] = s_ev[r * 64 + lane];
+    } else if (in_regs) {
         if (h == 0) {
             if (n_run > 1) {
                 uint32_t *seg = upos + range.x;
                 if (n_run <= 64) sort_run<1>(seg, n_run, gid_by_e, depths, lane, ev);
-                else if (n_run <= 128) sort_run<2>(seg, n_run, gid_by_e, depths, lane, ev);
-                else sort_run<4>(seg, n_run, gid_by_e, depths, lane, ev);
+                else sort_run<2>(seg, n_run, gid_by_e, depths, lane, ev);
             } else if (n_run == 1 && lane == 0) {
                 ev[0] = upos[range.x];
             }
