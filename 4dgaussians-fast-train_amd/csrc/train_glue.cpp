@@ -463,6 +463,42 @@ std::vector<torch::Tensor> heads_forward(const torch::Tensor &a, const std::vect
     return out;
 }
 
+// ---- heads block forward, both layers: (a, [out_i]) for h (P, W), W1 (kW, W), b1 (kW), W2_i (n_i, W), b2_i (n_i)
+std::vector<torch::Tensor> heads_block_forward(const torch::Tensor &h, const torch::Tensor &w1, const torch::Tensor &b1,
+                                               const std::vector<torch::Tensor> &w2s,
+                                               const std::vector<torch::Tensor> &b2s) {
+    const int k = (int)w2s.size();
+    need(k >= 1 && k <= GS4D_HEADS_MAX && (int)b2s.size() == k, "heads_block_forward: 1-8 heads");
+    for (const torch::Tensor *t : std::initializer_list<const torch::Tensor *>{&h, &w1, &b1})
+        gpu_f32(*t, "heads_block_forward operand");
+    need(h.dim() == 2 && h.is_contiguous() && w1.dim() == 2 && w1.is_contiguous() && b1.is_contiguous() &&
+             w1.size(1) == h.size(1) && w1.size(0) == k * h.size(1) && b1.numel() == w1.size(0),
+         "heads_block_forward: h (P, W), W1 (kW, W), b1 (kW) contiguous");
+    c10::hip::HIPGuard guard(h.device().index());
+    gs4d_heads_block_fwd b{};
+    b.P = (int)h.size(0), b.W = (int)h.size(1), b.k = k;
+    auto a = torch::empty({h.size(0), w1.size(0)}, h.options());
+    b.h = h.data_ptr<float>(), b.w1 = w1.data_ptr<float>(), b.b1 = b1.data_ptr<float>(), b.a = a.data_ptr<float>();
+    std::vector<torch::Tensor> out{a}, keep;
+    for (int i = 0; i < k; i++) {
+        auto w2 = w2s[i].contiguous();
+        auto b2 = b2s[i].contiguous();
+        need(w2.is_cuda() && w2.scalar_type() == torch::kFloat32 && w2.dim() == 2 && w2.size(1) == b.W &&
+                 b2.scalar_type() == torch::kFloat32 && b2.numel() == w2.size(0),
+             "heads_block_forward: W2_i (n_i, W), b2_i (n_i) float32");
+        b.n[i] = (int)w2.size(0);
+        b.w2[i] = w2.data_ptr<float>();
+        b.b2[i] = b2.data_ptr<float>();
+        auto o = torch::empty({h.size(0), w2.size(0)}, h.options());
+        b.out[i] = o.data_ptr<float>();
+        out.push_back(o);
+        keep.push_back(w2);
+        keep.push_back(b2);
+    }
+    check(gs4d_heads_block_forward(&b, (void *)stream_of(h)), "heads_block_forward");
+    return out;
+}
+
 // ---- first deformation layer forward: h = relu(x W^T + b)
 torch::Tensor feature_relu_forward(const torch::Tensor &x, const torch::Tensor &w, const torch::Tensor &b) {
     for (const torch::Tensor *t : std::initializer_list<const torch::Tensor *>{&x, &w, &b})
@@ -511,6 +547,7 @@ PYBIND11_MODULE(_C, m) {
     m.def("hexplane_points_backward", &hexplane_points_backward);
     m.def("feature_relu_forward", &feature_relu_forward);
     m.def("heads_forward", &heads_forward);
+    m.def("heads_block_forward", &heads_block_forward);
     m.def("feature_relu_backward", &feature_relu_backward);
     m.def("heads_backward", &heads_backward);
     m.def("linear_dw", &linear_dw);

@@ -1206,6 +1206,116 @@ __global__ __launch_bounds__(kHfThreads) void heads_fwd_kernel(HfArgs A, const f
         }
     }
 }
+// ---- the whole heads block, forward (scene/deformation.py:73-78: head i = relu(h W1_i^T + b1_i) W2_i^T + b2_i
+// on the shared h = relu(hidden)), first AND second layers in one pass on the f32 MFMA
+// (v_mfma_f32_16x16x4_f32), where torch runs one (P x W) @ (W x kW) GEMM for the first layers and this
+// library's heads_fwd pass read its (P, kW) result back.  Workgroup (x, head i): w1_i (W x W) and w2_i
+// (n_i x W) staged in LDS, its waves each taking 16-point blocks.  Both layers are computed TRANSPOSED
+// (features along the MFMA rows, the 16 points along its columns), so the first layer's accumulators are
+// already the second layer's B operand: in k-step (t, v) lane l supplies feature 16 t + 4 (l >> 4) + v of
+// point l & 15 -- the v-th register of its t-th accumulator (D[4 (l >> 4) + v][l & 15]) -- and the A operand
+// (w1 / w2 rows from LDS, one 16-byte read per 4 MFMAs) uses the same feature order; 16 waves per
+// workgroup, one workgroup per CU.  h is read as that
+// B operand directly (one float4 per lane per 16 features); a = relu(z + b1) is written once, for the
+// backward, and never read back.
+constexpr int kHbfThreads = 512;
+template <int W>
+__global__ __launch_bounds__(kHbfThreads) void heads_block_fwd_kernel(HfArgs A, const float *__restrict__ h,
+                                                                      const float *__restrict__ w1,
+                                                                      const float *__restrict__ b1,
+                                                                      float *__restrict__ a) {
+    constexpr int NT = W / 16, WS = W + 4, NW = kHbfThreads / 64;
+    extern __shared__ float4 s_v[];
+    float *s_w1 = reinterpret_cast<float *>(s_v);  // W rows x WS
+    float *s_b1 = s_w1 + W * WS;                   // W
+    float *s_w2 = s_b1 + W;                        // n_pad rows x WS (rows >= n zero)
+    const int head = blockIdx.y;
+    const int n = A.n[head], npad = (n + 15) & ~15;
+    const float *w1i = w1 + (size_t)head * W * W;
+    for (int e = threadIdx.x; e < W * W / 4; e += kHbfThreads) {
+        const int row = e / (W / 4), c4 = e % (W / 4);
+        reinterpret_cast<float4 *>(s_w1 + row * WS)[c4] = reinterpret_cast<const float4 *>(w1i + (size_t)row * W)[c4];
+    }
+    for (int e = threadIdx.x; e < W; e += kHbfThreads) s_b1[e] = b1[head * W + e];
+    for (int e = threadIdx.x; e < npad * (W / 4); e += kHbfThreads) {
+        const int row = e / (W / 4), c4 = e % (W / 4);
+        reinterpret_cast<float4 *>(s_w2 + row * WS)[c4] =
+            row < n ? reinterpret_cast<const float4 *>(A.w2[head] + (size_t)row * W)[c4] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, q = lane >> 4, c = lane & 15;
+    const int nblk = (A.P + 15) / 16;
+    const int stride = gridDim.x * NW;
+    float *out = A.out[head];
+    const float *b2 = A.b2[head];
+    float4 hn[NT];
+    auto load_h = [&](int blk) {
+        const int pt = blk * 16 + c;
+#pragma unroll
+        for (int t = 0; t < NT; t++)
+            hn[t] = (blk < nblk && pt < A.P) ? *reinterpret_cast<const float4 *>(h + (size_t)pt * W + 16 * t + 4 * q)
+                                             : make_float4(0.f, 0.f, 0.f, 0.f);
+    };
+    int blk = blockIdx.x * NW + wv;
+    load_h(blk);
+    for (; blk < nblk; blk += stride) {
+        float4 hv[NT];
+#pragma unroll
+        for (int t = 0; t < NT; t++) hv[t] = hn[t];
+        load_h(blk + stride);  // the next block's h loads fly while this one runs on the MFMA
+        // z^T (W x 16) = W1_i h^T (a compiler barrier per 16-feature chunk keeps the LDS reads of one chunk,
+        // 8 float4, in registers at a time)
+        f4v acc[NT];
+#pragma unroll
+        for (int m = 0; m < NT; m++) acc[m] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < NT; t++) {
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int m = 0; m < NT; m++) {
+                const float4 av = *reinterpret_cast<const float4 *>(s_w1 + (16 * m + c) * WS + 16 * t + 4 * q);
+                acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, hv[t].x, acc[m], 0, 0, 0);
+                acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, hv[t].y, acc[m], 0, 0, 0);
+                acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, hv[t].z, acc[m], 0, 0, 0);
+                acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, hv[t].w, acc[m], 0, 0, 0);
+            }
+        }
+        // a = relu(z + b1): lane holds features 16 m + 4 q + j of point c; written as float4 per m
+        const int pt = blk * 16 + c;
+#pragma unroll
+        for (int m = 0; m < NT; m++) {
+            const float4 bb = *reinterpret_cast<const float4 *>(s_b1 + 16 * m + 4 * q);
+            acc[m][0] = fmaxf(acc[m][0] + bb.x, 0.f);
+            acc[m][1] = fmaxf(acc[m][1] + bb.y, 0.f);
+            acc[m][2] = fmaxf(acc[m][2] + bb.z, 0.f);
+            acc[m][3] = fmaxf(acc[m][3] + bb.w, 0.f);
+            if (pt < A.P)
+                *reinterpret_cast<float4 *>(a + (size_t)pt * A.kW + head * W + 16 * m + 4 * q) =
+                    make_float4(acc[m][0], acc[m][1], acc[m][2], acc[m][3]);
+        }
+        // out^T (n_pad x 16) = W2_i a^T, B operand = the accumulators above
+        for (int j = 0; j < npad; j += 16) {
+            f4v o = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int m = 0; m < NT; m++) {
+                const float4 wv4 = *reinterpret_cast<const float4 *>(s_w2 + (j + c) * WS + 16 * m + 4 * q);
+                o = __builtin_amdgcn_mfma_f32_16x16x4f32(wv4.x, acc[m][0], o, 0, 0, 0);
+                o = __builtin_amdgcn_mfma_f32_16x16x4f32(wv4.y, acc[m][1], o, 0, 0, 0);
+                o = __builtin_amdgcn_mfma_f32_16x16x4f32(wv4.z, acc[m][2], o, 0, 0, 0);
+                o = __builtin_amdgcn_mfma_f32_16x16x4f32(wv4.w, acc[m][3], o, 0, 0, 0);
+            }
+            // D[output j + 4 q + r][point c]
+            if (pt < A.P) {
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int oi = j + 4 * q + r;
+                    if (oi < n) out[(size_t)pt * n + oi] = o[r] + b2[oi];
+                }
+            }
+        }
+    }
+}
+
 // ---- the deformation field's first layer, forward: h = relu(x W^T + b) (P, FOUT) from x (P, FIN) on the
 // f32 MFMA.  Per 16-row block: lane group q = l >> 4 reads columns 4q..4q+3 of its row l & 15 of a 16-column
 // K chunk as one float4 (the MFMA's k index in step s is column 4q + s), the matching W rows (LDS, row stride
@@ -1634,6 +1744,45 @@ int gs4d_heads_forward(const gs4d_heads_fwd *args, void *stream) {
             else one(heads_fwd_kernel<64, 4>, heads_fwd_kernel<128, 4>, heads_fwd_kernel<256, 4>);
         }
     }
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+int gs4d_heads_block_forward(const gs4d_heads_block_fwd *args, void *stream) {
+    if (!args) return 1;
+    const gs4d_heads_block_fwd &b = *args;
+    if (b.P < 0 || (b.W != 64 && b.W != 128) || b.k < 1 || b.k > kHbMaxHeads || !b.w1 || !b.b1) return 1;
+    HfArgs A{};
+    A.P = b.P, A.W = b.W, A.k = b.k, A.kW = b.k * b.W;
+    int npad_max = 0;
+    for (int i = 0; i < b.k; i++) {
+        if (b.n[i] < 1 || b.n[i] > 64 || !b.w2[i] || !b.b2[i] || (b.P > 0 && !b.out[i])) return 1;
+        if (((size_t)b.w2[i] & 15) != 0) return 1;
+        A.n[i] = b.n[i], A.w2[i] = b.w2[i], A.b2[i] = b.b2[i], A.out[i] = b.out[i];
+        npad_max = std::max(npad_max, (b.n[i] + 15) & ~15);
+    }
+    if (((size_t)b.w1 & 15) != 0 || ((size_t)b.b1 & 15) != 0) return 1;
+    if (b.P == 0) return 0;
+    if (!b.h || !b.a || (((size_t)b.h | (size_t)b.a) & 15) != 0) return 1;
+    const size_t lds = 4 * ((size_t)(b.W + npad_max) * (b.W + 4) + b.W);
+    const int nblk = (b.P + 15) / 16;
+    // ~1024 workgroups over the heads, one resident per CU (LDS): each stages its head's weights once and
+    // takes a few blocks per wave (measured at P = 100k, k = 5: 237 / 218 / 207 us for 256 / 512 / 1024)
+    const int per_head = std::max(1, std::min((nblk + 7) / 8, std::max(1, 1024 / b.k)));
+    hipStream_t s = (hipStream_t)stream;
+    static bool lds_attr = false;  // dynamic LDS above 64 KiB (gfx950: 160 KiB per CU)
+    if (!lds_attr) {
+        (void)hipFuncSetAttribute((const void *)heads_block_fwd_kernel<128>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void *)heads_block_fwd_kernel<64>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        lds_attr = true;
+    }
+    if (b.W == 128)
+        hipLaunchKernelGGL(heads_block_fwd_kernel<128>, dim3(per_head, b.k), dim3(kHbfThreads), lds, s, A, b.h, b.w1,
+                           b.b1, b.a);
+    else
+        hipLaunchKernelGGL(heads_block_fwd_kernel<64>, dim3(per_head, b.k), dim3(kHbfThreads), lds, s, A, b.h, b.w1,
+                           b.b1, b.a);
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 

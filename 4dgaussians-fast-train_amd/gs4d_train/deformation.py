@@ -171,7 +171,9 @@ class _DeformHeads(torch.autograd.Function):
     """The deformation heads (scene/deformation.py:73-78, each nn.Sequential(ReLU, Linear(W, W), ReLU,
     Linear(W, n)) applied to the same hidden features) evaluated together: one ReLU of the shared
     input, ONE (P x W) @ (W x kW) GEMM for the k first layers (weights concatenated), one ReLU, then
-    the k small second layers on column slices.  The backward mirrors it: the k (P x n) @ (n x W)
+    the k small second layers on column slices.  On the GPU (W in {64, 128}) both layers are one HIP
+    pass (gs4d_heads_block_forward) that writes the first layers' output a for the backward and never
+    reads it back.  The backward mirrors it: the k (P x n) @ (n x W)
     products land in column slices of one (P x kW) gradient, then one ReLU mask, one GEMM with K = kW
     for the input gradient and one split-K GEMM for the concatenated first-layer weight gradient.  On
     the GPU the second layers' backward, the ReLU mask and the first-layer bias gradient are one HIP
@@ -187,6 +189,15 @@ class _DeformHeads(torch.autograd.Function):
         k = len(second) // 2
         W = hidden.shape[1]
         h = hidden if relu_done else torch.relu(hidden)
+        if h.is_cuda and W in (64, 128) and k <= 8 and all(t.shape[0] <= 64 for t in second[0::2]):
+            # both layers in one MFMA pass (gs4d_heads_block_forward): a is written once, for the backward
+            from . import _C
+            a, *outs = _C.heads_block_forward(h.contiguous(), w1.contiguous(), b1.contiguous(),
+                                              [t.contiguous() for t in second[0::2]], list(second[1::2]))
+            ctx.save_for_backward(h, a, w1, *second[0::2])
+            ctx.W = W
+            ctx.relu_done = relu_done
+            return tuple(outs)
         a = torch._addmm_activation(b1, h, w1.t())  # bias + ReLU in the GEMM epilogue where supported
         if a.is_cuda and W in (64, 128, 256) and k <= 8 and all(t.shape[0] <= 64 for t in second[0::2]) and \
                 sum(t.shape[0] for t in second[0::2]) * (W + 4) * 4 <= 64 * 1024:

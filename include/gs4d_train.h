@@ -214,6 +214,24 @@ typedef struct gs4d_heads_fwd {
 } gs4d_heads_fwd;
 int gs4d_heads_forward(const gs4d_heads_fwd *args, void *stream);
 
+/* ---- The whole heads block, forward: a = relu(h W1^T + b1) (P, kW) AND out_i = a[:, iW:(i+1)W] W2_i^T + b2_i
+ * (P, n_i) in one pass (f32 MFMA, exact f32 products); a is written for the backward and not read back.
+ * Replaces the (P x W) @ (W x kW) first-layer GEMM plus gs4d_heads_forward.  W in {64, 128}, 1 <= k <= 8,
+ * 1 <= n_i <= 64; h (P, W), W1 (kW, W) = the heads' first-layer weights stacked, b1 (kW), a (P, kW) contiguous
+ * and 16-byte aligned, W2_i (n_i, W) 16-byte aligned, out_i (P, n_i) contiguous. */
+typedef struct gs4d_heads_block_fwd {
+    int P, W, k;
+    const float *h;
+    const float *w1;
+    const float *b1;
+    float *a;
+    int n[GS4D_HEADS_MAX];
+    const float *w2[GS4D_HEADS_MAX];
+    const float *b2[GS4D_HEADS_MAX];
+    float *out[GS4D_HEADS_MAX];
+} gs4d_heads_block_fwd;
+int gs4d_heads_block_forward(const gs4d_heads_block_fwd *args, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -293,6 +293,36 @@ def test_heads_forward_matches_fp64(P, W, ns):
             assert float(((out[i].double() - ref).abs() - 1e-5 * scale).max().clamp_min(0)) == 0.0
 
 
+@pytest.mark.parametrize("P,W,ns", [(100_003, 128, [3, 3, 4, 1, 48]), (777, 64, [2, 16, 5]), (1, 128, [1, 48]),
+                                     (0, 128, [3, 4]), (40, 128, [33, 64]), (5000, 64, [3, 3, 4])])
+def test_heads_block_forward_matches_fp64(P, W, ns):
+    """gs4d_heads_block_forward (both layers of the heads block in one MFMA pass) vs fp64 torch: a =
+    relu(h W1^T + b1) to 1e-5 of its |terms| sum, and every head output, formed from the kernel's own a,
+    to 1e-5 of its |terms| sum; ragged P, P = 1, P = 0, n_i from 1 to 64."""
+    from gs4d_train import _C
+    torch.manual_seed(P + 7 * W + len(ns))
+    k = len(ns)
+    h = torch.relu(torch.randn(P, W, device="cuda"))
+    w1 = torch.randn(k * W, W, device="cuda") / W ** 0.5
+    b1 = torch.randn(k * W, device="cuda") * 0.1
+    w2 = [torch.randn(n, W, device="cuda") / W ** 0.5 for n in ns]
+    b2 = [torch.randn(n, device="cuda") for n in ns]
+    a, *out = _C.heads_block_forward(h, w1, b1, w2, b2)
+    assert a.shape == (P, k * W) and len(out) == k
+    if P == 0:
+        return
+    hd = h.double()
+    z = hd @ w1.double().t() + b1.double()
+    za = hd.abs() @ w1.double().abs().t() + b1.double().abs()
+    assert float(((a.double() - torch.relu(z)).abs() - 1e-5 * za).max().clamp_min(0)) == 0.0
+    for i, (w, b) in enumerate(zip(w2, b2)):
+        x = a[:, i * W:(i + 1) * W].double()
+        ref = x @ w.double().t() + b.double()
+        scale = x.abs() @ w.double().abs().t() + b.double().abs()
+        assert out[i].shape == (P, ns[i])
+        assert float(((out[i].double() - ref).abs() - 1e-5 * scale).max().clamp_min(0)) == 0.0
+
+
 @pytest.mark.parametrize("P,Fin,Fout", [(100_003, 32, 128), (777, 64, 64), (1, 32, 128), (0, 32, 128),
                                         (333, 32, 64), (16, 64, 64)])
 def test_feature_relu_backward_matches_fp64(P, Fin, Fout):
