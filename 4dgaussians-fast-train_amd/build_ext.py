@@ -97,6 +97,7 @@ def build(force=False, verbose=False):
                    "-I" + sysconfig.get_paths()["include"]] + ["-I" + p for p in incs] + [
                 "-L" + os.path.join(tdir, "lib"), "-L/opt/rocm/lib", "-L" + OUT,
                 "-lgs4d", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python", "-lamdhip64",
+                "-lrocblas",
                 "-Wl,-rpath,$ORIGIN" + ("" if rel == "." else "/" + rel), "-Wl,-rpath," + os.path.join(tdir, "lib"),
                 "-Wl,-rpath,/opt/rocm/lib"]
             _run(cmd, verbose)

@@ -3,6 +3,7 @@
 #include <ATen/ATen.h>
 #include <c10/hip/HIPGuard.h>
 #include <c10/hip/HIPStream.h>
+#include <rocblas/rocblas.h>
 #include <torch/extension.h>
 
 #include <string>
@@ -542,6 +543,73 @@ torch::Tensor hexplane_points_backward(const torch::Tensor &dpts_, const torch::
     return dxyz;
 }
 
+// ---- plain f32 GEMMs of the deformation MLP on rocBLAS with a chosen kernel ---------------------------
+// torch dispatches these f32 GEMMs to hipBLASLt, whose heuristic pick for the MLP's shapes runs at
+// 100-125 TF/s of the 157 TF/s f32 peak.  TunableOp (tools/tunableop_probe.sh: every hipBLASLt and rocBLAS
+// solution timed for the P = 100k shapes on this image) found rocBLAS kernels 20-40 % faster; they are
+// called here by their solution index (rocblas_gemm_algo_solution_index) for any P.  An index rocBLAS
+// rejects for a shape falls back to rocBLAS's own choice; the return value says which ran.
+// Column-major semantics: C (m x n) [+ i * sC] = op(A) op(B) for batch i, f32 inputs, f32 accumulation.
+static rocblas_handle rocblas_for(const torch::Tensor &t) {
+    static rocblas_handle handles[64] = {};
+    const int d = t.device().index();
+    TORCH_CHECK(d >= 0 && d < 64, "gemm_f32: device index out of range");
+    if (!handles[d]) TORCH_CHECK(rocblas_create_handle(&handles[d]) == rocblas_status_success, "rocblas_create_handle");
+    TORCH_CHECK(rocblas_set_stream(handles[d], stream_of(t)) == rocblas_status_success, "rocblas_set_stream");
+    return handles[d];
+}
+bool gemm_f32(torch::Tensor A, torch::Tensor B, torch::Tensor C, bool ta, bool tb, int64_t m, int64_t n, int64_t k,
+              int64_t lda, int64_t ldb, int64_t ldc, int64_t batch, int64_t sA, int64_t sB, int64_t sC,
+              int64_t solution) {
+    for (const torch::Tensor *t : {&A, &B, &C})
+        TORCH_CHECK(t->is_cuda() && t->scalar_type() == torch::kFloat32, "gemm_f32: f32 device tensors");
+    TORCH_CHECK(m > 0 && n > 0 && k > 0 && batch > 0 && m < INT32_MAX && n < INT32_MAX && k < INT32_MAX,
+                "gemm_f32: sizes");
+    // every element the call touches lies inside the tensors' storage
+    auto span = [](const torch::Tensor &t, int64_t rows, int64_t cols, int64_t ld, int64_t stride, int64_t nb) {
+        const int64_t last = (nb - 1) * stride + (cols - 1) * ld + rows;  // elements from data_ptr
+        return t.storage_offset() + last <= (int64_t)(t.storage().nbytes() / sizeof(float));
+    };
+    TORCH_CHECK(lda >= (ta ? k : m) && ldb >= (tb ? n : k) && ldc >= m, "gemm_f32: leading dimensions");
+    TORCH_CHECK(span(A, ta ? k : m, ta ? m : k, lda, sA, batch) && span(B, tb ? n : k, tb ? k : n, ldb, sB, batch) &&
+                    span(C, m, n, ldc, sC, batch),
+                "gemm_f32: operands exceed their tensors");
+    const c10::hip::HIPGuard guard(A.device().index());
+    rocblas_handle h = rocblas_for(A);
+    const float one = 1.f, zero = 0.f;
+    const rocblas_operation oa = ta ? rocblas_operation_transpose : rocblas_operation_none;
+    const rocblas_operation ob = tb ? rocblas_operation_transpose : rocblas_operation_none;
+    auto run = [&](rocblas_gemm_algo algo, int32_t sol) {
+        if (batch == 1)
+            return rocblas_gemm_ex(h, oa, ob, (int)m, (int)n, (int)k, &one, A.data_ptr<float>(), rocblas_datatype_f32_r,
+                                   (int)lda, B.data_ptr<float>(), rocblas_datatype_f32_r, (int)ldb, &zero,
+                                   C.data_ptr<float>(), rocblas_datatype_f32_r, (int)ldc, C.data_ptr<float>(),
+                                   rocblas_datatype_f32_r, (int)ldc, rocblas_datatype_f32_r, algo, sol, 0);
+        return rocblas_gemm_strided_batched_ex(h, oa, ob, (int)m, (int)n, (int)k, &one, A.data_ptr<float>(),
+                                               rocblas_datatype_f32_r, (int)lda, sA, B.data_ptr<float>(),
+                                               rocblas_datatype_f32_r, (int)ldb, sB, &zero, C.data_ptr<float>(),
+                                               rocblas_datatype_f32_r, (int)ldc, sC, C.data_ptr<float>(),
+                                               rocblas_datatype_f32_r, (int)ldc, sC, (int)batch, rocblas_datatype_f32_r,
+                                               algo, sol, 0);
+    };
+    if (solution != 0 && run(rocblas_gemm_algo_solution_index, (int32_t)solution) == rocblas_status_success) return true;
+    const rocblas_status st = run(rocblas_gemm_algo_standard, 0);
+    TORCH_CHECK(st == rocblas_status_success, "gemm_f32: rocBLAS status ", (int)st);
+    return false;
+}
+
+// out[i] = sum over s of parts[s][i], s in order (a split-K GEMM's partials)
+torch::Tensor sum_slices(torch::Tensor parts) {
+    TORCH_CHECK(parts.is_cuda() && parts.scalar_type() == torch::kFloat32 && parts.is_contiguous() && parts.dim() >= 2,
+                "sum_slices: contiguous f32 (S, ...) device tensor");
+    const c10::hip::HIPGuard guard(parts.device().index());
+    auto out = torch::empty(parts.sizes().slice(1), parts.options());
+    const int64_t n = out.numel();
+    check(gs4d_sum_slices(parts.data_ptr<float>(), (int)parts.size(0), n, out.data_ptr<float>(), stream_of(parts)),
+          "gs4d_sum_slices");
+    return out;
+}
+
 PYBIND11_MODULE(_C, m) {
     m.def("hexplane_points", &hexplane_points);
     m.def("hexplane_points_backward", &hexplane_points_backward);
@@ -551,6 +619,8 @@ PYBIND11_MODULE(_C, m) {
     m.def("feature_relu_backward", &feature_relu_backward);
     m.def("heads_backward", &heads_backward);
     m.def("linear_dw", &linear_dw);
+    m.def("gemm_f32", &gemm_f32);
+    m.def("sum_slices", &sum_slices);
     m.def("hexplane_reg_forward", &hexplane_reg_forward);
     m.def("hexplane_reg_backward", &hexplane_reg_backward);
     m.def("hexplane_reg_accumulate", &hexplane_reg_accumulate);

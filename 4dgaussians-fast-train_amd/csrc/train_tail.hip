@@ -1402,6 +1402,38 @@ __global__ __launch_bounds__(256) void hex_points_bwd_kernel(int N, const float4
 
 using namespace gs4d;
 
+// sum of S slices of n floats in slice order (gs4d_sum_slices): four slices in flight per thread, float4
+// columns when n and the pointers allow
+template <bool V4>
+__global__ __launch_bounds__(kTailThreads) void sum_slices_kernel(const float *__restrict__ parts, int S, int64_t n,
+                                                                  float *__restrict__ out) {
+    const int64_t m = V4 ? n / 4 : n;
+    for (int64_t i = (int64_t)blockIdx.x * kTailThreads + threadIdx.x; i < m; i += (int64_t)gridDim.x * kTailThreads) {
+        if (V4) {
+            const float4 *p = reinterpret_cast<const float4 *>(parts) + i;
+            float4 acc = p[0];
+            int s = 1;
+            for (; s + 3 < S; s += 4) {  // the loads of four slices issued together, added in order
+                const float4 a = p[(size_t)s * m], b = p[(size_t)(s + 1) * m], c = p[(size_t)(s + 2) * m],
+                             d = p[(size_t)(s + 3) * m];
+                acc.x = (((acc.x + a.x) + b.x) + c.x) + d.x;
+                acc.y = (((acc.y + a.y) + b.y) + c.y) + d.y;
+                acc.z = (((acc.z + a.z) + b.z) + c.z) + d.z;
+                acc.w = (((acc.w + a.w) + b.w) + c.w) + d.w;
+            }
+            for (; s < S; s++) {
+                const float4 a = p[(size_t)s * m];
+                acc.x += a.x; acc.y += a.y; acc.z += a.z; acc.w += a.w;
+            }
+            reinterpret_cast<float4 *>(out)[i] = acc;
+        } else {
+            float acc = parts[i];
+            for (int s = 1; s < S; s++) acc += parts[(size_t)s * n + i];
+            out[i] = acc;
+        }
+    }
+}
+
 extern "C" {
 
 // the launches: maximal runs of heads of one class (narrow: n <= 16; wide: n = 48)
@@ -1631,6 +1663,20 @@ int gs4d_deform_tail_backward(int P, int K, const float *scales, const float *r,
     hipLaunchKernelGGL(deform_tail_bwd_kernel, dim3((unsigned)(nb_g + nb_s)), dim3(kTailThreads), 0, (hipStream_t)stream,
                        P, K, nb_g, scales, r, dr, opac, g_means, g_scales, g_rot, g_opac, g_shs, d_xyz, d_s, d_r, d_o,
                        d_fdc, d_frest, g_dx, g_ds, g_dr, g_do);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+int gs4d_sum_slices(const float *parts, int S, int64_t n, float *out, void *stream) {
+    if (S < 1 || n < 0 || (n > 0 && (!parts || !out))) return 1;
+    if (n == 0) return 0;
+    const bool v4 = n % 4 == 0 && ((uintptr_t)parts % 16) == 0 && ((uintptr_t)out % 16) == 0;
+    const int64_t m = v4 ? n / 4 : n;
+    const unsigned grid = (unsigned)std::min<int64_t>((m + kTailThreads - 1) / kTailThreads, 4096);
+    if (v4)
+        hipLaunchKernelGGL(sum_slices_kernel<true>, dim3(grid), dim3(kTailThreads), 0, (hipStream_t)stream, parts, S, n, out);
+    else
+        hipLaunchKernelGGL(sum_slices_kernel<false>, dim3(grid), dim3(kTailThreads), 0, (hipStream_t)stream, parts, S, n,
+                           out);
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 

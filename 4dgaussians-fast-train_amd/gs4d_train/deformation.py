@@ -9,6 +9,7 @@ unchanged (same parameter names and shapes: `deformation_net.grid.grids.{level}.
 (`gs4d_train.kernels.hexplane`), selected by `HexPlaneField.fused`.
 """
 import itertools
+import os
 from typing import Sequence
 
 import torch
@@ -153,18 +154,62 @@ class Linear(nn.Linear):
         return F.linear(x, self.weight, self.bias)
 
 
+# rocBLAS kernels (solution indices) for the MLP's f32 GEMMs, found by TunableOp on this image for the
+# P = 100k train step (tools/tunableop_probe.sh, profiles/r03_tunableop_results.csv): hipBLASLt's heuristic
+# picks took 129 (split-K dW, 97 chunks of 1024 rows), 14 (its 672-row remainder) and 158 us (the input
+# gradient da @ W1); these take 121, 8.7 and 126 us.  train_glue.cpp's gemm_f32 falls back to rocBLAS's own
+# choice for a shape a kernel does not serve.
+_SOL_DW_BATCHED = -624952225  # nt, batched: (K x N) chunk partials of dW^T
+_SOL_DW = -624951956          # nt: the remainder rows
+_SOL_DX = -624952408          # nn: dx = dy @ W (P x K) from (P x N) (N x K)
+
+
+_USE_ROCBLAS = os.environ.get("GS4D_MLP_ROCBLAS", "1") != "0"  # 0: torch's GEMMs (A/B runs)
+
+
+def _rocblas_ok(*ts):
+    return _USE_ROCBLAS and all(t.is_cuda and t.dtype == torch.float32 and t.dim() == 2 and t.stride(1) == 1 for t in ts)
+
+
 def _splitk_dw(dy, x):
     """dW = dy^T x reduced over the P rows as a split-K batched GEMM (see _LinearSplitK); x may be a
-    column slice of a wider row-major tensor (its rows are then strided)."""
+    column slice of a wider row-major tensor (its rows are then strided).  On the GPU: the chunks' partials
+    and the remainder's on rocBLAS (gemm_f32, the TunableOp kernels above) into one (S + 1, N, K) buffer,
+    summed in chunk order by one pass (gs4d_sum_slices) -- the bmm, its .sum(0), the remainder GEMM and
+    the add of the torch form in three launches."""
     P, c = x.shape[0], _LinearSplitK.kChunk
     S = P // c
     if S < 2:
         return dy.t() @ x
+    if _rocblas_ok(dy, x):
+        from . import _C
+        N, K = dy.shape[1], x.shape[1]
+        rem = P - S * c
+        parts = torch.empty(S + (1 if rem else 0), N, K, device=dy.device)
+        # column-major: part_s^T (K x N) = x_s^T (K x c) . dy_s (c x N)
+        _C.gemm_f32(x, dy, parts, False, True, K, N, c, x.stride(0), dy.stride(0), K, S, c * x.stride(0),
+                    c * dy.stride(0), N * K, _SOL_DW_BATCHED)
+        if rem:
+            _C.gemm_f32(x[S * c:], dy[S * c:], parts[S], False, True, K, N, rem, x.stride(0), dy.stride(0), K, 1,
+                        0, 0, 0, _SOL_DW)
+        return _C.sum_slices(parts)
     xs = x[:S * c].unflatten(0, (S, c))
     dw = torch.bmm(dy[:S * c].unflatten(0, (S, c)).transpose(1, 2), xs).sum(0)
     if P > S * c:
         dw = dw + dy[S * c:].t() @ x[S * c:]
     return dw
+
+
+def _mm_dx(dy, w):
+    """dy @ w (P x N)(N x K): the MLP's input gradient; on the GPU rocBLAS with the TunableOp kernel."""
+    if _rocblas_ok(dy, w) and w.is_contiguous() and dy.shape[0] > 0:
+        from . import _C
+        P, N, K = dy.shape[0], dy.shape[1], w.shape[1]
+        out = torch.empty(P, K, device=dy.device)
+        # column-major: out^T (K x P) = w^T (K x N) . dy^T (N x P)
+        _C.gemm_f32(w, dy, out, False, False, K, P, N, K, dy.stride(0), K, 1, 0, 0, 0, _SOL_DX)
+        return out
+    return dy @ w
 
 
 class _DeformHeads(torch.autograd.Function):
@@ -229,7 +274,7 @@ class _DeformHeads(torch.autograd.Function):
             out = _C.heads_backward(a, list(douts), [x.contiguous() for x in w2])
             da, db1 = out[0], out[1]
             dw1 = _splitk_dw(da, h)
-            dh = relu_in(da @ w1)
+            dh = relu_in(_mm_dx(da, w1))
             return tuple([dh, dw1, db1] + out[2:])
         da = torch.empty_like(a)
         dw2, db2 = [None] * k, [None] * k

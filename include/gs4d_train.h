@@ -43,6 +43,11 @@ int gs4d_deform_tail_backward(int P, int K, const float *scales, const float *r,
                               const float *g_shs, float *d_xyz, float *d_s, float *d_r, float *d_o, float *d_fdc,
                               float *d_frest, float *g_dx, float *g_ds, float *g_dr, float *g_do, void *stream);
 
+/* ---- split-K partial sums: out[i] = sum over s = 0 .. S-1 (in that order) of parts[s * n + i].  The
+ * deformation MLP's weight gradients dW = dY^T X over P ~ 1e5 rows are split-K GEMMs
+ * (gs4d_train/deformation.py _splitk_dw) whose per-chunk results this adds in one pass. */
+int gs4d_sum_slices(const float *parts, int S, int64_t n, float *out, void *stream);
+
 /* ---- densification statistics: train.py:346-349 and scene/gaussian_model.py:521-523.
  * For every i with visible[i]: max_radii[i] = max(max_radii[i], radii[i]) (skipped when radii is
  * NULL), grad_accum[i] += |viewspace_grad[i, 0:2]|, denom[i] += 1.  viewspace_grad is (P, 3). */

@@ -227,6 +227,39 @@ def test_heads_backward_matches_fp64(P, W, ns):
         assert float((out[3 + 2 * i].double() - rb).abs().max() / sb) <= 1e-5
 
 
+@pytest.mark.parametrize("P,N,K,col0", [(100_000, 640, 128, 0), (100_003, 640, 128, 0), (2048, 640, 128, 0),
+                                         (5000, 192, 64, 0), (3001, 256, 256, 0), (7777, 128, 128, 5)])
+def test_mlp_gemms_match_fp64(P, N, K, col0):
+    """The deformation MLP's GPU GEMMs on rocBLAS (deformation._splitk_dw: split-K chunk partials + their
+    remainder + gs4d_sum_slices; deformation._mm_dx: dy @ W) vs fp64 torch, to 1e-5 of each result's largest
+    |term| sum; P a multiple of the 1024-row chunk and not, x a column block of a wider matrix (col0 > 0),
+    W 64/128/256.  Also the library-choice fallback (solution 0) of gemm_f32 and gs4d_sum_slices' scalar form."""
+    from gs4d_train import _C, deformation as D
+    torch.manual_seed(P + N)
+    dy = torch.randn(P, N, device="cuda")
+    wide = torch.relu(torch.randn(P, col0 + K + 3, device="cuda"))
+    x = wide[:, col0:col0 + K]
+    dw = D._splitk_dw(dy, x)
+    ref = dy.double().t() @ x.double()
+    scale = (dy.double().abs().t() @ x.double().abs()).max()
+    assert dw.shape == (N, K)
+    assert float((dw.double() - ref).abs().max() / scale) <= 1e-5
+    w = torch.randn(N, K, device="cuda")
+    dx = D._mm_dx(dy, w)
+    refx = dy.double() @ w.double()
+    assert dx.shape == (P, K)
+    assert float(((dx.double() - refx).abs() - 1e-5 * (dy.double().abs() @ w.double().abs())).max()) <= 0
+    # the library's own kernel (solution 0) computes the same product
+    out = torch.empty(P, K, device="cuda")
+    assert _C.gemm_f32(w, dy, out, False, False, K, P, N, K, N, K, 1, 0, 0, 0, 0) is False
+    assert float(((out.double() - refx).abs() - 1e-5 * (dy.double().abs() @ w.double().abs())).max()) <= 0
+    # an operand that does not fit its tensor is refused before any launch
+    with pytest.raises(RuntimeError):
+        _C.gemm_f32(w, dy, out, False, False, K, P + 1, N, K, N, K, 1, 0, 0, 0, 0)
+    parts = torch.randn(5, 7, 3, device="cuda")  # n = 21: the scalar form
+    assert torch.equal(_C.sum_slices(parts), (((parts[0] + parts[1]) + parts[2]) + parts[3]) + parts[4])
+
+
 def test_hexplane_fused_matches_reference_module():
     """The fused HexPlane kernels (the field's input points, forward and backward in HIP) against vectors made
     by RUNNING the reference's scene/hexplane.py (tests/golden/ref_hexplane_vectors.npz; F = 4, two levels,
