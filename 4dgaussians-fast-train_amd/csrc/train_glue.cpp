@@ -478,8 +478,10 @@ std::vector<torch::Tensor> heads_block_forward(const torch::Tensor &h, const tor
     c10::hip::HIPGuard guard(h.device().index());
     gs4d_heads_block_fwd b{};
     b.P = (int)h.size(0), b.W = (int)h.size(1), b.k = k;
-    auto a = torch::empty({h.size(0), w1.size(0)}, h.options());
-    b.h = h.data_ptr<float>(), b.w1 = w1.data_ptr<float>(), b.b1 = b1.data_ptr<float>(), b.a = a.data_ptr<float>();
+    // whole 16-row blocks are stored (the ABI's padding rows); the caller sees the first P rows
+    auto a_pad = torch::empty({(h.size(0) + 15) / 16 * 16, w1.size(0)}, h.options());
+    auto a = a_pad.narrow(0, 0, h.size(0));
+    b.h = h.data_ptr<float>(), b.w1 = w1.data_ptr<float>(), b.b1 = b1.data_ptr<float>(), b.a = a_pad.data_ptr<float>();
     std::vector<torch::Tensor> out{a}, keep;
     for (int i = 0; i < k; i++) {
         auto w2 = w2s[i].contiguous();

@@ -783,20 +783,21 @@ __global__ __launch_bounds__(256) void heads_bwd_wide_mfma_kernel(HbArgs A, cons
     // a at the C positions (row 4q + j, column 16t + c); issued one block ahead of their use
     float4 gA[NKC];
     float gT[MT][4], av[CT][4];
+    // rows past P (and the prefetch past the last block) read row P - 1: the loads are unconditional, so
+    // the compiler's waits count exactly the loads issued after a block's (a branch around them made it wait
+    // for every load in flight, the next block's prefetch included); such rows are masked when the block
+    // comes up
     auto load_block = [&](int blk) {
-        const int r0 = blk * 16, rg = r0 + c;
+        const int r0 = blk * 16, rg = min(r0 + c, P - 1);
 #pragma unroll
-        for (int kc = 0; kc < NKC; kc++)
-            gA[kc] = (blk < nblk && rg < P) ? *reinterpret_cast<const float4 *>(g + (size_t)rg * N + 16 * kc + 4 * q)
-                                            : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int kc = 0; kc < NKC; kc++) gA[kc] = *reinterpret_cast<const float4 *>(g + (size_t)rg * N + 16 * kc + 4 * q);
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-            const int r = r0 + 4 * q + j;
-            const bool ok = blk < nblk && r < P;
+            const int r = min(r0 + 4 * q + j, P - 1);
 #pragma unroll
-            for (int m = 0; m < MT; m++) gT[m][j] = ok ? g[(size_t)r * N + 16 * m + c] : 0.f;
+            for (int m = 0; m < MT; m++) gT[m][j] = g[(size_t)r * N + 16 * m + c];
 #pragma unroll
-            for (int t = 0; t < CT; t++) av[t][j] = ok ? acol[(size_t)r * ld + 16 * t + c] : 0.f;
+            for (int t = 0; t < CT; t++) av[t][j] = acol[(size_t)r * ld + 16 * t + c];
         }
     };
     const int stride = gridDim.x * (NWV / 2);
@@ -807,13 +808,14 @@ __global__ __launch_bounds__(256) void heads_bwd_wide_mfma_kernel(HbArgs A, cons
         float4 gAc[NKC];
         float gTc[MT][4], avc[CT][4];
 #pragma unroll
-        for (int kc = 0; kc < NKC; kc++) gAc[kc] = gA[kc];
+        for (int kc = 0; kc < NKC; kc++) gAc[kc] = gA[kc];  // rows past P: da rows neither stored nor summed
 #pragma unroll
         for (int j = 0; j < 4; j++) {
+            const bool ok = r0 + 4 * q + j < P;
 #pragma unroll
-            for (int m = 0; m < MT; m++) gTc[m][j] = gT[m][j];
+            for (int m = 0; m < MT; m++) gTc[m][j] = ok ? gT[m][j] : 0.f;
 #pragma unroll
-            for (int t = 0; t < CT; t++) avc[t][j] = av[t][j];
+            for (int t = 0; t < CT; t++) avc[t][j] = ok ? av[t][j] : 0.f;
         }
         load_block(blk + stride);
         // da
@@ -980,23 +982,22 @@ __global__ __launch_bounds__(kFbThreads) void feature_bwd_kernel(int P, const fl
     constexpr int NIT = kFbRows / RPI;
     float2 gv[NIT], hv[NIT];
     float xb[4][NB];
+    // rows past P (and the prefetch past the last block) read row P - 1, masked when the block comes up:
+    // unconditional loads let the compiler's waits count exactly the loads issued after a block's (with a
+    // branch around them it waited for every load in flight, the next block's prefetch included)
     auto load_block = [&](int blk) {
         const int r0 = blk * kFbRows;
 #pragma unroll
         for (int it = 0; it < NIT; it++) {
-            const int r = r0 + it * RPI + rofs;
-            gv[it] = hv[it] = make_float2(0.f, 0.f);
-            if (blk < nblk && r < P) {
-                gv[it] = *reinterpret_cast<const float2 *>(g + (size_t)r * FOUT + o);
-                hv[it] = *reinterpret_cast<const float2 *>(h + (size_t)r * FOUT + o);
-            }
+            const int r = min(r0 + it * RPI + rofs, P - 1);
+            gv[it] = *reinterpret_cast<const float2 *>(g + (size_t)r * FOUT + o);
+            hv[it] = *reinterpret_cast<const float2 *>(h + (size_t)r * FOUT + o);
         }
 #pragma unroll
         for (int st = 0; st < 4; st++) {
-            const int r = r0 + 4 * st + (lane >> 4);
+            const int r = min(r0 + 4 * st + (lane >> 4), P - 1);
 #pragma unroll
-            for (int n = 0; n < NB; n++)
-                xb[st][n] = (blk < nblk && r < P) ? x[(size_t)r * FIN + 16 * n + (lane & 15)] : 0.f;
+            for (int n = 0; n < NB; n++) xb[st][n] = x[(size_t)r * FIN + 16 * n + (lane & 15)];
         }
     };
     const int stride = gridDim.x * NW;
@@ -1008,7 +1009,8 @@ __global__ __launch_bounds__(kFbThreads) void feature_bwd_kernel(int P, const fl
 #pragma unroll
         for (int it = 0; it < NIT; it++) {
             const int row = it * RPI + rofs;
-            const float d0 = hv[it].x > 0.f ? gv[it].x : 0.f, d1 = hv[it].y > 0.f ? gv[it].y : 0.f;
+            const bool ok = r0 + row < P;
+            const float d0 = ok && hv[it].x > 0.f ? gv[it].x : 0.f, d1 = ok && hv[it].y > 0.f ? gv[it].y : 0.f;
             db0 += d0;
             db1 += d1;
             t[row * TS + o] = d0;
@@ -1016,9 +1018,11 @@ __global__ __launch_bounds__(kFbThreads) void feature_bwd_kernel(int P, const fl
         }
         float xc[4][NB];
 #pragma unroll
-        for (int st = 0; st < 4; st++)
+        for (int st = 0; st < 4; st++) {
+            const bool ok = r0 + 4 * st + (lane >> 4) < P;
 #pragma unroll
-            for (int n = 0; n < NB; n++) xc[st][n] = xb[st][n];
+            for (int n = 0; n < NB; n++) xc[st][n] = ok ? xb[st][n] : 0.f;
+        }
         load_block(blk + stride);  // the next block's loads fly while this one runs on the MFMA
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the tile is written (LDS is in order per wave)
         __builtin_amdgcn_wave_barrier();
@@ -1231,6 +1235,8 @@ __global__ __launch_bounds__(kHbfThreads) void heads_block_fwd_kernel(HfArgs A, 
     float *s_w2 = s_b1 + W;                        // n_pad rows x WS (rows >= n zero)
     const int head = blockIdx.y;
     const int n = A.n[head], npad = (n + 15) & ~15;
+    float *s_b2 = s_w2 + npad * WS;  // n_pad (in LDS: a global load in the store loop would wait for every
+                                     // load and store in flight, the next block's h prefetch included)
     const float *w1i = w1 + (size_t)head * W * W;
     for (int e = threadIdx.x; e < W * W / 4; e += kHbfThreads) {
         const int row = e / (W / 4), c4 = e % (W / 4);
@@ -1242,19 +1248,21 @@ __global__ __launch_bounds__(kHbfThreads) void heads_block_fwd_kernel(HfArgs A, 
         reinterpret_cast<float4 *>(s_w2 + row * WS)[c4] =
             row < n ? reinterpret_cast<const float4 *>(A.w2[head] + (size_t)row * W)[c4] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
+    for (int e = threadIdx.x; e < npad; e += kHbfThreads) s_b2[e] = e < n ? A.b2[head][e] : 0.f;
     __syncthreads();
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, q = lane >> 4, c = lane & 15;
     const int nblk = (A.P + 15) / 16;
     const int stride = gridDim.x * NW;
     float *out = A.out[head];
-    const float *b2 = A.b2[head];
     float4 hn[NT];
+    // rows past P (the last block's, and the prefetch past the last block) read row P - 1: every load is
+    // unconditional, so the compiler's wait before a block's MFMAs counts exactly the loads issued after its
+    // h (a branch around them made it wait for ALL loads, the next block's prefetch included); those rows'
+    // results go to a's padding rows or are not stored
     auto load_h = [&](int blk) {
-        const int pt = blk * 16 + c;
+        const int pt = min(blk * 16 + c, A.P - 1);
 #pragma unroll
-        for (int t = 0; t < NT; t++)
-            hn[t] = (blk < nblk && pt < A.P) ? *reinterpret_cast<const float4 *>(h + (size_t)pt * W + 16 * t + 4 * q)
-                                             : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int t = 0; t < NT; t++) hn[t] = *reinterpret_cast<const float4 *>(h + (size_t)pt * W + 16 * t + 4 * q);
     };
     int blk = blockIdx.x * NW + wv;
     load_h(blk);
@@ -1289,9 +1297,9 @@ __global__ __launch_bounds__(kHbfThreads) void heads_block_fwd_kernel(HfArgs A, 
             acc[m][1] = fmaxf(acc[m][1] + bb.y, 0.f);
             acc[m][2] = fmaxf(acc[m][2] + bb.z, 0.f);
             acc[m][3] = fmaxf(acc[m][3] + bb.w, 0.f);
-            if (pt < A.P)
-                *reinterpret_cast<float4 *>(a + (size_t)pt * A.kW + head * W + 16 * m + 4 * q) =
-                    make_float4(acc[m][0], acc[m][1], acc[m][2], acc[m][3]);
+            // a has ceil(P / 16) * 16 rows (gs4d_heads_block_forward): no condition on the store
+            *reinterpret_cast<float4 *>(a + (size_t)pt * A.kW + head * W + 16 * m + 4 * q) =
+                make_float4(acc[m][0], acc[m][1], acc[m][2], acc[m][3]);
         }
         // out^T (n_pad x 16) = W2_i a^T, B operand = the accumulators above
         for (int j = 0; j < npad; j += 16) {
@@ -1309,7 +1317,7 @@ __global__ __launch_bounds__(kHbfThreads) void heads_block_fwd_kernel(HfArgs A, 
 #pragma unroll
                 for (int r = 0; r < 4; r++) {
                     const int oi = j + 4 * q + r;
-                    if (oi < n) out[(size_t)pt * n + oi] = o[r] + b2[oi];
+                    if (oi < n) out[(size_t)pt * n + oi] = o[r] + s_b2[oi];
                 }
             }
         }
@@ -1809,7 +1817,7 @@ int gs4d_heads_block_forward(const gs4d_heads_block_fwd *args, void *stream) {
     if (((size_t)b.w1 & 15) != 0 || ((size_t)b.b1 & 15) != 0) return 1;
     if (b.P == 0) return 0;
     if (!b.h || !b.a || (((size_t)b.h | (size_t)b.a) & 15) != 0) return 1;
-    const size_t lds = 4 * ((size_t)(b.W + npad_max) * (b.W + 4) + b.W);
+    const size_t lds = 4 * ((size_t)(b.W + npad_max) * (b.W + 4) + b.W + npad_max);
     const int nblk = (b.P + 15) / 16;
     // ~1024 workgroups over the heads, one resident per CU (LDS): each stages its head's weights once and
     // takes a few blocks per wave (measured at P = 100k, k = 5: 237 / 218 / 207 us for 256 / 512 / 1024)

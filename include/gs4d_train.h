@@ -223,7 +223,8 @@ int gs4d_heads_forward(const gs4d_heads_fwd *args, void *stream);
  * (P, n_i) in one pass (f32 MFMA, exact f32 products); a is written for the backward and not read back.
  * Replaces the (P x W) @ (W x kW) first-layer GEMM plus gs4d_heads_forward.  W in {64, 128}, 1 <= k <= 8,
  * 1 <= n_i <= 64; h (P, W), W1 (kW, W) = the heads' first-layer weights stacked, b1 (kW), a (P, kW) contiguous
- * and 16-byte aligned, W2_i (n_i, W) 16-byte aligned, out_i (P, n_i) contiguous. */
+ * and 16-byte aligned WITH ROOM FOR ceil(P / 16) * 16 ROWS (the padding rows receive don't-care values: the
+ * kernel stores whole 16-row blocks unconditionally), W2_i (n_i, W) 16-byte aligned, out_i (P, n_i) contiguous. */
 typedef struct gs4d_heads_block_fwd {
     int P, W, k;
     const float *h;
