@@ -421,6 +421,15 @@ __global__ __launch_bounds__(kCountThreads) void tile_scan_kernel(uint32_t *__re
 
 // tile_scatter: chunk c's offsets into LDS, one fetch-add per instance places its emission slot in
 // its tile's run (the order inside the run is the arbitrary order of the LDS atomics: see the header).
+// A tile's run holds each chunk's share (~1.5 slots at the metric config) in chunk order, so with chunk =
+// workgroup the 4-byte writes of one 64-byte line came from workgroups dealt round-robin to all 8 XCDs,
+// each L2 writing its partial line back (~8x write amplification).  Chunks are mapped so that each XCD
+// takes one contiguous range of them (workgroups b and b + 8 share an XCD: MI355X_MICROARCH.md, dispatch;
+// speed only, any mapping is correct): a tile's run is then written by at most 8 XCDs in 8 pieces.
+__device__ __forceinline__ int xcd_chunk(int b, int nblk) {
+    const int q = nblk >> 3, r = nblk & 7, x = b & 7, j = b >> 3;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + j;
+}
 template <int ITEMS>
 __global__ __launch_bounds__(kCountThreads) void tile_scatter_kernel(const uint32_t *__restrict__ keys,
                                                                      const uint32_t *__restrict__ n_dev, int T,
@@ -428,7 +437,8 @@ __global__ __launch_bounds__(kCountThreads) void tile_scatter_kernel(const uint3
                                                                      uint32_t *__restrict__ upos) {
     extern __shared__ uint32_t s_off[];
     const int n = count_of(0, n_dev), tid = threadIdx.x;
-    const size_t c0 = (size_t)blockIdx.x * (kCountThreads * ITEMS);
+    const int chunk = xcd_chunk((int)blockIdx.x, (int)gridDim.x);
+    const size_t c0 = (size_t)chunk * (kCountThreads * ITEMS);
     if (c0 >= (size_t)n) return;
     uint32_t key[ITEMS];
 #pragma unroll
@@ -436,7 +446,7 @@ __global__ __launch_bounds__(kCountThreads) void tile_scatter_kernel(const uint3
         const size_t i = c0 + (size_t)r * kCountThreads + tid;
         key[r] = i < (size_t)n ? keys[i] : ~0u;
     }
-    const uint32_t *h = offs + (size_t)blockIdx.x * T;
+    const uint32_t *h = offs + (size_t)chunk * T;
     for (int t = tid; t < T; t += kCountThreads) s_off[t] = h[t];
     __syncthreads();
 #pragma unroll

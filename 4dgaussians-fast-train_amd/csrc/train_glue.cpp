@@ -43,6 +43,23 @@ std::tuple<torch::Tensor, torch::Tensor> l1_forward(const torch::Tensor &x_, con
     return {loss, sign};
 }
 
+// value and gradient in one pass (gs4d_l1_loss_grad); dloss = the upstream gradient (1 for loss.backward())
+std::tuple<torch::Tensor, torch::Tensor> l1_loss_grad(const torch::Tensor &x_, const torch::Tensor &y_, double dloss) {
+    need(x_.sizes() == y_.sizes(), "l1_loss: shapes differ");
+    need(x_.is_cuda() && y_.is_cuda(), "l1_loss: inputs must be HIP (GPU) tensors");
+    c10::hip::HIPGuard guard(x_.device().index());
+    torch::Tensor x = x_.to(torch::kFloat32).contiguous(), y = y_.to(torch::kFloat32).contiguous();
+    const int64_t n = x.numel();
+    need(n % 4 == 0, "l1_loss_grad: numel must be a multiple of 4");
+    torch::Tensor grad = torch::empty(x.sizes(), x.options());
+    torch::Tensor loss = torch::empty({}, x.options());
+    torch::Tensor scratch = torch::empty({(int64_t)gs4d_l1_scratch_bytes(n)}, x.options().dtype(torch::kUInt8));
+    check(gs4d_l1_loss_grad(n, x.data_ptr<float>(), y.data_ptr<float>(), (float)dloss, loss.data_ptr<float>(),
+                            grad.data_ptr<float>(), scratch.data_ptr(), stream_of(x)),
+          "l1_loss_grad");
+    return {loss, grad};
+}
+
 torch::Tensor l1_backward(const torch::Tensor &sign, const torch::Tensor &dloss_) {
     c10::hip::HIPGuard guard(sign.device().index());
     torch::Tensor dloss = dloss_.to(torch::kFloat32).contiguous();
@@ -632,6 +649,7 @@ PYBIND11_MODULE(_C, m) {
     m.def("hexplane_backward", &hexplane_backward);
     m.def("l1_forward", &l1_forward);
     m.def("l1_backward", &l1_backward);
+    m.def("l1_loss_grad", &l1_loss_grad);
     m.def("densify_stats", &densify_stats);
     m.def("adam_step", &adam_step);
     m.def("version", []() { return std::string(gs4d_version()); });

@@ -20,6 +20,7 @@
 #include <math.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "../../include/gs4d_train.h"
 #include "gs4d_internal.h"
@@ -61,10 +62,14 @@ __global__ __launch_bounds__(kTailThreads) void l1_partial_kernel(int64_t n, con
 // The same pass over 16-byte words (n % 4 == 0, 16-byte aligned x / y and 4-byte aligned sign): each
 // thread takes two float4 of x and y and stores two char4 of signs -- a quarter of the memory
 // instructions of the scalar form, the same partial layout (kL1Chunk elements per workgroup).
+// GRAD: the loss's gradient for the upstream gradient `scale` = dloss * (1 / n) is stored instead of the signs
+// (gs4d_l1_loss_grad: value and gradient in one pass, where l1_backward would read the signs back)
+template <bool GRAD>
 __global__ __launch_bounds__(kTailThreads) void l1_partial_v4_kernel(int64_t n4, const float4 *__restrict__ x,
                                                                      const float4 *__restrict__ y,
                                                                      char4 *__restrict__ sign,
-                                                                     double *__restrict__ part) {
+                                                                     double *__restrict__ part, float4 *__restrict__ grad,
+                                                                     float scale) {
     const int64_t base = (int64_t)blockIdx.x * (kL1Chunk / 4);
     float acc = 0.f;
 #pragma unroll
@@ -78,7 +83,11 @@ __global__ __launch_bounds__(kTailThreads) void l1_partial_v4_kernel(int64_t n4,
             acc += fabsf(d2);
             acc += fabsf(d3);
             auto sg = [](float d) { return (signed char)((d > 0.f) - (d < 0.f)); };  // torch.sign
-            sign[i] = make_char4(sg(d0), sg(d1), sg(d2), sg(d3));
+            const char4 c = make_char4(sg(d0), sg(d1), sg(d2), sg(d3));
+            if (GRAD)  // as l1_backward_v4_kernel: sign * (dloss * (1 / n))
+                grad[i] = make_float4((float)c.x * scale, (float)c.y * scale, (float)c.z * scale, (float)c.w * scale);
+            else
+                sign[i] = c;
         }
     }
     double s = acc;
@@ -1621,10 +1630,25 @@ int gs4d_l1_loss_forward(int64_t n, const float *x, const float *y, int8_t *sign
     const int nblk = (int)((n + kL1Chunk - 1) / kL1Chunk);
     double *part = (double *)align_up((size_t)scratch, 8);
     if (n % 4 == 0 && (((size_t)x | (size_t)y) & 15) == 0 && ((size_t)sign & 3) == 0)
-        hipLaunchKernelGGL(l1_partial_v4_kernel, dim3(nblk), dim3(kTailThreads), 0, s, n / 4, (const float4 *)x,
-                           (const float4 *)y, (char4 *)sign, part);
+        hipLaunchKernelGGL(l1_partial_v4_kernel<false>, dim3(nblk), dim3(kTailThreads), 0, s, n / 4, (const float4 *)x,
+                           (const float4 *)y, (char4 *)sign, part, (float4 *)nullptr, 0.f);
     else
         hipLaunchKernelGGL(l1_partial_kernel, dim3(nblk), dim3(kTailThreads), 0, s, n, x, y, sign, part);
+    hipLaunchKernelGGL(l1_final_kernel, dim3(1), dim3(kTailThreads), 0, s, nblk, n, part, loss);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+int gs4d_l1_loss_grad(int64_t n, const float *x, const float *y, float dloss, float *loss, float *grad, void *scratch,
+                      void *stream) {
+    if (n < 0 || (n > 0 && (!x || !y || !grad || !scratch)) || !loss) return 1;
+    hipStream_t s = (hipStream_t)stream;
+    if (n == 0) return hipMemsetAsync(loss, 0, 4, s) == hipSuccess ? 0 : 3;
+    if (n % 4 != 0 || (((size_t)x | (size_t)y | (size_t)grad) & 15) != 0) return 1;  // the float4 form only
+    const int nblk = (int)((n + kL1Chunk - 1) / kL1Chunk);
+    double *part = (double *)align_up((size_t)scratch, 8);
+    const float scale = dloss * (1.0f / (float)n);  // torch's MeanBackward rounding, as l1_backward
+    hipLaunchKernelGGL(l1_partial_v4_kernel<true>, dim3(nblk), dim3(kTailThreads), 0, s, n / 4, (const float4 *)x,
+                       (const float4 *)y, (char4 *)nullptr, part, (float4 *)grad, scale);
     hipLaunchKernelGGL(l1_final_kernel, dim3(1), dim3(kTailThreads), 0, s, nblk, n, part, loss);
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
@@ -1821,6 +1845,7 @@ int gs4d_heads_block_forward(const gs4d_heads_block_fwd *args, void *stream) {
     const int nblk = (b.P + 15) / 16;
     // ~1024 workgroups over the heads, one resident per CU (LDS): each stages its head's weights once and
     // takes a few blocks per wave (measured at P = 100k, k = 5: 237 / 218 / 207 us for 256 / 512 / 1024)
+    // (16-wave workgroups measured no faster: 185-196 us for 256-1024 of them)
     const int per_head = std::max(1, std::min((nblk + 7) / 8, std::max(1, 1024 / b.k)));
     hipStream_t s = (hipStream_t)stream;
     static bool lds_attr = false;  // dynamic LDS above 64 KiB (gfx950: 160 KiB per CU)

@@ -35,6 +35,17 @@ def l1_loss(network_output, gt):
     return _L1Loss.apply(network_output, gt.detach())
 
 
+def l1_loss_and_grad(network_output, gt, dloss=1.0):
+    """(detached L1 value, its gradient w.r.t. network_output for the upstream gradient `dloss`) in one pass
+    (gs4d_l1_loss_grad): bitwise what l1_loss(...).backward(dloss) deposits, without the sign buffer and
+    the autograd node.  Falls back to the two-pass form when numel % 4 != 0."""
+    x, y = network_output.detach(), gt.detach()
+    if x.numel() % 4 == 0:
+        return _C.l1_loss_grad(x, y, float(dloss))
+    loss, sign = _C.l1_forward(x, y)
+    return loss, _C.l1_backward(sign, torch.full((1,), float(dloss), device=x.device)).to(x.dtype)
+
+
 @torch.no_grad()
 def densify_stats(viewspace_grad, visibility, radii, grad_accum, denom, max_radii2D):
     """train.py:346-349 + gaussian_model.py:521-523 in one launch, in place."""
@@ -54,6 +65,13 @@ class FusedAdam(torch.optim.Optimizer):
 
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps))
+        # Host-side step counts keyed by the identity of each state's "step" tensor (which the reference's
+        # optimizer-state surgery, gaussian_model.py:316-388, carries from a replaced parameter to its
+        # successor).  A torch add on each of ~50 CPU step tensors plus a .item() read cost ~0.45 ms of host
+        # time per step (the GPU idled behind it); the count is kept here and written through a numpy view
+        # of the tensor (the tensor stays current for any reader).  A step tensor the cache has not seen (a
+        # fresh state, load_state_dict) is read once.
+        self._step_cache = {}
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -61,35 +79,48 @@ class FusedAdam(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        by_hyper = {}
+        work = []  # (group, p, grad, state)
         for group in self.param_groups:
-            beta1, beta2 = group["betas"]
-            key = (beta1, beta2, group["eps"])
-            lists = by_hyper.setdefault(key, ([], [], [], [], [], []))
             for p in group["params"]:
-                if p.grad is None:
+                g = p.grad
+                if g is None:
                     continue
-                if p.grad.is_sparse:
+                if g.is_sparse:
                     raise RuntimeError("FusedAdam does not support sparse gradients")
                 st = self.state[p]
                 if len(st) == 0:
                     st["step"] = torch.tensor(0.0, dtype=torch.float32)
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                st["step"] += 1
-                step = st["step"].item()
-                bc1 = 1 - beta1 ** step
-                bc2 = 1 - beta2 ** step
-                g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
-                lists[0].append(p)
-                lists[1].append(g)
-                lists[2].append(st["exp_avg"])
-                lists[3].append(st["exp_avg_sq"])
-                lists[4].append((group["lr"] / bc1) * -1)
-                lists[5].append(bc2 ** 0.5)
+                work.append((group, p, g, st))
+        if not work:
+            return loss
+        cache = self._step_cache
+        if len(cache) > 4 * len(work) + 64:  # states of parameters no longer optimised
+            live = {id(w[3]["step"]) for w in work}
+            for k in [k for k in cache if k not in live]:
+                del cache[k]
+        by_hyper = {}
+        for group, p, g, st in work:
+            t = st["step"]
+            e = cache.get(id(t))
+            if e is None or e[0] is not t:
+                e = cache[id(t)] = [t, t.numpy(), t.item()]  # CPU float32 0-d tensor, as torch's Adam keeps it
+            e[2] += 1.0
+            e[1][()] = e[2]
+            step = e[2]
+            beta1, beta2 = group["betas"]
+            lists = by_hyper.get((beta1, beta2, group["eps"]))
+            if lists is None:
+                lists = by_hyper[(beta1, beta2, group["eps"])] = ([], [], [], [], [], [])
+            lists[0].append(p)
+            lists[1].append(g if g.is_contiguous() else g.contiguous())
+            lists[2].append(st["exp_avg"])
+            lists[3].append(st["exp_avg_sq"])
+            lists[4].append((group["lr"] / (1 - beta1 ** step)) * -1)
+            lists[5].append((1 - beta2 ** step) ** 0.5)
         for (beta1, beta2, eps), (ps, gs, ms, vs, ss, bs) in by_hyper.items():
-            if ps:
-                _C.adam_step(ps, gs, ms, vs, ss, bs, beta1, beta2, eps)
+            _C.adam_step(ps, gs, ms, vs, ss, bs, beta1, beta2, eps)
         return loss
 
 

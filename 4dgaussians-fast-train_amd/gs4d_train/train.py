@@ -51,16 +51,26 @@ def train_step(gaussians, views, opt, hyper, iteration, background, stage="fine"
                                                                                        device=dev)
         visibility_filter = torch.cat(vis_list).any(dim=0) if vis_list else torch.zeros(P, dtype=torch.bool,
                                                                                       device=dev)
+    image_grad = None  # fused path, no D-SSIM: the L1's image gradient, formed with its value in one pass
     if images:
         image_tensor = images[0] if one else torch.cat(images, 0)
         gt_image_tensor = gts[0] if one else torch.cat(gts, 0)
-        if fused:
+        # the batch mean over all views: each rank holds len(mine) of len(views)
+        share = len(mine) / len(views) if data_parallel else 1.0
+        if fused and opt.lambda_dssim == 0:
+            # loss = L1 * share (+ the regulariser, deferred below) is linear in the L1, so
+            # loss.backward() deposits exactly image.backward(sign / N * share): value and gradient in one
+            # pass (gs4d_l1_loss_grad), no L1 autograd node
+            from .kernels import l1_loss_and_grad
+            Ll1, image_grad = l1_loss_and_grad(image_tensor, gt_image_tensor[:, :3, :, :], share)
+            loss = Ll1 * share if data_parallel else Ll1
+        elif fused:
             from .kernels import l1_loss
             Ll1 = l1_loss(image_tensor, gt_image_tensor[:, :3, :, :])
+            loss = Ll1 * share if data_parallel else Ll1
         else:
             Ll1 = l1_loss_torch(image_tensor, gt_image_tensor[:, :3, :, :])
-        # the batch mean over all views: each rank holds len(mine) of len(views)
-        loss = Ll1 * (len(mine) / len(views)) if data_parallel else Ll1
+            loss = Ll1 * share if data_parallel else Ll1
     else:
         loss = torch.zeros((), device=dev)
     reg_w = (hyper.time_smoothness_weight, hyper.l1_time_planes, hyper.plane_tv_weight)
@@ -80,7 +90,10 @@ def train_step(gaussians, views, opt, hyper, iteration, background, stage="fine"
             len(mine) / len(views) if data_parallel else 1.0)
     # a data-parallel rank with no view of the batch (len(views) < world) and no regulariser has a
     # constant loss: nothing to back-propagate, its gradients are the zeros filled in below
-    if loss.requires_grad:
+    if image_grad is not None:
+        if image_tensor.requires_grad:
+            image_tensor.backward(image_grad)
+    elif loss.requires_grad:
         loss.backward()
     if reg_deferred is not None:
         gaussians.add_regulation_grad(*reg_w, scale=reg_scale)

@@ -205,15 +205,14 @@ def _bwd(C, d, radii, grad, gb, nr, bb, ib):
 
 def make_step(d, dev, seed, C, dist):
     from gs4d_train import _C as TC
-    one = torch.ones(1, device=dev)
     gt = torch.tensor(np.random.default_rng(seed + 1).uniform(0, 1, (3, d["H"], d["W"])).astype(np.float32),
                       device=dev)
 
     def step():
         nr, color, depth, radii, gb, bb, ib = _fwd(C, d)
-        # train.py:244 L1 loss and its gradient sign(color - gt) / N (fused kernels, csrc/train_tail.hip)
-        loss, sgn = TC.l1_forward(color, gt)
-        grad = TC.l1_backward(sgn, one)
+        # train.py:244 L1 loss and its gradient sign(color - gt) / N for loss.backward()'s dloss = 1: value and
+        # gradient in one pass (gs4d_l1_loss_grad, csrc/train_tail.hip; bitwise the two-pass form)
+        loss, grad = TC.l1_loss_grad(color, gt, 1.0)
         _bwd(C, d, radii, grad, gb, nr, bb, ib)
         if dist:
             import torch.distributed as tdist

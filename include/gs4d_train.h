@@ -21,6 +21,12 @@ extern "C" {
 size_t gs4d_l1_scratch_bytes(int64_t n);
 int gs4d_l1_loss_forward(int64_t n, const float *x, const float *y, int8_t *sign, float *loss, void *scratch,
                          void *stream);
+/* Value AND gradient in one pass, for an upstream gradient `dloss` known on the host (a training step's
+ * loss.backward() with dloss = 1): grad = sign(x - y) * (dloss * (1 / n)), bitwise what
+ * gs4d_l1_loss_forward + gs4d_l1_loss_backward give, without writing and re-reading the signs.  n % 4 == 0 and
+ * 16-byte aligned x, y, grad (GS4D_ERR_ARG otherwise). */
+int gs4d_l1_loss_grad(int64_t n, const float *x, const float *y, float dloss, float *loss, float *grad, void *scratch,
+                      void *stream);
 int gs4d_l1_loss_backward(int64_t n, const int8_t *sign, const float *dloss, float *grad, void *stream);
 
 /* ---- the deformation's tail and the activations before the rasterizer, in one pass each way:

@@ -287,6 +287,42 @@ def test_fused_adam_state_dict_interchanges_with_torch_adam():
     assert float(back.state[ps[0]]["step"]) == 2.0
 
 
+def test_fused_adam_host_step_counts(monkeypatch):
+    """FusedAdam keeps its step counts on the host (no per-parameter tensor op / .item() per step): the scalars
+    it passes to the launch follow torch's bias corrections for the right step, across the reference's
+    optimizer-state surgery (the state dict moved to a replacement parameter, gaussian_model.py:316-388) and a
+    state_dict() / load_state_dict() round trip, and the state's step tensors hold the count when read."""
+    import math
+    from gs4d_train import kernels as K
+    calls = []
+    monkeypatch.setattr(K, "_C", type("Fake", (), {"adam_step": staticmethod(lambda *a: calls.append(a))}))
+    ps = [torch.nn.Parameter(torch.randn(4)) for _ in range(3)]
+    for p in ps:
+        p.grad = torch.randn(4)
+    opt = K.FusedAdam([{"params": [p], "lr": 0.1} for p in ps], betas=(0.9, 0.99))
+    for _ in range(5):
+        opt.step()
+    check = lambda n: (abs(calls[-1][4][0] + 0.1 / (1 - 0.9 ** n)) < 1e-12 and
+                       abs(calls[-1][5][0] - math.sqrt(1 - 0.99 ** n)) < 1e-12)
+    assert check(5)
+    st = opt.state.pop(ps[0])  # surgery: the state follows a new tensor for the same group
+    q = torch.nn.Parameter(torch.randn(6))
+    q.grad = torch.randn(6)
+    st["exp_avg"], st["exp_avg_sq"] = torch.zeros(6), torch.zeros(6)
+    opt.param_groups[0]["params"][0] = q
+    opt.state[q] = st
+    opt.step()
+    assert check(6)
+    sd = opt.state_dict()
+    assert [float(v["step"]) for v in sd["state"].values()] == [6.0, 6.0, 6.0]
+    assert float(opt.state[q]["step"]) == 6.0
+    opt2 = K.FusedAdam([{"params": [p], "lr": 0.1} for p in [q] + ps[1:]], betas=(0.9, 0.99))
+    opt2.load_state_dict(sd)
+    opt2.step()
+    assert check(7)
+    assert float(opt2.state_dict()["state"][0]["step"]) == 7.0
+
+
 def test_ssim_restatement():
     """utils/loss_utils.py:26-66: window taps, ssim(x, x) = 1, and a direct float64 evaluation of the
     same formula (zero-padded 11x11 Gaussian window) on a small image."""

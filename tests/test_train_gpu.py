@@ -29,6 +29,23 @@ def test_l1_loss_matches_torch(H, W):
     torch.testing.assert_close(x.grad, x2.grad, rtol=0, atol=0)  # sign * (g / N): bitwise
 
 
+@pytest.mark.parametrize("dloss", [1.0, 0.37])
+def test_l1_loss_grad_one_pass_matches_two_pass(dloss):
+    """gs4d_l1_loss_grad (value and gradient in one pass, the bench step's form) is bitwise the two-pass
+    l1_forward + l1_backward for the same upstream gradient, and the value is torch's L1 to 1e-6."""
+    from gs4d_train import _C
+    torch.manual_seed(7)
+    x = torch.rand(3, 101, 76, device="cuda")
+    y = torch.rand(3, 101, 76, device="cuda")
+    y[0, 0, :8] = x[0, 0, :8]  # exact ties: sign 0
+    loss, grad = _C.l1_loss_grad(x, y, dloss)
+    loss2, sgn = _C.l1_forward(x, y)
+    grad2 = _C.l1_backward(sgn, torch.full((1,), dloss, device="cuda"))
+    assert torch.equal(loss, loss2) and torch.equal(grad, grad2)
+    assert abs(float(loss) - float((x - y).abs().mean())) <= 1e-6
+    assert float(grad[0, 0, :8].abs().max()) == 0.0
+
+
 def test_densify_stats_match_reference():
     from gs4d_train.kernels import densify_stats
     P = 10007
