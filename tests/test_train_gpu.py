@@ -31,7 +31,7 @@ def test_l1_loss_matches_torch(H, W):
 
 @pytest.mark.parametrize("dloss", [1.0, 0.37])
 def test_l1_loss_grad_one_pass_matches_two_pass(dloss):
-    """gs4d_l1_loss_grad (value and gradient in one pass, the bench step's form) is bitwise the two-pass
+    """gs4d_l1_loss_grad (value and gradient in one launch, the bench step's form) is bitwise the two-pass
     l1_forward + l1_backward for the same upstream gradient, and the value is torch's L1 to 1e-6."""
     from gs4d_train import _C
     torch.manual_seed(7)
@@ -39,6 +39,13 @@ def test_l1_loss_grad_one_pass_matches_two_pass(dloss):
     y = torch.rand(3, 101, 76, device="cuda")
     y[0, 0, :8] = x[0, 0, :8]  # exact ties: sign 0
     loss, grad = _C.l1_loss_grad(x, y, dloss)
+    for _ in range(3):  # one launch: its last workgroup sums the partials and re-zeroes the completion counter
+        again = _C.l1_loss_grad(x, y, dloss)
+        assert torch.equal(again[0], loss) and torch.equal(again[1], grad)
+    big = torch.rand(3, 1014, 1352, device="cuda")  # the bench image: ~2000 workgroups
+    lb, gb = _C.l1_loss_grad(big, y.new_zeros(big.shape), 1.0)
+    lb2, sb = _C.l1_forward(big, torch.zeros_like(big))
+    assert torch.equal(lb, lb2) and torch.equal(gb, _C.l1_backward(sb, torch.ones(1, device="cuda")))
     loss2, sgn = _C.l1_forward(x, y)
     grad2 = _C.l1_backward(sgn, torch.full((1,), dloss, device="cuda"))
     assert torch.equal(loss, loss2) and torch.equal(grad, grad2)
