@@ -569,8 +569,10 @@ torch::Tensor hexplane_points_backward(const torch::Tensor &dpts_, const torch::
 // called here by their solution index (rocblas_gemm_algo_solution_index) for any P.  An index rocBLAS
 // rejects for a shape falls back to rocBLAS's own choice; the return value says which ran.
 // Column-major semantics: C (m x n) [+ i * sC] = op(A) op(B) for batch i, f32 inputs, f32 accumulation.
+// One handle per (device, host thread): the forward and the autograd engine's backward thread may both call
+// in, and rocblas_set_stream on a shared handle would race.
 static rocblas_handle rocblas_for(const torch::Tensor &t) {
-    static rocblas_handle handles[64] = {};
+    static thread_local rocblas_handle handles[64] = {};
     const int d = t.device().index();
     TORCH_CHECK(d >= 0 && d < 64, "gemm_f32: device index out of range");
     if (!handles[d]) TORCH_CHECK(rocblas_create_handle(&handles[d]) == rocblas_status_success, "rocblas_create_handle");

@@ -103,12 +103,16 @@ class FusedAdam(torch.optim.Optimizer):
         by_hyper = {}
         for group, p, g, st in work:
             t = st["step"]
-            e = cache.get(id(t))
-            if e is None or e[0] is not t:
-                e = cache[id(t)] = [t, t.numpy(), t.item()]  # CPU float32 0-d tensor, as torch's Adam keeps it
-            e[2] += 1.0
-            e[1][()] = e[2]
-            step = e[2]
+            if t.device.type != "cpu":  # a step tensor moved off the host (not torch's default): plain update
+                t += 1
+                step = t.item()
+            else:
+                e = cache.get(id(t))
+                if e is None or e[0] is not t:
+                    e = cache[id(t)] = [t, t.numpy(), t.item()]  # CPU float32 0-d tensor, as torch's Adam keeps it
+                e[2] += 1.0
+                e[1][()] = e[2]
+                step = e[2]
             beta1, beta2 = group["betas"]
             lists = by_hyper.get((beta1, beta2, group["eps"]))
             if lists is None:
