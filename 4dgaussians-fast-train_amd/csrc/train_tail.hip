@@ -907,28 +907,32 @@ struct HbOut {
     float *dw2[kHbMaxHeads];
     float *db2[kHbMaxHeads];
 };
+// 16 outputs per workgroup (16 interleaved sixteenths of the workgroups each, combined in a fixed order): the
+// ~2k outputs of a launch then fill ~120 CUs instead of ~60
+constexpr int kHbRedOut = 16, kHbRedSlices = 256 / kHbRedOut;
 __global__ __launch_bounds__(256) void heads_bwd_reduce_kernel(HbArgs A, HbOut O, int nwg, const float *__restrict__ part) {
-    __shared__ float s_sum[8][32];
+    __shared__ float s_sum[kHbRedSlices][kHbRedOut];
     const int per = A.poff[A.hk];
-    const int o = threadIdx.x & 31, q = threadIdx.x >> 5;
-    const int i = blockIdx.x * 32 + o;
+    const int o = threadIdx.x % kHbRedOut, q = threadIdx.x / kHbRedOut;
+    const int i = blockIdx.x * kHbRedOut + o;
     float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
     if (i < per) {
         int w = q;
-        for (; w + 24 < nwg; w += 32) {
+        constexpr int K = kHbRedSlices;
+        for (; w + 3 * K < nwg; w += 4 * K) {
             v0 += part[(size_t)w * per + i];
-            v1 += part[(size_t)(w + 8) * per + i];
-            v2 += part[(size_t)(w + 16) * per + i];
-            v3 += part[(size_t)(w + 24) * per + i];
+            v1 += part[(size_t)(w + K) * per + i];
+            v2 += part[(size_t)(w + 2 * K) * per + i];
+            v3 += part[(size_t)(w + 3 * K) * per + i];
         }
-        for (; w < nwg; w += 8) v0 += part[(size_t)w * per + i];
+        for (; w < nwg; w += K) v0 += part[(size_t)w * per + i];
     }
     s_sum[q][o] = (v0 + v1) + (v2 + v3);
     __syncthreads();
     if (q == 0 && i < per) {
         float t = 0.f;
 #pragma unroll
-        for (int e = 0; e < 8; e++) t += s_sum[e][o];
+        for (int e = 0; e < kHbRedSlices; e++) t += s_sum[e][o];
         if (i < A.poff[0]) {
             O.db1[A.h0 * A.W + i] = t;
         } else {
@@ -1421,22 +1425,26 @@ using namespace gs4d;
 
 // sum of S slices of n floats in slice order (gs4d_sum_slices): four slices in flight per thread, float4
 // columns when n and the pointers allow
+// 64-thread workgroups: a column per thread, so the (P / 1024)-slice sums of the MLP's 128 x 640 weight
+// gradient (20480 float4 columns) spread over 320 workgroups, every CU, where 256-thread ones filled 80 CUs
+constexpr int kSumThreads = 64;
 template <bool V4>
-__global__ __launch_bounds__(kTailThreads) void sum_slices_kernel(const float *__restrict__ parts, int S, int64_t n,
-                                                                  float *__restrict__ out) {
+__global__ __launch_bounds__(kSumThreads) void sum_slices_kernel(const float *__restrict__ parts, int S, int64_t n,
+                                                                 float *__restrict__ out) {
     const int64_t m = V4 ? n / 4 : n;
-    for (int64_t i = (int64_t)blockIdx.x * kTailThreads + threadIdx.x; i < m; i += (int64_t)gridDim.x * kTailThreads) {
+    for (int64_t i = (int64_t)blockIdx.x * kSumThreads + threadIdx.x; i < m; i += (int64_t)gridDim.x * kSumThreads) {
         if (V4) {
             const float4 *p = reinterpret_cast<const float4 *>(parts) + i;
             float4 acc = p[0];
             int s = 1;
-            for (; s + 3 < S; s += 4) {  // the loads of four slices issued together, added in order
-                const float4 a = p[(size_t)s * m], b = p[(size_t)(s + 1) * m], c = p[(size_t)(s + 2) * m],
-                             d = p[(size_t)(s + 3) * m];
-                acc.x = (((acc.x + a.x) + b.x) + c.x) + d.x;
-                acc.y = (((acc.y + a.y) + b.y) + c.y) + d.y;
-                acc.z = (((acc.z + a.z) + b.z) + c.z) + d.z;
-                acc.w = (((acc.w + a.w) + b.w) + c.w) + d.w;
+            for (; s + 7 < S; s += 8) {  // the loads of eight slices issued together, added in order
+                float4 v[8];
+#pragma unroll
+                for (int k = 0; k < 8; k++) v[k] = p[(size_t)(s + k) * m];
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    acc.x += v[k].x; acc.y += v[k].y; acc.z += v[k].z; acc.w += v[k].w;
+                }
             }
             for (; s < S; s++) {
                 const float4 a = p[(size_t)s * m];
@@ -1533,7 +1541,7 @@ int gs4d_heads_backward(const gs4d_heads_bwd *args, void *scratch, void *stream)
                 hipLaunchKernelGGL(heads_bwd_kernel, dim3(nwg), dim3(hk * b.W), 0, s, A, b.a, b.da, g[0], g[1], g[2],
                                    g[3], g[4], g[5], g[6], g[7], part);
         }
-        hipLaunchKernelGGL(heads_bwd_reduce_kernel, dim3((A.poff[hk] + 31) / 32), dim3(256), 0, s, A, O, nwg,
+        hipLaunchKernelGGL(heads_bwd_reduce_kernel, dim3((A.poff[hk] + kHbRedOut - 1) / kHbRedOut), dim3(256), 0, s, A, O, nwg,
                            (const float *)part);
     });
     if (err) return err;
@@ -1703,11 +1711,11 @@ int gs4d_sum_slices(const float *parts, int S, int64_t n, float *out, void *stre
     if (n == 0) return 0;
     const bool v4 = n % 4 == 0 && ((uintptr_t)parts % 16) == 0 && ((uintptr_t)out % 16) == 0;
     const int64_t m = v4 ? n / 4 : n;
-    const unsigned grid = (unsigned)std::min<int64_t>((m + kTailThreads - 1) / kTailThreads, 4096);
+    const unsigned grid = (unsigned)std::min<int64_t>((m + kSumThreads - 1) / kSumThreads, 16384);
     if (v4)
-        hipLaunchKernelGGL(sum_slices_kernel<true>, dim3(grid), dim3(kTailThreads), 0, (hipStream_t)stream, parts, S, n, out);
+        hipLaunchKernelGGL(sum_slices_kernel<true>, dim3(grid), dim3(kSumThreads), 0, (hipStream_t)stream, parts, S, n, out);
     else
-        hipLaunchKernelGGL(sum_slices_kernel<false>, dim3(grid), dim3(kTailThreads), 0, (hipStream_t)stream, parts, S, n,
+        hipLaunchKernelGGL(sum_slices_kernel<false>, dim3(grid), dim3(kSumThreads), 0, (hipStream_t)stream, parts, S, n,
                            out);
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
