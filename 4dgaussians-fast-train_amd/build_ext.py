@@ -27,6 +27,10 @@ HIP_SOURCES = ["preprocess.hip", "binning.hip", "render.hip", "preprocess_backwa
 # (package, pybind glue) pairs: each package gets an in-tree `_C` module over libgs4d
 BINDINGS = [("diff_gaussian_rasterization", "torch_glue.cpp"), ("simple_knn", "knn_glue.cpp"), ("gs4d_train", "train_glue.cpp")]
 NO_CONTRACT = {"preprocess.hip", "preprocess_backward.hip", "binning.hip", "knn.hip", "train_tail.hip", "hexplane.hip"}
+# The blend kernels pack pixel pairs explicitly (ext_vector_type(2) -> v_pk_*_f32); the SLP vectorizer
+# would also pack their scalar horizontal adds, paying register moves for a v_pk_add_f32 (4 issue cycles)
+# where two v_add_f32 cost about 5 (tools/bench/valu_rates.hip), so it is off for render.hip.
+NO_SLP = {"render.hip"}
 HIPCC_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics", "-Wall",
                "-Wno-unused-result", "-I" + INCLUDE]
 
@@ -68,7 +72,7 @@ def build(force=False, verbose=False):
         s = os.path.join(CSRC, src)
         o = os.path.join(OBJ, src + ".o")
         if force or _newer(o, [s] + headers):
-            extra = ["-ffp-contract=off"] if src in NO_CONTRACT else []
+            extra = (["-ffp-contract=off"] if src in NO_CONTRACT else []) + (["-fno-slp-vectorize"] if src in NO_SLP else [])
             _run([hipcc, *HIPCC_FLAGS, *extra, "-c", s, "-o", o], verbose)
         return o
 

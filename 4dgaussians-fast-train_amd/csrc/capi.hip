@@ -14,7 +14,13 @@ namespace gs4d {
 
 static thread_local std::string g_last_error;
 static thread_local bool g_profiling = false;
+// profiling level >= 2: the blend kernels (idempotent: pure functions of their inputs, the forward's
+// in-place run sort included) are launched this many times back to back inside their stage, and the
+// stage reports the per-launch average -- a kernel duration free of the event brackets' gaps, which is
+// what rocprofv3's kernel trace measures (bench.py's roofline)
+static thread_local int g_stage_repeats = 1;
 static thread_local std::vector<std::pair<const char *, hipEvent_t>> g_marks;
+static thread_local std::vector<int> g_mark_div;
 static thread_local std::vector<std::pair<const char *, float>> g_timings;
 
 static int fail(int code, const std::string &msg) {
@@ -41,16 +47,33 @@ static int fail(int code, const std::string &msg) {
         mark(name, stream);                                                                                            \
     } while (0)
 
-static void mark(const char *name, hipStream_t s) {
+// A blend-kernel stage: under profiling level >= 2 its launch is preceded by a bracket of its own and
+// repeated g_stage_repeats times, and the stage's time is the per-launch average.
+#define GS4D_REPEATED_STAGE(name, expr)                                                                                 \
+    do {                                                                                                               \
+        const int reps_ = g_profiling ? g_stage_repeats : 1;                                                           \
+        if (reps_ > 1) mark(name "_pre", stream);                                                                      \
+        for (int r_ = 0; r_ < reps_; r_++) GS4D_HIP(expr);                                                             \
+        if (debug) {                                                                                                   \
+            hipError_t e_ = hipStreamSynchronize(stream);                                                              \
+            if (e_ != hipSuccess)                                                                                      \
+                return fail(GS4D_ERR_HIP, std::string("[HIP ERROR] in stage ") + name + ": " + hipGetErrorString(e_)); \
+        }                                                                                                              \
+        mark(name, stream, reps_);                                                                                     \
+    } while (0)
+
+static void mark(const char *name, hipStream_t s, int div = 1) {
     if (!g_profiling) return;
     hipEvent_t ev;
     if (hipEventCreate(&ev) != hipSuccess) return;
     (void)hipEventRecord(ev, s);
     g_marks.emplace_back(name, ev);
+    g_mark_div.push_back(div);
 }
 static void begin_marks(hipStream_t s) {
     for (auto &m : g_marks) (void)hipEventDestroy(m.second);
     g_marks.clear();
+    g_mark_div.clear();
     mark("begin", s);
 }
 static void end_marks() {
@@ -60,10 +83,11 @@ static void end_marks() {
     for (size_t i = 1; i < g_marks.size(); i++) {
         float ms = 0.f;
         (void)hipEventElapsedTime(&ms, g_marks[i - 1].second, g_marks[i].second);
-        g_timings.emplace_back(g_marks[i].first, ms);
+        g_timings.emplace_back(g_marks[i].first, ms / (float)g_mark_div[i]);
     }
     for (auto &m : g_marks) (void)hipEventDestroy(m.second);
     g_marks.clear();
+    g_mark_div.clear();
 }
 
 static char *carve(char *&p, size_t bytes) {
@@ -177,7 +201,10 @@ extern "C" {
 
 const char *gs4d_last_error(void) { return g_last_error.c_str(); }
 const char *gs4d_version(void) { return "gs4d 0.1.0 gfx950"; }
-void gs4d_set_profiling(int enabled) { g_profiling = enabled != 0; }
+void gs4d_set_profiling(int enabled) {
+    g_profiling = enabled != 0;
+    g_stage_repeats = enabled >= 2 ? enabled : 1;
+}
 int gs4d_last_timings(const char **names, float *ms, int max_entries) {
     int n = (int)g_timings.size();
     for (int i = 0; i < n && i < max_entries; i++) {
@@ -280,7 +307,7 @@ int gs4d_forward_ex(gs4d_alloc_fn geometry_alloc, void *geometry_ctx, gs4d_alloc
     if (!bbuf) return fail(GS4D_ERR_ALLOC, "forward: binning buffer allocation failed");
     BinningState b = BinningState::carve(bbuf, L, T);
     GS4D_STAGE("binning", launch_binning(a, g, radii_ptr, b, L, img, stream));
-    GS4D_STAGE("render", launch_render_forward(a, g, b, img, out_color, out_depth, stream));
+    GS4D_REPEATED_STAGE("render", launch_render_forward(a, g, b, img, out_color, out_depth, stream));
     end_marks();
     return GS4D_OK;
 }
@@ -327,8 +354,8 @@ int gs4d_backward_ex(int P, int D, int M, int R, const float *background, int wi
     if (R > 0) {
         b = BinningState::carve(binning_buffer, R, T);
         const float *color_ptr = colors_precomp;  // NULL -> the forward's rgb (rasterizer_impl.cu:392)
-        GS4D_STAGE("render_backward",
-                   launch_render_backward(a, g, b.gid_by_e, b.upos, img, color_ptr, dL_dpix, contrib, stream));
+        GS4D_REPEATED_STAGE("render_backward",
+                            launch_render_backward(a, g, b.gid_by_e, b.upos, img, color_ptr, dL_dpix, contrib, stream));
     }
     GS4D_STAGE("contrib_reduce", launch_contrib_reduce(a, g, b, R, contrib, reduce_scratch, dL_dmean2D, dconic,
                                                        dL_dopacity, dL_dcolor, stream));

@@ -205,7 +205,7 @@ PYBIND11_MODULE(_C, m) {
     m.def("rasterize_gaussians", &RasterizeGaussians);
     m.def("rasterize_gaussians_backward", &RasterizeGaussiansBackward);
     m.def("mark_visible", &MarkVisible);
-    m.def("set_profiling", [](bool on) { gs4d_set_profiling(on ? 1 : 0); });
+    m.def("set_profiling", [](int level) { gs4d_set_profiling(level); });
     m.def("last_timings", &last_timings);
     m.def("version", []() { return std::string(gs4d_version()); });
 }

@@ -36,6 +36,7 @@ import torch  # noqa: E402
 # BASELINE.json's metric; value = the rasterizer fwd+bwd MGaussians/s, train_step.ms = the train-step ms
 BASELINE_METRIC = "train-step ms + rasterizer fwd+bwd MGaussians/s @100k pts, 1352×1014"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: 8.0 TB/s spec
+KERNEL_REPEATS = 10    # back-to-back launches per event bracket for the blend kernels' own durations
 
 
 def algorithmic_bytes(P, L, W, H, K=16):
@@ -128,11 +129,14 @@ def main(argv=None):
     value = world * P * args.steps / elapsed / 1e6
 
     stage_avg = stage_timings(scene, dgr._C, args.steps)
+    kernel_avg = stage_timings(scene, dgr._C, args.steps, repeats=KERNEL_REPEATS)
 
     extras = {}
     if not args.no_extras:
+        extras["forward_only"] = forward_timing(scene, dgr._C, args.steps, args.warmup)
         extras["autograd_wrapper"] = autograd_timing(scene, dgr, args.steps, args.warmup, P)
         extras["train_like_scene"] = train_like_timing(P, W, H, dev, args.steps, args.warmup, dgr._C, rank)
+        extras["configs"] = config_timings(dev, args.steps, args.warmup, dgr._C)
 
     # ---- the full fine-stage train step (the metric's "train-step ms") ----
     train = None if args.no_train_step else train_step_timing(P, W, H, dev, world, rank, args.train_steps,
@@ -142,7 +146,9 @@ def main(argv=None):
         L = int(nr)
         ab = algorithmic_bytes(P, L, W, H)
         dom = max(stage_avg, key=stage_avg.get)
-        dom_ms = stage_avg[dom]
+        # the kernel's own duration: back-to-back launches between two events (agrees with rocprofv3's
+        # kernel-trace average; the per-stage brackets of stage_ms add their gaps)
+        dom_ms = kernel_avg.get(dom, stage_avg[dom])
         dom_bytes = ab["render_backward"] if dom == "bwd.render_backward" else (
             ab["render"] if dom == "fwd.render" else None)
         achieved = dom_bytes / (dom_ms * 1e-3) / 1e9 if dom_bytes else None
@@ -165,7 +171,11 @@ def main(argv=None):
                          "traffic_note": "PMC bytes per launch (profiles/pmc_traffic.json): traffic = 2 x FETCH_SIZE + "
                                          "WRITE_SIZE (gfx950 wide-read correction), traffic_raw = FETCH_SIZE + "
                                          "WRITE_SIZE; the kernel's reads are mostly gathers, so the truth lies between",
-                         "algorithmic_bytes": dom_bytes, "avg_ms": round(dom_ms, 4)},
+                         "algorithmic_bytes": dom_bytes, "avg_ms": round(dom_ms, 4),
+                         "avg_ms_note": f"hipEvent average over {KERNEL_REPEATS} back-to-back launches on the "
+                                        f"launch stream; stage_ms (one launch per event bracket) reads "
+                                        f"{stage_avg[dom]:.4f}"},
+            "kernel_ms": {k: round(v, 4) for k, v in kernel_avg.items()},
             "step_roofline": {"algorithmic_bytes": ab["step"],
                               "achieved_GBs": round(ab["step"] / (ms_per_step * 1e-3) / 1e9, 2),
                               "frac": round(ab["step"] / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)},
@@ -257,9 +267,12 @@ def gather_per_rank(row, world, dev, dist):
     return tab.cpu().tolist()
 
 
-def stage_timings(d, C, steps):
-    """Per-kernel hipEvent timings on the launch stream (same workload, a few more steps)."""
-    C.set_profiling(True)
+def stage_timings(d, C, steps, repeats=1):
+    """Per-kernel hipEvent timings on the launch stream (same workload, a few more steps).  With
+    repeats > 1 the two blend kernels run `repeats` times back to back inside their stage and report the
+    per-launch average (gs4d_set_profiling(level)): a kernel duration without the event brackets' gaps,
+    the quantity rocprofv3's kernel trace reports (the roofline's avg_ms)."""
+    C.set_profiling(repeats if repeats > 1 else 1)
     stage_ms = {}
     gt = torch.tensor(np.random.default_rng(1).uniform(0, 1, (3, d["H"], d["W"])).astype(np.float32),
                       device=d["bg"].device)
@@ -271,8 +284,37 @@ def stage_timings(d, C, steps):
         _bwd(C, d, radii, grad, gb, nr, bb, ib)
         for name, ms in C.last_timings():
             stage_ms.setdefault("bwd." + name, []).append(ms)
-    C.set_profiling(False)
-    return {k: float(np.mean(v)) for k, v in stage_ms.items()}
+    C.set_profiling(0)
+    out = {k: float(np.mean(v)) for k, v in stage_ms.items()}
+    if repeats > 1:   # only the blend kernels are repeated; the other entries include the repeats' gaps
+        out = {k: v for k, v in out.items() if k in ("fwd.render", "bwd.render_backward")}
+    return out
+
+
+def forward_timing(d, C, steps, warmup):
+    """Forward only (the inference path render.py times: rasterizer forward of one view), ms and FPS."""
+    el, nr = timed_steps(lambda: _fwd(C, d)[0], steps, warmup, False)
+    ms = el / steps * 1e3
+    return {"ms": round(ms, 4), "fps": round(1e3 / ms, 1), "num_rendered": int(nr)}
+
+
+def config_timings(dev, steps, warmup, C, names=("c2_800", "c4_per_view", "c5_broom"), fwd_only=("c2_800",)):
+    """BASELINE configs C2 (100k, 800x800), C4 (300k, 1352x1014: one view of the 8-GPU run) and C5 (1M,
+    960x536): the headline step (fwd + L1 + bwd) per config, MGaussians/s and L; forward-only at C2."""
+    from gs4d_train.synthetic import CONFIGS, make_scene
+    res = {}
+    for name in names:
+        P, W, H = CONFIGS[name]
+        d = upload_scene(make_scene(P, W, H, seed=0), dev)
+        el, nr = timed_steps(make_step(d, dev, 0, C, False), steps, warmup, False)
+        ms = el / steps * 1e3
+        res[name] = {"P": P, "image": f"{W}x{H}", "ms_per_step": round(ms, 4),
+                     "MGaussians_s": round(P / (ms * 1e-3) / 1e6, 3), "num_rendered": int(nr)}
+        if name in fwd_only:
+            res[name]["forward_only"] = forward_timing(d, C, steps, warmup)
+        del d
+        torch.cuda.empty_cache()
+    return res
 
 
 def autograd_timing(d, dgr, steps, warmup, P):
@@ -445,14 +487,19 @@ def cpu_baseline(s, budget_s):
     """The oracle (C restatement, OpenMP) on the host cores: same scene, full fwd+bwd per sample, with
     the box's CPU share (<= 16 threads) and with one thread."""
     try:
-        cores = len(os.sched_getaffinity(0))
+        affinity = len(os.sched_getaffinity(0))
     except Exception:
-        cores = os.cpu_count() or 1
-    cores = min(cores, 16)   # the GPU box gives this job a 16-CPU share
+        affinity = os.cpu_count() or 1
+    # threads: OMP_NUM_THREADS when set (the GPU box sets it to this job's CPU share), else the affinity
+    env_threads = os.environ.get("OMP_NUM_THREADS", "")
+    cores = int(env_threads) if env_threads.isdigit() and int(env_threads) > 0 else affinity
+    cores = min(cores, affinity)
     P, W, H = s["means3D"].shape[0], s["W"], s["H"]
     med, n = _cpu_sample(s, cores, budget_s, 20)
     med1, n1 = _cpu_sample(s, 1, 0.0, 1)     # one sample: a full view takes seconds on one thread
     return {"value": round(P / med / 1e6, 4), "unit": "MGaussians/s", "cores": cores, "kind": "port",
+            "affinity_cpus": affinity, "threads_used": cores,
+            "threads_source": "OMP_NUM_THREADS" if env_threads.isdigit() else "sched_getaffinity",
             "sample": f"{n} full fwd+bwd of the same metric view (P={P}, {W}x{H}) by the OpenMP C oracle, "
                       f"median {med * 1e3:.1f} ms",
             "one_thread": {"value": round(P / med1 / 1e6, 5), "cores": 1,

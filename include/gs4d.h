@@ -119,7 +119,9 @@ const char *gs4d_version(void);
 
 /* Per-kernel timing of the most recent gs4d_forward / gs4d_backward on this thread, recorded with
  * hipEvents on the launch stream when profiling is enabled (bench.py).  names[i] / ms[i] for
- * i < *count; returns the number of entries. */
+ * i < *count; returns the number of entries.  enabled >= 2 launches the two blend kernels (render,
+ * render_backward) that many times back to back and reports their per-launch average (an entry
+ * "<name>_pre" then holds the time up to that stage). */
 void gs4d_set_profiling(int enabled);
 int gs4d_last_timings(const char **names, float *ms, int max_entries);
 

@@ -18,7 +18,8 @@ for v in cur $VARIANTS; do
 import json,sys
 j=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1])
 tl=j.get('train_like_scene',{}); st=tl.get('stage_ms',{})
-print(f"{sys.argv[2]:8s} ms {j['ms_per_step']} fwd {j['stage_ms']['fwd.render']*1e3:.1f} bwd {j['stage_ms']['bwd.render_backward']*1e3:.1f} bin {j['stage_ms']['fwd.binning']*1e3:.1f} | train_like ms {tl.get('ms_per_step')} fwd {st.get('fwd.render',0)*1e3:.1f} bwd {st.get('bwd.render_backward',0)*1e3:.1f} bin {st.get('fwd.binning',0)*1e3:.1f}")
+km=j.get('kernel_ms',{})
+print(f"{sys.argv[2]:8s} ms {j['ms_per_step']} fwd {j['stage_ms']['fwd.render']*1e3:.1f} bwd {j['stage_ms']['bwd.render_backward']*1e3:.1f} (kernel {km.get('fwd.render',0)*1e3:.1f} / {km.get('bwd.render_backward',0)*1e3:.1f}) bin {j['stage_ms']['fwd.binning']*1e3:.1f} | train_like ms {tl.get('ms_per_step')} fwd {st.get('fwd.render',0)*1e3:.1f} bwd {st.get('bwd.render_backward',0)*1e3:.1f} bin {st.get('fwd.binning',0)*1e3:.1f}")
 PY
 done
 done

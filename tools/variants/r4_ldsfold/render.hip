@@ -18,11 +18,12 @@
 // carried as one scalar A = accum_rec . dL/dpix, updated eagerly after each contributing splat
 // (A = alpha CD + (1 - alpha) A, the same recurrence as backward.cu:515-517).  The 9 gradient terms of
 // a splat (backward.cu:523,545-554) are linear in 6 per-pixel moments (sum u, sum u dx, sum u dy,
-// sum u dx^2, sum u dx dy, sum u dy^2 with u = G dL/dalpha) and 3 colour sums; these 9 values are
-// reduced over the wave with two v_permlane swaps and a 16-lane DPP tree (reduce-scatter), staged in
-// LDS, and stored once per (tile, splat) instance at its emission slot (coalesced 48-byte records,
-// no float atomics).  The per-Gaussian pass (preprocess_backward.hip) sums a Gaussian's records in
-// a fixed order and applies the moment -> gradient map once (bitwise reproducible).
+// sum u dx^2, sum u dx dy, sum u dy^2 with u = G dL/dalpha) and 3 colour sums; they are accumulated in
+// tile-centred pixel coordinates, reduced over the wave per pair of splats (an LDS fold over the 4
+// lanes of each column, then a 16-lane DPP reduce-scatter) and stored once per (tile, splat) instance
+// at its emission slot (no float atomics).  The per-Gaussian pass (preprocess_backward.hip) shifts
+// each record to the splat's centre, sums a Gaussian's records in a fixed order and applies the
+// moment -> gradient map once (bitwise reproducible).
 #include <type_traits>
 
 #include "gs4d_internal.h"
@@ -32,13 +33,6 @@ namespace gs4d {
 typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 __device__ __forceinline__ f2 bc2(float x) { return f2{x, x}; }
-// x + y of a pixel pair as one v_add_f32 (the backend would form a v_pk_add_f32 with op_sel, 4 issue
-// cycles against ~2.5 for the plain add when other waves share the SIMD: tools/bench/valu_rates.hip)
-__device__ __forceinline__ float hsum(f2 v) {
-    float r;
-    asm("v_add_f32 %0, %1, %2" : "=v"(r) : "v"(v.x), "v"(v.y));
-    return r;
-}
 
 
 // Blend-ready splat constants.  geo = (x, y - yc, -a/2 log2e, -b log2e), opc = (-c/2 log2e, opacity, -, -),
@@ -422,64 +416,62 @@ hipError_t launch_render_forward(const Args &a, GeomState g, BinningState b, Ima
 }
 
 // ---------------------------------------------------------------------------------------------
-// lanes 0-31 of the result hold a's half-wave sums, lanes 32-63 b's (v_permlane32_swap)
-__device__ __forceinline__ float swap32_add(float a, float b) {
-    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
-    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-}
-// rows (0,1,2,3) of the result hold (a rows 0+1, b rows 0+1, a rows 2+3, b rows 2+3) (v_permlane16_swap)
-__device__ __forceinline__ float swap16_add(float a, float b) {
-    auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
-    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-}
-
-// Per-lane partial sums of one splat of the reverse walk, its pixel pair already added: the moments
-// of u = G dL/dalpha in the tile-centred row coordinate yl (sum u, sum u yl, sum u yl^2) and the
-// colour sums (sum w dL/dpix_c, w = alpha T).
+// Per-lane partial sums of one splat of the reverse walk, its pixel pair already added: the moments of
+// u = G dL/dalpha in the tile-centred coordinates xl = px - xc, yl = py - yc (sum u, sum u yl,
+// sum u yl^2, and sum u xl, sum u xl yl pre-weighted by the lane's column) and the colour sums
+// (sum w dL/dpix_c, w = alpha T).
 struct SplatPart {
-    float u0, u1, u2, w0, w1, w2;
+    float u0, u1, u2, w0, w1, w2, xu0, xu1;
 };
 
-// Wave64 totals of two splats' partial sums, left in LDS as their 9 record values:
-//   0 sum u, 1 sum dx u, 2 sum u yl, 3 sum dx^2 u, 4 sum dx u yl, 5 sum u yl^2, 6-8 colour sums
-// (dx = mean.x - pixel x, per lane column).  v_permlane32_swap then v_permlane16_swap sum each value
-// over the 4 lanes of a column (reduce-scatter: row r of x1 ends with (a.u0, a.u1, b.u0, b.u1)[r], of x2
-// (a.u2, a.w0, b.u2, b.w0)[r], of x3 (a.w1, a.w2, b.w1, b.w2)[r]); the dx-weighted moments x4, x5 are
-// formed on those column sums.  The 16 columns of each row are then reduce-scattered too, with DPP:
-// pairs of registers halve at each of the four stages (column c with c ^ 8, the half-row mirror, c ^ 2,
-// c ^ 1), so every lane ends with one finished total (15 DPP-stage instructions for the 5 registers
-// instead of 20 for 5 butterflies) and writes it with ONE ds_write at a lane-constant offset `roff`
-// (red_offset(); -1: nothing to write).
+// Wave64 totals of two splats' partial sums, each finished total stored straight into its splat's
+// gradient record (raw tile-centred moments, 10 floats of the 12-float record at the instance's emission
+// slot; contrib_segments shifts them to the splat's centre):
+//   0 S u, 1 S xl u, 2 S yl u, 3 S xl^2 u, 4 S xl yl u, 5 S yl^2 u, 6-8 colour sums, 9 xc, 10 yc.
+// Step 1, the 4 lanes of each column (the row groups r = lane / 16), through LDS: every lane writes its
+// 16 values as 4 float4 groups (group r = the quantities row r will hold; one contiguous 1 KiB block per
+// store) and reads group r of the 4 lanes of its column (4 ds_read_b128), 12 adds -- the LDS pipe moves
+// the data, where v_permlane32/16_swap cost 8 VALU issue cycles each (tools/bench/valu_rates.hip).  Row
+// r then holds the column sums of (a: S u, S yl u, S yl^2 u, W0 | a: W1, W2, S xl u, S xl yl u | the
+// same for b), and x5 = xl * (column sum of xl u) = the column's S xl^2 u on rows 1 and 3.
+// Step 2, the 16 columns of each row, by DPP reduce-scatter: pairs of registers halve at each of the
+// four stages (column c with c ^ 8, the half-row mirror, c ^ 2, c ^ 1), so every lane ends with one
+// finished total (red_field() names it).
 template <int CTRL>
 __device__ __forceinline__ float dpp(float v) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
 }
-// record float offset (from record j's start; record j + 1 follows at +12) of this lane's total
-__device__ __forceinline__ int red_offset(int lane) {
-    const int r = lane >> 4, c = lane & 15, splat = (r >> 1) * 12, odd = r & 1;
+// record field of this lane's total (-1: none); *splat_b: the pair's second splat.  Fields 9 and 10 are
+// the tile centre (lane constants, written by otherwise idle lanes).
+__device__ __forceinline__ int red_field(int lane, bool *splat_b) {
+    const int r = lane >> 4, c = lane & 15;
+    const bool odd = r & 1;
+    *splat_b = r >= 2;
     switch (c) {
-    case 0: return splat + (odd ? 2 : 0);   // x1: S u, S u yl
-    case 4: return splat + (odd ? 8 : 7);   // x3: W1, W2
-    case 8: return splat + (odd ? 6 : 5);   // x2: S u yl^2, W0
-    case 12: return splat + (odd ? 4 : 1);  // x4: S dx u yl, S dx u
-    case 2: return odd ? -1 : splat + 3;    // x5: S dx^2 u (odd rows hold nothing)
+    case 0: return odd ? 7 : 0;    // row 0/2: S u        row 1/3: W1
+    case 8: return odd ? 8 : 2;    //          S yl u              W2
+    case 4: return odd ? 1 : 5;    //          S yl^2 u            S xl u
+    case 12: return odd ? 4 : 6;   //          W0                  S xl yl u
+    case 2: return odd ? 3 : -1;   //          -                   S xl^2 u (x5)
+    case 1: return odd ? -1 : 9;   //          xc
+    case 3: return odd ? -1 : 10;  //          yc
     default: return -1;
     }
 }
-__device__ __forceinline__ void wave_sum_pair_to_lds(const SplatPart &a, const SplatPart &b, float dxa, float dxb,
-                                                     float *rec_pair, int lane, int roff) {
-    const float h0 = swap32_add(a.u0, b.u0);  // lanes 0-31: a, 32-63: b
-    const float h1 = swap32_add(a.u1, b.u1);
-    const float h2 = swap32_add(a.u2, b.u2);
-    const float h3 = swap32_add(a.w0, b.w0);
-    const float h4 = swap32_add(a.w1, b.w1);
-    const float h5 = swap32_add(a.w2, b.w2);
-    const float x1 = swap16_add(h0, h1);
-    const float x2 = swap16_add(h2, h3);
-    const float x3 = swap16_add(h4, h5);
-    const float dxs = lane < 32 ? dxa : dxb;  // rows 0-1 hold splat a, rows 2-3 splat b
-    const float x4 = x1 * dxs;                 // (dx a.u0, dx a.u1, dx b.u0, dx b.u1)
-    const float x5 = x4 * dxs;                 // (dx^2 a.u0, -, dx^2 b.u0, -)
+__device__ __forceinline__ float pair_totals(const SplatPart &a, const SplatPart &b, float xl, float4 (*s_fold)[64],
+                                             int lane) {
+    s_fold[0][lane] = make_float4(a.u0, a.u1, a.u2, a.w0);
+    s_fold[1][lane] = make_float4(a.w1, a.w2, a.xu0, a.xu1);
+    s_fold[2][lane] = make_float4(b.u0, b.u1, b.u2, b.w0);
+    s_fold[3][lane] = make_float4(b.w1, b.w2, b.xu0, b.xu1);
+    const int r = lane >> 4, c = lane & 15;
+    // one wave writes and reads: LDS operations of a wave complete in order
+    const float4 k0 = s_fold[r][c], k1 = s_fold[r][c + 16], k2 = s_fold[r][c + 32], k3 = s_fold[r][c + 48];
+    const float x1 = ((k0.x + k1.x) + k2.x) + k3.x;
+    const float x2 = ((k0.y + k1.y) + k2.y) + k3.y;
+    const float x3 = ((k0.z + k1.z) + k2.z) + k3.z;
+    const float x4 = ((k0.w + k1.w) + k2.w) + k3.w;
+    const float x5 = xl * x3;  // rows 1, 3: S xl^2 u of the column
     const bool c8 = (lane & 8) == 0, c4 = (lane & 4) == 0, c2 = (lane & 2) == 0;
     // stage A (c, c ^ 8): x1 | x2 -> z12, x3 | x4 -> z34, x5 -> z5
     const float z12 = (c8 ? x1 : x2) + dpp<0x128>(c8 ? x2 : x1);  // row_ror:8
@@ -490,8 +482,7 @@ __device__ __forceinline__ void wave_sum_pair_to_lds(const SplatPart &a, const S
     const float w5 = z5 + dpp<0x141>(z5);
     // stage C (c ^ 2): w | w5 -> v; stage D (c ^ 1)
     const float v = (c2 ? w : w5) + dpp<0x4E>(c2 ? w5 : w);  // quad_perm [2, 3, 0, 1]
-    const float u = v + dpp<0xB1>(v);                         // quad_perm [1, 0, 3, 2]
-    if (roff >= 0) rec_pair[roff] = u;
+    return v + dpp<0xB1>(v);                                  // quad_perm [1, 0, 3, 2]
 }
 
 // Per-pixel state of the reverse walk (pairs): T (recovered backwards), A = accum_rec . dL/dpix and
@@ -512,14 +503,12 @@ struct BwdPixels {
 //        the image have T = dL/dpix = 0 and contribute exact zeros).
 //   GEN: the general splat: `chk` = its conic is not positive definite (power > 0 skips, forward.cu:341),
 //        and the 0.99 cap applies; without GEN the opacity is <= kCapFree, so o * G never reaches the cap.
-// The per-splat half of a step: falloff, the reference's skip decisions and alpha.
-struct HalfAlpha {
-    f2 ale, ae, om;  // o G with the skips applied, alpha, 1 - alpha
-};
 template <bool ALL, bool GEN>
-__device__ __forceinline__ HalfAlpha half_alpha(const f2 Y2, const f2 C2, const f2 O2, const f2 pa2, const f2 pb2,
-                                                f2 yl, bool chk, uint32_t contributor, uint32_t last0,
-                                                uint32_t last1) {
+__device__ __forceinline__ void half_step(f2 &T, f2 &A, const f2 dp0, const f2 dp1, const f2 dp2,
+                                          const f2 Y2, const f2 C2, const f2 O2, const f2 R2, const f2 G2,
+                                          const f2 B2, const f2 pa2, const f2 pb2, f2 yl, f2 yl2, bool chk,
+                                          uint32_t contributor, uint32_t last0, uint32_t last1, f2 &U0, f2 &U1,
+                                          f2 &U2, f2 &W0, f2 &W1, f2 &W2) {
     const f2 dy = Y2 - yl;  // Y2 = my - yc
     const f2 pw = fma2(dy, fma2(C2, dy, pb2), pa2);
     const f2 G = f2{__builtin_amdgcn_exp2f(pw.x), __builtin_amdgcn_exp2f(pw.y)};
@@ -535,71 +524,24 @@ __device__ __forceinline__ HalfAlpha half_alpha(const f2 Y2, const f2 C2, const 
         k1 = k1 && (!chk || pw.y <= 0.0f);
     }
     // the skip applied to o G: a skipped pixel has alpha 0 exactly
-    HalfAlpha h;
-    h.ale = f2{k0 ? al.x : 0.f, k1 ? al.y : 0.f};
-    h.ae = GEN ? f2{fminf(0.99f, h.ale.x), fminf(0.99f, h.ale.y)} : h.ale;
-    h.om = bc2(1.f) - h.ae;
-    return h;
-}
-// The rest of a step once the splat's T (the transmittance in front of it, Tn) is known.
-template <bool GEN>
-__device__ __forceinline__ void half_accum(const HalfAlpha &h, const f2 Tn, f2 &A, const f2 dp0, const f2 dp1,
-                                           const f2 dp2, const f2 R2, const f2 G2, const f2 B2, f2 yl, f2 yl2,
-                                           f2 &U0, f2 &U1, f2 &U2, f2 &W0, f2 &W1, f2 &W2) {
+    const f2 ale = f2{k0 ? al.x : 0.f, k1 ? al.y : 0.f};
+    const f2 ae = GEN ? f2{fminf(0.99f, ale.x), fminf(0.99f, ale.y)} : ale;
+    const f2 om = bc2(1.f) - ae;
+    const f2 inv = f2{__builtin_amdgcn_rcpf(om.x), __builtin_amdgcn_rcpf(om.y)};
+    const f2 Tn = T * inv;  // backward.cu:503
+    T = Tn;
     const f2 diff = fma2(B2, dp2, fma2(G2, dp1, fma2(R2, dp0, -A)));  // c . dL/dpix - accum_rec . dL/dpix
-    A = fma2(h.ae, diff, A);                    // accum_rec for the next splat in front
-    const f2 w = h.ae * Tn;                     // dchannel_dcolor (backward.cu:521)
+    A = fma2(ae, diff, A);                      // accum_rec for the next splat in front
+    const f2 w = ae * Tn;                       // dchannel_dcolor (backward.cu:521)
     // u' = o G dL/dalpha = o G T diff (backward.cu:519-534, bg term in A's start value); without the
     // cap o G T = w
-    const f2 u = (GEN ? h.ale * Tn : w) * diff;
+    const f2 u = (GEN ? ale * Tn : w) * diff;
     U0 += u;
     U1 = fma2(u, yl, U1);
     U2 = fma2(u, yl2, U2);
     W0 = fma2(w, dp0, W0);
     W1 = fma2(w, dp1, W1);
     W2 = fma2(w, dp2, W2);
-}
-// One half tile of one splat of the reverse walk: updates the half's pixel state and adds its
-// per-lane partial sums (moments of u' = o G dL/dalpha in the tile-centred row coordinate yl -- the
-// record divides them by o once -- and the colour sums) to U0..U2 / W0..W2.  The falloff is the
-// forward's sequence (falloff()) on operand pairs: identical blend decisions.  Branch-free, so that the
-// pair walk below is one basic block.
-//   ALL: the splat lies below every pixel's n_contrib (the contributor test passes; pixels outside
-//        the image have T = dL/dpix = 0 and contribute exact zeros).
-//   GEN: the general splat: `chk` = its conic is not positive definite (power > 0 skips, forward.cu:341),
-//        and the 0.99 cap applies; without GEN the opacity is <= kCapFree, so o * G never reaches the cap.
-// Two splats walking the same half share one reciprocal (half_pair_step): T in front of the back splat
-// a is T / (1 - alpha_a), in front of b T / ((1 - alpha_a)(1 - alpha_b)) -- one v_rcp_f32 of the
-// product per pixel (8 issue cycles each) and two multiplies instead of two reciprocals.
-struct SplatOps {
-    f2 Y2, C2, O2, R2, G2, B2, pa2, pb2;
-    bool chk;
-    uint32_t contributor;
-};
-template <bool ALL, bool GEN>
-__device__ __forceinline__ void half_step(f2 &T, f2 &A, const f2 dp0, const f2 dp1, const f2 dp2, const SplatOps &s,
-                                          f2 yl, f2 yl2, uint32_t last0, uint32_t last1, f2 (&U)[6]) {
-    const HalfAlpha h = half_alpha<ALL, GEN>(s.Y2, s.C2, s.O2, s.pa2, s.pb2, yl, s.chk, s.contributor, last0, last1);
-    const f2 inv = f2{__builtin_amdgcn_rcpf(h.om.x), __builtin_amdgcn_rcpf(h.om.y)};
-    const f2 Tn = T * inv;  // backward.cu:503
-    T = Tn;
-    half_accum<GEN>(h, Tn, A, dp0, dp1, dp2, s.R2, s.G2, s.B2, yl, yl2, U[0], U[1], U[2], U[3], U[4], U[5]);
-}
-template <bool ALL, bool GEN>
-__device__ __forceinline__ void half_pair_step(f2 &T, f2 &A, const f2 dp0, const f2 dp1, const f2 dp2,
-                                               const SplatOps &sa, const SplatOps &sb, f2 yl, f2 yl2, uint32_t last0,
-                                               uint32_t last1, f2 (&Ua)[6], f2 (&Ub)[6]) {
-    const HalfAlpha ha = half_alpha<ALL, GEN>(sa.Y2, sa.C2, sa.O2, sa.pa2, sa.pb2, yl, sa.chk, sa.contributor,
-                                              last0, last1);
-    const HalfAlpha hb = half_alpha<ALL, GEN>(sb.Y2, sb.C2, sb.O2, sb.pa2, sb.pb2, yl, sb.chk, sb.contributor,
-                                              last0, last1);
-    const f2 prod = ha.om * hb.om;
-    const f2 r = f2{__builtin_amdgcn_rcpf(prod.x), __builtin_amdgcn_rcpf(prod.y)};
-    const f2 Tb = T * r;         // backward.cu:503 twice: T / (1 - alpha_a) / (1 - alpha_b)
-    const f2 Ta = Tb * hb.om;    // T / (1 - alpha_a)
-    half_accum<GEN>(ha, Ta, A, dp0, dp1, dp2, sa.R2, sa.G2, sa.B2, yl, yl2, Ua[0], Ua[1], Ua[2], Ua[3], Ua[4], Ua[5]);
-    half_accum<GEN>(hb, Tb, A, dp0, dp1, dp2, sb.R2, sb.G2, sb.B2, yl, yl2, Ub[0], Ub[1], Ub[2], Ub[3], Ub[4], Ub[5]);
-    T = Tb;
 }
 
 // 4 waves per SIMD (<= 128 VGPRs, no spills): the reach-combo blocks hold at most the four falloff chains
@@ -611,7 +553,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
                             const uint32_t *__restrict__ n_contrib, const float *__restrict__ dL_dpixels,
                             float *__restrict__ contrib) {
     __shared__ SplatLDS s_sp[64];
-    __shared__ float4 s_rec[64][3];  // reduced sums of the batch's splats
+    __shared__ float4 s_fold[4][64];  // one pair's per-lane sums on their way across the column's lanes
     const int tile = (int)__builtin_amdgcn_readfirstlane(order[blockIdx.x]);  // longest runs first
     const int tx = tile % a.gx, ty = tile / a.gx;
     const int lane = threadIdx.x;
@@ -629,7 +571,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     const f2 yl[2] = {f2{ylane, ylane + 4.f}, f2{ylane + 8.f, ylane + 12.f}};
     const f2 yl2[2] = {yl[0] * yl[0], yl[1] * yl[1]};
     const float yc = (float)(ty * kBlockY) + 7.5f;
-    const int roff = red_offset(lane);
+    const float xc = (float)(tx * kBlockX) + 7.5f;
+    const float xl = (float)(lane & 15) - 7.5f;  // this lane's column, tile-centred
+    bool fld_b;
+    const int fld = red_field(lane, &fld_b);
+    const bool fld_const = fld >= 9;              // the lane stores the tile centre, not a total
+    const float fld_cval = fld == 9 ? xc : yc;
+    const bool fld_a = fld >= 0 && !fld_b, fld_bb = fld >= 0 && fld_b;
 
     BwdPixels st;
     uint32_t lastc[4];
@@ -672,7 +620,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
         float4 *rec = reinterpret_cast<float4 *>(contrib + (size_t)upos[range.x + p] * kContribStride);
         rec[0] = z4;
         rec[1] = z4;
-        rec[2] = z4;
+        rec[2] = make_float4(0.f, xc, yc, 0.f);
     }
     // The walk's instances: emission slot e (where the gradient record goes) and gid_by_e[e] of list
     // position end-1-lane of each batch, loaded 2 batches at a time (independent loads, one wait per
@@ -738,40 +686,43 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
             constexpr bool ALL = decltype(all)::value, GEN = decltype(gen)::value;
             constexpr int M[2] = {decltype(m0)::value, decltype(m1)::value};
             SplatPart part[2];
-            float dxs[2], pa[2], pb[2];
+            float pa[2], pb[2];
             float4 geo[2], opc[2], col[2];
 #pragma unroll
             for (int i = 0; i < 2; i++) {
                 geo[i] = s_sp[j + i].geo; opc[i] = s_sp[j + i].opc; col[i] = s_sp[j + i].col;
-                dxs[i] = geo[i].x - pfx;
-                pa[i] = geo[i].z * dxs[i] * dxs[i];  // forward: geo.z * dx * dx, geo.w * dx
-                pb[i] = geo[i].w * dxs[i];
+                const float dx = geo[i].x - pfx;
+                pa[i] = geo[i].z * dx * dx;  // forward: geo.z * dx * dx, geo.w * dx
+                pb[i] = geo[i].w * dx;
             }
             f2 U[2][6];
 #pragma unroll
             for (int i = 0; i < 2; i++)
 #pragma unroll
                 for (int k = 0; k < 6; k++) U[i][k] = bc2(0.f);
-            SplatOps so[2];
 #pragma unroll
-            for (int i = 0; i < 2; i++)
-                so[i] = SplatOps{bc2(geo[i].y), bc2(opc[i].x), bc2(opc[i].y), bc2(col[i].x), bc2(col[i].y),
-                                 bc2(col[i].z), bc2(pa[i]), bc2(pb[i]), ((nonpd >> (j + i)) & 1) != 0,
-                                 (uint32_t)(end - 1 - (j + i))};
+            for (int h = 0; h < 2; h++)
 #pragma unroll
-            for (int h = 0; h < 2; h++) {
-                if (M[h] == 3)
-                    half_pair_step<ALL, GEN>(st.T[h], st.A[h], st.dp0[h], st.dp1[h], st.dp2[h], so[0], so[1], yl[h],
-                                             yl2[h], lastc[2 * h], lastc[2 * h + 1], U[0], U[1]);
-                else if (M[h] != 0)
-                    half_step<ALL, GEN>(st.T[h], st.A[h], st.dp0[h], st.dp1[h], st.dp2[h], so[M[h] >> 1], yl[h],
-                                        yl2[h], lastc[2 * h], lastc[2 * h + 1], U[M[h] >> 1]);
+                for (int i = 0; i < 2; i++)
+                    if ((M[h] >> i) & 1)
+                    half_step<ALL, GEN>(st.T[h], st.A[h], st.dp0[h], st.dp1[h], st.dp2[h], bc2(geo[i].y),
+                                        bc2(opc[i].x), bc2(opc[i].y), bc2(col[i].x), bc2(col[i].y), bc2(col[i].z),
+                                        bc2(pa[i]), bc2(pb[i]), yl[h], yl2[h], (nonpd >> (j + i)) & 1,
+                                        (uint32_t)(end - 1 - (j + i)), lastc[2 * h], lastc[2 * h + 1], U[i][0],
+                                        U[i][1], U[i][2], U[i][3], U[i][4], U[i][5]);
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+                const float u0 = U[i][0].x + U[i][0].y, u1 = U[i][1].x + U[i][1].y;
+                part[i] = SplatPart{u0, u1, U[i][2].x + U[i][2].y, U[i][3].x + U[i][3].y, U[i][4].x + U[i][4].y,
+                                    U[i][5].x + U[i][5].y, xl * u0, xl * u1};
             }
-#pragma unroll
-            for (int i = 0; i < 2; i++)
-                part[i] = SplatPart{hsum(U[i][0]), hsum(U[i][1]), hsum(U[i][2]), hsum(U[i][3]), hsum(U[i][4]),
-                                    hsum(U[i][5])};
-            wave_sum_pair_to_lds(part[0], part[1], dxs[0], dxs[1], reinterpret_cast<float *>(s_rec[j]), lane, roff);
+            const float tot = pair_totals(part[0], part[1], xl, s_fold, lane);
+            // each finished total goes straight to its splat's record (the pair's ~20 lanes, one store
+            // per splat with the record base in SGPRs); an odd batch's zero splat has none
+            const float val = fld_const ? fld_cval : tot;
+            const uint32_t sa = __builtin_amdgcn_readlane(ucur, j), sb = __builtin_amdgcn_readlane(ucur, j + 1);
+            if (fld_a) contrib[(size_t)sa * kContribStride + fld] = val;
+            if (fld_bb && j + 1 < n) contrib[(size_t)sb * kContribStride + fld] = val;
         };
         using I3 = std::integral_constant<int, 3>;
         auto walk_batch = [&](auto all) {
@@ -808,23 +759,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
         // batches wholly below every inside pixel's n_contrib: the contributor test passes everywhere
         if ((uint32_t)(end - 1) < min_last) walk_batch(std::true_type{});
         else walk_batch(std::false_type{});
-        __syncthreads();
-        if (lane < n) {
-            // lane j writes splat j's record, its y moments moved from the tile centre to the splat's
-            // centre row: dy = my_l - yl (backward.cu:545-551 moments of dy)
-            const float4 r0 = s_rec[lane][0], r1 = s_rec[lane][1], r2 = s_rec[lane][2];
-            const float my_l = s_sp[lane].geo.y;  // this lane's splat, my - yc
-            const float io = s_sp[lane].opc.z;    // 1 / o: the moments were taken on u' = o u
-            // r0 = (S u, S dx u, S u yl, S dx^2 u), r1 = (S dx u yl, S u yl^2, W0, W1), r2 = (W2, -, -, -)
-            const float s_u = r0.x, s_uyl = r0.z;
-            const float v2 = my_l * s_u - s_uyl;                 // S u dy
-            const float v4 = my_l * r0.y - r1.x;                 // S dx u dy
-            const float v5 = my_l * v2 - (my_l * s_uyl - r1.y);  // S u dy^2
-            float4 *rec = reinterpret_cast<float4 *>(contrib + (size_t)ucur * kContribStride);
-            rec[0] = make_float4(s_u * io, r0.y * io, v2 * io, r0.w * io);
-            rec[1] = make_float4(v4 * io, v5 * io, r1.z, r1.w);
-            rec[2] = r2;
-        }
     }
 }
 
