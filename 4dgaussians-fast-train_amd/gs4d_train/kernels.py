@@ -108,7 +108,9 @@ class FusedAdam(torch.optim.Optimizer):
                 step = t.item()
             else:
                 e = cache.get(id(t))
-                if e is None or e[0] is not t:
+                # reload when the tensor is new to the cache or was edited in place since the last step
+                # (zero_(), copy_(), a manual reset): a host read through the numpy view, no sync
+                if e is None or e[0] is not t or float(e[1][()]) != e[2]:
                     e = cache[id(t)] = [t, t.numpy(), t.item()]  # CPU float32 0-d tensor, as torch's Adam keeps it
                 e[2] += 1.0
                 e[1][()] = e[2]

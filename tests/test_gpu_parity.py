@@ -1,17 +1,9 @@
 """GPU parity: the HIP path (through the `_C` binding over the C ABI) against the CPU oracle.
 
-Tolerances (north_star): RGB within 1e-4, depth within 1e-4 of the depth range (max(1, max depth)),
-gradients within 1e-3 per Gaussian, normalised by the tensor's largest magnitude.
-
-Every element must meet them except where the oracle itself says a discrete decision may flip.  The
-blend has two thresholds, alpha >= 1/255 and T(1 - alpha) >= 1e-4 (forward.cu:346-354,
-backward.cu:486-503); two correct float implementations (here exp2/FMA on gfx950 against the oracle's
-libm/no-FMA arithmetic) can land on either side when the operand lies within rounding of the
-threshold.  `oracle.flip_flags` replays the walk and flags the pixels with an operand within
-FLIP_BAND_ALPHA / FLIP_BAND_T (relative) of a threshold, and the Gaussians that are those near-threshold
-splats.  Unflagged elements: the tolerances above, no exception.  Flagged elements: a hard bound on the
-size one flip can have (a termination flip adds or removes one splat of weight alpha*T <= 0.99 * 1e-2;
-an alpha flip one of weight 1/255), and the flagged pixels must stay a small fraction of the image.
+The bars (north_star's 1e-4 on RGB/depth and 1e-3 on gradients, per element, plus sharper bars at the
+measured maxima, and the flip-flag allowances for the blend's two discrete thresholds) are defined and
+asserted in oracle/parity.py; every case prints its report, so each config's measured maxima are in
+the log.
 """
 import math
 
@@ -19,21 +11,15 @@ import numpy as np
 import pytest
 import torch
 
-from gpu_helpers import (c_backward, c_forward, grad_errors, grad_parity, o_backward, o_forward, split_max,
-                         to_dev)
+from gpu_helpers import c_backward, c_forward, o_backward, o_forward, to_dev
 from gs4d_train.synthetic import make_scene, make_upstream_grad
+from oracle import parity as PAR
 
 pytestmark = pytest.mark.gpu
-
-IMG_ATOL = 1e-4
-GRAD_RTOL = 1e-3
-GRAD_FRAC = 5e-3          # test_autograd_api only (no oracle state at hand there)
-FLIP_BAND_ALPHA = 3e-5    # |255 alpha - 1| within which the alpha test may flip
-FLIP_BAND_T = 3e-4        # |T(1 - alpha) / 1e-4 - 1| within which the termination may flip
-FLIP_COLOR_MAX = 0.03     # one splat of weight <= 0.99e-2 times |colour - bg| <= ~3
-FLIP_DEPTH_REL = 0.012    # one splat of weight <= 0.99e-2 times its depth (<= max depth)
-FLIP_GRAD_MAX = 2e-2      # a flipping splat's own gradient term at one pixel, normalised
-FLIP_PIX_FRAC = 2e-2      # the flagged pixels stay a small fraction of the image (measured <= 1.0 %)
+# measured flagged shares above oracle/parity.py's defaults: the train-like scene's large splats (9.3 % of
+# the Gaussians have a near-1/255 pixel); the 2^20-tile grid's few hundred splats with huge footprints (56 %)
+TRAIN_LIKE_GAUSS_FRAC = 0.12
+GRID_GAUSS_FRAC = 0.7
 
 
 @pytest.fixture(scope="module")
@@ -49,7 +35,8 @@ def dev():
     return torch.device("cuda:0")
 
 
-def _check(C, O, s, dev, colors=None, cov3D=None, use_sh=True, degree=None, report=None, pix_frac=FLIP_PIX_FRAC):
+def _check(C, O, s, dev, colors=None, cov3D=None, use_sh=True, degree=None, report=None,
+           pix_frac=PAR.FLIP_PIX_FRAC, gauss_frac=PAR.FLIP_GAUSS_FRAC):
     d = to_dev(s, dev)
     col_t = None if colors is None else torch.tensor(colors, device=dev)
     cov_t = None if cov3D is None else torch.tensor(cov3D, device=dev)
@@ -58,43 +45,19 @@ def _check(C, O, s, dev, colors=None, cov3D=None, use_sh=True, degree=None, repo
     nr, color, depth, radii, st = o_forward(O, s, colors=colors, cov3D=cov3D, use_sh=use_sh, degree=degree)
     assert fwd[0] == nr, f"num_rendered {fwd[0]} != oracle {nr}"
     assert np.array_equal(fwd[3].cpu().numpy(), radii), "radii differ"
-    pflag, gflag = O.flip_flags(st, FLIP_BAND_ALPHA, FLIP_BAND_T) if st is not None else (
+    pflag, gflag = O.flip_flags(st, PAR.FLIP_BAND_ALPHA, PAR.FLIP_BAND_T) if st is not None else (
         np.zeros((s["H"], s["W"]), np.uint8), np.zeros(len(radii), np.uint8))
-    cerr = np.abs(fwd[1].cpu().numpy().astype(np.float64) - color).max(0)
-    derr = np.abs(fwd[2].cpu().numpy().astype(np.float64) - depth)[0]
-    dscale = max(1.0, float(np.abs(depth).max()))
     g, _ = make_upstream_grad(color)
     g = g * (3 * s["W"] * s["H"])
     grads_c = c_backward(C, s, d, fwd, torch.tensor(g, device=dev), colors=col_t, cov3D=cov_t, use_sh=use_sh,
                          degree=degree)
     torch.cuda.synchronize()
     grads_o = o_backward(O, s, st, radii, g, colors=colors, cov3D=cov3D, use_sh=use_sh, degree=degree)
-    names = ["dL_dmeans2D", "dL_dcolors", "dL_dopacity", "dL_dmeans3D", "dL_dcov3D", "dL_dsh", "dL_dscales",
-             "dL_drotations"]
-    flagged = pflag != 0
-    res = {"L": nr, "flagged_pix": int(flagged.sum()), "flagged_gauss": int((gflag != 0).sum()),
-           "color": split_max(cerr, flagged), "depth": split_max(derr, flagged)}
-    for n, a, b in zip(names, grads_c, grads_o):
-        a = a.cpu().numpy()
-        assert a.shape == b.shape, f"{n} shape {a.shape} != {b.shape}"
-        if a.size:
-            assert np.isfinite(a).all(), f"{n} has non-finite values"
-        res[n] = split_max(grad_errors(a, b), gflag != 0)
+    res = PAR.check(fwd[1].cpu().numpy(), fwd[2].cpu().numpy(), [a.cpu().numpy() for a in grads_c], color, depth,
+                    grads_o, pflag, gflag, pix_frac=pix_frac, gauss_frac=gauss_frac)
+    res["L"] = nr
     if report is not None:
         report.append(res)
-    print(res)
-    # (max over unflagged, max over flagged) for every quantity
-    assert flagged.mean() <= pix_frac, f"{flagged.mean():.2e} of the pixels flagged"
-    assert res["color"][0] <= IMG_ATOL, f"colour: unflagged pixel off by {res['color'][0]:.3e} at " \
-                                         f"{np.unravel_index(np.argmax(np.where(flagged, 0, cerr)), cerr.shape)}"
-    assert res["color"][1] <= FLIP_COLOR_MAX, f"colour: flagged pixel off by {res['color'][1]:.3e}"
-    assert res["depth"][0] <= IMG_ATOL * dscale, f"depth: unflagged pixel off by {res['depth'][0]:.3e} at " \
-                                                  f"{np.unravel_index(np.argmax(np.where(flagged, 0, derr)), derr.shape)}"
-    assert res["depth"][1] <= FLIP_DEPTH_REL * dscale, f"depth: flagged pixel off by {res['depth'][1]:.3e}"
-    for n in names:
-        unf, fl = res[n]
-        assert unf <= GRAD_RTOL, f"{n}: an unflagged Gaussian off by {unf:.3e} of the tensor's max"
-        assert fl <= FLIP_GRAD_MAX, f"{n}: a flagged Gaussian off by {fl:.3e} of the tensor's max"
     return fwd, grads_c
 
 
@@ -173,7 +136,7 @@ def test_parity_long_tiles(C, oracle, dev):
     s = make_scene(30000, 64, 48, seed=19, log_scale=math.log(0.3))
     s["opacities"] = np.full_like(s["opacities"], 0.03)
     # thousands of faint splats per pixel: ~6 % of the pixels hold a near-1/255 splat
-    fwd, _ = _check(C, oracle, s, dev, pix_frac=0.1)
+    fwd, _ = _check(C, oracle, s, dev, pix_frac=0.1)  # ~6.5 % of the pixels hold a near-1/255 splat
     assert fwd[0] > 12 * 4096
 
 
@@ -252,7 +215,7 @@ def test_train_like_scene(C, oracle, dev):
     create_from_pcd leaves it, ~1,200 instances per touched tile, runs sorted by tile_sort_kernel)."""
     from gs4d_train.synthetic import make_train_like_scene
     s = make_train_like_scene(100_000, 1352, 1014, seed=0)
-    _check(C, oracle, s, dev)
+    _check(C, oracle, s, dev, gauss_frac=TRAIN_LIKE_GAUSS_FRAC)
 
 
 def test_parity_mid_tiles(C, oracle, dev):
@@ -299,11 +262,14 @@ def test_autograd_api(dev, oracle):
     (img * torch.tensor(g, device=dev)).sum().backward()
     nr, color, depth_o, radii_o, st = o_forward(oracle, s)
     go = o_backward(oracle, s, st, radii_o, g)
-    for name, t, ref in [("means3D", leaves["means3D"].grad, go[3]), ("shs", leaves["shs"].grad, go[5]),
-                         ("opacities", leaves["opacities"].grad, go[2]), ("scales", leaves["scales"].grad, go[6]),
-                         ("rotations", leaves["rotations"].grad, go[7]), ("means2D", screenspace.grad, go[0])]:
-        emax, efrac = grad_parity(t.cpu().numpy(), ref)
-        assert efrac <= GRAD_FRAC, f"{name}: {efrac:.3e} beyond tol (max {emax:.3e})"
+    pflag, gflag = oracle.flip_flags(st, PAR.FLIP_BAND_ALPHA, PAR.FLIP_BAND_T)
+    # the Python API's gradients: (means3D, shs, opacities, scales, rotations, means2D) against the
+    # oracle's (dL_dmeans3D, dL_dsh, dL_dopacity, dL_dscales, dL_drotations, dL_dmeans2D)
+    res = PAR.check(img.detach().cpu().numpy(), depth.detach().cpu().numpy(),
+                    [leaves[k].grad.cpu().numpy() for k in ("means3D", "shs", "opacities", "scales", "rotations")]
+                    + [screenspace.grad.cpu().numpy()], color, depth_o,
+                    [go[3], go[5], go[2], go[6], go[7], go[0]], pflag, gflag,
+                    names=["means3D", "shs", "opacities", "scales", "rotations", "means2D"])
     vis = raster.markVisible(leaves["means3D"].detach())
     assert vis.dtype == torch.bool and vis.shape == (3000,)
 
@@ -380,13 +346,10 @@ def test_grid_of_2pow20_tiles(C, oracle, dev):
     torch.cuda.synchronize()
     nr, color, depth, radii, st = o_forward(oracle, s)
     assert fwd[0] == nr and np.array_equal(fwd[3].cpu().numpy(), radii)
-    pflag, gflag = oracle.flip_flags(st, FLIP_BAND_ALPHA, FLIP_BAND_T)
-    cerr = np.abs(fwd[1].cpu().numpy() - color).max(0)
-    assert split_max(cerr, pflag != 0)[0] <= IMG_ATOL
-    del cerr
+    pflag, gflag = oracle.flip_flags(st, PAR.FLIP_BAND_ALPHA, PAR.FLIP_BAND_T)
     g = np.sign(color - 0.5).astype(np.float32)
     grads_c = c_backward(C, s, d, fwd, torch.tensor(g, device=dev))
     torch.cuda.synchronize()
     grads_o = o_backward(oracle, s, st, radii, g)
-    for a, b in zip(grads_c, grads_o):
-        assert split_max(grad_errors(a.cpu().numpy(), b), gflag != 0)[0] <= GRAD_RTOL
+    res = PAR.check(fwd[1].cpu().numpy(), fwd[2].cpu().numpy(), [a.cpu().numpy() for a in grads_c], color, depth,
+                    grads_o, pflag, gflag, gauss_frac=GRID_GAUSS_FRAC)

@@ -321,6 +321,11 @@ def test_fused_adam_host_step_counts(monkeypatch):
     opt2.step()
     assert check(7)
     assert float(opt2.state_dict()["state"][0]["step"]) == 7.0
+    # an in-place edit of a step tensor (a manual reset) is seen: the next step is step 1
+    for st in opt2.state.values():
+        st["step"].zero_()
+    opt2.step()
+    assert check(1)
 
 
 def test_ssim_restatement():
