@@ -22,9 +22,18 @@
 //     small box of the field and each plane sees only a small window of cells;
 //   - grid gradients are gathered, not scattered: the workgroup's points are bucketed by bilinear
 //     anchor cell in LDS and each touched (cell, feature) sums its neighbouring buckets with plain LDS
-//     reads, then goes to HBM with one no-return float atomic per workgroup; a plane whose anchor box
-//     is too large falls back to direct atomics.  The channels-last gradient buffer is repacked to
-//     the (1, F, H, W) parameter layout by one launch.
+//     reads, then goes to HBM with one no-return atomic per workgroup; a plane whose anchor box is too
+//     large falls back to direct atomics.  The channels-last gradient buffer is repacked to the
+//     (1, F, H, W) parameter layout by one launch;
+//   - deterministic mode (opt-in; the default sums with float atomics like the reference's
+//     grid_sampler backward, and is faster): inside a workgroup a cell's taps are summed in a fixed rank order
+//     (tap slot, wave, lane: ballot-matched peers, no LDS atomics), and each workgroup's sum is
+//     converted to a 64-bit fixed-point integer (round to nearest, a power-of-two scale) and added
+//     across workgroups by integer atomics -- exact, so no schedule changes a bit.  The scale
+//     (hex_scale_of) bounds every cell's sum by 2^61: |dv| <= max|dfeat| max|param|^5 (a product of
+//     5 bilinear samples, each a convex combination of parameters) and a cell takes at most one tap per
+//     point, so |sum| <= N max|dfeat| max|param|^5; the resolution is that bound times 2^-61 (~1e-13
+//     of the largest possible sum at 10^5 points, below fp32 rounding of any sum it can affect).
 #include <algorithm>
 #include <climits>
 
@@ -186,13 +195,58 @@ __device__ __forceinline__ int block_excl_scan(int v, int *s_tmp, int &tot) {
     return base + x - v;
 }
 
+// The fixed-point scale 2^e with e chosen so that N max|dfeat| max|param|^5 * 2^e <= 2^61 (mx[0] =
+// max|dfeat|, mx[1] = max|param| as float bits, hex_max_kernel); 1 when the bound is 0 or not finite.
+__device__ __forceinline__ float hex_scale_of(int N, const uint32_t *mx) {
+    const float a = __uint_as_float(mx[0]), m = __uint_as_float(mx[1]);
+    const float m2 = m * m;
+    const float bound = (float)N * a * (m2 * m2 * m);
+    if (!(bound > 0.f) || !(bound < 3.0e38f)) return 1.f;
+    int ex;
+    (void)frexpf(bound, &ex);  // bound < 2^ex
+    return ldexpf(1.f, max(-126, min(127, 61 - ex)));
+}
+__device__ __forceinline__ unsigned long long hex_fix(float v, float scale) {
+    return (unsigned long long)__float2ll_rn(v * scale);  // scale is a power of two: v * scale is exact
+}
+// max |x| over n floats into *mx (float bits of a non-negative value order like unsigned integers)
+__global__ __launch_bounds__(256) void hex_max_kernel(int64_t n, const float *__restrict__ x, uint32_t *__restrict__ mx) {
+    float m = 0.f;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) m = fmaxf(m, fabsf(x[i]));
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+    __shared__ float s_m[4];
+    if ((threadIdx.x & 63) == 0) s_m[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        m = fmaxf(fmaxf(s_m[0], s_m[1]), fmaxf(s_m[2], s_m[3]));
+        if (m > 0.f) atomicMax(mx, __float_as_uint(m));
+    }
+}
+// the fixed-point sums back to floats (channels-last packed layout)
+__global__ __launch_bounds__(256) void hex_fix_to_float_kernel(int64_t n, int N, const uint32_t *__restrict__ mx,
+                                                               const long long *__restrict__ acc,
+                                                               float *__restrict__ out) {
+    const float inv = 1.f / hex_scale_of(N, mx);
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+        out[i] = (float)acc[i] * inv;
+}
+
+// DET: the deterministic sums (fixed rank order in the workgroup, 64-bit fixed-point atomics across
+// workgroups, dacc = the fixed-point accumulators); otherwise the reference's kind of sum -- float
+// atomics straight into the packed float gradients (dacc), LDS-atomic tap ranks -- which is faster.
+template <bool DET>
 __global__ __launch_bounds__(kHexThreads) void hexplane_backward_kernel(int N, const float *__restrict__ pts,
                                                                         const uint32_t *__restrict__ order,
                                                                         gs4d_hexplane_layout lay,
                                                                         const float *__restrict__ packed,
                                                                         const float *__restrict__ dfeat,
-                                                                        float *__restrict__ dpacked,
+                                                                        const uint32_t *__restrict__ mx,
+                                                                        void *__restrict__ dacc,
                                                                         float *__restrict__ dpts) {
+    const float scale = DET ? hex_scale_of(N, mx) : 1.f;
+    unsigned long long *const dfix = (unsigned long long *)dacc;
+    float *const dflt = (float *)dacc;
     __shared__ float smem[kHexLdsWords];
     const int F = lay.F, G = F / 4, ppc = kHexThreads / G;
     const int npw = hex_points_per_wg(F), cpw = npw / ppc;
@@ -336,7 +390,8 @@ __global__ __launch_bounds__(kHexThreads) void hexplane_backward_kernel(int N, c
             const float *dvp = s_dv + p * npw * F;
             const int *ancp = s_anc + p * npw;
             const float2 *ixyp = s_ixy + p * npw;
-            float *dpl = dpacked + pl.offset;
+            unsigned long long *dpl = dfix + pl.offset;
+            float *dplf = dflt + pl.offset;
             if ((min(ax0 + aw, pl.W - 1) - ax0 + 1) * (min(ay0 + ah, pl.H - 1) - ay0 + 1) > kHexMaxCells) {
                 // uniform: a box too large for the cell offsets -- direct atomics per (point, feature)
                 for (int e = threadIdx.x; e < npw * F; e += kHexThreads) {
@@ -349,11 +404,20 @@ __global__ __launch_bounds__(kHexThreads) void hexplane_backward_kernel(int N, c
                     const float xa = (float)(x0 + 1) - ixy.x, xb = ixy.x - (float)x0;
                     const float ya = (float)(y0 + 1) - ixy.y, yb = ixy.y - (float)y0;
                     const bool in_x1 = x0 + 1 < pl.W, in_y1 = y0 + 1 < pl.H;
-                    float *b0 = dpl + ((size_t)y0 * pl.W + x0) * F + f;
-                    unsafeAtomicAdd(b0, (xa * ya) * d);
-                    if (in_x1) unsafeAtomicAdd(b0 + F, (xb * ya) * d);
-                    if (in_y1) unsafeAtomicAdd(b0 + (size_t)pl.W * F, (xa * yb) * d);
-                    if (in_x1 && in_y1) unsafeAtomicAdd(b0 + (size_t)(pl.W + 1) * F, (xb * yb) * d);
+                    const size_t i0 = ((size_t)y0 * pl.W + x0) * F + f;
+                    if (DET) {
+                        unsigned long long *b0 = dpl + i0;
+                        atomicAdd(b0, hex_fix((xa * ya) * d, scale));
+                        if (in_x1) atomicAdd(b0 + F, hex_fix((xb * ya) * d, scale));
+                        if (in_y1) atomicAdd(b0 + (size_t)pl.W * F, hex_fix((xa * yb) * d, scale));
+                        if (in_x1 && in_y1) atomicAdd(b0 + (size_t)(pl.W + 1) * F, hex_fix((xb * yb) * d, scale));
+                    } else {
+                        float *b0 = dplf + i0;
+                        unsafeAtomicAdd(b0, (xa * ya) * d);
+                        if (in_x1) unsafeAtomicAdd(b0 + F, (xb * ya) * d);
+                        if (in_y1) unsafeAtomicAdd(b0 + (size_t)pl.W * F, (xa * yb) * d);
+                        if (in_x1 && in_y1) unsafeAtomicAdd(b0 + (size_t)(pl.W + 1) * F, (xb * yb) * d);
+                    }
                 }
                 continue;
             }
@@ -379,12 +443,38 @@ __global__ __launch_bounds__(kHexThreads) void hexplane_backward_kernel(int N, c
                     if (in_x1) tc[1] = tc[0] + 1, tw[1] = xb * ya;
                     if (in_y1) tc[2] = tc[0] + cw, tw[2] = xa * yb;
                     if (in_x1 && in_y1) tc[3] = tc[0] + cw + 1, tw[3] = xb * yb;
+                }
+            }
+            // deterministic ranks of the taps within their cells: tap slot by tap slot, wave by wave in
+            // order, lane by lane (peer lanes of a cell found by ballots over its 10 bits), so a cell's taps
+            // are summed in the same order on every run
+            if (!DET) {
+                if (threadIdx.x < npw)
 #pragma unroll
                     for (int t = 0; t < 4; t++)
                         if (tc[t] >= 0) tr[t] = atomicAdd(&s_off[tc[t]], 1);
+                __syncthreads();
+            }
+            const uint64_t lt_mask = ((threadIdx.x & 63) == 0) ? 0ull : (~0ull >> (64 - (threadIdx.x & 63)));
+            for (int t = 0; t < 4 && DET; t++) {
+                for (int w = 0; w * 64 < npw; w++) {
+                    if ((int)(threadIdx.x >> 6) == w) {
+                        const int c = tc[t];
+                        uint64_t peers = __builtin_amdgcn_ballot_w64(c >= 0);
+#pragma unroll
+                        for (int bit = 0; bit < 10; bit++) {
+                            const bool set = (c >> bit) & 1;
+                            const uint64_t m = __builtin_amdgcn_ballot_w64(set);
+                            peers &= set ? m : ~m;
+                        }
+                        const int old = c >= 0 ? s_off[c] : 0;
+                        __builtin_amdgcn_wave_barrier();
+                        if (c >= 0 && (peers & lt_mask) == 0) s_off[c] = old + __popcll(peers);
+                        tr[t] = old + __popcll(peers & lt_mask);
+                    }
+                    __syncthreads();
                 }
             }
-            __syncthreads();
             int ntouched;
             {
                 // exclusive scan of s_off[0, nc) (four entries per thread, nc <= kHexMaxCells), the tap
@@ -427,6 +517,7 @@ __global__ __launch_bounds__(kHexThreads) void hexplane_backward_kernel(int N, c
             for (int e = threadIdx.x; e < ntouched * nb; e += kHexThreads) {
                 const int r = e / nb, b4 = e - r * nb;
                 const int cell = s_cells[r], k0 = s_cstart[r], k1 = s_cstart[r + 1];
+                // the cell's taps in their deterministic rank order, then one exact fixed-point atomic
                 float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
                 for (int k = k0; k < k1; k++) {
                     const int j = s_pj[k];
@@ -435,11 +526,20 @@ __global__ __launch_bounds__(kHexThreads) void hexplane_backward_kernel(int N, c
                     acc.x += w * d.x; acc.y += w * d.y; acc.z += w * d.z; acc.w += w * d.w;
                 }
                 const int ry = cell / cw, rx = cell - ry * cw;
-                float *dst = dpl + ((size_t)(ay0 + ry) * pl.W + ax0 + rx) * F + 4 * b4;
-                if (acc.x != 0.f) unsafeAtomicAdd(dst + 0, acc.x);
-                if (acc.y != 0.f) unsafeAtomicAdd(dst + 1, acc.y);
-                if (acc.z != 0.f) unsafeAtomicAdd(dst + 2, acc.z);
-                if (acc.w != 0.f) unsafeAtomicAdd(dst + 3, acc.w);
+                const size_t i0 = ((size_t)(ay0 + ry) * pl.W + ax0 + rx) * F + 4 * b4;
+                if (DET) {
+                    unsigned long long *dst = dpl + i0;
+                    if (acc.x != 0.f) atomicAdd(dst + 0, hex_fix(acc.x, scale));
+                    if (acc.y != 0.f) atomicAdd(dst + 1, hex_fix(acc.y, scale));
+                    if (acc.z != 0.f) atomicAdd(dst + 2, hex_fix(acc.z, scale));
+                    if (acc.w != 0.f) atomicAdd(dst + 3, hex_fix(acc.w, scale));
+                } else {
+                    float *dst = dplf + i0;
+                    if (acc.x != 0.f) unsafeAtomicAdd(dst + 0, acc.x);
+                    if (acc.y != 0.f) unsafeAtomicAdd(dst + 1, acc.y);
+                    if (acc.z != 0.f) unsafeAtomicAdd(dst + 2, acc.z);
+                    if (acc.w != 0.f) unsafeAtomicAdd(dst + 3, acc.w);
+                }
             }
             __syncthreads();
         }
@@ -669,16 +769,40 @@ int gs4d_hexplane_forward(int N, const float *pts, const uint32_t *order, const 
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
+// backward scratch (deterministic mode): the max words and the 64-bit fixed-point accumulators
+size_t gs4d_hexplane_backward_scratch_bytes(int N, const gs4d_hexplane_layout *lay) {
+    (void)N;
+    if (!lay) return 256;
+    return 256 + 8 * (size_t)lay->total + 256;
+}
+
 int gs4d_hexplane_backward(int N, const float *pts, const uint32_t *order, const gs4d_hexplane_layout *lay,
-                           const float *packed, const float *dfeat, float *dpacked, float *dpts, void *stream) {
+                           const float *packed, const float *dfeat, float *dpacked, float *dpts, void *scratch,
+                           int deterministic, void *stream) {
     if (N < 0 || !lay || (N > 0 && (!pts || !packed || !dfeat || !dpacked || !dpts))) return 1;
+    if (deterministic && N > 0 && !scratch) return 1;
     if (((size_t)pts & 15) || ((size_t)packed & 15) || ((size_t)dfeat & 15) || ((size_t)dpts & 15)) return 1;
-    if (N == 0) return 0;
+    hipStream_t s = (hipStream_t)stream;
+    if (N == 0) return hipMemsetAsync(dpacked, 0, 4 * (size_t)lay->total, s) == hipSuccess ? 0 : 3;
     const int64_t per_wg = hex_points_per_wg(lay->F);
     const int64_t nwg = ((int64_t)N + per_wg - 1) / per_wg;
     if (hex_bwd_lds_words(lay->F) > kHexLdsWords) return 1;
-    hipLaunchKernelGGL(hexplane_backward_kernel, dim3((unsigned)nwg), dim3(kHexThreads), 0, (hipStream_t)stream, N, pts,
-                       order, *lay, packed, dfeat, dpacked, dpts);
+    if (!deterministic) {
+        if (hipMemsetAsync(dpacked, 0, 4 * (size_t)lay->total, s) != hipSuccess) return 3;
+        hipLaunchKernelGGL(hexplane_backward_kernel<false>, dim3((unsigned)nwg), dim3(kHexThreads), 0, s, N, pts, order,
+                           *lay, packed, dfeat, nullptr, (void *)dpacked, dpts);
+        return hipGetLastError() == hipSuccess ? 0 : 3;
+    }
+    uint32_t *mx = (uint32_t *)align_up((size_t)scratch, 256);
+    unsigned long long *dfix = (unsigned long long *)(mx + 64);
+    if (hipMemsetAsync(mx, 0, 256 + 8 * (size_t)lay->total, s) != hipSuccess) return 3;
+    const int64_t nfeat = (int64_t)N * lay->levels * lay->F;
+    hipLaunchKernelGGL(hex_max_kernel, dim3(256), dim3(256), 0, s, nfeat, dfeat, mx);
+    hipLaunchKernelGGL(hex_max_kernel, dim3(256), dim3(256), 0, s, lay->total, packed, mx + 1);
+    hipLaunchKernelGGL(hexplane_backward_kernel<true>, dim3((unsigned)nwg), dim3(kHexThreads), 0, s, N, pts, order,
+                       *lay, packed, dfeat, mx, (void *)dfix, dpts);
+    hipLaunchKernelGGL(hex_fix_to_float_kernel, dim3(1024), dim3(256), 0, s, lay->total, N, mx,
+                       (const long long *)dfix, dpacked);
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 

@@ -200,14 +200,17 @@ std::tuple<torch::Tensor, std::vector<torch::Tensor>> hexplane_backward(const to
                                                                          std::vector<torch::Tensor> planes,
                                                                          const torch::Tensor &packed,
                                                                          const torch::Tensor &dfeat_,
-                                                                         const torch::Tensor &order) {
+                                                                         const torch::Tensor &order,
+                                                                         bool deterministic) {
     c10::hip::HIPGuard guard(pts_.device().index());
     torch::Tensor pts = pts_.to(torch::kFloat32).contiguous(), dfeat = dfeat_.to(torch::kFloat32).contiguous();
     gs4d_hexplane_layout lay = hex_layout(planes);
     const int N = (int)pts.size(0);
     need(packed.numel() == lay.total, "hexplane backward: packed buffer size");
     need(dfeat.dim() == 2 && dfeat.size(0) == N && dfeat.size(1) == (int64_t)lay.levels * lay.F, "hexplane backward: dfeat shape");
-    torch::Tensor dpacked = torch::zeros({lay.total}, pts.options());
+    torch::Tensor dpacked = torch::empty({lay.total}, pts.options());  // every element written
+    torch::Tensor scratch = torch::empty({deterministic ? (int64_t)gs4d_hexplane_backward_scratch_bytes(N, &lay) : 0},
+                                         pts.options().dtype(torch::kUInt8));
     torch::Tensor dpts = torch::empty({N, 4}, pts.options());
     std::vector<torch::Tensor> grads;
     for (size_t i = 0; i < planes.size(); i++) {
@@ -218,7 +221,8 @@ std::tuple<torch::Tensor, std::vector<torch::Tensor>> hexplane_backward(const to
     need(order.numel() == N && order.scalar_type() == torch::kInt32 && order.is_contiguous(), "hexplane backward: order");
     check(gs4d_hexplane_backward(N, pts.data_ptr<float>(), (const uint32_t *)order.data_ptr<int>(), &lay,
                                  packed.data_ptr<float>(), dfeat.data_ptr<float>(), dpacked.data_ptr<float>(),
-                                 dpts.data_ptr<float>(), (void *)s),
+                                 dpts.data_ptr<float>(), deterministic ? scratch.data_ptr() : nullptr,
+                                 deterministic ? 1 : 0, (void *)s),
           "hexplane backward");
     check(gs4d_hexplane_unpack(&lay, dpacked.data_ptr<float>(), (void *)s), "hexplane unpack");
     return {dpts, grads};
@@ -648,7 +652,8 @@ PYBIND11_MODULE(_C, m) {
     m.def("deform_tail_forward", &deform_tail_forward);
     m.def("deform_tail_backward", &deform_tail_backward);
     m.def("hexplane_forward", &hexplane_forward, py::arg("pts"), py::arg("planes"), py::arg("order") = py::none());
-    m.def("hexplane_backward", &hexplane_backward);
+    m.def("hexplane_backward", &hexplane_backward, py::arg("pts"), py::arg("planes"), py::arg("packed"),
+          py::arg("dfeat"), py::arg("order"), py::arg("deterministic") = false);
     m.def("l1_forward", &l1_forward);
     m.def("l1_backward", &l1_backward);
     m.def("l1_loss_grad", &l1_loss_grad);

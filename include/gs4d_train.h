@@ -92,9 +92,12 @@ int gs4d_adam_step(const gs4d_adam_batch *batch, void *stream);
  * feat: (N, levels * F) = for each level the product over the 6 coordinate pairs (0,1) (0,2) (0,3)
  * (1,2) (1,3) (2,3) of the pair's bilinear sample.  Plane 6*l + p of level l is a (1, F, H, W)
  * parameter tensor with W = reso[c0], H = reso[c1]; the kernels read a packed channels-last copy
- * of all planes (gs4d_hexplane_pack) and accumulate plane gradients into a zeroed packed buffer
- * that gs4d_hexplane_unpack writes back to (1, F, H, W) gradient tensors.  dpts receives the
- * gradient w.r.t. pts (all 4 columns). */
+ * of all planes (gs4d_hexplane_pack); the backward writes the plane gradients (every element: no zero
+ * fill needed) into a packed buffer that gs4d_hexplane_unpack writes back to (1, F, H, W) gradient
+ * tensors.  dpts receives the gradient w.r.t. pts (all 4 columns).  deterministic != 0: the plane
+ * gradients are bitwise reproducible (each workgroup's sum in a fixed order, exact 64-bit fixed-point
+ * integer atomics across workgroups; needs the scratch); 0: float atomics (the reference's kind of sum,
+ * faster; scratch may be NULL). */
 #define GS4D_HEXPLANE_MAX_LEVELS 4
 typedef struct {
     int W, H;
@@ -118,8 +121,11 @@ size_t gs4d_hexplane_order_scratch_bytes(int N);
 int gs4d_hexplane_order(int N, const float *pts, uint32_t *order, void *scratch, void *stream);
 int gs4d_hexplane_forward(int N, const float *pts, const uint32_t *order, const gs4d_hexplane_layout *lay,
                           const float *packed, float *feat, void *stream);
+/* scratch of gs4d_hexplane_backward's deterministic mode: 64-bit accumulators for the packed buffer */
+size_t gs4d_hexplane_backward_scratch_bytes(int N, const gs4d_hexplane_layout *lay);
 int gs4d_hexplane_backward(int N, const float *pts, const uint32_t *order, const gs4d_hexplane_layout *lay,
-                           const float *packed, const float *dfeat, float *dpacked, float *dpts, void *stream);
+                           const float *packed, const float *dfeat, float *dpacked, float *dpts, void *scratch,
+                           int deterministic, void *stream);
 
 /* ---- The field's input points, scene/hexplane.py:20-21 (normalize_aabb with aabb = (max corner, min corner))
  * + :166 (torch.cat((pts, timestamps), -1)) in one pass: pts (N, 4) = ((xyz - aabb[0]) * s - 1, t) with

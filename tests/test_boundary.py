@@ -35,7 +35,7 @@ def test_header_declares_the_reference_entry_points():
     names = declared()
     for n in ("gs4d_forward", "gs4d_backward", "gs4d_mark_visible", "gs4d_last_error", "gs4d_version",
               "gs4d_knn_mean_dist", "gs4d_l1_loss_forward", "gs4d_adam_step", "gs4d_densify_stats",
-              "gs4d_hexplane_forward", "gs4d_hexplane_backward", "gs4d_hexplane_order",
+              "gs4d_hexplane_forward", "gs4d_hexplane_backward", "gs4d_hexplane_backward_scratch_bytes", "gs4d_hexplane_order",
               "gs4d_hexplane_reg_forward", "gs4d_hexplane_reg_backward"):
         assert n in names
 

@@ -139,8 +139,8 @@ def test_hexplane_point_order_is_only_locality():
 
 @pytest.mark.parametrize("F,N", [(4, 20000), (8, 20000), (16, 20000), (32, 20000), (16, 100_000)])
 def test_hexplane_fused_matches_grid_sample(F, N):
-    """N = 20000 points spread over the field: many workgroups' cell boxes exceed the LDS bound and take
-    the direct-atomic path; N = 100k: dense enough that most go through the LDS tap sort + gather."""
+    """The fused field against interpolate_ms_features' grid_sample graph: F = 4..32 (the gather's lane
+    split between tap slots and feature groups), points spread over the field and border-clipped."""
     from gs4d_train.deformation import interpolate_ms_features
     from gs4d_train.kernels import hexplane
     f = _field(F)
@@ -159,6 +159,73 @@ def test_hexplane_fused_matches_grid_sample(F, N):
     torch.testing.assert_close(gb[0], ga[0], rtol=1e-4, atol=1e-4 * ga[0].abs().max().item())
     for a, b in zip(ga[1:], gb[1:]):
         torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-5 * max(a.abs().max().item(), 1e-6))
+
+
+@pytest.mark.parametrize("one_time", [False, True])
+def test_hexplane_backward_deterministic(one_time):
+    """Deterministic mode: each workgroup sums a cell's taps in a fixed rank order and the workgroups'
+    sums meet in exact 64-bit fixed-point atomics: two backward passes give bitwise-equal gradients,
+    which match grid_sample's graph.  one_time: every point at one timestamp, as in a training step (a
+    single view), so the time planes' cells collect the taps of thousands of points."""
+    from gs4d_train import _C
+    from gs4d_train.deformation import interpolate_ms_features
+    f = _field(16)
+    planes = [p.detach() for l in f.grids for p in l]
+    g = torch.Generator(device="cuda").manual_seed(11)
+    pts = torch.rand(100_000, 4, device="cuda", generator=g) * 2 - 1
+    if one_time:
+        pts[:, 3] = 0.3137
+    feat, packed, order = _C.hexplane_forward(pts, planes)
+    dfeat = torch.randn_like(feat)
+    d0, g0 = _C.hexplane_backward(pts, planes, packed, dfeat, order, True)
+    d1, g1 = _C.hexplane_backward(pts, planes, packed, dfeat, order, True)
+    assert torch.equal(d0, d1)
+    for a, b in zip(g0, g1):
+        assert torch.equal(a, b)
+    pa = pts.clone().requires_grad_(True)
+    fa = interpolate_ms_features(pa, f.grids)
+    ga = torch.autograd.grad(fa, [pa] + [p for l in f.grids for p in l], dfeat)
+    torch.testing.assert_close(d0, ga[0], rtol=1e-4, atol=1e-4 * ga[0].abs().max().item())
+    for a, b in zip(ga[1:], g0):
+        torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-5 * max(a.abs().max().item(), 1e-6))
+
+
+def test_train_step_deterministic():
+    """Two fused fine-stage train steps from the same state give bitwise-equal gradients of every
+    parameter and bitwise-equal statistics, with kernels.set_deterministic(True) (the HexPlane field's
+    fixed-point backward; every other kernel of the step is deterministic by construction)."""
+    from gs4d_train import config
+    from gs4d_train import kernels as K
+    K.set_deterministic(True)
+    from gs4d_train.gaussians import GaussianModel
+    from gs4d_train.synthetic import make_point_cloud, make_training_views
+    from gs4d_train.train import train_step
+    hyper, opt = config.dynerf()
+    opt.iterations = 0
+    pts, cols = make_point_cloud(20000, seed=5)
+    views = make_training_views(2, 320, 240, seed=6)
+    bg = torch.ones(3, device="cuda")
+    runs = []
+    for _ in range(2):
+        torch.manual_seed(7)
+        g = GaussianModel(3, hyper, fused=True)
+        g.create_from_pcd(pts, cols, 1.0)
+        g._deformation.deformation_net.grid.fused = True
+        g._deformation.deformation_net.fused_heads = True
+        g.training_setup(opt)
+        g.active_sh_degree = 3
+        loss = float(train_step(g, views, opt, hyper, 3001, bg))
+        grads = {n: p.grad.detach().clone() for n, p in g._deformation.named_parameters() if p.grad is not None}
+        for name in ("_xyz", "_features_dc", "_features_rest", "_opacity", "_scaling", "_rotation"):
+            grads[name] = getattr(g, name).grad.detach().clone()
+        runs.append((loss, grads, g.xyz_gradient_accum.clone()))
+    K.set_deterministic(False)
+    (la, ga, aa), (lb, gb, ab) = runs
+    assert la == lb
+    assert any("grid" in k for k in ga)
+    for k in ga:
+        assert torch.equal(ga[k], gb[k]), k
+    assert torch.equal(aa, ab)
 
 
 def test_hexplane_regulation_fused_matches_torch():
