@@ -103,13 +103,15 @@ constexpr float kCapFree = 0.98f;
 struct Falloff {
     f2 dy, pw, G, alpha;
 };
+template <bool CAP = true>
 __device__ __forceinline__ Falloff falloff(const float4 &geo, const float4 &opc, float pa, float pb, f2 yl) {
     Falloff f;
     f.dy = bc2(geo.y) - yl;
     f.pw = fma2(f.dy, fma2(bc2(opc.x), f.dy, bc2(pb)), bc2(pa));
     f.G = f2{__builtin_amdgcn_exp2f(f.pw.x), __builtin_amdgcn_exp2f(f.pw.y)};
     const f2 al = bc2(opc.y) * f.G;
-    f.alpha = f2{fminf(0.99f, al.x), fminf(0.99f, al.y)};
+    // without CAP every splat of the batch has opacity <= kCapFree: min(0.99, o G) = o G
+    f.alpha = CAP ? f2{fminf(0.99f, al.x), fminf(0.99f, al.y)} : al;
     return f;
 }
 __device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
@@ -222,10 +224,12 @@ __global__ __launch_bounds__(128) void render_forward_kernel(Args a, const uint2
     const float yc = (float)(ty * kBlockY) + 7.5f;
     const float ylane = (float)(8 * h + (lane >> 4)) - 7.5f;
     const f2 yl = f2{ylane, ylane + 4.f};
-    // live pixels (forward.cu:287-289: pixels outside the image never blend)
-    uint64_t alive[2];
-#pragma unroll
-    for (int k = 0; k < 2; k++) alive[k] = ballot(px < a.W && py0 + 4 * k < a.H);
+    // live pixels (forward.cu:287-289: pixels outside the image never blend) as a per-lane alpha
+    // threshold: 1/255 while the pixel blends, 2 (above any alpha) once it is outside or retired, so the
+    // alpha test is one compare per pixel and needs no scalar mask
+    f2 thr;
+    thr.x = (px < a.W && py0 < a.H) ? kAlphaMin : 2.f;
+    thr.y = (px < a.W && py0 + 4 < a.H) ? kAlphaMin : 2.f;
     f2 T = bc2(1.f), C0 = bc2(0.f), C1 = bc2(0.f), C2 = bc2(0.f), Dp = bc2(0.f);
     uint32_t stop[2] = {0, 0};  // list position of the terminating splat (retired pixels)
     uint2 range = ranges[tile];
@@ -332,13 +336,14 @@ __global__ __launch_bounds__(128) void render_forward_kernel(Args a, const uint2
     };
     if (range.x < range.y) fetch(range.x);
     for (uint32_t base = range.x; base < range.y; base += 64) {
-        if ((alive[0] | alive[1]) == 0) break;  // forward.cu:312-314 (this half)
+        if (ballot(thr.x < 1.f || thr.y < 1.f) == 0) break;  // forward.cu:312-314 (this half)
         SplatRegs nxt;
         const bool valid = base + lane < range.y;
         read_raw_lds(nxt, s_raw, lane, valid, yc, false);  // this wave's own staging: no block barrier
         nxt.reach = valid ? rnxt : 0u;
         const uint64_t reach = ballot((nxt.reach >> h) & 1u);
         const uint64_t nonpd = ballot(!conic_pd(nxt.geo, nxt.opc));
+        const bool cap = ballot(valid && nxt.opc.y > kCapFree) != 0;  // wave-uniform: a splat the 0.99 cap can bind
         // one wave writes and reads its own staging area: LDS operations of a wave complete in order
         __builtin_amdgcn_wave_barrier();
         s_sp[lane].geo = nxt.geo;
@@ -349,25 +354,22 @@ __global__ __launch_bounds__(128) void render_forward_kernel(Args a, const uint2
         const uint32_t pos0 = base - range.x;
         // the batch's splats that reach this half, two at a time: both falloffs are independent, only
         // the blend updates chain (a lone last splat runs alone)
-        auto blend = [&](const Falloff &f, const float4 &col, uint32_t j) {
-            uint64_t m0 = ballot(f.alpha.x >= kAlphaMin) & alive[0];  // forward.cu:346-348
-            uint64_t m1 = ballot(f.alpha.y >= kAlphaMin) & alive[1];
-            if ((nonpd >> j) & 1) {  // forward.cu:341-342
-                m0 &= ballot(f.pw.x <= 0.0f);
-                m1 &= ballot(f.pw.y <= 0.0f);
+        auto blend = [&](const Falloff &f, const float4 &col, uint32_t j, auto pwc) {
+            bool k0 = f.alpha.x >= thr.x, k1 = f.alpha.y >= thr.y;  // forward.cu:346-348 (live pixels)
+            if (decltype(pwc)::value && ((nonpd >> j) & 1)) {  // forward.cu:341-342
+                k0 = k0 && f.pw.x <= 0.0f;
+                k1 = k1 && f.pw.y <= 0.0f;
             }
-            f2 ae = f2{lane_bit(m0) ? f.alpha.x : 0.f, lane_bit(m1) ? f.alpha.y : 0.f};
+            f2 ae = f2{k0 ? f.alpha.x : 0.f, k1 ? f.alpha.y : 0.f};
             f2 tT = T * (bc2(1.f) - ae);  // forward.cu:349
-            const uint64_t t0m = ballot(tT.x < 0.0001f), t1m = ballot(tT.y < 0.0001f);
-            if ((t0m | t1m) != 0) {
+            if (ballot(fminf(tT.x, tT.y) < 0.0001f) != 0) {
                 // forward.cu:350-354: the splat that would drop T below 1e-4 is not blended; the pixel retires
-                const bool t0 = lane_bit(t0m), t1 = lane_bit(t1m);
+                const bool t0 = tT.x < 0.0001f, t1 = tT.y < 0.0001f;
                 ae = f2{t0 ? 0.f : ae.x, t1 ? 0.f : ae.y};
                 tT = f2{t0 ? T.x : tT.x, t1 ? T.y : tT.y};
                 stop[0] = t0 ? pos0 + j : stop[0];
                 stop[1] = t1 ? pos0 + j : stop[1];
-                alive[0] &= ~t0m;
-                alive[1] &= ~t1m;
+                thr = f2{t0 ? 2.f : thr.x, t1 ? 2.f : thr.y};
             }
             // every live pixel takes the update; pixels the splat does not touch have ae = 0
             const f2 w = ae * T;  // forward.cu:357-358
@@ -377,20 +379,28 @@ __global__ __launch_bounds__(128) void render_forward_kernel(Args a, const uint2
             Dp = fma2(bc2(col.w), w, Dp);
             T = tT;
         };
-        for (uint64_t todo = reach; todo != 0;) {
-            const uint32_t j0 = (uint32_t)__builtin_ctzll(todo);
-            todo &= todo - 1;
-            const bool two = todo != 0;
-            const uint32_t j1 = two ? (uint32_t)__builtin_ctzll(todo) : j0;
-            todo &= todo - (two ? 1 : 0);
-            const float4 geo0 = s_sp[j0].geo, opc0 = s_sp[j0].opc, col0 = s_sp[j0].col;
-            const float4 geo1 = s_sp[j1].geo, opc1 = s_sp[j1].opc, col1 = s_sp[j1].col;
-            const float dx0 = geo0.x - pfx, dx1 = geo1.x - pfx;
-            const Falloff f0 = falloff(geo0, opc0, geo0.z * dx0 * dx0, geo0.w * dx0, yl);
-            const Falloff f1 = falloff(geo1, opc1, geo1.z * dx1 * dx1, geo1.w * dx1, yl);
-            blend(f0, col0, j0);
-            if (two) blend(f1, col1, j1);
-        }
+        auto walk = [&](auto capc, auto pwc) {
+            constexpr bool CAP = decltype(capc)::value;
+            for (uint64_t todo = reach; todo != 0;) {
+                const uint32_t j0 = (uint32_t)__builtin_ctzll(todo);
+                todo &= todo - 1;
+                const bool two = todo != 0;
+                const uint32_t j1 = two ? (uint32_t)__builtin_ctzll(todo) : j0;
+                todo &= todo - (two ? 1 : 0);
+                const float4 geo0 = s_sp[j0].geo, opc0 = s_sp[j0].opc, col0 = s_sp[j0].col;
+                const float4 geo1 = s_sp[j1].geo, opc1 = s_sp[j1].opc, col1 = s_sp[j1].col;
+                const float dx0 = geo0.x - pfx, dx1 = geo1.x - pfx;
+                const Falloff f0 = falloff<CAP>(geo0, opc0, geo0.z * dx0 * dx0, geo0.w * dx0, yl);
+                const Falloff f1 = falloff<CAP>(geo1, opc1, geo1.z * dx1 * dx1, geo1.w * dx1, yl);
+                blend(f0, col0, j0, pwc);
+                if (two) blend(f1, col1, j1, pwc);
+            }
+        };
+        // the batch's walk without the 0.99 cap unless one of its splats has opacity > kCapFree, and
+        // without the power test unless one has a conic that is not positive definite (cov3D_precomp)
+        if (nonpd != 0) walk(std::true_type{}, std::true_type{});
+        else if (cap) walk(std::true_type{}, std::false_type{});
+        else walk(std::false_type{}, std::false_type{});
     }
     __builtin_amdgcn_s_waitcnt(0x0f70);  // an early exit may leave the next batch's LDS-DMA loads in flight
     const size_t HW = (size_t)a.W * a.H;
@@ -404,7 +414,7 @@ __global__ __launch_bounds__(128) void render_forward_kernel(Args a, const uint2
             final_T[pix] = t;
             // splats at positions >= n_contrib never blended into this pixel (the backward's bound):
             // the terminating splat's position, or the list length for pixels that never terminated
-            n_contrib[pix] = lane_bit(alive[k]) ? range.y - range.x : stop[k];
+            n_contrib[pix] = (k ? thr.y : thr.x) < 1.f ? range.y - range.x : stop[k];
             out_color[pix] = (k ? C0.y : C0.x) + t * bg.x;
             out_color[HW + pix] = (k ? C1.y : C1.x) + t * bg.y;
             out_color[2 * HW + pix] = (k ? C2.y : C2.x) + t * bg.z;
