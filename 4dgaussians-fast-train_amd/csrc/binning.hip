@@ -24,8 +24,8 @@
 //   4. tile_sort: each tile's run is sorted by the 64-bit key (depth bits, Gaussian id) -- exactly the
 //      reference's within-tile order (the key is unique inside a tile).  Runs of up to kWaveSortMax
 //      (256) are sorted by the render forward itself, in registers, before it blends them
-//      (render.hip); here runs of up to 4096 by one workgroup in LDS, longer ones as LDS-sorted
-//      4096-runs merged by the same network's global steps.
+//      (render.hip); here runs of up to 2048 by one workgroup in LDS (register sorts + merge path),
+//      longer ones as LDS-sorted 2048-runs merged by the bitonic network's global steps.
 // The P Gaussians are never sorted by depth globally (the reference's 45-bit key needs 6 passes; a
 // global depth sort needs 4 more over the Gaussians).  Prefix sums publish per-chunk counts (one
 // 32-bit status+count word per chunk, agent-scope relaxed atomics) and sum the lower chunks' words
@@ -41,7 +41,7 @@ namespace gs4d {
 constexpr int kEmitPer = kEmitChunk / 256;  // candidates per lane in the emission pass
 constexpr int kSortThreads = 1024;          // radix-sort workgroup: 16 waves rank one chunk together
 constexpr int kItemsL = 8;                  // keys per lane for the instance sort (8192 per workgroup)
-constexpr int kSortCap = 4096;              // tile runs sorted in LDS by one workgroup (48 KiB)
+constexpr int kSortCap = 2048;              // tile runs sorted in LDS by one workgroup (see tile_sort_kernel)
 
 // ---------------------------------------------------------------------------------------------
 // Zero-region layouts (u32 words).
@@ -509,76 +509,13 @@ __device__ void lds_network(TileSortLds &s, int n, int space, int k_lo, int k_hi
     }
 }
 
-// Runs of kWaveSortMax < n <= 256*R instances: one 256-thread workgroup, thread (wave w, lane l) holding
-// positions i = w*64R + r*64 + l in R registers, key = depth bits << 32 | emission slot (as the forward's
-// register sort: the slot grows with the id inside a tile, so this is the (depth, id) order and the
-// key carries its value).  The bitonic network's partner i ^ mask is a lane shuffle for mask bits
-// below 64, a register select for bits below 64R and an LDS exchange (two barriers) above: for
-// n = 2048 that is 3 LDS steps of the network's 66.
-template <int R>
-__device__ __forceinline__ void block_sort(uint32_t *__restrict__ seg, int n, const uint32_t *__restrict__ gid_by_e,
-                                           const float *__restrict__ depths, uint64_t *__restrict__ s_x) {
-    constexpr int M = 256 * R;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int base = w * 64 * R;
-    uint64_t key[R];
-#pragma unroll
-    for (int r = 0; r < R; r++) {
-        const int i = base + r * 64 + lane;
-        const uint32_t e = i < n ? seg[i] : 0u;
-        const uint32_t gid = i < n ? gid_by_e[e] & kGidMask : 0u;
-        key[r] = i < n ? ((uint64_t)__float_as_uint(depths[gid]) << 32) | e : ~0ull;  // depths > 0.2
-    }
-#pragma unroll
-    for (int k = 2; k <= M; k <<= 1) {
-#pragma unroll
-        for (int j = k >> 1; j >= 1; j >>= 1) {
-            const int mask = j == (k >> 1) ? k - 1 : j;  // flip, then half-cleaners
-            const int lx = mask & 63, rx = (mask >> 6) & (R - 1), wx = mask / (64 * R);
-            uint64_t pk[R];
-            if (wx != 0) {
-                // partner in another wave: exchange through LDS
-#pragma unroll
-                for (int r = 0; r < R; r++) s_x[base + r * 64 + lane] = key[r];
-                __syncthreads();
-#pragma unroll
-                for (int r = 0; r < R; r++) pk[r] = s_x[(base + r * 64 + lane) ^ mask];
-                __syncthreads();
-            } else {
-#pragma unroll
-                for (int r = 0; r < R; r++) {
-                    const int rq = r ^ rx;
-                    if (lx == 0) {
-                        pk[r] = key[rq];
-                    } else {
-                        const uint32_t hi = xor_lane((uint32_t)(key[rq] >> 32), lx);
-                        const uint32_t lo = xor_lane((uint32_t)key[rq], lx);
-                        pk[r] = ((uint64_t)hi << 32) | lo;
-                    }
-                }
-            }
-#pragma unroll
-            for (int r = 0; r < R; r++) {
-                const bool lower = ((base + r * 64 + lane) & j) == 0;
-                const uint64_t kr = key[r];
-                key[r] = lower ? (pk[r] < kr ? pk[r] : kr) : (pk[r] > kr ? pk[r] : kr);
-            }
-        }
-    }
-#pragma unroll
-    for (int r = 0; r < R; r++) {
-        const int i = base + r * 64 + lane;
-        if (i < n) seg[i] = (uint32_t)key[r];
-    }
-}
-
 // Runs of kWaveSortMax < n <= 2048 instances (one 256-thread workgroup): each wave sorts 256-key chunks
 // in registers (the bitonic network of the forward's short-run sort, lane l holding chunk positions
 // l, 64 + l, ..), then merge-path rounds in LDS double the sorted runs up to the power of two >= n:
 // every thread emits total / 256 consecutive outputs of its pair of runs, its start found by a binary
 // search on its diagonal, the last round straight into the segment.  Chunks past n are +inf keys
-// (already in order).  O(n log n) compare-selects against the bitonic network's O(n log^2 n): block_sort
-// at n = 2048 spent 66 network steps of 8 registers per thread.
+// (already in order).  O(n log n) compare-selects against the bitonic network's O(n log^2 n): a bitonic
+// block sort at n = 2048 spent 66 network steps of 8 registers per thread.
 __device__ __forceinline__ void wave_sort256(uint64_t key[4], int lane) {
 #pragma unroll
     for (int k = 2; k <= 256; k <<= 1) {
@@ -740,16 +677,21 @@ __global__ __launch_bounds__(1024) void tile_order_kernel(const uint2 *__restric
 
 // Tiles with more than kWaveSortMax instances (shorter runs are sorted in registers by the render
 // forward): one workgroup each (workgroup t + 1 for tile t).  Up to 2048: wave sorts + merge path
-// (merge_sort_run); up to kSortCap: register + LDS bitonic (block_sort); longer: runs of kSortCap in LDS merged by the network's global steps.  Workgroup 0
+// (merge_sort_run); longer: runs of kSortCap in LDS merged by the bitonic network's global steps.  Workgroup 0
 // orders the tiles (order_tiles), so one launch does both (a launch costs ~4 us of the timeline).
 __global__ __launch_bounds__(256) void tile_sort_kernel(const uint2 *__restrict__ ranges, int T,
                                                         uint32_t *__restrict__ order,
                                                         const uint32_t *__restrict__ gid_by_e,
                                                         const float *__restrict__ depths, uint32_t *__restrict__ upos,
                                                         uint32_t *__restrict__ tkey_hi, uint32_t *__restrict__ tkey_lo) {
-    __shared__ TileSortLds s;
+    // 32 KiB of LDS, five workgroups per CU: the merge path's two 2048-key buffers, or a long tile's
+    // 2048-key run (TileSortLds, 24 KiB).  (A 48 KiB layout for 4096-key LDS runs held three per CU; this
+    // kernel is latency-bound per workgroup -- dependent key gathers, binary searches, barriers -- so the
+    // runs of 257..2048 that dominate a training scene want the occupancy.)
+    __shared__ uint64_t s_mem[2 * kSortCap];
+    TileSortLds &s = *reinterpret_cast<TileSortLds *>(s_mem);
     if (blockIdx.x == 0) {
-        order_tiles(ranges, T, order, reinterpret_cast<uint32_t *>(s.key));
+        order_tiles(ranges, T, order, reinterpret_cast<uint32_t *>(s_mem));
         return;
     }
     const uint2 r = ranges[blockIdx.x - 1];
@@ -757,8 +699,7 @@ __global__ __launch_bounds__(256) void tile_sort_kernel(const uint2 *__restrict_
     if (n <= kWaveSortMax) return;  // the render forward sorts these
     uint32_t *seg = upos + r.x;
     if (n <= kSortCap) {
-        if (n <= 2048) merge_sort_run(seg, n, gid_by_e, depths, s.key);
-        else block_sort<16>(seg, n, gid_by_e, depths, s.key);
+        merge_sort_run(seg, n, gid_by_e, depths, s_mem);
         return;
     }
     // long tile: sort runs of kSortCap in LDS, then continue the network with its global steps

@@ -131,7 +131,7 @@ def test_parity_opaque_stack_termination(C, oracle, dev):
 
 
 def test_parity_long_tiles(C, oracle, dev):
-    """Tiles holding more instances than one workgroup sorts in LDS (4096): 30k large, faint splats
+    """Tiles holding more instances than one workgroup sorts in LDS (2048): 30k large, faint splats
     over a 12-tile image (9k-16k instances per tile) exercise the per-tile sort's global merge steps."""
     s = make_scene(30000, 64, 48, seed=19, log_scale=math.log(0.3))
     s["opacities"] = np.full_like(s["opacities"], 0.03)
@@ -219,7 +219,7 @@ def test_train_like_scene(C, oracle, dev):
 
 
 def test_parity_mid_tiles(C, oracle, dev):
-    """Tile runs between 256 and 4096 instances, the regime of a training scene's early iterations
+    """Tile runs between 256 and 2048+ instances, the regime of a training scene's early iterations
     (dense, large, faint splats): sorted in LDS by tile_sort_kernel before the forward blends them."""
     s = make_scene(20000, 192, 128, seed=22, log_scale=math.log(0.08))
     s["opacities"] = np.full_like(s["opacities"], 0.1)
