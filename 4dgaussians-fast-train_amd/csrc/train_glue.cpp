@@ -396,15 +396,16 @@ std::vector<torch::Tensor> heads_backward(const torch::Tensor &a, const std::vec
                                           const std::vector<torch::Tensor> &w2s) {
     const int k = (int)gs.size();
     need(k >= 1 && k <= GS4D_HEADS_MAX && (int)w2s.size() == k, "heads_backward: 1-8 heads");
-    need(a.is_cuda() && a.scalar_type() == torch::kFloat32 && a.dim() == 2 && a.is_contiguous(),
-         "heads_backward: a contiguous float32 (P, kW) GPU tensor");
+    const bool bf = a.scalar_type() == torch::kBFloat16;  // the bf16 path: a and da bf16, the rest fp32
+    need(a.is_cuda() && (a.scalar_type() == torch::kFloat32 || bf) && a.dim() == 2 && a.is_contiguous(),
+         "heads_backward: a contiguous float32 or bfloat16 (P, kW) GPU tensor");
     need(a.size(1) % k == 0, "heads_backward: a must be (P, kW)");
     c10::hip::HIPGuard guard(a.device().index());
     gs4d_heads_bwd b{};
     b.P = (int)a.size(0), b.k = k, b.W = (int)(a.size(1) / k);
     auto da = torch::empty_like(a);
-    auto db1 = torch::empty({a.size(1)}, a.options());
-    b.a = a.data_ptr<float>(), b.da = da.data_ptr<float>(), b.db1 = db1.data_ptr<float>();
+    auto db1 = torch::empty({a.size(1)}, a.options().dtype(torch::kFloat32));
+    b.a = (const float *)a.data_ptr(), b.da = (float *)da.data_ptr(), b.db1 = db1.data_ptr<float>();
     std::vector<torch::Tensor> out = {da, db1};
     std::vector<torch::Tensor> keep;
     for (int i = 0; i < k; i++) {
@@ -418,8 +419,8 @@ std::vector<torch::Tensor> heads_backward(const torch::Tensor &a, const std::vec
         b.n[i] = (int)g.size(1);
         b.g[i] = g.data_ptr<float>();
         b.w2[i] = w2.data_ptr<float>();
-        auto dw2 = torch::empty({g.size(1), b.W}, a.options());
-        auto db2 = torch::empty({g.size(1)}, a.options());
+        auto dw2 = torch::empty({g.size(1), b.W}, g.options());
+        auto db2 = torch::empty({g.size(1)}, g.options());
         b.dw2[i] = dw2.data_ptr<float>(), b.db2[i] = db2.data_ptr<float>();
         out.push_back(dw2);
         out.push_back(db2);
@@ -427,7 +428,17 @@ std::vector<torch::Tensor> heads_backward(const torch::Tensor &a, const std::vec
     }
     const size_t sb = gs4d_heads_backward_scratch_bytes(b.P, b.W, k, b.n);
     auto scratch = torch::empty({(int64_t)sb}, a.options().dtype(torch::kUInt8));
-    check(gs4d_heads_backward(&b, scratch.data_ptr(), (void *)stream_of(a)), "heads_backward");
+    if (bf) {
+        // same field layout, a / da as bf16 bits
+        gs4d_heads_bwd_bf16 bb{};
+        bb.P = b.P, bb.W = b.W, bb.k = b.k, bb.db1 = b.db1;
+        bb.a = (const uint16_t *)a.data_ptr(), bb.da = (uint16_t *)da.data_ptr();
+        for (int i = 0; i < k; i++)
+            bb.n[i] = b.n[i], bb.g[i] = b.g[i], bb.w2[i] = b.w2[i], bb.dw2[i] = b.dw2[i], bb.db2[i] = b.db2[i];
+        check(gs4d_heads_backward_bf16(&bb, scratch.data_ptr(), (void *)stream_of(a)), "heads_backward_bf16");
+    } else {
+        check(gs4d_heads_backward(&b, scratch.data_ptr(), (void *)stream_of(a)), "heads_backward");
+    }
     return out;
 }
 
@@ -523,6 +534,46 @@ std::vector<torch::Tensor> heads_block_forward(const torch::Tensor &h, const tor
     return out;
 }
 
+// ---- heads block forward on bf16 operands: (a bf16, hb bf16, [out_i fp32]); same operands as above
+std::vector<torch::Tensor> heads_block_forward_bf16(const torch::Tensor &h, const torch::Tensor &w1,
+                                                    const torch::Tensor &b1, const std::vector<torch::Tensor> &w2s,
+                                                    const std::vector<torch::Tensor> &b2s) {
+    const int k = (int)w2s.size();
+    need(k >= 1 && k <= GS4D_HEADS_MAX && (int)b2s.size() == k, "heads_block_forward_bf16: 1-8 heads");
+    for (const torch::Tensor *t : std::initializer_list<const torch::Tensor *>{&h, &w1, &b1})
+        gpu_f32(*t, "heads_block_forward_bf16 operand");
+    need(h.dim() == 2 && h.is_contiguous() && w1.dim() == 2 && w1.is_contiguous() && b1.is_contiguous() &&
+             w1.size(1) == h.size(1) && w1.size(0) == k * h.size(1) && b1.numel() == w1.size(0),
+         "heads_block_forward_bf16: h (P, W), W1 (kW, W), b1 (kW) contiguous");
+    c10::hip::HIPGuard guard(h.device().index());
+    gs4d_heads_block_fwd_bf16 b{};
+    b.P = (int)h.size(0), b.W = (int)h.size(1), b.k = k;
+    const int64_t rows = (h.size(0) + 15) / 16 * 16;
+    auto bopt = h.options().dtype(torch::kBFloat16);
+    auto a_pad = torch::empty({rows, w1.size(0)}, bopt);
+    auto hb_pad = torch::empty({rows, h.size(1)}, bopt);
+    b.h = h.data_ptr<float>(), b.w1 = w1.data_ptr<float>(), b.b1 = b1.data_ptr<float>();
+    b.a = (uint16_t *)a_pad.data_ptr(), b.hb = (uint16_t *)hb_pad.data_ptr();
+    std::vector<torch::Tensor> out{a_pad.narrow(0, 0, h.size(0)), hb_pad.narrow(0, 0, h.size(0))}, keep;
+    for (int i = 0; i < k; i++) {
+        auto w2 = w2s[i].contiguous();
+        auto b2 = b2s[i].contiguous();
+        need(w2.is_cuda() && w2.scalar_type() == torch::kFloat32 && w2.dim() == 2 && w2.size(1) == b.W &&
+                 b2.scalar_type() == torch::kFloat32 && b2.numel() == w2.size(0),
+             "heads_block_forward_bf16: W2_i (n_i, W), b2_i (n_i) float32");
+        b.n[i] = (int)w2.size(0);
+        b.w2[i] = w2.data_ptr<float>();
+        b.b2[i] = b2.data_ptr<float>();
+        auto o = torch::empty({h.size(0), w2.size(0)}, h.options());
+        b.out[i] = o.data_ptr<float>();
+        out.push_back(o);
+        keep.push_back(w2);
+        keep.push_back(b2);
+    }
+    check(gs4d_heads_block_forward_bf16(&b, (void *)stream_of(h)), "heads_block_forward_bf16");
+    return out;
+}
+
 // ---- first deformation layer forward: h = relu(x W^T + b)
 torch::Tensor feature_relu_forward(const torch::Tensor &x, const torch::Tensor &w, const torch::Tensor &b) {
     for (const torch::Tensor *t : std::initializer_list<const torch::Tensor *>{&x, &w, &b})
@@ -583,17 +634,22 @@ static rocblas_handle rocblas_for(const torch::Tensor &t) {
     TORCH_CHECK(rocblas_set_stream(handles[d], stream_of(t)) == rocblas_status_success, "rocblas_set_stream");
     return handles[d];
 }
+// A and B may instead both be bf16 (the bf16 MLP path): bf16 products, f32 accumulation, f32 C.
 bool gemm_f32(torch::Tensor A, torch::Tensor B, torch::Tensor C, bool ta, bool tb, int64_t m, int64_t n, int64_t k,
               int64_t lda, int64_t ldb, int64_t ldc, int64_t batch, int64_t sA, int64_t sB, int64_t sC,
               int64_t solution) {
-    for (const torch::Tensor *t : {&A, &B, &C})
-        TORCH_CHECK(t->is_cuda() && t->scalar_type() == torch::kFloat32, "gemm_f32: f32 device tensors");
+    const bool bf = A.scalar_type() == torch::kBFloat16;
+    const auto ab_type = bf ? torch::kBFloat16 : torch::kFloat32;
+    TORCH_CHECK(A.is_cuda() && B.is_cuda() && C.is_cuda() && A.scalar_type() == ab_type && B.scalar_type() == ab_type &&
+                    C.scalar_type() == torch::kFloat32,
+                "gemm_f32: A, B both f32 or both bf16, C f32 device tensors");
+    const rocblas_datatype abt = bf ? rocblas_datatype_bf16_r : rocblas_datatype_f32_r;
     TORCH_CHECK(m > 0 && n > 0 && k > 0 && batch > 0 && m < INT32_MAX && n < INT32_MAX && k < INT32_MAX,
                 "gemm_f32: sizes");
     // every element the call touches lies inside the tensors' storage
     auto span = [](const torch::Tensor &t, int64_t rows, int64_t cols, int64_t ld, int64_t stride, int64_t nb) {
         const int64_t last = (nb - 1) * stride + (cols - 1) * ld + rows;  // elements from data_ptr
-        return t.storage_offset() + last <= (int64_t)(t.storage().nbytes() / sizeof(float));
+        return t.storage_offset() + last <= (int64_t)(t.storage().nbytes() / t.element_size());
     };
     TORCH_CHECK(lda >= (ta ? k : m) && ldb >= (tb ? n : k) && ldc >= m, "gemm_f32: leading dimensions");
     TORCH_CHECK(span(A, ta ? k : m, ta ? m : k, lda, sA, batch) && span(B, tb ? n : k, tb ? k : n, ldb, sB, batch) &&
@@ -606,18 +662,21 @@ bool gemm_f32(torch::Tensor A, torch::Tensor B, torch::Tensor C, bool ta, bool t
     const rocblas_operation ob = tb ? rocblas_operation_transpose : rocblas_operation_none;
     auto run = [&](rocblas_gemm_algo algo, int32_t sol) {
         if (batch == 1)
-            return rocblas_gemm_ex(h, oa, ob, (int)m, (int)n, (int)k, &one, A.data_ptr<float>(), rocblas_datatype_f32_r,
-                                   (int)lda, B.data_ptr<float>(), rocblas_datatype_f32_r, (int)ldb, &zero,
+            return rocblas_gemm_ex(h, oa, ob, (int)m, (int)n, (int)k, &one, A.data_ptr(), abt, (int)lda, B.data_ptr(),
+                                   abt, (int)ldb, &zero,
                                    C.data_ptr<float>(), rocblas_datatype_f32_r, (int)ldc, C.data_ptr<float>(),
                                    rocblas_datatype_f32_r, (int)ldc, rocblas_datatype_f32_r, algo, sol, 0);
-        return rocblas_gemm_strided_batched_ex(h, oa, ob, (int)m, (int)n, (int)k, &one, A.data_ptr<float>(),
-                                               rocblas_datatype_f32_r, (int)lda, sA, B.data_ptr<float>(),
-                                               rocblas_datatype_f32_r, (int)ldb, sB, &zero, C.data_ptr<float>(),
+        return rocblas_gemm_strided_batched_ex(h, oa, ob, (int)m, (int)n, (int)k, &one, A.data_ptr(), abt, (int)lda,
+                                               sA, B.data_ptr(), abt, (int)ldb, sB, &zero, C.data_ptr<float>(),
                                                rocblas_datatype_f32_r, (int)ldc, sC, C.data_ptr<float>(),
                                                rocblas_datatype_f32_r, (int)ldc, sC, (int)batch, rocblas_datatype_f32_r,
                                                algo, sol, 0);
     };
-    if (solution != 0 && run(rocblas_gemm_algo_solution_index, (int32_t)solution) == rocblas_status_success) return true;
+    if (solution != 0) {
+        if (run(rocblas_gemm_algo_solution_index, (int32_t)solution) == rocblas_status_success) return true;
+        TORCH_WARN_ONCE("gemm_f32: rocBLAS rejected solution ", solution, " for m=", m, " n=", n, " k=", k,
+                        "; using rocBLAS's default kernel");
+    }
     const rocblas_status st = run(rocblas_gemm_algo_standard, 0);
     TORCH_CHECK(st == rocblas_status_success, "gemm_f32: rocBLAS status ", (int)st);
     return false;
@@ -641,6 +700,7 @@ PYBIND11_MODULE(_C, m) {
     m.def("feature_relu_forward", &feature_relu_forward);
     m.def("heads_forward", &heads_forward);
     m.def("heads_block_forward", &heads_block_forward);
+    m.def("heads_block_forward_bf16", &heads_block_forward_bf16);
     m.def("feature_relu_backward", &feature_relu_backward);
     m.def("heads_backward", &heads_backward);
     m.def("linear_dw", &linear_dw);

@@ -20,6 +20,7 @@
 #include <math.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 
 #include "../../include/gs4d_train.h"
@@ -523,9 +524,11 @@ struct HbArgs {
 // through v_readlane.  The next block's loads are issued before the current block is used.  db2: the
 // lead wave adds the blocks elementwise (flattened index i holds output i mod n) and folds them at the
 // end in a fixed order.
-template <int N, bool EXACT, int U>
-__device__ __forceinline__ void heads_bwd_cols(const HbArgs &A, int h, const float *__restrict__ a,
-                                               float *__restrict__ da, const float *__restrict__ g,
+// TA: the element type of a and da -- float, or __bf16 on the bf16 path (hyper.mlp_dtype = "bf16"), where
+// the products still run in f32 on the bf16 values and da is rounded once when stored.
+template <int N, bool EXACT, int U, class TA>
+__device__ __forceinline__ void heads_bwd_cols(const HbArgs &A, int h, const TA *__restrict__ a,
+                                               TA *__restrict__ da, const float *__restrict__ g,
                                                float *__restrict__ part, float *s_fold) {
     constexpr int KG = (U * N + 63) / 64;
     static_assert(EXACT || KG == 1, "runtime widths keep the block in one register");
@@ -547,10 +550,13 @@ __device__ __forceinline__ void heads_bwd_cols(const HbArgs &A, int h, const flo
     float csum = 0.f;
     const int64_t p0 = (int64_t)blockIdx.x * A.rows_per_wg, p1 = min((int64_t)A.P, p0 + A.rows_per_wg);
     const int64_t gend = p1 * n;
-    float xn[U], gn[KG];
+    // xn holds the raw elements: a bf16 value widened right after its (conditional) load would make the
+    // compiler wait for that load inside the branch
+    TA xn[U];
+    float gn[KG];
     auto fetch = [&](int64_t p) {
 #pragma unroll
-        for (int u = 0; u < U; u++) xn[u] = p + u < p1 ? a[(p + u) * ld + col] : 0.f;
+        for (int u = 0; u < U; u++) xn[u] = p + u < p1 ? a[(p + u) * ld + col] : (TA)0.f;
 #pragma unroll
         for (int k = 0; k < KG; k++) {
             const int64_t i = p * n + lane + 64 * k;
@@ -561,7 +567,7 @@ __device__ __forceinline__ void heads_bwd_cols(const HbArgs &A, int h, const flo
     for (int64_t p = p0; p < p1; p += U) {
         float x[U], gv[KG];
 #pragma unroll
-        for (int u = 0; u < U; u++) x[u] = xn[u];
+        for (int u = 0; u < U; u++) x[u] = (float)xn[u];
 #pragma unroll
         for (int k = 0; k < KG; k++) gv[k] = gn[k], gacc[k] += gn[k];
         if (p + U < p1) fetch(p + U);
@@ -580,7 +586,7 @@ __device__ __forceinline__ void heads_bwd_cols(const HbArgs &A, int h, const flo
                         acc[r] = fmaf(dv, x[u], acc[r]);
                     }
                 const float gvv = x[u] > 0.f ? sdot : 0.f;
-                da[(p + u) * ld + col] = gvv;
+                da[(p + u) * ld + col] = (TA)gvv;
                 csum += gvv;
             }
         }
@@ -606,7 +612,8 @@ __device__ __forceinline__ void heads_bwd_cols(const HbArgs &A, int h, const flo
     }
 }
 
-__global__ __launch_bounds__(768) void heads_bwd_kernel(HbArgs A, const float *__restrict__ a, float *__restrict__ da,
+template <class TA>
+__global__ __launch_bounds__(768) void heads_bwd_kernel(HbArgs A, const TA *__restrict__ a, TA *__restrict__ da,
                                                          const float *__restrict__ g0, const float *__restrict__ g1,
                                                          const float *__restrict__ g2, const float *__restrict__ g3,
                                                          const float *__restrict__ g4, const float *__restrict__ g5,
@@ -617,13 +624,13 @@ __global__ __launch_bounds__(768) void heads_bwd_kernel(HbArgs A, const float *_
     const float *__restrict__ g = h == 0 ? g0 : h == 1 ? g1 : h == 2 ? g2 : h == 3 ? g3 : h == 4 ? g4 : h == 5 ? g5
                                 : h == 6 ? g6 : g7;
     switch (A.n[h]) {
-    case 1: heads_bwd_cols<1, true, 8>(A, h, a, da, g, part, s_fold); break;
-    case 2: heads_bwd_cols<2, true, 8>(A, h, a, da, g, part, s_fold); break;
-    case 3: heads_bwd_cols<3, true, 8>(A, h, a, da, g, part, s_fold); break;
-    case 4: heads_bwd_cols<4, true, 8>(A, h, a, da, g, part, s_fold); break;
+    case 1: heads_bwd_cols<1, true, 8, TA>(A, h, a, da, g, part, s_fold); break;
+    case 2: heads_bwd_cols<2, true, 8, TA>(A, h, a, da, g, part, s_fold); break;
+    case 3: heads_bwd_cols<3, true, 8, TA>(A, h, a, da, g, part, s_fold); break;
+    case 4: heads_bwd_cols<4, true, 8, TA>(A, h, a, da, g, part, s_fold); break;
     default:
-        if (A.n[h] <= 8) heads_bwd_cols<8, false, 8>(A, h, a, da, g, part, s_fold);
-        else heads_bwd_cols<16, false, 4>(A, h, a, da, g, part, s_fold);
+        if (A.n[h] <= 8) heads_bwd_cols<8, false, 8, TA>(A, h, a, da, g, part, s_fold);
+        else heads_bwd_cols<16, false, 4, TA>(A, h, a, da, g, part, s_fold);
     }
 }
 
@@ -755,9 +762,9 @@ __global__ __launch_bounds__(512) void heads_bwd_wide_kernel(HbArgs A, const flo
 //   db1 (column sums of da) and db2 (column sums of g) on the way.
 // The waves' partials are added in wave order in LDS, the workgroups' by heads_bwd_reduce_kernel (the
 // same partial layout as heads_bwd_wide_kernel).
-template <int W, int N>
-__global__ __launch_bounds__(256) void heads_bwd_wide_mfma_kernel(HbArgs A, const float *__restrict__ a,
-                                                                   float *__restrict__ da,
+template <int W, int N, class TA>
+__global__ __launch_bounds__(256) void heads_bwd_wide_mfma_kernel(HbArgs A, const TA *__restrict__ a,
+                                                                   TA *__restrict__ da,
                                                                    const float *__restrict__ g,
                                                                    float *__restrict__ part) {
     // each wave takes half of the head's W columns (CT tiles of 16) of a row block: waves 2i and 2i + 1
@@ -786,12 +793,13 @@ __global__ __launch_bounds__(256) void heads_bwd_wide_mfma_kernel(HbArgs A, cons
 #pragma unroll
     for (int m = 0; m < MT; m++) bsum[m] = 0.f;
     const int P = A.P, nblk = (P + 15) / 16;
-    const float *acol = a + h * W + cb;
-    float *dacol = da + h * W + cb;
+    const TA *acol = a + h * W + cb;
+    TA *dacol = da + h * W + cb;
     // a block's loads: g rows as the da A operand, g at (row 4q + s, output 16m + c) as the dW2 A operand,
     // a at the C positions (row 4q + j, column 16t + c); issued one block ahead of their use
     float4 gA[NKC];
-    float gT[MT][4], av[CT][4];
+    float gT[MT][4];
+    TA av[CT][4];  // raw elements, widened when the block comes up (see heads_bwd_cols)
     // rows past P (and the prefetch past the last block) read row P - 1: the loads are unconditional, so
     // the compiler's waits count exactly the loads issued after a block's (a branch around them made it wait
     // for every load in flight, the next block's prefetch included); such rows are masked when the block
@@ -824,7 +832,7 @@ __global__ __launch_bounds__(256) void heads_bwd_wide_mfma_kernel(HbArgs A, cons
 #pragma unroll
             for (int m = 0; m < MT; m++) gTc[m][j] = ok ? gT[m][j] : 0.f;
 #pragma unroll
-            for (int t = 0; t < CT; t++) avc[t][j] = ok ? av[t][j] : 0.f;
+            for (int t = 0; t < CT; t++) avc[t][j] = ok ? (float)av[t][j] : 0.f;
         }
         load_block(blk + stride);
         // da
@@ -843,7 +851,7 @@ __global__ __launch_bounds__(256) void heads_bwd_wide_mfma_kernel(HbArgs A, cons
             for (int j = 0; j < 4; j++) {
                 const int r = r0 + 4 * q + j;
                 const float v = avc[t][j] > 0.f ? acc[j] : 0.f;
-                if (r < P) dacol[(size_t)r * ld + 16 * t + c] = v;
+                if (r < P) dacol[(size_t)r * ld + 16 * t + c] = (TA)v;
                 csum[t] += v;
             }
         }
@@ -1337,6 +1345,126 @@ __global__ __launch_bounds__(kHbfThreads) void heads_block_fwd_kernel(HfArgs A, 
     }
 }
 
+// ---- the heads block forward on bf16 operands (hyper.mlp_dtype = "bf16", BASELINE C3's bf16 leg): the
+// structure of heads_block_fwd_kernel on v_mfma_f32_16x16x32_bf16 (16x the f32 MFMA's rate), fp32
+// accumulation, fp32 outputs.  Workgroup (x, head i): W1_i and W2_i converted to bf16 into LDS (row stride
+// W + 8 elements); per 16-point block the first layer z^T (W x 16) = W1_i h^T is TRANSPOSED as in the f32
+// kernel: in k-step t lane (q = l >> 4, c = l & 15) supplies h[point c][32 t + 8 q .. + 7] (converted to bf16
+// on load) and W1_i[16 m + c][32 t + 8 q .. + 7] (one 16-byte LDS read); accumulator m then holds
+// z[16 m + 4 q + v][point c], v = 0..3.  a = relu(z + b1) is rounded to bf16 once: stored (8 bytes per tile,
+// for the backward) and used as the second layer's B operand straight from the registers -- k-step s of
+// out^T = W2_i a^T takes the lane's values of accumulators 2s and 2s + 1, i.e. MFMA k index 8 q + j <->
+// feature 16 (2 s + (j >> 2)) + 4 q + (j & 3), and the A operand (W2_i rows, two 8-byte LDS reads) uses
+// that same feature order.
+typedef __attribute__((ext_vector_type(8))) __bf16 bf8v;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf4v;
+template <int W>
+__global__ __launch_bounds__(kHbfThreads) void heads_block_fwd_bf16_kernel(HfArgs A, const float *__restrict__ h,
+                                                                           const float *__restrict__ w1,
+                                                                           const float *__restrict__ b1,
+                                                                           __bf16 *__restrict__ a,
+                                                                           __bf16 *__restrict__ hb) {
+    constexpr int NT = W / 16, NK = W / 32, WS = W + 8, NW = kHbfThreads / 64;
+    extern __shared__ float4 s_v[];
+    __bf16 *s_w1 = reinterpret_cast<__bf16 *>(s_v);       // W rows x WS
+    const int head = blockIdx.y;
+    const int n = A.n[head], npad = (n + 15) & ~15;
+    __bf16 *s_w2 = s_w1 + W * WS;                            // npad rows x WS (rows >= n zero)
+    float *s_b1 = reinterpret_cast<float *>(s_w2 + npad * WS);  // W
+    float *s_b2 = s_b1 + W;                                  // npad
+    const float *w1i = w1 + (size_t)head * W * W;
+    for (int e = threadIdx.x; e < W * W / 4; e += kHbfThreads) {
+        const int row = e / (W / 4), c4 = e % (W / 4);
+        const float4 v = reinterpret_cast<const float4 *>(w1i + (size_t)row * W)[c4];
+        *reinterpret_cast<bf4v *>(s_w1 + row * WS + 4 * c4) = bf4v{(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+    }
+    for (int e = threadIdx.x; e < npad * (W / 4); e += kHbfThreads) {
+        const int row = e / (W / 4), c4 = e % (W / 4);
+        const float4 v = row < n ? reinterpret_cast<const float4 *>(A.w2[head] + (size_t)row * W)[c4]
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+        *reinterpret_cast<bf4v *>(s_w2 + row * WS + 4 * c4) = bf4v{(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+    }
+    for (int e = threadIdx.x; e < W; e += kHbfThreads) s_b1[e] = b1[head * W + e];
+    for (int e = threadIdx.x; e < npad; e += kHbfThreads) s_b2[e] = e < n ? A.b2[head][e] : 0.f;
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, q = lane >> 4, c = lane & 15;
+    const int nblk = (A.P + 15) / 16;
+    const int stride = gridDim.x * NW;
+    float *out = A.out[head];
+    float4 hn[2 * NK];
+    // unconditional loads (rows past P read row P - 1), as in heads_block_fwd_kernel
+    auto load_h = [&](int blk) {
+        const int pt = min(blk * 16 + c, A.P - 1);
+        const float4 *src = reinterpret_cast<const float4 *>(h + (size_t)pt * W + 8 * q);
+#pragma unroll
+        for (int t = 0; t < NK; t++) {
+            hn[2 * t] = src[8 * t];
+            hn[2 * t + 1] = src[8 * t + 1];
+        }
+    };
+    int blk = blockIdx.x * NW + wv;
+    load_h(blk);
+    for (; blk < nblk; blk += stride) {
+        bf8v hv[NK];
+#pragma unroll
+        for (int t = 0; t < NK; t++) {
+            const float4 x = hn[2 * t], y = hn[2 * t + 1];
+            hv[t] = bf8v{(__bf16)x.x, (__bf16)x.y, (__bf16)x.z, (__bf16)x.w, (__bf16)y.x, (__bf16)y.y, (__bf16)y.z,
+                         (__bf16)y.w};
+        }
+        load_h(blk + stride);  // the next block's h loads fly while this one runs on the MFMA
+        if (hb && head == 0) {  // bf16 h for the backward's weight-gradient GEMM (ceil(P / 16) * 16 rows)
+            __bf16 *dst = hb + (size_t)(blk * 16 + c) * W + 8 * q;
+#pragma unroll
+            for (int t = 0; t < NK; t++) *reinterpret_cast<bf8v *>(dst + 32 * t) = hv[t];
+        }
+        f4v acc[NT];
+#pragma unroll
+        for (int m = 0; m < NT; m++) acc[m] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < NK; t++) {
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int m = 0; m < NT; m++) {
+                const bf8v av = *reinterpret_cast<const bf8v *>(s_w1 + (16 * m + c) * WS + 32 * t + 8 * q);
+                acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, hv[t], acc[m], 0, 0, 0);
+            }
+        }
+        // a = relu(z + b1) in bf16: lane holds features 16 m + 4 q + v of point c
+        const int pt = blk * 16 + c;
+        bf4v ab[NT];
+#pragma unroll
+        for (int m = 0; m < NT; m++) {
+            const float4 bb = *reinterpret_cast<const float4 *>(s_b1 + 16 * m + 4 * q);
+            ab[m] = bf4v{(__bf16)fmaxf(acc[m][0] + bb.x, 0.f), (__bf16)fmaxf(acc[m][1] + bb.y, 0.f),
+                         (__bf16)fmaxf(acc[m][2] + bb.z, 0.f), (__bf16)fmaxf(acc[m][3] + bb.w, 0.f)};
+            // a has ceil(P / 16) * 16 rows: no condition on the store
+            *reinterpret_cast<bf4v *>(a + (size_t)pt * A.kW + head * W + 16 * m + 4 * q) = ab[m];
+        }
+        // out^T (n_pad x 16) = W2_i a^T, B operand = the lane's bf16 a values (k-step s: tiles 2s, 2s + 1)
+        for (int j = 0; j < npad; j += 16) {
+            f4v o = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s2 = 0; s2 < NT / 2; s2++) {
+                const __bf16 *wr = s_w2 + (j + c) * WS + 32 * s2 + 4 * q;
+                const bf4v lo = *reinterpret_cast<const bf4v *>(wr), hi = *reinterpret_cast<const bf4v *>(wr + 16);
+                const bf8v wa = bf8v{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                const bf4v x0 = ab[2 * s2], x1 = ab[2 * s2 + 1];
+                const bf8v xb = bf8v{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+                o = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, xb, o, 0, 0, 0);
+            }
+            // D[output j + 4 q + r][point c]
+            if (pt < A.P) {
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int oi = j + 4 * q + r;
+                    if (oi < n) out[(size_t)pt * n + oi] = o[r] + s_b2[oi];
+                }
+            }
+        }
+    }
+}
+
 // ---- the deformation field's first layer, forward: h = relu(x W^T + b) (P, FOUT) from x (P, FIN) on the
 // f32 MFMA.  Per 16-row block: lane group q = l >> 4 reads columns 4q..4q+3 of its row l & 15 of a 16-column
 // K chunk as one float4 (the MFMA's k index in step s is column 4q + s), the matching W rows (LDS, row stride
@@ -1494,9 +1622,13 @@ size_t gs4d_heads_backward_scratch_bytes(int P, int W, int k, const int *n) {
     return total;
 }
 
-int gs4d_heads_backward(const gs4d_heads_bwd *args, void *scratch, void *stream) {
+extern "C++" {
+template <class TA, class Args>
+static int heads_backward_t(const Args *args, void *scratch, void *stream) {
     if (!args || !scratch) return 1;
-    const gs4d_heads_bwd &b = *args;
+    const Args &b = *args;
+    const TA *ba = reinterpret_cast<const TA *>(b.a);
+    TA *bda = reinterpret_cast<TA *>(b.da);
     if (b.P < 0 || (b.W != 64 && b.W != 128 && b.W != 256) || b.k < 1 || b.k > kHbMaxHeads || b.k * b.W > 768 ||
         !b.db1)
         return 1;
@@ -1529,16 +1661,19 @@ int gs4d_heads_backward(const gs4d_heads_bwd *args, void *scratch, void *stream)
         } else {
             if (hb_wide(b.n[h0]) && hb_mfma(b.W, b.n[h0])) {
                 if (b.W == 128)
-                    hipLaunchKernelGGL((heads_bwd_wide_mfma_kernel<128, 48>), dim3(nwg), dim3(256), 0, s, A, b.a, b.da,
+                    hipLaunchKernelGGL((heads_bwd_wide_mfma_kernel<128, 48, TA>), dim3(nwg), dim3(256), 0, s, A, ba,
+                                       bda, g[h0], part);
+                else
+                    hipLaunchKernelGGL((heads_bwd_wide_mfma_kernel<64, 48, TA>), dim3(nwg), dim3(256), 0, s, A, ba, bda,
+                                       g[h0], part);
+            } else if (hb_wide(b.n[h0])) {
+                if constexpr (std::is_same<TA, float>::value)
+                    hipLaunchKernelGGL(heads_bwd_wide_kernel<48>, dim3(nwg), dim3(kWideGroups * b.W), 0, s, A, ba, bda,
                                        g[h0], part);
                 else
-                    hipLaunchKernelGGL((heads_bwd_wide_mfma_kernel<64, 48>), dim3(nwg), dim3(256), 0, s, A, b.a, b.da,
-                                       g[h0], part);
-            } else if (hb_wide(b.n[h0]))
-                hipLaunchKernelGGL(heads_bwd_wide_kernel<48>, dim3(nwg), dim3(kWideGroups * b.W), 0, s, A, b.a, b.da,
-                                   g[h0], part);
-            else
-                hipLaunchKernelGGL(heads_bwd_kernel, dim3(nwg), dim3(hk * b.W), 0, s, A, b.a, b.da, g[0], g[1], g[2],
+                    err = 1;  // the bf16 path serves the wide head on the MFMA kernel only (W in {64, 128})
+            } else
+                hipLaunchKernelGGL(heads_bwd_kernel<TA>, dim3(nwg), dim3(hk * b.W), 0, s, A, ba, bda, g[0], g[1], g[2],
                                    g[3], g[4], g[5], g[6], g[7], part);
         }
         hipLaunchKernelGGL(heads_bwd_reduce_kernel, dim3((A.poff[hk] + kHbRedOut - 1) / kHbRedOut), dim3(256), 0, s, A, O, nwg,
@@ -1546,6 +1681,18 @@ int gs4d_heads_backward(const gs4d_heads_bwd *args, void *scratch, void *stream)
     });
     if (err) return err;
     return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+}
+
+int gs4d_heads_backward(const gs4d_heads_bwd *args, void *scratch, void *stream) {
+    return heads_backward_t<float>(args, scratch, stream);
+}
+
+int gs4d_heads_backward_bf16(const gs4d_heads_bwd_bf16 *args, void *scratch, void *stream) {
+    if (args)
+        for (int i = 0; i < args->k && i < kHbMaxHeads; i++)
+            if (hb_wide(args->n[i]) && !hb_mfma(args->W, args->n[i])) return 1;
+    return heads_backward_t<__bf16>(args, scratch, stream);
 }
 
 size_t gs4d_linear_dw_scratch_bytes(int P, int W, int count, const int *n) {
@@ -1833,6 +1980,26 @@ int gs4d_heads_forward(const gs4d_heads_fwd *args, void *stream) {
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) is per device: done once per (device, kernel set), and
+// false when the device's per-workgroup LDS cannot hold `need` bytes
+constexpr int kErrLds = 4;
+static bool raise_lds_limit(const void *k0, const void *k1, int set, size_t need) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
+    static int state[2][64] = {};  // 0 unknown, 1 raised, 2 unavailable
+    int &st = state[set][dev];
+    if (st == 0) {
+        int maxlds = 0;
+        (void)hipDeviceGetAttribute(&maxlds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev);
+        const bool ok = hipFuncSetAttribute(k0, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess &&
+                        hipFuncSetAttribute(k1, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+        (void)hipGetLastError();
+        st = ok ? 1 : 2;
+        if (ok && maxlds > 0 && (size_t)maxlds < 96 * 1024) st = 2;  // not a gfx950-class LDS
+    }
+    return st == 1 && need <= 160 * 1024;
+}
+
 int gs4d_heads_block_forward(const gs4d_heads_block_fwd *args, void *stream) {
     if (!args) return 1;
     const gs4d_heads_block_fwd &b = *args;
@@ -1856,20 +2023,48 @@ int gs4d_heads_block_forward(const gs4d_heads_block_fwd *args, void *stream) {
     // (16-wave workgroups measured no faster: 185-196 us for 256-1024 of them)
     const int per_head = std::max(1, std::min((nblk + 7) / 8, std::max(1, 1024 / b.k)));
     hipStream_t s = (hipStream_t)stream;
-    static bool lds_attr = false;  // dynamic LDS above 64 KiB (gfx950: 160 KiB per CU)
-    if (!lds_attr) {
-        (void)hipFuncSetAttribute((const void *)heads_block_fwd_kernel<128>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        (void)hipFuncSetAttribute((const void *)heads_block_fwd_kernel<64>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        lds_attr = true;
-    }
+    // dynamic LDS above 64 KiB (gfx950: 160 KiB per CU), set once per device; a device that cannot give it
+    // returns GS4D_TRAIN_ERR_LDS (the caller falls back to the GEMM formulation)
+    if (!raise_lds_limit((const void *)heads_block_fwd_kernel<128>, (const void *)heads_block_fwd_kernel<64>, 0, lds))
+        return kErrLds;
     if (b.W == 128)
         hipLaunchKernelGGL(heads_block_fwd_kernel<128>, dim3(per_head, b.k), dim3(kHbfThreads), lds, s, A, b.h, b.w1,
                            b.b1, b.a);
     else
         hipLaunchKernelGGL(heads_block_fwd_kernel<64>, dim3(per_head, b.k), dim3(kHbfThreads), lds, s, A, b.h, b.w1,
                            b.b1, b.a);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+int gs4d_heads_block_forward_bf16(const gs4d_heads_block_fwd_bf16 *args, void *stream) {
+    if (!args) return 1;
+    const gs4d_heads_block_fwd_bf16 &b = *args;
+    if (b.P < 0 || (b.W != 64 && b.W != 128) || b.k < 1 || b.k > kHbMaxHeads || !b.w1 || !b.b1) return 1;
+    HfArgs A{};
+    A.P = b.P, A.W = b.W, A.k = b.k, A.kW = b.k * b.W;
+    int npad_max = 0;
+    for (int i = 0; i < b.k; i++) {
+        if (b.n[i] < 1 || b.n[i] > 64 || !b.w2[i] || !b.b2[i] || (b.P > 0 && !b.out[i])) return 1;
+        if (((size_t)b.w2[i] & 15) != 0) return 1;
+        A.n[i] = b.n[i], A.w2[i] = b.w2[i], A.b2[i] = b.b2[i], A.out[i] = b.out[i];
+        npad_max = std::max(npad_max, (b.n[i] + 15) & ~15);
+    }
+    if (((size_t)b.w1 & 15) != 0 || ((size_t)b.b1 & 15) != 0) return 1;
+    if (b.P == 0) return 0;
+    if (!b.h || !b.a || (((size_t)b.h | (size_t)b.a | (size_t)b.hb) & 15) != 0) return 1;
+    const size_t lds = 2 * (size_t)(b.W + npad_max) * (b.W + 8) + 4 * (size_t)(b.W + npad_max);
+    const int nblk = (b.P + 15) / 16;
+    const int per_head = std::max(1, std::min((nblk + 7) / 8, std::max(1, 1024 / b.k)));
+    hipStream_t s = (hipStream_t)stream;
+    if (!raise_lds_limit((const void *)heads_block_fwd_bf16_kernel<128>, (const void *)heads_block_fwd_bf16_kernel<64>,
+                         1, lds))
+        return kErrLds;
+    if (b.W == 128)
+        hipLaunchKernelGGL(heads_block_fwd_bf16_kernel<128>, dim3(per_head, b.k), dim3(kHbfThreads), lds, s, A, b.h,
+                           b.w1, b.b1, (__bf16 *)b.a, (__bf16 *)b.hb);
+    else
+        hipLaunchKernelGGL(heads_block_fwd_bf16_kernel<64>, dim3(per_head, b.k), dim3(kHbfThreads), lds, s, A, b.h,
+                           b.w1, b.b1, (__bf16 *)b.a, (__bf16 *)b.hb);
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 

@@ -10,6 +10,7 @@ unchanged (same parameter names and shapes: `deformation_net.grid.grids.{level}.
 """
 import itertools
 import os
+import warnings
 from typing import Sequence
 
 import torch
@@ -168,7 +169,9 @@ _USE_ROCBLAS = os.environ.get("GS4D_MLP_ROCBLAS", "1") != "0"  # 0: torch's GEMM
 
 
 def _rocblas_ok(*ts):
-    return _USE_ROCBLAS and all(t.is_cuda and t.dtype == torch.float32 and t.dim() == 2 and t.stride(1) == 1 for t in ts)
+    """rocBLAS through gemm_f32: device matrices with unit column stride, all f32 or all bf16 (C is f32)."""
+    return _USE_ROCBLAS and len({t.dtype for t in ts}) == 1 and ts[0].dtype in (torch.float32, torch.bfloat16) and \
+        all(t.is_cuda and t.dim() == 2 and t.stride(1) == 1 for t in ts)
 
 
 def _splitk_dw(dy, x):
@@ -179,19 +182,24 @@ def _splitk_dw(dy, x):
     the add of the torch form in three launches."""
     P, c = x.shape[0], _LinearSplitK.kChunk
     S = P // c
-    if S < 2:
-        return dy.t() @ x
+    if S < 2 and not (_rocblas_ok(dy, x) and P > 0):
+        return (dy.t() @ x).float()
     if _rocblas_ok(dy, x):
         from . import _C
         N, K = dy.shape[1], x.shape[1]
+        if S < 2:  # one GEMM, f32 out (a bf16 torch GEMM would round the result to bf16)
+            out = torch.empty(N, K, device=dy.device)
+            _C.gemm_f32(x, dy, out, False, True, K, N, P, x.stride(0), dy.stride(0), K, 1, 0, 0, 0, 0)
+            return out
         rem = P - S * c
+        f32 = x.dtype == torch.float32  # the tuned solutions are f32 kernels; bf16 takes rocBLAS's choice
         parts = torch.empty(S + (1 if rem else 0), N, K, device=dy.device)
         # column-major: part_s^T (K x N) = x_s^T (K x c) . dy_s (c x N)
         _C.gemm_f32(x, dy, parts, False, True, K, N, c, x.stride(0), dy.stride(0), K, S, c * x.stride(0),
-                    c * dy.stride(0), N * K, _SOL_DW_BATCHED)
+                    c * dy.stride(0), N * K, _SOL_DW_BATCHED if f32 else 0)
         if rem:
             _C.gemm_f32(x[S * c:], dy[S * c:], parts[S], False, True, K, N, rem, x.stride(0), dy.stride(0), K, 1,
-                        0, 0, 0, _SOL_DW)
+                        0, 0, 0, _SOL_DW if f32 else 0)
         return _C.sum_slices(parts)
     xs = x[:S * c].unflatten(0, (S, c))
     dw = torch.bmm(dy[:S * c].unflatten(0, (S, c)).transpose(1, 2), xs).sum(0)
@@ -207,9 +215,24 @@ def _mm_dx(dy, w):
         P, N, K = dy.shape[0], dy.shape[1], w.shape[1]
         out = torch.empty(P, K, device=dy.device)
         # column-major: out^T (K x P) = w^T (K x N) . dy^T (N x P)
-        _C.gemm_f32(w, dy, out, False, False, K, P, N, K, dy.stride(0), K, 1, 0, 0, 0, _SOL_DX)
+        _C.gemm_f32(w, dy, out, False, False, K, P, N, K, dy.stride(0), K, 1, 0, 0, 0,
+                    _SOL_DX if w.dtype == torch.float32 else 0)
         return out
-    return dy @ w
+    return (dy @ w).float()
+
+
+_NO_BLOCK_FORWARD = set()  # devices whose LDS cannot hold the heads block forward's weights
+
+
+def _block_forward_ok(dev):
+    return dev.index not in _NO_BLOCK_FORWARD
+
+
+def _block_forward_unavailable(dev, err):
+    """gs4d_heads_block_forward[_bf16] returned GS4D_TRAIN_ERR_LDS (the device cannot give the kernel the
+    LDS its weights need): this device uses the GEMM formulation from now on."""
+    _NO_BLOCK_FORWARD.add(dev.index)
+    warnings.warn(f"heads block forward unavailable on {dev} ({err}); using the GEMM formulation")
 
 
 class _DeformHeads(torch.autograd.Function):
@@ -234,15 +257,22 @@ class _DeformHeads(torch.autograd.Function):
         k = len(second) // 2
         W = hidden.shape[1]
         h = hidden if relu_done else torch.relu(hidden)
-        if h.is_cuda and W in (64, 128) and k <= 8 and all(t.shape[0] <= 64 for t in second[0::2]):
+        if h.is_cuda and W in (64, 128) and k <= 8 and all(t.shape[0] <= 64 for t in second[0::2]) and \
+                _block_forward_ok(h.device):
             # both layers in one MFMA pass (gs4d_heads_block_forward): a is written once, for the backward
             from . import _C
-            a, *outs = _C.heads_block_forward(h.contiguous(), w1.contiguous(), b1.contiguous(),
-                                              [t.contiguous() for t in second[0::2]], list(second[1::2]))
-            ctx.save_for_backward(h, a, w1, *second[0::2])
-            ctx.W = W
-            ctx.relu_done = relu_done
-            return tuple(outs)
+            try:
+                a, *outs = _C.heads_block_forward(h.contiguous(), w1.contiguous(), b1.contiguous(),
+                                                  [t.contiguous() for t in second[0::2]], list(second[1::2]))
+            except RuntimeError as e:
+                if "status 4" not in str(e):
+                    raise
+                _block_forward_unavailable(h.device, e)
+            else:
+                ctx.save_for_backward(h, a, w1, *second[0::2])
+                ctx.W = W
+                ctx.relu_done = relu_done
+                return tuple(outs)
         a = torch._addmm_activation(b1, h, w1.t())  # bias + ReLU in the GEMM epilogue where supported
         if a.is_cuda and W in (64, 128, 256) and k <= 8 and all(t.shape[0] <= 64 for t in second[0::2]) and \
                 sum(t.shape[0] for t in second[0::2]) * (W + 4) * 4 <= 64 * 1024:
@@ -336,17 +366,62 @@ def _colsum(x):
 
 
 class _DeformHeadsBF16(torch.autograd.Function):
-    """The opt-in bf16 form of _DeformHeads (hyper.mlp_dtype = "bf16"): the same block -- ONE first-layer
-    GEMM for the k heads, bias + ReLU in its epilogue, the k second layers -- on bf16 operands with fp32
-    accumulation (hipBLASLt).  The first-layer output a is kept in bf16 (half the bytes of the fp32
-    block); the second layers write fp32 (aten addmm.dtype).  Backward: the k second layers' input
-    gradients as ONE GEMM against the block-diagonal second-layer weights, their weight gradients as
-    one split-K GEMM of the concatenated output gradients against a (the diagonal blocks kept), the
-    ReLU mask in bf16, then the first layer's split-K weight gradient and input gradient (fp32 out).
-    Parameters and their gradients stay fp32."""
+    """The opt-in bf16 form of _DeformHeads (hyper.mlp_dtype = "bf16", BASELINE C3's bf16 leg): the same
+    block on bf16 operands with fp32 accumulation; parameters, their gradients and the heads' outputs stay
+    fp32.  On the GPU (W in {64, 128}, n_i <= 16 or 48) every piece is a HIP or rocBLAS bf16 kernel:
+      forward   gs4d_heads_block_forward_bf16: both layers on v_mfma_f32_16x16x32_bf16 in one pass, a =
+                relu(h W1^T + b1) written once in bf16 (half the fp32 block's bytes) with h in bf16 for the
+                weight gradient;
+      backward  gs4d_heads_backward_bf16: the second layers' backward, the ReLU mask and db1 in one pass
+                over a (da in bf16, sums fp32); dW1 = da^T h as a split-K bf16 GEMM (rocBLAS, f32 out) and
+                dh = da W1 as one bf16 GEMM (f32 out).
+    Rounding: h, W1, W2, a and da are rounded to bf16 once each (tests/test_train_gpu.py bounds the effect
+    on a train step against the fp32 path).  Elsewhere (CPU, other widths) the same function in torch bf16
+    ops: _torch_forward / _torch_backward."""
+
+    @staticmethod
+    def _fast(h, second):
+        W, w2 = h.shape[1], second[0::2]
+        return h.is_cuda and W in (64, 128) and len(w2) <= 8 and _block_forward_ok(h.device) and \
+            all(t.shape[0] <= 16 or t.shape[0] == 48 for t in w2)
 
     @staticmethod
     def forward(ctx, h, w1, b1, *second):
+        """h: relu already applied (every head starts with ReLU; _FeatureReLU)."""
+        ctx.W = h.shape[1]
+        if _DeformHeadsBF16._fast(h, second):
+            from . import _C
+            try:
+                a, hb, *outs = _C.heads_block_forward_bf16(h.contiguous(), w1.contiguous(), b1.contiguous(),
+                                                           [t.contiguous() for t in second[0::2]],
+                                                           [t.contiguous() for t in second[1::2]])
+            except RuntimeError as e:
+                if "status 4" not in str(e):
+                    raise
+                _block_forward_unavailable(h.device, e)
+            else:
+                ctx.fast = True
+                ctx.save_for_backward(hb, a, w1, *second[0::2])
+                return tuple(outs)
+        ctx.fast = False
+        return _DeformHeadsBF16._torch_forward(ctx, h, w1, b1, *second)
+
+    @staticmethod
+    def backward(ctx, *douts):
+        if not ctx.fast:
+            return _DeformHeadsBF16._torch_backward(ctx, *douts)
+        from . import _C
+        hb, a, w1, *w2 = ctx.saved_tensors
+        douts = [d if d is not None else torch.zeros(a.shape[0], w2[i].shape[0], device=a.device)
+                 for i, d in enumerate(douts)]
+        out = _C.heads_backward(a, list(douts), [x.contiguous() for x in w2])
+        da, db1 = out[0], out[1]                       # da (P, kW) bf16, masked by the first ReLU
+        dw1 = _splitk_dw(da, hb)                       # (kW, W) fp32
+        dh = _mm_dx(da, w1.to(torch.bfloat16))         # (P, W) fp32
+        return tuple([dh, dw1, db1] + out[2:])
+
+    @staticmethod
+    def _torch_forward(ctx, h, w1, b1, *second):
         bf = torch.bfloat16
         k = len(second) // 2
         W = h.shape[1]
@@ -356,24 +431,19 @@ class _DeformHeadsBF16(torch.autograd.Function):
         w2b = [second[2 * i].to(bf) for i in range(k)]
         outs = [torch.addmm(second[2 * i + 1].to(bf), a[:, i * W:(i + 1) * W], w2b[i].t()).float() for i in range(k)]
         ctx.save_for_backward(hb, a, w1b, *w2b)
-        ctx.W = W
         return tuple(outs)
 
     @staticmethod
-    def backward(ctx, *douts):
+    def _torch_backward(ctx, *douts):
         bf = torch.bfloat16
         hb, a, w1b, *w2b = ctx.saved_tensors
         W, k = ctx.W, len(w2b)
         P = a.shape[0]
         ns = [x.shape[0] for x in w2b]
-        pad = -sum(ns) % 64  # GEMM dimensions in multiples of 64 (hipBLASLt's fast paths, host and device)
-        do32 = torch.cat([d if d is not None else torch.zeros(P, n, device=a.device) for d, n in zip(douts, ns)] +
-                         [torch.zeros(P, pad, device=a.device)], 1)
+        do32 = torch.cat([d if d is not None else torch.zeros(P, n, device=a.device) for d, n in zip(douts, ns)], 1)
         do = do32.to(bf)
-        # block-diagonal second-layer weights: row block i (head i's n_i outputs) x column block i (W)
-        w2bd = torch.cat([torch.block_diag(*w2b), torch.zeros(pad, k * W, dtype=bf, device=a.device)], 0)
-        da = torch.ops.aten.threshold_backward(do @ w2bd, a, 0)  # (P, kW) bf16, masked by the first ReLU
-        dw2full = _splitk_dw_bf16(do, a)                           # (sum n, kW): keep the diagonal blocks
+        da = torch.ops.aten.threshold_backward(do @ torch.block_diag(*w2b), a, 0)  # (P, kW) bf16
+        dw2full = _splitk_dw_bf16(do, a)                                            # keep the diagonal blocks
         db2full = _colsum(do32)
         grads2, o = [], 0
         for i in range(k):
@@ -423,9 +493,10 @@ class Deformation(nn.Module):
         self.pos_deform, self.scales_deform, self.rotations_deform = head(3), head(3), head(4)
         self.opacity_deform, self.shs_deform = head(1), head(16 * 3)
         self.fused_heads = False  # True: the heads as one _DeformHeads block (GPU training)
-        # "bf16" (opt-in, GPU): feature_out and the heads run their GEMMs on bf16 operands with fp32
-        # accumulation; parameters, their gradients and the heads' outputs stay fp32 (BASELINE C3's
-        # "bf16/fp32" train loop).  "fp32" (default) is the reference's precision.
+        # "bf16" (opt-in, GPU): the heads block (the MLP's FLOPs) runs on bf16 operands with fp32
+        # accumulation (_DeformHeadsBF16); feature_out (K = feat_dim, a few % of the FLOPs) stays fp32, as do
+        # parameters, their gradients and the heads' outputs (BASELINE C3's "bf16/fp32" train loop).
+        # "fp32" (default) is the reference's precision.
         self.mlp_dtype = getattr(args, "mlp_dtype", "fp32")
 
     def deltas(self, xyz, time):

@@ -202,6 +202,20 @@ typedef struct gs4d_heads_bwd {
 } gs4d_heads_bwd;
 size_t gs4d_heads_backward_scratch_bytes(int P, int W, int k, const int *n);
 int gs4d_heads_backward(const gs4d_heads_bwd *args, void *scratch, void *stream);
+/* The same pass on the bf16 path: a and da bf16 (uint16 bits; da rounded once from the f32 products), the
+ * sums and g, W2, dW2, db1, db2 fp32.  n_i <= 16, or n_i = 48 with W in {64, 128}.  Same scratch size. */
+typedef struct gs4d_heads_bwd_bf16 {
+    int P, W, k;
+    const uint16_t *a;
+    uint16_t *da;
+    float *db1;
+    int n[GS4D_HEADS_MAX];
+    const float *g[GS4D_HEADS_MAX];
+    const float *w2[GS4D_HEADS_MAX];
+    float *dw2[GS4D_HEADS_MAX];
+    float *db2[GS4D_HEADS_MAX];
+} gs4d_heads_bwd_bf16;
+int gs4d_heads_backward_bf16(const gs4d_heads_bwd_bf16 *args, void *scratch, void *stream);
 
 /* ---- The deformation field's first layer, backward, when feature_out is ONE Linear (defor_depth <= 1,
  * scene/deformation.py:51-55: hidden = x W^T + b) and every head begins with ReLU, so the heads read
@@ -249,6 +263,24 @@ typedef struct gs4d_heads_block_fwd {
     float *out[GS4D_HEADS_MAX];
 } gs4d_heads_block_fwd;
 int gs4d_heads_block_forward(const gs4d_heads_block_fwd *args, void *stream);
+/* The same block on bf16 operands (hyper.mlp_dtype = "bf16"): h, W1, W2 rounded to bf16, fp32 accumulation
+ * (v_mfma_f32_16x16x32_bf16), a = relu(z + b1) stored as bf16 (uint16 bits, (ceil(P/16)*16, kW)), out_i fp32.
+ * hb (nullable): h rounded to bf16, (ceil(P/16)*16, W), for the backward's weight-gradient GEMM.
+ * Returns 4 (GS4D_TRAIN_ERR_LDS) when the device cannot give the kernel its LDS (also for the fp32 form). */
+#define GS4D_TRAIN_ERR_LDS 4
+typedef struct gs4d_heads_block_fwd_bf16 {
+    int P, W, k;
+    const float *h;
+    const float *w1;
+    const float *b1;
+    uint16_t *a;
+    uint16_t *hb;
+    int n[GS4D_HEADS_MAX];
+    const float *w2[GS4D_HEADS_MAX];
+    const float *b2[GS4D_HEADS_MAX];
+    float *out[GS4D_HEADS_MAX];
+} gs4d_heads_block_fwd_bf16;
+int gs4d_heads_block_forward_bf16(const gs4d_heads_block_fwd_bf16 *args, void *stream);
 
 #ifdef __cplusplus
 }

@@ -339,6 +339,15 @@ def test_mlp_gemms_match_fp64(P, N, K, col0):
     dx = D._mm_dx(dy, w)
     refx = dy.double() @ w.double()
     assert dx.shape == (P, K)
+    if (N, K) == (640, 128) and col0 == 0:
+        # the tuned kernels (TunableOp solution indices) are the ones that run at the train step's shapes
+        from gs4d_train import _C
+        o = torch.empty(P, K, device="cuda")
+        assert _C.gemm_f32(w, dy, o, False, False, K, P, N, K, N, K, 1, 0, 0, 0, D._SOL_DX) is True
+        S = P // 1024
+        parts = torch.empty(S, N, K, device="cuda")
+        assert _C.gemm_f32(x, dy, parts, False, True, K, N, 1024, x.stride(0), N, K, S, 1024 * x.stride(0),
+                           1024 * N, N * K, D._SOL_DW_BATCHED) is True
     assert float(((dx.double() - refx).abs() - 1e-5 * (dy.double().abs() @ w.double().abs())).max()) <= 0
     # the library's own kernel (solution 0) computes the same product
     out = torch.empty(P, K, device="cuda")
@@ -445,6 +454,104 @@ def test_heads_block_forward_matches_fp64(P, W, ns):
         scale = x.abs() @ w.double().abs().t() + b.double().abs()
         assert out[i].shape == (P, ns[i])
         assert float(((out[i].double() - ref).abs() - 1e-5 * scale).max().clamp_min(0)) == 0.0
+
+
+BF16_ULP = 2.0 ** -8  # one bf16 ulp relative (8 significant bits): a value rounded once lands within it
+
+
+@pytest.mark.parametrize("P,W,ns", [(100_003, 128, [3, 3, 4, 1, 48]), (777, 64, [2, 16, 5]), (1, 128, [1, 48]),
+                                     (0, 128, [3, 4]), (40, 128, [33, 64]), (5000, 64, [3, 3, 4])])
+def test_heads_block_forward_bf16_matches_fp64(P, W, ns):
+    """gs4d_heads_block_forward_bf16 (both layers on the bf16 MFMA) vs fp64 torch on the same bf16-rounded
+    operands: hb is exactly h rounded to bf16 (round-to-nearest-even, as torch); a = bf16(relu(h W1^T + b1))
+    within one bf16 ulp of the fp64 value + 1e-5 of its |terms| sum (fp32 accumulation); every head output,
+    formed from the kernel's own bf16 a and bf16 W2, within 1e-5 of its |terms| sum.  Ragged P, P = 1, 0."""
+    from gs4d_train import _C
+    torch.manual_seed(P + 7 * W + len(ns))
+    k = len(ns)
+    h = torch.relu(torch.randn(P, W, device="cuda"))
+    w1 = torch.randn(k * W, W, device="cuda") / W ** 0.5
+    b1 = torch.randn(k * W, device="cuda") * 0.1
+    w2 = [torch.randn(n, W, device="cuda") / W ** 0.5 for n in ns]
+    b2 = [torch.randn(n, device="cuda") for n in ns]
+    a, hb, *out = _C.heads_block_forward_bf16(h, w1, b1, w2, b2)
+    assert a.dtype == hb.dtype == torch.bfloat16 and a.shape == (P, k * W) and hb.shape == (P, W) and len(out) == k
+    if P == 0:
+        return
+    bf = torch.bfloat16
+    assert torch.equal(hb, h.to(bf))
+    hd = h.to(bf).double()
+    z = hd @ w1.to(bf).double().t() + b1.double()
+    za = hd.abs() @ w1.to(bf).double().abs().t() + b1.double().abs()
+    err = (a.double() - torch.relu(z)).abs() - BF16_ULP * torch.relu(z) - 1e-5 * za
+    assert float(err.max().clamp_min(0)) == 0.0
+    for i, (w, b) in enumerate(zip(w2, b2)):
+        x = a[:, i * W:(i + 1) * W].double()
+        wd = w.to(bf).double()
+        ref = x @ wd.t() + b.double()
+        scale = x.abs() @ wd.abs().t() + b.double().abs()
+        assert out[i].dtype == torch.float32 and out[i].shape == (P, ns[i])
+        assert float(((out[i].double() - ref).abs() - 1e-5 * scale).max().clamp_min(0)) == 0.0
+
+
+@pytest.mark.parametrize("P,W,ns", [(100_003, 128, [3, 3, 4, 1, 48]), (777, 64, [2, 16, 5]), (1, 128, [1, 48]),
+                                     (0, 128, [3, 4]), (1001, 64, [48, 3, 48]), (300, 256, [16, 1])])
+def test_heads_backward_bf16_matches_fp64(P, W, ns):
+    """gs4d_heads_backward_bf16 (a and da in bf16, everything else fp32) vs fp64 torch on the same bf16 a:
+    da within one bf16 ulp + 1e-5 of its row's |terms| sum, the mask exact; db1 (summed before da is
+    rounded), dW2 and db2 to 1e-5 of their largest |term| sum.  A wide head the bf16 path has no kernel
+    for (n = 40) is refused."""
+    from gs4d_train import _C
+    torch.manual_seed(P + W + 11 * len(ns))
+    k = len(ns)
+    a = torch.relu(torch.randn(P, k * W, device="cuda")).to(torch.bfloat16)
+    gs = [torch.randn(P, n, device="cuda") for n in ns]
+    w2 = [torch.randn(n, W, device="cuda") for n in ns]
+    out = _C.heads_backward(a, gs, w2)
+    da, db1 = out[0], out[1]
+    assert da.dtype == torch.bfloat16 and da.shape == a.shape and db1.dtype == torch.float32
+    ad = a.double()
+    ref = torch.cat([g.double() @ w.double() for g, w in zip(gs, w2)], 1) * (ad > 0)
+    scale = torch.cat([g.double().abs() @ w.double().abs() for g, w in zip(gs, w2)], 1)
+    if P:
+        assert bool(((da == 0) == ((a <= 0) | (ref.abs() < 1e-38))).all())
+        err = (da.double() - ref).abs() - BF16_ULP * ref.abs() - 1e-5 * scale
+        assert float(err.max().clamp_min(0)) == 0.0
+    s1 = (ref.abs().sum(0).max() if P else torch.tensor(1.0)).clamp_min(1e-30)
+    assert float((db1.double() - ref.sum(0)).abs().max() / s1) <= 1e-5
+    for i, (g, w) in enumerate(zip(gs, w2)):
+        x = ad[:, i * W:(i + 1) * W]
+        rw, rb = g.double().t() @ x, g.double().sum(0)
+        sw = (g.double().abs().t() @ x.abs()).max().clamp_min(1e-30)
+        sb = g.double().abs().sum(0).max().clamp_min(1e-30)
+        assert out[2 + 2 * i].dtype == torch.float32
+        assert float((out[2 + 2 * i].double() - rw).abs().max() / sw) <= 1e-5
+        assert float((out[3 + 2 * i].double() - rb).abs().max() / sb) <= 1e-5
+    if P:
+        with pytest.raises(RuntimeError):
+            _C.heads_backward(a[:, :W].contiguous(), [torch.randn(P, 40, device="cuda")], [torch.randn(40, W, device="cuda")])
+
+
+@pytest.mark.parametrize("P,N,K", [(100_003, 640, 128), (2048, 640, 128), (5000, 192, 64), (700, 640, 128)])
+def test_mlp_gemms_bf16_match_fp64(P, N, K):
+    """The bf16 path's GEMMs on rocBLAS (bf16 operands, f32 accumulation and output): the split-K weight
+    gradient (deformation._splitk_dw on bf16 da, hb) and the input gradient (deformation._mm_dx on bf16
+    W1) vs fp64 products of the same bf16 values, to 1e-5 of each result's |term| sum."""
+    from gs4d_train import deformation as D
+    torch.manual_seed(P + N + K)
+    bf = torch.bfloat16
+    dy = torch.randn(P, N, device="cuda").to(bf)
+    x = torch.relu(torch.randn(P, K, device="cuda")).to(bf)
+    dw = D._splitk_dw(dy, x)
+    assert dw.dtype == torch.float32 and dw.shape == (N, K)
+    ref = dy.double().t() @ x.double()
+    scale = (dy.double().abs().t() @ x.double().abs()).max()
+    assert float((dw.double() - ref).abs().max() / scale) <= 1e-5
+    w = torch.randn(N, K, device="cuda").to(bf)
+    dx = D._mm_dx(dy, w)
+    assert dx.dtype == torch.float32 and dx.shape == (P, K)
+    refx = dy.double() @ w.double()
+    assert float(((dx.double() - refx).abs() - 1e-5 * (dy.double().abs() @ w.double().abs())).max()) <= 0
 
 
 @pytest.mark.parametrize("P,Fin,Fout", [(100_003, 32, 128), (777, 64, 64), (1, 32, 128), (0, 32, 128),

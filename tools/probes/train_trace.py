@@ -18,6 +18,8 @@ def main(cfg="metric", steps=20, fused=True):
     P, W, H = CONFIGS[cfg]
     dev = torch.device("cuda:0")
     hyper, opt = config.dynerf()
+    if "--bf16" in sys.argv:
+        hyper.mlp_dtype = "bf16"
     torch.manual_seed(0)
     g = GaussianModel(3, hyper, fused=fused)
     pts, cols = make_point_cloud(P, seed=0)
@@ -38,7 +40,7 @@ def main(cfg="metric", steps=20, fused=True):
     el = (time.perf_counter() - t0) / steps * 1e3
     # host-side cost: the same steps with the GPU work queued but not waited on is not separable; report
     # the wall time and let the kernel trace give the device time
-    print(f"train_step {cfg} fused={fused}: {el:.3f} ms/step")
+    print(f"train_step {cfg} fused={fused} mlp={hyper.mlp_dtype}: {el:.3f} ms/step")
 
 
 def op_profile(cfg="metric", steps=5):
@@ -75,4 +77,5 @@ if __name__ == "__main__":
     if "--ops" in sys.argv:
         op_profile()
     else:
-        main(sys.argv[1] if len(sys.argv) > 1 else "metric")
+        args = [a for a in sys.argv[1:] if not a.startswith("--")]
+        main(args[0] if args else "metric")

@@ -4,7 +4,7 @@
 export TMPDIR=/tmp
 OUT=gpurun_out/trainseq_${TAG:-a}
 mkdir -p $OUT
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 tools/probes/train_trace.py > $OUT/log.txt 2>&1 || { echo "rc=$?"; tail -20 $OUT/log.txt; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 ${PROBE:-tools/probes/train_trace.py} ${PROBE_ARGS} > $OUT/log.txt 2>&1 || { echo "rc=$?"; tail -20 $OUT/log.txt; exit 1; }
 cat $OUT/log.txt | grep ms/step
 f=$(find $OUT/trace -name "*kernel_trace.csv" | head -1)
 python3 - "$f" <<'PY' | tee $OUT/seq.txt
