@@ -1275,6 +1275,7 @@ __global__ __launch_bounds__(kHbfThreads) void heads_block_fwd_kernel(HfArgs A, 
     const int nblk = (A.P + 15) / 16;
     const int stride = gridDim.x * NW;
     float *out = A.out[head];
+    const bool v4out = (n & 3) == 0 && ((size_t)out & 15) == 0;
     float4 hn[NT];
     // rows past P (the last block's, and the prefetch past the last block) read row P - 1: every load is
     // unconditional, so the compiler's wait before a block's MFMAs counts exactly the loads issued after its
@@ -1333,12 +1334,17 @@ __global__ __launch_bounds__(kHbfThreads) void heads_block_fwd_kernel(HfArgs A, 
                 o = __builtin_amdgcn_mfma_f32_16x16x4f32(wv4.z, acc[m][2], o, 0, 0, 0);
                 o = __builtin_amdgcn_mfma_f32_16x16x4f32(wv4.w, acc[m][3], o, 0, 0, 0);
             }
-            // D[output j + 4 q + r][point c]
+            // D[output j + 4 q + r][point c]: one float4 per lane when the rows are 16-byte aligned
             if (pt < A.P) {
+                const int o0 = j + 4 * q;
+                if (v4out && o0 + 3 < n) {
+                    const float4 bb = *reinterpret_cast<const float4 *>(s_b2 + o0);
+                    *reinterpret_cast<float4 *>(out + (size_t)pt * n + o0) =
+                        make_float4(o[0] + bb.x, o[1] + bb.y, o[2] + bb.z, o[3] + bb.w);
+                } else {
 #pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    const int oi = j + 4 * q + r;
-                    if (oi < n) out[(size_t)pt * n + oi] = o[r] + s_b2[oi];
+                    for (int r = 0; r < 4; r++)
+                        if (o0 + r < n) out[(size_t)pt * n + o0 + r] = o[r] + s_b2[o0 + r];
                 }
             }
         }
@@ -1391,6 +1397,7 @@ __global__ __launch_bounds__(kHbfThreads) void heads_block_fwd_bf16_kernel(HfArg
     const int nblk = (A.P + 15) / 16;
     const int stride = gridDim.x * NW;
     float *out = A.out[head];
+    const bool v4out = (n & 3) == 0 && ((size_t)out & 15) == 0;
     float4 hn[2 * NK];
     // unconditional loads (rows past P read row P - 1), as in heads_block_fwd_kernel
     auto load_h = [&](int blk) {
@@ -1453,12 +1460,17 @@ __global__ __launch_bounds__(kHbfThreads) void heads_block_fwd_bf16_kernel(HfArg
                 const bf8v xb = bf8v{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
                 o = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, xb, o, 0, 0, 0);
             }
-            // D[output j + 4 q + r][point c]
+            // D[output j + 4 q + r][point c]: one float4 per lane when the rows are 16-byte aligned
             if (pt < A.P) {
+                const int o0 = j + 4 * q;
+                if (v4out && o0 + 3 < n) {
+                    const float4 bb = *reinterpret_cast<const float4 *>(s_b2 + o0);
+                    *reinterpret_cast<float4 *>(out + (size_t)pt * n + o0) =
+                        make_float4(o[0] + bb.x, o[1] + bb.y, o[2] + bb.z, o[3] + bb.w);
+                } else {
 #pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    const int oi = j + 4 * q + r;
-                    if (oi < n) out[(size_t)pt * n + oi] = o[r] + s_b2[oi];
+                    for (int r = 0; r < 4; r++)
+                        if (o0 + r < n) out[(size_t)pt * n + o0 + r] = o[r] + s_b2[o0 + r];
                 }
             }
         }
@@ -1980,6 +1992,18 @@ int gs4d_heads_forward(const gs4d_heads_fwd *args, void *stream) {
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
+static int cu_count() {  // compute units of the current device (cached per device)
+    static int cus[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (cus[dev] == 0) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        cus[dev] = n;
+    }
+    return cus[dev];
+}
+
 // hipFuncSetAttribute(MaxDynamicSharedMemorySize) is per device: done once per (device, kernel set), and
 // false when the device's per-workgroup LDS cannot hold `need` bytes
 constexpr int kErrLds = 4;
@@ -2054,7 +2078,10 @@ int gs4d_heads_block_forward_bf16(const gs4d_heads_block_fwd_bf16 *args, void *s
     if (!b.h || !b.a || (((size_t)b.h | (size_t)b.a | (size_t)b.hb) & 15) != 0) return 1;
     const size_t lds = 2 * (size_t)(b.W + npad_max) * (b.W + 8) + 4 * (size_t)(b.W + npad_max);
     const int nblk = (b.P + 15) / 16;
-    const int per_head = std::max(1, std::min((nblk + 7) / 8, std::max(1, 1024 / b.k)));
+    // two workgroups per CU (the bf16 kernel's VGPRs allow two 512-thread workgroups): one round of
+    // workgroups, each loading and converting its head's weights once (measured 85 -> 80 us at P = 100k, five
+    // heads, against the fp32 kernel's 1024 / k)
+    const int per_head = std::max(1, std::min((nblk + 7) / 8, std::max(1, 2 * cu_count() / b.k)));
     hipStream_t s = (hipStream_t)stream;
     if (!raise_lds_limit((const void *)heads_block_fwd_bf16_kernel<128>, (const void *)heads_block_fwd_bf16_kernel<64>,
                          1, lds))
