@@ -31,6 +31,11 @@ NO_CONTRACT = {"preprocess.hip", "preprocess_backward.hip", "binning.hip", "knn.
 # would also pack their scalar horizontal adds, paying register moves for a v_pk_add_f32 (4 issue cycles)
 # where two v_add_f32 cost about 5 (tools/bench/valu_rates.hip), so it is off for render.hip.
 NO_SLP = {"render.hip"}
+# The blend kernels and the binning take LLVM's iterative ILP scheduler: measured on one box, render forward
+# 104.5 -> 103.3 us, backward 162.9 -> 161.2 us, the train-like tile sort 43.4 -> 42.5 us (tools/ab_lib.sh,
+# tools/ab_train_kernels.sh); the HexPlane backward got slower with it (+4 us) and train_tail.hip crashes the
+# register allocator under it, so the other files keep the default.
+SCHED_ILP = {"render.hip", "binning.hip"}
 HIPCC_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics", "-Wall",
                "-Wno-unused-result", "-I" + INCLUDE]
 
@@ -71,8 +76,9 @@ def build(force=False, verbose=False):
     def compile_one(src):
         s = os.path.join(CSRC, src)
         o = os.path.join(OBJ, src + ".o")
-        if force or _newer(o, [s] + headers):
-            extra = (["-ffp-contract=off"] if src in NO_CONTRACT else []) + (["-fno-slp-vectorize"] if src in NO_SLP else [])
+        if force or _newer(o, [s, os.path.abspath(__file__)] + headers):
+            extra = (["-ffp-contract=off"] if src in NO_CONTRACT else []) + (["-fno-slp-vectorize"] if src in NO_SLP else []) \
+                + (["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"] if src in SCHED_ILP else [])
             _run([hipcc, *HIPCC_FLAGS, *extra, "-c", s, "-o", o], verbose)
         return o
 

@@ -727,3 +727,48 @@ def test_train_step_bf16_mlp_tracks_fp32():
         assert gb[k].dtype == torch.float32, k
         rel = float((gb[k] - ga[k]).norm() / ga[k].norm().clamp_min(1e-30))
         assert rel <= 5e-2, (k, rel)
+
+
+def test_heads_block_forward_lds_fallback(monkeypatch):
+    """A device that cannot give the heads block forward its LDS (status 4, GS4D_TRAIN_ERR_LDS) makes the
+    wrapper warn once and use the GEMM formulation on that device from then on: same outputs and gradients
+    as the block pass to fp32 rounding (simulated: the binding raises as it would)."""
+    from gs4d_train import _C, deformation as D
+    torch.manual_seed(5)
+    P, W, ns = 3000, 128, [3, 3, 4, 1, 48]
+    k = len(ns)
+    h = torch.relu(torch.randn(P, W, device="cuda"))
+    w1 = (torch.randn(k * W, W, device="cuda") / W ** 0.5).requires_grad_(True)
+    b1 = (torch.randn(k * W, device="cuda") * 0.1).requires_grad_(True)
+    second = []
+    for n in ns:
+        second += [(torch.randn(n, W, device="cuda") / W ** 0.5).requires_grad_(True),
+                   torch.randn(n, device="cuda").requires_grad_(True)]
+    gs = [torch.randn(P, n, device="cuda") for n in ns]
+
+    def run():
+        outs = D._DeformHeads.apply(True, h, w1, b1, *second)
+        torch.autograd.backward(outs, gs)
+        grads = [t.grad.clone() for t in [w1, b1] + second]
+        for t in [w1, b1] + second:
+            t.grad = None
+        return [o.detach() for o in outs], grads
+
+    ref_out, ref_grad = run()
+    real = _C.heads_block_forward
+
+    def refuse(*args):
+        raise RuntimeError("heads_block_forward failed (status 4)")
+    monkeypatch.setattr(_C, "heads_block_forward", refuse)
+    try:
+        with pytest.warns(UserWarning, match="heads block forward unavailable"):
+            out, grad = run()
+        assert h.device.index in D._NO_BLOCK_FORWARD
+        out2, _ = run()  # no second attempt, no second warning
+    finally:
+        D._NO_BLOCK_FORWARD.discard(h.device.index)
+        monkeypatch.setattr(_C, "heads_block_forward", real)
+    for a, b in zip(out + out2, ref_out + ref_out):
+        assert float((a - b).abs().max()) <= 1e-4 * max(float(b.abs().max()), 1.0)
+    for a, b in zip(grad, ref_grad):
+        assert float((a - b).abs().max()) <= 1e-4 * max(float(b.abs().max()), 1e-20)

@@ -16,7 +16,9 @@ for SRC in "$@"; do
   if [ "$REV" = WORKTREE ]; then cp $PKG/csrc/$SRC $PKG/csrc/.variant_$SRC; else git -C $ROOT show $REV:4dgaussians-fast-train_amd/csrc/$SRC > $PKG/csrc/.variant_$SRC; fi
   FLAGS="$BASE"
   case $SRC in preprocess.hip|binning.hip|preprocess_backward.hip|knn.hip|train_tail.hip|hexplane.hip) FLAGS="$FLAGS -ffp-contract=off";; esac
-  case $SRC in render.hip) FLAGS="$FLAGS ${RENDER_FLAGS--fno-slp-vectorize}";; esac
+  case $SRC in render.hip) FLAGS="$FLAGS ${RENDER_FLAGS--fno-slp-vectorize -mllvm -amdgpu-sched-strategy=iterative-ilp}";; esac
+  case $SRC in binning.hip) FLAGS="$FLAGS ${BINNING_FLAGS--mllvm -amdgpu-sched-strategy=iterative-ilp}";; esac
+  FLAGS="$FLAGS $EXTRA_FLAGS"  # e.g. EXTRA_FLAGS="-mllvm -amdgpu-sched-strategy=iterative-ilp"
   /opt/rocm/bin/hipcc $FLAGS -c $PKG/csrc/.variant_$SRC -o $OUT/${SRC}.o
   rm -f $PKG/csrc/.variant_$SRC
 done
