@@ -24,9 +24,10 @@ grid gradients of both are summed with float atomics).  Measured over seeds at K
 800 + 2500 iterations, test PSNR spreads by +-0.6 dB run to run for EITHER formulation
 (tools/probes/conv_diag.py, conv_ablate.py); at 300 + 300 iterations without densification the two
 runs already differ by ~0.1 dB.  Hence two tests:
-  * short horizon (no densification, 200 + 200 iterations, 3 seeds): the formulations' mean held-out
-    PSNR within 0.1 dB, each seed's two runs within 0.25 dB (one seed's pair alone measured 0.104 dB
-    apart: one run is at the noise of the bar) and their last-50-iteration mean losses within 1 %;
+  * short horizon (no densification, 200 + 200 iterations, 6 seeds): the formulations' mean held-out
+    PSNR within 0.1 dB, each seed's two runs within 0.25 dB (single seeds measured 0.02-0.16 dB apart,
+    so one pair, or the mean of three, sits at the noise of a 0.1 dB bar) and their last-50-iteration
+    mean losses within 1 %;
   * long horizon (the full miniature schedule, 5 seeds each): every run converges (above RUN_FLOOR and
     PSNR_GAIN over its start), each formulation's median above PSNR_FLOOR, the median fused PSNR within
     PSNR_DELTA of the median unfused PSNR, and the same for the fused run with the opt-in bf16
@@ -53,7 +54,7 @@ PSNR_DELTA = 1.0      # dB between the medians of the fused and the unfused runs
 SEEDS = 5
 SHORT_DELTA = 0.1     # dB between the two formulations' mean short-horizon PSNR over SHORT_SEEDS seeds
 SHORT_RUN_DELTA = 0.25  # dB between the two runs of any one seed (measured up to 0.104 on one seed)
-SHORT_SEEDS = 3
+SHORT_SEEDS = 6
 
 
 def _cameras(n, seed, offset):
