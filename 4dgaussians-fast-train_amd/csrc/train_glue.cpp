@@ -4,6 +4,8 @@
 #include <c10/hip/HIPGuard.h>
 #include <c10/hip/HIPStream.h>
 #include <rocblas/rocblas.h>
+
+#include <unordered_map>
 #include <torch/extension.h>
 
 #include <string>
@@ -624,15 +626,20 @@ torch::Tensor hexplane_points_backward(const torch::Tensor &dpts_, const torch::
 // called here by their solution index (rocblas_gemm_algo_solution_index) for any P.  An index rocBLAS
 // rejects for a shape falls back to rocBLAS's own choice; the return value says which ran.
 // Column-major semantics: C (m x n) [+ i * sC] = op(A) op(B) for batch i, f32 inputs, f32 accumulation.
-// One handle per (device, host thread): the forward and the autograd engine's backward thread may both call
-// in, and rocblas_set_stream on a shared handle would race.
+// One handle per (host thread, stream): the forward and the autograd engine's backward thread may both call
+// in (rocblas_set_stream on a shared handle would race), and GEMMs queued on two streams must not share a
+// handle's workspace.  A stream belongs to one device, so the stream keys the device too.  Handles live for
+// the process (a handful: one per thread and stream that ever ran a GEMM).
 static rocblas_handle rocblas_for(const torch::Tensor &t) {
-    static thread_local rocblas_handle handles[64] = {};
-    const int d = t.device().index();
-    TORCH_CHECK(d >= 0 && d < 64, "gemm_f32: device index out of range");
-    if (!handles[d]) TORCH_CHECK(rocblas_create_handle(&handles[d]) == rocblas_status_success, "rocblas_create_handle");
-    TORCH_CHECK(rocblas_set_stream(handles[d], stream_of(t)) == rocblas_status_success, "rocblas_set_stream");
-    return handles[d];
+    static thread_local std::unordered_map<hipStream_t, rocblas_handle> handles;
+    const hipStream_t st = stream_of(t);
+    auto it = handles.find(st);
+    if (it != handles.end()) return it->second;
+    rocblas_handle h = nullptr;
+    TORCH_CHECK(rocblas_create_handle(&h) == rocblas_status_success, "rocblas_create_handle");
+    TORCH_CHECK(rocblas_set_stream(h, st) == rocblas_status_success, "rocblas_set_stream");
+    handles.emplace(st, h);
+    return h;
 }
 // A and B may instead both be bf16 (the bf16 MLP path): bf16 products, f32 accumulation, f32 C.
 bool gemm_f32(torch::Tensor A, torch::Tensor B, torch::Tensor C, bool ta, bool tb, int64_t m, int64_t n, int64_t k,
