@@ -536,7 +536,7 @@ std::vector<torch::Tensor> heads_block_forward(const torch::Tensor &h, const tor
     return out;
 }
 
-// ---- heads block forward on bf16 operands: (a bf16, hb bf16, [out_i fp32]); same operands as above
+// ---- heads block forward on bf16 operands: (a bf16, hb bf16, W1 bf16, [out_i fp32]); same operands as above
 std::vector<torch::Tensor> heads_block_forward_bf16(const torch::Tensor &h, const torch::Tensor &w1,
                                                     const torch::Tensor &b1, const std::vector<torch::Tensor> &w2s,
                                                     const std::vector<torch::Tensor> &b2s) {
@@ -554,9 +554,10 @@ std::vector<torch::Tensor> heads_block_forward_bf16(const torch::Tensor &h, cons
     auto bopt = h.options().dtype(torch::kBFloat16);
     auto a_pad = torch::empty({rows, w1.size(0)}, bopt);
     auto hb_pad = torch::empty({rows, h.size(1)}, bopt);
+    auto w1b = torch::empty_like(w1, bopt);
     b.h = h.data_ptr<float>(), b.w1 = w1.data_ptr<float>(), b.b1 = b1.data_ptr<float>();
-    b.a = (uint16_t *)a_pad.data_ptr(), b.hb = (uint16_t *)hb_pad.data_ptr();
-    std::vector<torch::Tensor> out{a_pad.narrow(0, 0, h.size(0)), hb_pad.narrow(0, 0, h.size(0))}, keep;
+    b.a = (uint16_t *)a_pad.data_ptr(), b.hb = (uint16_t *)hb_pad.data_ptr(), b.w1b = (uint16_t *)w1b.data_ptr();
+    std::vector<torch::Tensor> out{a_pad.narrow(0, 0, h.size(0)), hb_pad.narrow(0, 0, h.size(0)), w1b}, keep;
     for (int i = 0; i < k; i++) {
         auto w2 = w2s[i].contiguous();
         auto b2 = b2s[i].contiguous();

@@ -634,6 +634,121 @@ __global__ __launch_bounds__(768) void heads_bwd_kernel(HbArgs A, const TA *__re
     }
 }
 
+// The bf16 form with two columns per thread (W a multiple of 128: a head is whole waves of W / 2 threads):
+// a and da move as bf16 pairs (4-byte loads and stores, half the memory instructions of one column per
+// thread), the products and sums as in heads_bwd_cols, column by column.
+typedef __attribute__((ext_vector_type(2))) __bf16 bf2v;
+template <int N, bool EXACT, int U>
+__device__ __forceinline__ void heads_bwd_cols2(const HbArgs &A, int h, const __bf16 *__restrict__ a,
+                                                __bf16 *__restrict__ da, const float *__restrict__ g,
+                                                float *__restrict__ part, float *s_fold) {
+    constexpr int KG = (U * N + 63) / 64;
+    static_assert(EXACT || KG == 1, "runtime widths keep the block in one register");
+    const int W = A.W, ld = A.k * W, hl = h - A.h0;
+    const int c = 2 * ((int)threadIdx.x - hl * (W / 2));  // this thread's first column in the head
+    const int col = (A.h0 + hl) * W + c;
+    const int lane = threadIdx.x & 63;
+    const bool lead = c < 128;  // the head's first wave: db2 partials
+    const int n = EXACT ? N : A.n[h];
+    const float *__restrict__ w2 = A.w2[h];
+    float w0[N], w1[N], acc0[N], acc1[N];
+#pragma unroll
+    for (int r = 0; r < N; r++) {
+        const float2 wv = (EXACT || r < n) ? *reinterpret_cast<const float2 *>(w2 + r * W + c) : make_float2(0.f, 0.f);
+        w0[r] = wv.x, w1[r] = wv.y;
+        acc0[r] = acc1[r] = 0.f;
+    }
+    float gacc[KG];
+#pragma unroll
+    for (int k = 0; k < KG; k++) gacc[k] = 0.f;
+    float csum0 = 0.f, csum1 = 0.f;
+    const int64_t p0 = (int64_t)blockIdx.x * A.rows_per_wg, p1 = min((int64_t)A.P, p0 + A.rows_per_wg);
+    const int64_t gend = p1 * n;
+    bf2v xn[U];  // raw pairs until use (see heads_bwd_cols)
+    float gn[KG];
+    auto fetch = [&](int64_t p) {
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            xn[u] = p + u < p1 ? *reinterpret_cast<const bf2v *>(a + (p + u) * ld + col) : bf2v{(__bf16)0.f, (__bf16)0.f};
+#pragma unroll
+        for (int k = 0; k < KG; k++) {
+            const int64_t i = p * n + lane + 64 * k;
+            gn[k] = (lane + 64 * k < U * n && i < gend) ? g[i] : 0.f;
+        }
+    };
+    if (p0 < p1) fetch(p0);
+    for (int64_t p = p0; p < p1; p += U) {
+        float x0[U], x1[U], gv[KG];
+#pragma unroll
+        for (int u = 0; u < U; u++) x0[u] = (float)xn[u][0], x1[u] = (float)xn[u][1];
+#pragma unroll
+        for (int k = 0; k < KG; k++) gv[k] = gn[k], gacc[k] += gn[k];
+        if (p + U < p1) fetch(p + U);
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            if (p + u < p1) {
+                float sd0 = 0.f, sd1 = 0.f;
+#pragma unroll
+                for (int r = 0; r < N; r++)
+                    if (EXACT || r < n) {
+                        const int idx = EXACT ? u * N + r : u * n + r;
+                        const float dv = __builtin_bit_cast(
+                            float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, gv[EXACT ? idx / 64 : 0]),
+                                                             EXACT ? idx % 64 : idx));
+                        sd0 = fmaf(dv, w0[r], sd0);
+                        sd1 = fmaf(dv, w1[r], sd1);
+                        acc0[r] = fmaf(dv, x0[u], acc0[r]);
+                        acc1[r] = fmaf(dv, x1[u], acc1[r]);
+                    }
+                const float g0 = x0[u] > 0.f ? sd0 : 0.f, g1 = x1[u] > 0.f ? sd1 : 0.f;
+                *reinterpret_cast<bf2v *>(da + (p + u) * ld + col) = bf2v{(__bf16)g0, (__bf16)g1};
+                csum0 += g0;
+                csum1 += g1;
+            }
+        }
+    }
+    float *pw = part + (size_t)blockIdx.x * A.poff[A.hk];
+    pw[hl * W + c] = csum0;
+    pw[hl * W + c + 1] = csum1;
+    float *ph = pw + A.poff[hl];
+#pragma unroll
+    for (int r = 0; r < N; r++)
+        if (EXACT || r < n) ph[r * (W + 1) + c] = acc0[r], ph[r * (W + 1) + c + 1] = acc1[r];
+    if (lead) {
+        float *f = s_fold + (threadIdx.x >> 6) * 64 * KG;
+#pragma unroll
+        for (int k = 0; k < KG; k++) f[lane + 64 * k] = gacc[k];
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        if (lane < n) {
+            float t = 0.f;
+            for (int i = lane; i < 64 * KG; i += n) t += f[i];
+            ph[lane * (W + 1) + W] = t;
+        }
+    }
+}
+
+__global__ __launch_bounds__(512) void heads_bwd2_kernel(HbArgs A, const __bf16 *__restrict__ a, __bf16 *__restrict__ da,
+                                                        const float *__restrict__ g0, const float *__restrict__ g1,
+                                                        const float *__restrict__ g2, const float *__restrict__ g3,
+                                                        const float *__restrict__ g4, const float *__restrict__ g5,
+                                                        const float *__restrict__ g6, const float *__restrict__ g7,
+                                                        float *__restrict__ part) {
+    __shared__ float s_fold[8 * 64];
+    const int h = A.h0 + __builtin_amdgcn_readfirstlane((int)threadIdx.x / (A.W / 2));
+    const float *__restrict__ g = h == 0 ? g0 : h == 1 ? g1 : h == 2 ? g2 : h == 3 ? g3 : h == 4 ? g4 : h == 5 ? g5
+                                : h == 6 ? g6 : g7;
+    switch (A.n[h]) {
+    case 1: heads_bwd_cols2<1, true, 8>(A, h, a, da, g, part, s_fold); break;
+    case 2: heads_bwd_cols2<2, true, 8>(A, h, a, da, g, part, s_fold); break;
+    case 3: heads_bwd_cols2<3, true, 8>(A, h, a, da, g, part, s_fold); break;
+    case 4: heads_bwd_cols2<4, true, 8>(A, h, a, da, g, part, s_fold); break;
+    default:
+        if (A.n[h] <= 8) heads_bwd_cols2<8, false, 8>(A, h, a, da, g, part, s_fold);
+        else heads_bwd_cols2<16, false, 4>(A, h, a, da, g, part, s_fold);
+    }
+}
+
 // The wide head (n = 48: the SH-coefficient deformation): the same products, VALU-bound rather than
 // streaming (96 FMAs per row and column).  Thread c owns column c of the head (W threads); the head's
 // output-gradient rows are staged in LDS in tiles of kWideTile rows (one coalesced load of a contiguous
@@ -1369,7 +1484,8 @@ __global__ __launch_bounds__(kHbfThreads) void heads_block_fwd_bf16_kernel(HfArg
                                                                            const float *__restrict__ w1,
                                                                            const float *__restrict__ b1,
                                                                            __bf16 *__restrict__ a,
-                                                                           __bf16 *__restrict__ hb) {
+                                                                           __bf16 *__restrict__ hb,
+                                                                           __bf16 *__restrict__ w1b) {
     constexpr int NT = W / 16, NK = W / 32, WS = W + 8, NW = kHbfThreads / 64;
     extern __shared__ float4 s_v[];
     __bf16 *s_w1 = reinterpret_cast<__bf16 *>(s_v);       // W rows x WS
@@ -1382,7 +1498,10 @@ __global__ __launch_bounds__(kHbfThreads) void heads_block_fwd_bf16_kernel(HfArg
     for (int e = threadIdx.x; e < W * W / 4; e += kHbfThreads) {
         const int row = e / (W / 4), c4 = e % (W / 4);
         const float4 v = reinterpret_cast<const float4 *>(w1i + (size_t)row * W)[c4];
-        *reinterpret_cast<bf4v *>(s_w1 + row * WS + 4 * c4) = bf4v{(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+        const bf4v vb = bf4v{(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+        *reinterpret_cast<bf4v *>(s_w1 + row * WS + 4 * c4) = vb;
+        // workgroup 0 of each head also stores W1_i in bf16 for the backward's input-gradient GEMM
+        if (w1b && blockIdx.x == 0) *reinterpret_cast<bf4v *>(w1b + (size_t)head * W * W + (size_t)row * W + 4 * c4) = vb;
     }
     for (int e = threadIdx.x; e < npad * (W / 4); e += kHbfThreads) {
         const int row = e / (W / 4), c4 = e % (W / 4);
@@ -1684,7 +1803,10 @@ static int heads_backward_t(const Args *args, void *scratch, void *stream) {
                                        g[h0], part);
                 else
                     err = 1;  // the bf16 path serves the wide head on the MFMA kernel only (W in {64, 128})
-            } else
+            } else if (std::is_same<TA, __bf16>::value && b.W % 128 == 0 && hk * b.W <= 1024)
+                hipLaunchKernelGGL(heads_bwd2_kernel, dim3(nwg), dim3(hk * b.W / 2), 0, s, A, (const __bf16 *)ba,
+                                   (__bf16 *)bda, g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], part);
+            else
                 hipLaunchKernelGGL(heads_bwd_kernel<TA>, dim3(nwg), dim3(hk * b.W), 0, s, A, ba, bda, g[0], g[1], g[2],
                                    g[3], g[4], g[5], g[6], g[7], part);
         }
@@ -2075,7 +2197,7 @@ int gs4d_heads_block_forward_bf16(const gs4d_heads_block_fwd_bf16 *args, void *s
     }
     if (((size_t)b.w1 & 15) != 0 || ((size_t)b.b1 & 15) != 0) return 1;
     if (b.P == 0) return 0;
-    if (!b.h || !b.a || (((size_t)b.h | (size_t)b.a | (size_t)b.hb) & 15) != 0) return 1;
+    if (!b.h || !b.a || (((size_t)b.h | (size_t)b.a | (size_t)b.hb) & 15) != 0 || ((size_t)b.w1b & 7) != 0) return 1;
     const size_t lds = 2 * (size_t)(b.W + npad_max) * (b.W + 8) + 4 * (size_t)(b.W + npad_max);
     const int nblk = (b.P + 15) / 16;
     // two workgroups per CU (the bf16 kernel's VGPRs allow two 512-thread workgroups): one round of
@@ -2088,10 +2210,10 @@ int gs4d_heads_block_forward_bf16(const gs4d_heads_block_fwd_bf16 *args, void *s
         return kErrLds;
     if (b.W == 128)
         hipLaunchKernelGGL(heads_block_fwd_bf16_kernel<128>, dim3(per_head, b.k), dim3(kHbfThreads), lds, s, A, b.h,
-                           b.w1, b.b1, (__bf16 *)b.a, (__bf16 *)b.hb);
+                           b.w1, b.b1, (__bf16 *)b.a, (__bf16 *)b.hb, (__bf16 *)b.w1b);
     else
         hipLaunchKernelGGL(heads_block_fwd_bf16_kernel<64>, dim3(per_head, b.k), dim3(kHbfThreads), lds, s, A, b.h,
-                           b.w1, b.b1, (__bf16 *)b.a, (__bf16 *)b.hb);
+                           b.w1, b.b1, (__bf16 *)b.a, (__bf16 *)b.hb, (__bf16 *)b.w1b);
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 

@@ -370,8 +370,8 @@ class _DeformHeadsBF16(torch.autograd.Function):
     block on bf16 operands with fp32 accumulation; parameters, their gradients and the heads' outputs stay
     fp32.  On the GPU (W in {64, 128}, n_i <= 16 or 48) every piece is a HIP or rocBLAS bf16 kernel:
       forward   gs4d_heads_block_forward_bf16: both layers on v_mfma_f32_16x16x32_bf16 in one pass, a =
-                relu(h W1^T + b1) written once in bf16 (half the fp32 block's bytes) with h in bf16 for the
-                weight gradient;
+                relu(h W1^T + b1) written once in bf16 (half the fp32 block's bytes) with h and W1 in bf16 for
+                the backward's GEMMs;
       backward  gs4d_heads_backward_bf16: the second layers' backward, the ReLU mask and db1 in one pass
                 over a (da in bf16, sums fp32); dW1 = da^T h as a split-K bf16 GEMM (rocBLAS, f32 out) and
                 dh = da W1 as one bf16 GEMM (f32 out).
@@ -392,7 +392,7 @@ class _DeformHeadsBF16(torch.autograd.Function):
         if _DeformHeadsBF16._fast(h, second):
             from . import _C
             try:
-                a, hb, *outs = _C.heads_block_forward_bf16(h.contiguous(), w1.contiguous(), b1.contiguous(),
+                a, hb, w1b, *outs = _C.heads_block_forward_bf16(h.contiguous(), w1.contiguous(), b1.contiguous(),
                                                            [t.contiguous() for t in second[0::2]],
                                                            [t.contiguous() for t in second[1::2]])
             except RuntimeError as e:
@@ -401,7 +401,7 @@ class _DeformHeadsBF16(torch.autograd.Function):
                 _block_forward_unavailable(h.device, e)
             else:
                 ctx.fast = True
-                ctx.save_for_backward(hb, a, w1, *second[0::2])
+                ctx.save_for_backward(hb, a, w1b, *second[0::2])
                 return tuple(outs)
         ctx.fast = False
         return _DeformHeadsBF16._torch_forward(ctx, h, w1, b1, *second)
@@ -411,13 +411,13 @@ class _DeformHeadsBF16(torch.autograd.Function):
         if not ctx.fast:
             return _DeformHeadsBF16._torch_backward(ctx, *douts)
         from . import _C
-        hb, a, w1, *w2 = ctx.saved_tensors
+        hb, a, w1b, *w2 = ctx.saved_tensors
         douts = [d if d is not None else torch.zeros(a.shape[0], w2[i].shape[0], device=a.device)
                  for i, d in enumerate(douts)]
         out = _C.heads_backward(a, list(douts), [x.contiguous() for x in w2])
         da, db1 = out[0], out[1]                       # da (P, kW) bf16, masked by the first ReLU
         dw1 = _splitk_dw(da, hb)                       # (kW, W) fp32
-        dh = _mm_dx(da, w1.to(torch.bfloat16))         # (P, W) fp32
+        dh = _mm_dx(da, w1b)                           # (P, W) fp32
         return tuple([dh, dw1, db1] + out[2:])
 
     @staticmethod

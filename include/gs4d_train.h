@@ -265,7 +265,8 @@ typedef struct gs4d_heads_block_fwd {
 int gs4d_heads_block_forward(const gs4d_heads_block_fwd *args, void *stream);
 /* The same block on bf16 operands (hyper.mlp_dtype = "bf16"): h, W1, W2 rounded to bf16, fp32 accumulation
  * (v_mfma_f32_16x16x32_bf16), a = relu(z + b1) stored as bf16 (uint16 bits, (ceil(P/16)*16, kW)), out_i fp32.
- * hb (nullable): h rounded to bf16, (ceil(P/16)*16, W), for the backward's weight-gradient GEMM.
+ * hb (nullable): h rounded to bf16, (ceil(P/16)*16, W), for the backward's weight-gradient GEMM; w1b (nullable):
+ * W1 rounded to bf16 (kW, W), for its input-gradient GEMM.
  * Returns 4 (GS4D_TRAIN_ERR_LDS) when the device cannot give the kernel its LDS (also for the fp32 form). */
 #define GS4D_TRAIN_ERR_LDS 4
 typedef struct gs4d_heads_block_fwd_bf16 {
@@ -275,6 +276,7 @@ typedef struct gs4d_heads_block_fwd_bf16 {
     const float *b1;
     uint16_t *a;
     uint16_t *hb;
+    uint16_t *w1b;
     int n[GS4D_HEADS_MAX];
     const float *w2[GS4D_HEADS_MAX];
     const float *b2[GS4D_HEADS_MAX];

@@ -474,8 +474,10 @@ def test_heads_block_forward_bf16_matches_fp64(P, W, ns):
     b1 = torch.randn(k * W, device="cuda") * 0.1
     w2 = [torch.randn(n, W, device="cuda") / W ** 0.5 for n in ns]
     b2 = [torch.randn(n, device="cuda") for n in ns]
-    a, hb, *out = _C.heads_block_forward_bf16(h, w1, b1, w2, b2)
+    a, hb, w1b, *out = _C.heads_block_forward_bf16(h, w1, b1, w2, b2)
     assert a.dtype == hb.dtype == torch.bfloat16 and a.shape == (P, k * W) and hb.shape == (P, W) and len(out) == k
+    if P:
+        assert torch.equal(w1b, w1.to(torch.bfloat16))
     if P == 0:
         return
     bf = torch.bfloat16
