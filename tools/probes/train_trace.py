@@ -49,6 +49,8 @@ def op_profile(cfg="metric", steps=5):
     P, W, H = CONFIGS[cfg]
     dev = torch.device("cuda:0")
     hyper, opt = config.dynerf()
+    if "--bf16" in sys.argv:
+        hyper.mlp_dtype = "bf16"
     torch.manual_seed(0)
     g = GaussianModel(3, hyper, fused=True)
     pts, cols = make_point_cloud(P, seed=0)
@@ -70,7 +72,8 @@ def op_profile(cfg="metric", steps=5):
         print(prof.key_averages(group_by_input_shape=True).table(sort_by="cuda_time_total", row_limit=400,
                                                                  max_name_column_width=40, max_shapes_column_width=70))
     else:
-        print(prof.key_averages().table(sort_by="cuda_time_total", row_limit=45, max_name_column_width=60))
+        key = "self_cpu_time_total" if "--cpu" in sys.argv else "cuda_time_total"
+        print(prof.key_averages().table(sort_by=key, row_limit=45, max_name_column_width=60))
 
 
 if __name__ == "__main__":
