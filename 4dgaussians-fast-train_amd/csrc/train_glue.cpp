@@ -536,7 +536,7 @@ std::vector<torch::Tensor> heads_block_forward(const torch::Tensor &h, const tor
     return out;
 }
 
-// ---- heads block forward on bf16 operands: (a bf16, hb bf16, W1 bf16, [out_i fp32]); same operands as above
+// ---- heads block forward on bf16 operands: (a bf16, hb bf16, W1^T bf16, [out_i fp32]); same operands as above
 std::vector<torch::Tensor> heads_block_forward_bf16(const torch::Tensor &h, const torch::Tensor &w1,
                                                     const torch::Tensor &b1, const std::vector<torch::Tensor> &w2s,
                                                     const std::vector<torch::Tensor> &b2s) {
@@ -554,10 +554,10 @@ std::vector<torch::Tensor> heads_block_forward_bf16(const torch::Tensor &h, cons
     auto bopt = h.options().dtype(torch::kBFloat16);
     auto a_pad = torch::empty({rows, w1.size(0)}, bopt);
     auto hb_pad = torch::empty({rows, h.size(1)}, bopt);
-    auto w1b = torch::empty_like(w1, bopt);
+    auto w1t = torch::empty({w1.size(1), w1.size(0)}, bopt);  // W1^T (W, kW)
     b.h = h.data_ptr<float>(), b.w1 = w1.data_ptr<float>(), b.b1 = b1.data_ptr<float>();
-    b.a = (uint16_t *)a_pad.data_ptr(), b.hb = (uint16_t *)hb_pad.data_ptr(), b.w1b = (uint16_t *)w1b.data_ptr();
-    std::vector<torch::Tensor> out{a_pad.narrow(0, 0, h.size(0)), hb_pad.narrow(0, 0, h.size(0)), w1b}, keep;
+    b.a = (uint16_t *)a_pad.data_ptr(), b.hb = (uint16_t *)hb_pad.data_ptr(), b.w1t = (uint16_t *)w1t.data_ptr();
+    std::vector<torch::Tensor> out{a_pad.narrow(0, 0, h.size(0)), hb_pad.narrow(0, 0, h.size(0)), w1t}, keep;
     for (int i = 0; i < k; i++) {
         auto w2 = w2s[i].contiguous();
         auto b2 = b2s[i].contiguous();
@@ -575,6 +575,20 @@ std::vector<torch::Tensor> heads_block_forward_bf16(const torch::Tensor &h, cons
     }
     check(gs4d_heads_block_forward_bf16(&b, (void *)stream_of(h)), "heads_block_forward_bf16");
     return out;
+}
+
+// ---- the bf16 block's input gradient: dh (P, W) fp32 = da (P, KW) bf16 @ W1 from W1^T (W, KW) bf16
+torch::Tensor mlp_dx_bf16(const torch::Tensor &da, const torch::Tensor &w1t) {
+    need(da.is_cuda() && w1t.is_cuda() && da.scalar_type() == torch::kBFloat16 && w1t.scalar_type() == torch::kBFloat16,
+         "mlp_dx_bf16: bf16 GPU tensors");
+    need(da.dim() == 2 && w1t.dim() == 2 && da.is_contiguous() && w1t.is_contiguous() && w1t.size(1) == da.size(1),
+         "mlp_dx_bf16: da (P, KW), W1^T (W, KW), contiguous");
+    c10::hip::HIPGuard guard(da.device().index());
+    auto dh = torch::empty({da.size(0), w1t.size(0)}, da.options().dtype(torch::kFloat32));
+    check(gs4d_mlp_dx_bf16((int)da.size(0), (int)da.size(1), (int)w1t.size(0), (const uint16_t *)da.data_ptr(),
+                           (const uint16_t *)w1t.data_ptr(), dh.data_ptr<float>(), (void *)stream_of(da)),
+          "mlp_dx_bf16");
+    return dh;
 }
 
 // ---- first deformation layer forward: h = relu(x W^T + b)
@@ -709,6 +723,7 @@ PYBIND11_MODULE(_C, m) {
     m.def("heads_forward", &heads_forward);
     m.def("heads_block_forward", &heads_block_forward);
     m.def("heads_block_forward_bf16", &heads_block_forward_bf16);
+    m.def("mlp_dx_bf16", &mlp_dx_bf16);
     m.def("feature_relu_backward", &feature_relu_backward);
     m.def("heads_backward", &heads_backward);
     m.def("linear_dw", &linear_dw);

@@ -1485,7 +1485,7 @@ __global__ __launch_bounds__(kHbfThreads) void heads_block_fwd_bf16_kernel(HfArg
                                                                            const float *__restrict__ b1,
                                                                            __bf16 *__restrict__ a,
                                                                            __bf16 *__restrict__ hb,
-                                                                           __bf16 *__restrict__ w1b) {
+                                                                           __bf16 *__restrict__ w1t) {
     constexpr int NT = W / 16, NK = W / 32, WS = W + 8, NW = kHbfThreads / 64;
     extern __shared__ float4 s_v[];
     __bf16 *s_w1 = reinterpret_cast<__bf16 *>(s_v);       // W rows x WS
@@ -1500,8 +1500,6 @@ __global__ __launch_bounds__(kHbfThreads) void heads_block_fwd_bf16_kernel(HfArg
         const float4 v = reinterpret_cast<const float4 *>(w1i + (size_t)row * W)[c4];
         const bf4v vb = bf4v{(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
         *reinterpret_cast<bf4v *>(s_w1 + row * WS + 4 * c4) = vb;
-        // workgroup 0 of each head also stores W1_i in bf16 for the backward's input-gradient GEMM
-        if (w1b && blockIdx.x == 0) *reinterpret_cast<bf4v *>(w1b + (size_t)head * W * W + (size_t)row * W + 4 * c4) = vb;
     }
     for (int e = threadIdx.x; e < npad * (W / 4); e += kHbfThreads) {
         const int row = e / (W / 4), c4 = e % (W / 4);
@@ -1512,6 +1510,17 @@ __global__ __launch_bounds__(kHbfThreads) void heads_block_fwd_bf16_kernel(HfArg
     for (int e = threadIdx.x; e < W; e += kHbfThreads) s_b1[e] = b1[head * W + e];
     for (int e = threadIdx.x; e < npad; e += kHbfThreads) s_b2[e] = e < n ? A.b2[head][e] : 0.f;
     __syncthreads();
+    if (w1t && blockIdx.x == 0) {
+        // workgroup 0 of each head also writes W1_i^T in bf16 for the backward's input gradient
+        // (gs4d_mlp_dx_bf16): 8 rows of one column of the LDS image per 16-byte store
+        for (int e = threadIdx.x; e < W * W / 8; e += kHbfThreads) {
+            const int col = e / (W / 8), r8 = e % (W / 8);
+            bf8v v;
+#pragma unroll
+            for (int j = 0; j < 8; j++) v[j] = s_w1[(8 * r8 + j) * WS + col];
+            *reinterpret_cast<bf8v *>(w1t + (size_t)col * A.kW + head * W + 8 * r8) = v;
+        }
+    }
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, q = lane >> 4, c = lane & 15;
     const int nblk = (A.P + 15) / 16;
     const int stride = gridDim.x * NW;
@@ -1593,6 +1602,94 @@ __global__ __launch_bounds__(kHbfThreads) void heads_block_fwd_bf16_kernel(HfArg
                 }
             }
         }
+    }
+}
+
+// ---- the bf16 heads block's input gradient: dh (P x W, fp32) = da (P x KW, bf16) W1 (KW x W, bf16), computed
+// as dh^T = W1^T da^T on v_mfma_f32_16x16x32_bf16: the A operand is W1^T (W x KW, written by the block forward),
+// the B operand da's rows as they lie in memory (lane (q, c): row c of a 16-row block, k = 32 s + 8 q .. + 7:
+// one 16-byte load), and D[n = 16 m + 4 q + r][row c] leaves as one float4 per lane and tile.  A 512-thread
+// workgroup takes 256 rows (32 per wave); W1^T is staged per 64-wide k chunk in LDS (16 KiB, double-buffered,
+// row stride 144 B so the 16 rows of a fragment read fall on distinct banks) and shared by the 8 waves, so it
+// is read from L2 once per workgroup instead of once per wave; da is prefetched one chunk ahead.  fp32
+// accumulation over KW.
+constexpr int kDxThreads = 512, kDxRowsPerWave = 32, kDxChunk = 64, kDxLdsStride = kDxChunk + 8;  // bf16 units
+template <int W>
+__global__ __launch_bounds__(kDxThreads) void mlp_dx_bf16_kernel(int P, int KW, const __bf16 *__restrict__ da,
+                                                                 const __bf16 *__restrict__ w1t,
+                                                                 float *__restrict__ dh) {
+    constexpr int NT = W / 16, RB = kDxRowsPerWave / 16;
+    constexpr int kPieces = W * kDxChunk / 8 / kDxThreads;  // 16-byte pieces of a chunk per thread (W = 128: 2)
+    __shared__ __attribute__((aligned(16))) __bf16 s_a[2][W * kDxLdsStride];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, q = lane >> 4, c = lane & 15;
+    const int64_t row0 = (int64_t)blockIdx.x * (kDxThreads / 64) * kDxRowsPerWave + (int64_t)wv * kDxRowsPerWave;
+    const __bf16 *brow[RB];
+#pragma unroll
+    for (int rb = 0; rb < RB; rb++)  // rows past P read row P - 1 (unconditional loads; not stored)
+        brow[rb] = da + (size_t)min(row0 + 16 * rb + c, (int64_t)P - 1) * KW + 8 * q;
+    f4v acc[NT][RB];
+#pragma unroll
+    for (int m = 0; m < NT; m++)
+#pragma unroll
+        for (int rb = 0; rb < RB; rb++) acc[m][rb] = f4v{0.f, 0.f, 0.f, 0.f};
+    const int nch = KW / kDxChunk;
+    bf8v ga[kPieces];
+    auto load_a = [&](int ch) {  // piece e: W1^T row e / 8, 16-byte column piece e % 8 of the chunk
+#pragma unroll
+        for (int i = 0; i < kPieces; i++) {
+            const int e = threadIdx.x + i * kDxThreads;
+            ga[i] = *reinterpret_cast<const bf8v *>(w1t + (size_t)(e >> 3) * KW + ch * kDxChunk + 8 * (e & 7));
+        }
+    };
+    auto store_a = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < kPieces; i++) {
+            const int e = threadIdx.x + i * kDxThreads;
+            *reinterpret_cast<bf8v *>(&s_a[buf][(e >> 3) * kDxLdsStride + 8 * (e & 7)]) = ga[i];
+        }
+    };
+    bf8v bn[2][RB];
+    auto load_b = [&](int ch) {
+#pragma unroll
+        for (int st = 0; st < 2; st++)
+#pragma unroll
+            for (int rb = 0; rb < RB; rb++)
+                bn[st][rb] = *reinterpret_cast<const bf8v *>(brow[rb] + ch * kDxChunk + 32 * st);
+    };
+    load_a(0);
+    load_b(0);
+    store_a(0);
+    __syncthreads();
+    for (int ch = 0; ch < nch; ch++) {
+        bf8v b[2][RB];
+#pragma unroll
+        for (int st = 0; st < 2; st++)
+#pragma unroll
+            for (int rb = 0; rb < RB; rb++) b[st][rb] = bn[st][rb];
+        const int nx = min(ch + 1, nch - 1);  // the last chunk re-loads itself: loads stay unconditional
+        load_a(nx);
+        load_b(nx);
+        const __bf16 *sa = s_a[ch & 1];
+#pragma unroll
+        for (int st = 0; st < 2; st++)
+#pragma unroll
+            for (int m = 0; m < NT; m++) {
+                const bf8v a = *reinterpret_cast<const bf8v *>(sa + (16 * m + c) * kDxLdsStride + 32 * st + 8 * q);
+#pragma unroll
+                for (int rb = 0; rb < RB; rb++)
+                    acc[m][rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[st][rb], acc[m][rb], 0, 0, 0);
+            }
+        if (ch + 1 < nch) store_a((ch + 1) & 1);  // the other buffer: read by nobody since the last barrier
+        __syncthreads();
+    }
+#pragma unroll
+    for (int rb = 0; rb < RB; rb++) {
+        const int64_t row = row0 + 16 * rb + c;
+        if (row < P)
+#pragma unroll
+            for (int m = 0; m < NT; m++)
+                *reinterpret_cast<float4 *>(dh + (size_t)row * W + 16 * m + 4 * q) =
+                    make_float4(acc[m][rb][0], acc[m][rb][1], acc[m][rb][2], acc[m][rb][3]);
     }
 }
 
@@ -2197,7 +2294,7 @@ int gs4d_heads_block_forward_bf16(const gs4d_heads_block_fwd_bf16 *args, void *s
     }
     if (((size_t)b.w1 & 15) != 0 || ((size_t)b.b1 & 15) != 0) return 1;
     if (b.P == 0) return 0;
-    if (!b.h || !b.a || (((size_t)b.h | (size_t)b.a | (size_t)b.hb) & 15) != 0 || ((size_t)b.w1b & 7) != 0) return 1;
+    if (!b.h || !b.a || (((size_t)b.h | (size_t)b.a | (size_t)b.hb | (size_t)b.w1t) & 15) != 0) return 1;
     const size_t lds = 2 * (size_t)(b.W + npad_max) * (b.W + 8) + 4 * (size_t)(b.W + npad_max);
     const int nblk = (b.P + 15) / 16;
     // two workgroups per CU (the bf16 kernel's VGPRs allow two 512-thread workgroups): one round of
@@ -2210,10 +2307,25 @@ int gs4d_heads_block_forward_bf16(const gs4d_heads_block_fwd_bf16 *args, void *s
         return kErrLds;
     if (b.W == 128)
         hipLaunchKernelGGL(heads_block_fwd_bf16_kernel<128>, dim3(per_head, b.k), dim3(kHbfThreads), lds, s, A, b.h,
-                           b.w1, b.b1, (__bf16 *)b.a, (__bf16 *)b.hb, (__bf16 *)b.w1b);
+                           b.w1, b.b1, (__bf16 *)b.a, (__bf16 *)b.hb, (__bf16 *)b.w1t);
     else
         hipLaunchKernelGGL(heads_block_fwd_bf16_kernel<64>, dim3(per_head, b.k), dim3(kHbfThreads), lds, s, A, b.h,
-                           b.w1, b.b1, (__bf16 *)b.a, (__bf16 *)b.hb, (__bf16 *)b.w1b);
+                           b.w1, b.b1, (__bf16 *)b.a, (__bf16 *)b.hb, (__bf16 *)b.w1t);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+int gs4d_mlp_dx_bf16(int P, int KW, int W, const uint16_t *da, const uint16_t *w1t, float *dh, void *stream) {
+    if (P < 0 || KW < kDxChunk || KW % kDxChunk != 0 || (W != 64 && W != 128)) return 1;
+    if (P == 0) return 0;
+    if (!da || !w1t || !dh || (((size_t)da | (size_t)w1t | (size_t)dh) & 15) != 0) return 1;
+    const int64_t rows_per_wg = (kDxThreads / 64) * kDxRowsPerWave;
+    const dim3 grid((unsigned)(((int64_t)P + rows_per_wg - 1) / rows_per_wg));
+    if (W == 128)
+        hipLaunchKernelGGL(mlp_dx_bf16_kernel<128>, grid, dim3(kDxThreads), 0, (hipStream_t)stream, P, KW,
+                           (const __bf16 *)da, (const __bf16 *)w1t, dh);
+    else
+        hipLaunchKernelGGL(mlp_dx_bf16_kernel<64>, grid, dim3(kDxThreads), 0, (hipStream_t)stream, P, KW,
+                           (const __bf16 *)da, (const __bf16 *)w1t, dh);
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 

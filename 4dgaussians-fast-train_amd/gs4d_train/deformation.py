@@ -392,7 +392,7 @@ class _DeformHeadsBF16(torch.autograd.Function):
         if _DeformHeadsBF16._fast(h, second):
             from . import _C
             try:
-                a, hb, w1b, *outs = _C.heads_block_forward_bf16(h.contiguous(), w1.contiguous(), b1.contiguous(),
+                a, hb, w1t, *outs = _C.heads_block_forward_bf16(h.contiguous(), w1.contiguous(), b1.contiguous(),
                                                            [t.contiguous() for t in second[0::2]],
                                                            [t.contiguous() for t in second[1::2]])
             except RuntimeError as e:
@@ -401,7 +401,7 @@ class _DeformHeadsBF16(torch.autograd.Function):
                 _block_forward_unavailable(h.device, e)
             else:
                 ctx.fast = True
-                ctx.save_for_backward(hb, a, w1b, *second[0::2])
+                ctx.save_for_backward(hb, a, w1t, *second[0::2])
                 return tuple(outs)
         ctx.fast = False
         return _DeformHeadsBF16._torch_forward(ctx, h, w1, b1, *second)
@@ -411,13 +411,14 @@ class _DeformHeadsBF16(torch.autograd.Function):
         if not ctx.fast:
             return _DeformHeadsBF16._torch_backward(ctx, *douts)
         from . import _C
-        hb, a, w1b, *w2 = ctx.saved_tensors
+        hb, a, w1t, *w2 = ctx.saved_tensors
         douts = [d if d is not None else torch.zeros(a.shape[0], w2[i].shape[0], device=a.device)
                  for i, d in enumerate(douts)]
         out = _C.heads_backward(a, list(douts), [x.contiguous() for x in w2])
         da, db1 = out[0], out[1]                       # da (P, kW) bf16, masked by the first ReLU
         dw1 = _splitk_dw(da, hb)                       # (kW, W) fp32
-        dh = _mm_dx(da, w1b)                           # (P, W) fp32
+        # (P, W) fp32: gs4d_mlp_dx_bf16 (bf16 MFMA) when KW is a multiple of its 64-wide k chunk
+        dh = _C.mlp_dx_bf16(da, w1t) if da.shape[1] % 64 == 0 else _mm_dx(da, w1t.t().contiguous())
         return tuple([dh, dw1, db1] + out[2:])
 
     @staticmethod

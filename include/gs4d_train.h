@@ -216,6 +216,9 @@ typedef struct gs4d_heads_bwd_bf16 {
     float *db2[GS4D_HEADS_MAX];
 } gs4d_heads_bwd_bf16;
 int gs4d_heads_backward_bf16(const gs4d_heads_bwd_bf16 *args, void *scratch, void *stream);
+/* The bf16 block's input gradient dh (P, W) fp32 = da (P, KW) bf16 @ W1 (KW, W), given W1^T (W, KW) bf16 (the block
+ * forward's w1t); bf16 MFMA, fp32 accumulation.  KW a multiple of 64, W in {64, 128}, 16-byte aligned. */
+int gs4d_mlp_dx_bf16(int P, int KW, int W, const uint16_t *da, const uint16_t *w1t, float *dh, void *stream);
 
 /* ---- The deformation field's first layer, backward, when feature_out is ONE Linear (defor_depth <= 1,
  * scene/deformation.py:51-55: hidden = x W^T + b) and every head begins with ReLU, so the heads read
@@ -265,8 +268,8 @@ typedef struct gs4d_heads_block_fwd {
 int gs4d_heads_block_forward(const gs4d_heads_block_fwd *args, void *stream);
 /* The same block on bf16 operands (hyper.mlp_dtype = "bf16"): h, W1, W2 rounded to bf16, fp32 accumulation
  * (v_mfma_f32_16x16x32_bf16), a = relu(z + b1) stored as bf16 (uint16 bits, (ceil(P/16)*16, kW)), out_i fp32.
- * hb (nullable): h rounded to bf16, (ceil(P/16)*16, W), for the backward's weight-gradient GEMM; w1b (nullable):
- * W1 rounded to bf16 (kW, W), for its input-gradient GEMM.
+ * hb (nullable): h rounded to bf16, (ceil(P/16)*16, W), for the backward's weight-gradient GEMM; w1t (nullable):
+ * W1^T rounded to bf16 (W, kW), for its input gradient (gs4d_mlp_dx_bf16).
  * Returns 4 (GS4D_TRAIN_ERR_LDS) when the device cannot give the kernel its LDS (also for the fp32 form). */
 #define GS4D_TRAIN_ERR_LDS 4
 typedef struct gs4d_heads_block_fwd_bf16 {
@@ -276,7 +279,7 @@ typedef struct gs4d_heads_block_fwd_bf16 {
     const float *b1;
     uint16_t *a;
     uint16_t *hb;
-    uint16_t *w1b;
+    uint16_t *w1t;
     int n[GS4D_HEADS_MAX];
     const float *w2[GS4D_HEADS_MAX];
     const float *b2[GS4D_HEADS_MAX];

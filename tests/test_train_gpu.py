@@ -474,10 +474,10 @@ def test_heads_block_forward_bf16_matches_fp64(P, W, ns):
     b1 = torch.randn(k * W, device="cuda") * 0.1
     w2 = [torch.randn(n, W, device="cuda") / W ** 0.5 for n in ns]
     b2 = [torch.randn(n, device="cuda") for n in ns]
-    a, hb, w1b, *out = _C.heads_block_forward_bf16(h, w1, b1, w2, b2)
+    a, hb, w1t, *out = _C.heads_block_forward_bf16(h, w1, b1, w2, b2)
     assert a.dtype == hb.dtype == torch.bfloat16 and a.shape == (P, k * W) and hb.shape == (P, W) and len(out) == k
     if P:
-        assert torch.equal(w1b, w1.to(torch.bfloat16))
+        assert torch.equal(w1t, w1.t().to(torch.bfloat16))
     if P == 0:
         return
     bf = torch.bfloat16
@@ -532,6 +532,25 @@ def test_heads_backward_bf16_matches_fp64(P, W, ns):
     if P:
         with pytest.raises(RuntimeError):
             _C.heads_backward(a[:, :W].contiguous(), [torch.randn(P, 40, device="cuda")], [torch.randn(40, W, device="cuda")])
+
+
+@pytest.mark.parametrize("P,KW,W", [(100_003, 640, 128), (1, 640, 128), (0, 640, 128), (777, 192, 64), (300, 64, 128),
+                                     (513, 1024, 128)])
+def test_mlp_dx_bf16_matches_fp64(P, KW, W):
+    """gs4d_mlp_dx_bf16 (dh = da W1 on the bf16 MFMA from W1^T, the k chunks staged in LDS) vs fp64 products of the
+    same bf16 values, to 1e-5 of each element's |terms| sum; ragged P (rows past P read row P - 1 and are not
+    stored; partial workgroups), P = 1, 0, one k chunk and sixteen."""
+    from gs4d_train import _C
+    torch.manual_seed(P + KW + W)
+    bf = torch.bfloat16
+    da = torch.randn(P, KW, device="cuda").to(bf)
+    w1 = (torch.randn(KW, W, device="cuda") / KW ** 0.5).to(bf)
+    dh = _C.mlp_dx_bf16(da, w1.t().contiguous())
+    assert dh.dtype == torch.float32 and dh.shape == (P, W)
+    if P:
+        ref = da.double() @ w1.double()
+        scale = da.double().abs() @ w1.double().abs()
+        assert float(((dh.double() - ref).abs() - 1e-5 * scale).max().clamp_min(0)) == 0.0
 
 
 @pytest.mark.parametrize("P,N,K", [(100_003, 640, 128), (2048, 640, 128), (5000, 192, 64), (700, 640, 128)])

@@ -34,7 +34,7 @@ def main():
     b2 = [torch.randn(n, device=dev) for n in ns]
     gs = [torch.randn(P, n, device=dev) for n in ns]
     a32, *_ = _C.heads_block_forward(h, w1, b1, w2, b2)
-    abf, hb, _, *_ = _C.heads_block_forward_bf16(h, w1, b1, w2, b2)
+    abf, hb, w1t, *_ = _C.heads_block_forward_bf16(h, w1, b1, w2, b2)
     da32 = _C.heads_backward(a32.contiguous(), gs, w2)[0]
     dabf = _C.heads_backward(abf.contiguous(), gs, w2)[0]
     w1b = w1.to(torch.bfloat16)
@@ -46,7 +46,8 @@ def main():
         ("dW1 split-K fp32", lambda: D._splitk_dw(da32, h)),
         ("dW1 split-K bf16", lambda: D._splitk_dw(dabf, hb)),
         ("dh fp32", lambda: D._mm_dx(da32, w1)),
-        ("dh bf16", lambda: D._mm_dx(dabf, w1b)),
+        ("dh bf16 (rocBLAS)", lambda: D._mm_dx(dabf, w1b)),
+        ("dh bf16 (mlp_dx_bf16)", lambda: _C.mlp_dx_bf16(dabf, w1t)),
     ]
     for name, fn in rows:
         print(f"{name:24s} {timed(fn):8.1f} us", flush=True)
