@@ -131,16 +131,17 @@ def main(argv=None):
     stage_avg = stage_timings(scene, dgr._C, args.steps)
     kernel_avg = stage_timings(scene, dgr._C, args.steps, repeats=KERNEL_REPEATS)
 
+    # ---- the full fine-stage train step (the metric's "train-step ms"), before the extras: run after their
+    # large scenes, the host-heavier bf16 leg measured 1.62-2.29 ms instead of 1.50-1.52 (fp32 unaffected)
+    train = None if args.no_train_step else train_step_timing(P, W, H, dev, world, rank, args.train_steps,
+                                                              args.warmup, dist)
+
     extras = {}
     if not args.no_extras:
         extras["forward_only"] = forward_timing(scene, dgr._C, args.steps, args.warmup)
         extras["autograd_wrapper"] = autograd_timing(scene, dgr, args.steps, args.warmup, P)
         extras["train_like_scene"] = train_like_timing(P, W, H, dev, args.steps, args.warmup, dgr._C, rank)
         extras["configs"] = config_timings(dev, args.steps, args.warmup, dgr._C)
-
-    # ---- the full fine-stage train step (the metric's "train-step ms") ----
-    train = None if args.no_train_step else train_step_timing(P, W, H, dev, world, rank, args.train_steps,
-                                                              args.warmup, dist)
 
     if rank == 0:
         L = int(nr)
