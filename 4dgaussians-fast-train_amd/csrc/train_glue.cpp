@@ -591,6 +591,23 @@ torch::Tensor mlp_dx_bf16(const torch::Tensor &da, const torch::Tensor &w1t) {
     return dh;
 }
 
+// ---- the bf16 block's first-layer weight gradient: dW1 (KW, W) fp32 = da^T hb
+torch::Tensor mlp_dw_bf16(const torch::Tensor &da, const torch::Tensor &hb) {
+    need(da.is_cuda() && hb.is_cuda() && da.scalar_type() == torch::kBFloat16 && hb.scalar_type() == torch::kBFloat16,
+         "mlp_dw_bf16: bf16 GPU tensors");
+    need(da.dim() == 2 && hb.dim() == 2 && da.size(0) == hb.size(0) && da.stride(1) == 1 && hb.stride(1) == 1 &&
+             da.stride(0) == da.size(1) && hb.stride(0) == hb.size(1),
+         "mlp_dw_bf16: da (P, KW), hb (P, W), rows contiguous");
+    c10::hip::HIPGuard guard(da.device().index());
+    const int P = (int)da.size(0), KW = (int)da.size(1), W = (int)hb.size(1);
+    auto dw = torch::empty({KW, W}, da.options().dtype(torch::kFloat32));
+    auto scratch = torch::empty({(int64_t)gs4d_mlp_dw_bf16_scratch_bytes(P, KW, W)}, da.options().dtype(torch::kUInt8));
+    check(gs4d_mlp_dw_bf16(P, KW, W, (const uint16_t *)da.data_ptr(), (const uint16_t *)hb.data_ptr(),
+                           dw.data_ptr<float>(), scratch.data_ptr(), (void *)stream_of(da)),
+          "mlp_dw_bf16");
+    return dw;
+}
+
 // ---- first deformation layer forward: h = relu(x W^T + b)
 torch::Tensor feature_relu_forward(const torch::Tensor &x, const torch::Tensor &w, const torch::Tensor &b) {
     for (const torch::Tensor *t : std::initializer_list<const torch::Tensor *>{&x, &w, &b})
@@ -724,6 +741,7 @@ PYBIND11_MODULE(_C, m) {
     m.def("heads_block_forward", &heads_block_forward);
     m.def("heads_block_forward_bf16", &heads_block_forward_bf16);
     m.def("mlp_dx_bf16", &mlp_dx_bf16);
+    m.def("mlp_dw_bf16", &mlp_dw_bf16);
     m.def("feature_relu_backward", &feature_relu_backward);
     m.def("heads_backward", &heads_backward);
     m.def("linear_dw", &linear_dw);

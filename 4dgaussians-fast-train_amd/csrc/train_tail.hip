@@ -1693,6 +1693,106 @@ __global__ __launch_bounds__(kDxThreads) void mlp_dx_bf16_kernel(int P, int KW, 
     }
 }
 
+// ---- the bf16 heads block's first-layer weight gradient: dW1 (KW x W, fp32) = da^T hb, reduced over the P rows.
+// Workgroup (row chunk s of 1024 rows, head i) forms the 128 x 128 block of head i's rows of dW1 over its chunk
+// into parts[s] (summed over the chunks in order by gs4d_sum_slices): D[da feature 16 m + 4 q + r][hb feature
+// 16 n + c] on v_mfma_f32_16x16x32_bf16 with K = rows.  Both operands need 8 consecutive ROWS of one column, so
+// each 64-row step stages the da and hb tiles (64 x 128 bf16 each, row-major as loaded) in LDS and reads them
+// back with ds_read_b64_tr_b16 (a 16-lane group reads a 4 x 16 block and receives it column-major): two
+// transposed reads give an operand's 8 rows.  The tiles use the XOR-swizzled 256-byte rows of the guide's
+// dual-use image (conflict-free transposed reads); rows past P are staged as zeros.  Double-buffered: the
+// next step's tiles are loaded while this step's MFMAs run.
+constexpr int kDwbThreads = 256, kDwbChunkRows = 1024, kDwbStepRows = 64;  // two MFMA k-steps per staged tile
+typedef short s4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ int dwb_off(int row, int ch) {  // byte offset of 16-byte chunk ch of tile row `row`
+    return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+__device__ __forceinline__ bf8v dwb_tr_frag(const unsigned char *tile, int rb, int g, int li, int c0) {
+    // rows rb + 8 g .. + 7 of the 16 columns starting at chunk c0, as an MFMA operand fragment (lane li gets
+    // column li): lane 4 q + p of the group addresses row (base + q), columns 4 p .. 4 p + 3
+    const int q = li >> 2, p = li & 3;
+    const unsigned char *a0 = tile + dwb_off(rb + 8 * g + q, c0 + (p >> 1)) + 8 * (p & 1);
+    const unsigned char *a1 = tile + dwb_off(rb + 8 * g + 4 + q, c0 + (p >> 1)) + 8 * (p & 1);
+    typedef __attribute__((address_space(3))) s4v lds_s4v;
+    const s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v *)a0);
+    const s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v *)a1);
+    const s4v v[2] = {lo, hi};
+    return __builtin_bit_cast(bf8v, v);
+}
+__global__ __launch_bounds__(kDwbThreads) void mlp_dw_bf16_kernel(int P, int KW, const __bf16 *__restrict__ da,
+                                                                  const __bf16 *__restrict__ hb,
+                                                                  float *__restrict__ parts) {
+    constexpr int W = 128, NT = W / 16, MW = NT / (kDwbThreads / 64);  // m tiles per wave: 2
+    constexpr int kPer = kDwbStepRows * 16 / kDwbThreads;  // 16-byte chunks per thread and tile
+    __shared__ __attribute__((aligned(16))) unsigned char s_t[2][2][kDwbStepRows * 256];  // [buffer][da, hb][tile]
+    const int head = blockIdx.y;
+    const int64_t r0 = (int64_t)blockIdx.x * kDwbChunkRows;
+    const int nst = (int)((min((int64_t)P, r0 + kDwbChunkRows) - r0 + kDwbStepRows - 1) / kDwbStepRows);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4, li = lane & 15;
+    f4v acc[MW][NT];
+#pragma unroll
+    for (int m = 0; m < MW; m++)
+#pragma unroll
+        for (int n = 0; n < NT; n++) acc[m][n] = f4v{0.f, 0.f, 0.f, 0.f};
+    // staging: thread t moves chunks t, t + 256, ... of each tile: row e / 16, chunk e % 16
+    bf8v ld[2][kPer];
+    auto load = [&](int st) {
+#pragma unroll
+        for (int i = 0; i < kPer; i++) {
+            const int e = threadIdx.x + i * kDwbThreads, row = e >> 4, ch = e & 15;
+            const int64_t pr = r0 + kDwbStepRows * st + row;
+            const bool ok = pr < P;
+            const int64_t prc = ok ? pr : 0;
+            const bf8v z = bf8v{};
+            const bf8v va = *reinterpret_cast<const bf8v *>(da + (size_t)prc * KW + head * W + 8 * ch);
+            const bf8v vh = *reinterpret_cast<const bf8v *>(hb + (size_t)prc * W + 8 * ch);
+            ld[0][i] = ok ? va : z;
+            ld[1][i] = ok ? vh : z;
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < kPer; i++) {
+            const int e = threadIdx.x + i * kDwbThreads, row = e >> 4, ch = e & 15;
+            *reinterpret_cast<bf8v *>(&s_t[buf][0][dwb_off(row, ch)]) = ld[0][i];
+            *reinterpret_cast<bf8v *>(&s_t[buf][1][dwb_off(row, ch)]) = ld[1][i];
+        }
+    };
+    if (nst > 0) {
+        load(0);
+        store(0);
+    }
+    __syncthreads();
+    for (int st = 0; st < nst; st++) {
+        if (st + 1 < nst) load(st + 1);
+        const unsigned char *ta = s_t[st & 1][0], *th = s_t[st & 1][1];
+#pragma unroll
+        for (int kk = 0; kk < kDwbStepRows / 32; kk++) {
+            bf8v a[MW];
+#pragma unroll
+            for (int m = 0; m < MW; m++) a[m] = dwb_tr_frag(ta, 32 * kk, g, li, 2 * (wv * MW + m));
+#pragma unroll
+            for (int n = 0; n < NT; n++) {
+                const bf8v b = dwb_tr_frag(th, 32 * kk, g, li, 2 * n);
+#pragma unroll
+                for (int m = 0; m < MW; m++)
+                    acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[m], b, acc[m][n], 0, 0, 0);
+            }
+        }
+        if (st + 1 < nst) store((st + 1) & 1);  // the other buffer: nobody reads it since the last barrier
+        __syncthreads();
+    }
+    // D[da feature 16 m + 4 g + r][hb feature 16 n + li] of head `head` -> parts[s]
+    float *o = parts + (size_t)blockIdx.x * KW * W + (size_t)head * W * W;
+#pragma unroll
+    for (int m = 0; m < MW; m++)
+#pragma unroll
+        for (int n = 0; n < NT; n++)
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+                o[(size_t)(16 * (wv * MW + m) + 4 * g + r) * W + 16 * n + li] = acc[m][n][r];
+}
+
 // ---- the deformation field's first layer, forward: h = relu(x W^T + b) (P, FOUT) from x (P, FIN) on the
 // f32 MFMA.  Per 16-row block: lane group q = l >> 4 reads columns 4q..4q+3 of its row l & 15 of a 16-column
 // K chunk as one float4 (the MFMA's k index in step s is column 4q + s), the matching W rows (LDS, row stride
@@ -2327,6 +2427,26 @@ int gs4d_mlp_dx_bf16(int P, int KW, int W, const uint16_t *da, const uint16_t *w
         hipLaunchKernelGGL(mlp_dx_bf16_kernel<64>, grid, dim3(kDxThreads), 0, (hipStream_t)stream, P, KW,
                            (const __bf16 *)da, (const __bf16 *)w1t, dh);
     return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+size_t gs4d_mlp_dw_bf16_scratch_bytes(int P, int KW, int W) {
+    if (P <= 0 || KW <= 0 || W <= 0) return 256;
+    const size_t S = ((size_t)P + kDwbChunkRows - 1) / kDwbChunkRows;
+    return 4 * S * (size_t)KW * W + 256;
+}
+
+int gs4d_mlp_dw_bf16(int P, int KW, int W, const uint16_t *da, const uint16_t *hb, float *dw, void *scratch,
+                     void *stream) {
+    if (P < 0 || W != 128 || KW < W || KW % W != 0 || !dw) return 1;
+    hipStream_t s = (hipStream_t)stream;
+    if (P == 0) return hipMemsetAsync(dw, 0, 4 * (size_t)KW * W, s) == hipSuccess ? 0 : 3;
+    if (!da || !hb || !scratch || (((size_t)da | (size_t)hb) & 15) != 0) return 1;
+    const int S = (int)(((int64_t)P + kDwbChunkRows - 1) / kDwbChunkRows);
+    float *parts = (float *)align_up((size_t)scratch, 256);
+    hipLaunchKernelGGL(mlp_dw_bf16_kernel, dim3(S, KW / W), dim3(kDwbThreads), 0, s, P, KW, (const __bf16 *)da,
+                       (const __bf16 *)hb, parts);
+    if (hipGetLastError() != hipSuccess) return 3;
+    return gs4d_sum_slices(parts, S, (int64_t)KW * W, dw, stream);
 }
 
 int gs4d_feature_relu_forward(int P, int Fin, int Fout, const float *x, const float *w, const float *b, float *h,

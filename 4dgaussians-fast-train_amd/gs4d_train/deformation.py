@@ -368,13 +368,13 @@ def _colsum(x):
 class _DeformHeadsBF16(torch.autograd.Function):
     """The opt-in bf16 form of _DeformHeads (hyper.mlp_dtype = "bf16", BASELINE C3's bf16 leg): the same
     block on bf16 operands with fp32 accumulation; parameters, their gradients and the heads' outputs stay
-    fp32.  On the GPU (W in {64, 128}, n_i <= 16 or 48) every piece is a HIP or rocBLAS bf16 kernel:
+    fp32.  On the GPU (W in {64, 128}, n_i <= 16 or 48) every piece is a HIP bf16-MFMA kernel:
       forward   gs4d_heads_block_forward_bf16: both layers on v_mfma_f32_16x16x32_bf16 in one pass, a =
-                relu(h W1^T + b1) written once in bf16 (half the fp32 block's bytes) with h and W1 in bf16 for
-                the backward's GEMMs;
+                relu(h W1^T + b1) written once in bf16 (half the fp32 block's bytes) with h and W1^T in bf16
+                for the backward;
       backward  gs4d_heads_backward_bf16: the second layers' backward, the ReLU mask and db1 in one pass
-                over a (da in bf16, sums fp32); dW1 = da^T h as a split-K bf16 GEMM (rocBLAS, f32 out) and
-                dh = da W1 as one bf16 GEMM (f32 out).
+                over a (da in bf16, sums fp32); dW1 = da^T h by gs4d_mlp_dw_bf16 and dh = da W1 by
+                gs4d_mlp_dx_bf16 (f32 out; rocBLAS bf16 GEMMs for widths those do not serve).
     Rounding: h, W1, W2, a and da are rounded to bf16 once each (tests/test_train_gpu.py bounds the effect
     on a train step against the fp32 path).  Elsewhere (CPU, other widths) the same function in torch bf16
     ops: _torch_forward / _torch_backward."""
@@ -416,7 +416,8 @@ class _DeformHeadsBF16(torch.autograd.Function):
                  for i, d in enumerate(douts)]
         out = _C.heads_backward(a, list(douts), [x.contiguous() for x in w2])
         da, db1 = out[0], out[1]                       # da (P, kW) bf16, masked by the first ReLU
-        dw1 = _splitk_dw(da, hb)                       # (kW, W) fp32
+        # (kW, W) fp32: gs4d_mlp_dw_bf16 (bf16 MFMA, LDS transpose reads) for W = 128, else rocBLAS split-K
+        dw1 = _C.mlp_dw_bf16(da, hb) if hb.shape[1] == 128 and da.shape[1] % 128 == 0 else _splitk_dw(da, hb)
         # (P, W) fp32: gs4d_mlp_dx_bf16 (bf16 MFMA) when KW is a multiple of its 64-wide k chunk
         dh = _C.mlp_dx_bf16(da, w1t) if da.shape[1] % 64 == 0 else _mm_dx(da, w1t.t().contiguous())
         return tuple([dh, dw1, db1] + out[2:])

@@ -219,6 +219,11 @@ int gs4d_heads_backward_bf16(const gs4d_heads_bwd_bf16 *args, void *scratch, voi
 /* The bf16 block's input gradient dh (P, W) fp32 = da (P, KW) bf16 @ W1 (KW, W), given W1^T (W, KW) bf16 (the block
  * forward's w1t); bf16 MFMA, fp32 accumulation.  KW a multiple of 64, W in {64, 128}, 16-byte aligned. */
 int gs4d_mlp_dx_bf16(int P, int KW, int W, const uint16_t *da, const uint16_t *w1t, float *dh, void *stream);
+/* Its weight gradient dW1 (KW, W) fp32 = da^T hb over the P rows (da (P, KW), hb (P, W) bf16; W = 128, KW a multiple
+ * of W): per 1024-row chunk and head a bf16-MFMA block (LDS transpose reads), the chunks summed in order. */
+size_t gs4d_mlp_dw_bf16_scratch_bytes(int P, int KW, int W);
+int gs4d_mlp_dw_bf16(int P, int KW, int W, const uint16_t *da, const uint16_t *hb, float *dw, void *scratch,
+                     void *stream);
 
 /* ---- The deformation field's first layer, backward, when feature_out is ONE Linear (defor_depth <= 1,
  * scene/deformation.py:51-55: hidden = x W^T + b) and every head begins with ReLU, so the heads read

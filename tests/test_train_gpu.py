@@ -553,6 +553,23 @@ def test_mlp_dx_bf16_matches_fp64(P, KW, W):
         assert float(((dh.double() - ref).abs() - 1e-5 * scale).max().clamp_min(0)) == 0.0
 
 
+@pytest.mark.parametrize("P,KW", [(100_003, 640), (1, 640), (0, 640), (1024, 128), (3000, 256), (33, 640)])
+def test_mlp_dw_bf16_matches_fp64(P, KW):
+    """gs4d_mlp_dw_bf16 (dW1 = da^T hb on the bf16 MFMA, tiles read back with LDS transpose reads, 1024-row
+    chunks summed in order) vs fp64 products of the same bf16 values, to 1e-5 of each element's |terms| sum:
+    ragged P (a partial last chunk and a partial 32-row step, staged as zeros), P = 1, 0, one head and five."""
+    from gs4d_train import _C
+    torch.manual_seed(P + KW)
+    bf = torch.bfloat16
+    da = torch.randn(P, KW, device="cuda").to(bf)
+    hb = torch.relu(torch.randn(P, 128, device="cuda")).to(bf)
+    dw = _C.mlp_dw_bf16(da, hb)
+    assert dw.dtype == torch.float32 and dw.shape == (KW, 128)
+    ref = da.double().t() @ hb.double()
+    scale = da.double().abs().t() @ hb.double().abs()
+    assert float(((dw.double() - ref).abs() - 1e-5 * scale).max().clamp_min(0)) == 0.0
+
+
 @pytest.mark.parametrize("P,N,K", [(100_003, 640, 128), (2048, 640, 128), (5000, 192, 64), (700, 640, 128)])
 def test_mlp_gemms_bf16_match_fp64(P, N, K):
     """The bf16 path's GEMMs on rocBLAS (bf16 operands, f32 accumulation and output): the split-K weight

@@ -44,7 +44,8 @@ def main():
         ("heads backward fp32", lambda: _C.heads_backward(a32.contiguous(), gs, w2)),
         ("heads backward bf16", lambda: _C.heads_backward(abf.contiguous(), gs, w2)),
         ("dW1 split-K fp32", lambda: D._splitk_dw(da32, h)),
-        ("dW1 split-K bf16", lambda: D._splitk_dw(dabf, hb)),
+        ("dW1 split-K bf16 (rocBLAS)", lambda: D._splitk_dw(dabf, hb)),
+        ("dW1 bf16 (mlp_dw_bf16)", lambda: _C.mlp_dw_bf16(dabf, hb)),
         ("dh fp32", lambda: D._mm_dx(da32, w1)),
         ("dh bf16 (rocBLAS)", lambda: D._mm_dx(dabf, w1b)),
         ("dh bf16 (mlp_dx_bf16)", lambda: _C.mlp_dx_bf16(dabf, w1t)),
