@@ -1793,6 +1793,145 @@ __global__ __launch_bounds__(kDwbThreads) void mlp_dw_bf16_kernel(int P, int KW,
                 o[(size_t)(16 * (wv * MW + m) + 4 * g + r) * W + 16 * n + li] = acc[m][n][r];
 }
 
+// ---- the wide head's second-layer backward on the bf16 path (n = 48, W = 128): heads_bwd_wide_mfma_kernel's
+// products on v_mfma_f32_16x16x32_bf16 with g rounded to bf16 (the bf16 leg's operands), sums in fp32.  A
+// workgroup takes 32-row steps (grid-stride): the a tile (32 x 128 bf16) and the g tile (32 x 48 -> bf16,
+// columns 48..63 zero) are staged in LDS (the swizzled 256-byte rows of mlp_dw_bf16_kernel), W2^T (128 x 64
+// bf16, zero-padded k) once per workgroup.
+//   da^T = W2^T g^T: A = W2^T rows (LDS row reads), B = g rows (LDS row reads), D = 4 consecutive columns of one
+//        row per lane: masked by a > 0 and stored as 8 bytes; db1 summed from the fp32 results;
+//   dW2 += g^T a: both operands by ds_read_b64_tr_b16 (K = the 32 rows);
+//   db2: the fp32 g values summed as staged.
+// Partials in heads_bwd_reduce_kernel's layout (fixed-order sums: deterministic).
+__global__ __launch_bounds__(256) void heads_bwd_wide_bf16_kernel(HbArgs A, const __bf16 *__restrict__ a,
+                                                                  __bf16 *__restrict__ da, const float *__restrict__ g,
+                                                                  float *__restrict__ part) {
+    constexpr int W = 128, N = 48, KS = 72;  // W2^T row stride (bf16): 64 + 8 (144 B)
+    __shared__ __attribute__((aligned(16))) __bf16 s_w2t[W * KS];
+    __shared__ __attribute__((aligned(16))) unsigned char s_ta[32 * 256], s_tg[32 * 256];
+    __shared__ float4 s_red[192];
+    const int ld = A.k * W, h = A.h0;
+    const float *__restrict__ w2 = A.w2[h];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, q = lane >> 4, c = lane & 15;
+    for (int e = threadIdx.x; e < W * 64; e += 256) {
+        const int n = e / 64, k = e % 64;
+        s_w2t[n * KS + k] = (__bf16)(k < N ? w2[k * W + n] : 0.f);
+    }
+    for (int e = threadIdx.x; e < 32 * 10; e += 256) {  // g tile chunks 6..15 stay zero
+        const int row = e / 10, ch = 6 + e % 10;
+        *reinterpret_cast<bf8v *>(&s_tg[dwb_off(row, ch)]) = bf8v{};
+    }
+    f4v accw[3][2];
+#pragma unroll
+    for (int m = 0; m < 3; m++) accw[m][0] = accw[m][1] = f4v{0.f, 0.f, 0.f, 0.f};
+    float4 dsum[2][2];  // [n local][row block]: this lane's da column sums (4 columns)
+#pragma unroll
+    for (int i = 0; i < 2; i++) dsum[i][0] = dsum[i][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 gsum = make_float4(0.f, 0.f, 0.f, 0.f);  // threads < 192: fp32 column sums of g, columns 4 (t % 12) ..
+    const int P = A.P, nb32 = (P + 31) / 32;
+    for (int blk = blockIdx.x; blk < nb32; blk += gridDim.x) {
+        const int64_t r0 = (int64_t)blk * 32;
+        // stage the a tile (512 16-byte chunks, two per thread) and the g tile (384 float4, two per thread < 192)
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            const int e = threadIdx.x + 256 * i, row = e >> 4, ch = e & 15;
+            const int64_t pr = r0 + row;
+            bf8v v = bf8v{};
+            if (pr < P) v = *reinterpret_cast<const bf8v *>(a + (size_t)pr * ld + h * W + 8 * ch);
+            *reinterpret_cast<bf8v *>(&s_ta[dwb_off(row, ch)]) = v;
+        }
+        if (threadIdx.x < 192) {
+            const int c4 = threadIdx.x % 12;
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+                const int row = threadIdx.x / 12 + 16 * i;
+                const int64_t pr = r0 + row;
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (pr < P) v = *reinterpret_cast<const float4 *>(g + (size_t)pr * N + 4 * c4);
+                gsum.x += v.x; gsum.y += v.y; gsum.z += v.z; gsum.w += v.w;
+                *reinterpret_cast<bf4v *>(&s_tg[dwb_off(row, c4 >> 1) + 8 * (c4 & 1)]) =
+                    bf4v{(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+            }
+        }
+        __syncthreads();
+        // da^T: wave wv takes columns tiles n = 2 wv, 2 wv + 1 for both 16-row blocks
+#pragma unroll
+        for (int nl = 0; nl < 2; nl++) {
+            const int n = 2 * wv + nl;
+#pragma unroll
+            for (int rb = 0; rb < 2; rb++) {
+                f4v d = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int st = 0; st < 2; st++) {
+                    const bf8v wa = *reinterpret_cast<const bf8v *>(&s_w2t[(16 * n + c) * KS + 32 * st + 8 * q]);
+                    const bf8v gb = *reinterpret_cast<const bf8v *>(&s_tg[dwb_off(16 * rb + c, 4 * st + q)]);
+                    d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, gb, d, 0, 0, 0);
+                }
+                // D[column 16 n + 4 q + r][row 16 rb + c]
+                const int row = 16 * rb + c;
+                const bf4v av = *reinterpret_cast<const bf4v *>(&s_ta[dwb_off(row, 2 * n + (q >> 1)) + 8 * (q & 1)]);
+                const float v0 = (float)av[0] > 0.f ? d[0] : 0.f, v1 = (float)av[1] > 0.f ? d[1] : 0.f;
+                const float v2 = (float)av[2] > 0.f ? d[2] : 0.f, v3 = (float)av[3] > 0.f ? d[3] : 0.f;
+                if (r0 + row < P) {
+                    *reinterpret_cast<bf4v *>(da + (size_t)(r0 + row) * ld + h * W + 16 * n + 4 * q) =
+                        bf4v{(__bf16)v0, (__bf16)v1, (__bf16)v2, (__bf16)v3};
+                    dsum[nl][rb].x += v0; dsum[nl][rb].y += v1; dsum[nl][rb].z += v2; dsum[nl][rb].w += v3;
+                }
+            }
+        }
+        // dW2 += g^T a: tiles (m = 0..2, n = 2 wv, 2 wv + 1), K = the 32 rows
+#pragma unroll
+        for (int m = 0; m < 3; m++) {
+            const bf8v ga = dwb_tr_frag(s_tg, 0, q, c, 2 * m);
+#pragma unroll
+            for (int nl = 0; nl < 2; nl++) {
+                const bf8v ab = dwb_tr_frag(s_ta, 0, q, c, 2 * (2 * wv + nl));
+                accw[m][nl] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ga, ab, accw[m][nl], 0, 0, 0);
+            }
+        }
+        __syncthreads();  // the tiles are restaged by the next step
+    }
+    float *pw = part + (size_t)blockIdx.x * (W + N * (W + 1));
+    // db1: the 16 lanes of a lane group (rows) summed by a fixed butterfly, both row blocks in order
+#pragma unroll
+    for (int nl = 0; nl < 2; nl++) {
+        float4 t = make_float4(dsum[nl][0].x + dsum[nl][1].x, dsum[nl][0].y + dsum[nl][1].y,
+                               dsum[nl][0].z + dsum[nl][1].z, dsum[nl][0].w + dsum[nl][1].w);
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) {
+            t.x += __shfl_xor(t.x, off, 16); t.y += __shfl_xor(t.y, off, 16);
+            t.z += __shfl_xor(t.z, off, 16); t.w += __shfl_xor(t.w, off, 16);
+        }
+        if (c == 0) {
+            const int col = 16 * (2 * wv + nl) + 4 * q;
+            pw[col] = t.x, pw[col + 1] = t.y, pw[col + 2] = t.z, pw[col + 3] = t.w;
+        }
+    }
+    // dW2: D[output 16 m + 4 q + r][column 16 n + c]
+#pragma unroll
+    for (int m = 0; m < 3; m++)
+#pragma unroll
+        for (int nl = 0; nl < 2; nl++)
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+                pw[W + (16 * m + 4 * q + r) * (W + 1) + 16 * (2 * wv + nl) + c] = accw[m][nl][r];
+    // db2: the 16 threads of each column group summed in thread order
+    if (threadIdx.x < 192) s_red[threadIdx.x] = gsum;
+    __syncthreads();
+    if (threadIdx.x < 12) {
+        float4 t = s_red[threadIdx.x];
+        for (int j = 1; j < 16; j++) {
+            const float4 v = s_red[threadIdx.x + 12 * j];
+            t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+        }
+        const int o = 4 * threadIdx.x;
+        pw[W + (o + 0) * (W + 1) + W] = t.x;
+        pw[W + (o + 1) * (W + 1) + W] = t.y;
+        pw[W + (o + 2) * (W + 1) + W] = t.z;
+        pw[W + (o + 3) * (W + 1) + W] = t.w;
+    }
+}
+
 // ---- the deformation field's first layer, forward: h = relu(x W^T + b) (P, FOUT) from x (P, FIN) on the
 // f32 MFMA.  Per 16-row block: lane group q = l >> 4 reads columns 4q..4q+3 of its row l & 15 of a 16-column
 // K chunk as one float4 (the MFMA's k index in step s is column 4q + s), the matching W rows (LDS, row stride
@@ -1920,6 +2059,10 @@ extern "C" {
 // the launches: maximal runs of heads of one class (narrow: n <= 16; wide: n = 48)
 static bool hb_wide(int n) { return n > 16; }  // n = 48 (validated), one head per launch
 static bool hb_mfma(int W, int n) { return (W == 64 || W == 128) && n == 48; }  // heads_bwd_wide_mfma_kernel
+#ifndef HB_WIDE_BF16
+#define HB_WIDE_BF16 1
+#endif
+static const bool hb_wide_bf16 = HB_WIDE_BF16 != 0;  // the bf16 path's wide head on heads_bwd_wide_bf16_kernel
 static int hb_rows_per_wg(int P, bool wide) {
     // narrow heads stream a: about two workgroups per CU; the wide head's waves are compute-heavy and
     // its per-workgroup partials large: 256-row blocks
@@ -1987,7 +2130,11 @@ static int heads_backward_t(const Args *args, void *scratch, void *stream) {
         if (b.P == 0) {  // empty sums: the partials of one empty workgroup
             if (hipMemsetAsync(part, 0, 4 * (size_t)A.poff[hk], s) != hipSuccess) err = 3;
         } else {
-            if (hb_wide(b.n[h0]) && hb_mfma(b.W, b.n[h0])) {
+            if (hb_wide(b.n[h0]) && hb_mfma(b.W, b.n[h0]) && std::is_same<TA, __bf16>::value && b.W == 128 &&
+                hb_wide_bf16) {
+                hipLaunchKernelGGL(heads_bwd_wide_bf16_kernel, dim3(nwg), dim3(256), 0, s, A, (const __bf16 *)ba,
+                                   (__bf16 *)bda, g[h0], part);
+            } else if (hb_wide(b.n[h0]) && hb_mfma(b.W, b.n[h0])) {
                 if (b.W == 128)
                     hipLaunchKernelGGL((heads_bwd_wide_mfma_kernel<128, 48, TA>), dim3(nwg), dim3(256), 0, s, A, ba,
                                        bda, g[h0], part);

@@ -501,20 +501,26 @@ def test_heads_block_forward_bf16_matches_fp64(P, W, ns):
 def test_heads_backward_bf16_matches_fp64(P, W, ns):
     """gs4d_heads_backward_bf16 (a and da in bf16, everything else fp32) vs fp64 torch on the same bf16 a:
     da within one bf16 ulp + 1e-5 of its row's |terms| sum, the mask exact; db1 (summed before da is
-    rounded), dW2 and db2 to 1e-5 of their largest |term| sum.  A wide head the bf16 path has no kernel
-    for (n = 40) is refused."""
+    rounded), dW2 and db2 to 1e-5 of their largest |term| sum.  The 48-wide head at W = 128 runs on the bf16
+    MFMA (heads_bwd_wide_bf16_kernel) with g and W2 rounded to bf16 as operands: its references use those
+    rounded values (db2 stays the fp32 g's sum).  A wide head the bf16 path has no kernel for (n = 40) is
+    refused."""
     from gs4d_train import _C
     torch.manual_seed(P + W + 11 * len(ns))
     k = len(ns)
-    a = torch.relu(torch.randn(P, k * W, device="cuda")).to(torch.bfloat16)
+    bf = torch.bfloat16
+    a = torch.relu(torch.randn(P, k * W, device="cuda")).to(bf)
     gs = [torch.randn(P, n, device="cuda") for n in ns]
     w2 = [torch.randn(n, W, device="cuda") for n in ns]
     out = _C.heads_backward(a, gs, w2)
     da, db1 = out[0], out[1]
     assert da.dtype == torch.bfloat16 and da.shape == a.shape and db1.dtype == torch.float32
     ad = a.double()
-    ref = torch.cat([g.double() @ w.double() for g, w in zip(gs, w2)], 1) * (ad > 0)
-    scale = torch.cat([g.double().abs() @ w.double().abs() for g, w in zip(gs, w2)], 1)
+    wide = [n == 48 and W == 128 for n in ns]
+    gq = [g.to(bf).double() if wd else g.double() for g, wd in zip(gs, wide)]
+    wq = [w.to(bf).double() if wd else w.double() for w, wd in zip(w2, wide)]
+    ref = torch.cat([g @ w for g, w in zip(gq, wq)], 1) * (ad > 0)
+    scale = torch.cat([g.abs() @ w.abs() for g, w in zip(gq, wq)], 1)
     if P:
         assert bool(((da == 0) == ((a <= 0) | (ref.abs() < 1e-38))).all())
         err = (da.double() - ref).abs() - BF16_ULP * ref.abs() - 1e-5 * scale
@@ -523,8 +529,8 @@ def test_heads_backward_bf16_matches_fp64(P, W, ns):
     assert float((db1.double() - ref.sum(0)).abs().max() / s1) <= 1e-5
     for i, (g, w) in enumerate(zip(gs, w2)):
         x = ad[:, i * W:(i + 1) * W]
-        rw, rb = g.double().t() @ x, g.double().sum(0)
-        sw = (g.double().abs().t() @ x.abs()).max().clamp_min(1e-30)
+        rw, rb = gq[i].t() @ x, g.double().sum(0)
+        sw = (gq[i].abs().t() @ x.abs()).max().clamp_min(1e-30)
         sb = g.double().abs().sum(0).max().clamp_min(1e-30)
         assert out[2 + 2 * i].dtype == torch.float32
         assert float((out[2 + 2 * i].double() - rw).abs().max() / sw) <= 1e-5
