@@ -120,6 +120,8 @@ void adam_step(std::vector<torch::Tensor> params, std::vector<torch::Tensor> gra
     reset();
     int64_t chunks = 0;
     for (size_t i = 0; i < n; i++) {
+        need(grads[i].layout() == torch::kStrided, "FusedAdam does not support sparse gradients");
+        if (!grads[i].is_contiguous()) grads[i] = grads[i].contiguous();  // kept alive by the vector until launch
         for (auto *t : {&params[i], &grads[i], &exp_avgs[i], &exp_avg_sqs[i]}) gpu_f32(*t, "adam tensor");
         need(params[i].device() == params[0].device(), "adam_step: tensors on several devices");
         need(grads[i].numel() == params[i].numel() && exp_avgs[i].numel() == params[i].numel() &&

@@ -7,6 +7,7 @@ callers -- GaussianModel(fused=False), losses.l1_loss_torch -- and serve the par
 import math
 
 import torch
+import torch.optim.optimizer as _optim_mod
 
 from . import _C
 
@@ -72,59 +73,83 @@ class FusedAdam(torch.optim.Optimizer):
         # of the tensor (the tensor stays current for any reader).  A step tensor the cache has not seen (a
         # fresh state, load_state_dict) is read once.
         self._step_cache = {}
+        # torch.optim.Optimizer wraps step() in a profiler range plus the step-hook loops (~25 us of host time
+        # per call).  The instance-level step below skips that wrapper while no hook is registered and no
+        # profiler runs, and takes the wrapped class method otherwise (hooks and profiler ranges behave as
+        # with torch's optimizers).
+        self.step = self._step_unwrapped
+
+    def _step_unwrapped(self, closure=None):
+        if (_optim_mod._global_optimizer_pre_hooks or _optim_mod._global_optimizer_post_hooks
+                or self._optimizer_step_pre_hooks or self._optimizer_step_post_hooks
+                or torch.autograd.profiler._is_profiler_enabled):
+            return type(self).step(self, closure)
+        return self._step(closure)
+
+    def step(self, closure=None):
+        return self._step(closure)
 
     @torch.no_grad()
-    def step(self, closure=None):
+    def _step(self, closure=None):
         loss = None
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        work = []  # (group, p, grad, state)
+        # One pass over the parameters with the per-parameter work kept to a few attribute and dict reads:
+        # this loop is host time every train step (~50 parameters), and the GPU waits behind it.  The rare
+        # cases (a fresh state, a step tensor the cache has not seen or that was edited, a sparse gradient)
+        # take the slow branch.  Non-contiguous gradients are made contiguous by the extension.
+        state, cache = self.state, self._step_cache
+        by_hyper = {}
+        live = 0
         for group in self.param_groups:
+            lists = None
+            lr = group["lr"]
+            beta1, beta2 = group["betas"]
             for p in group["params"]:
                 g = p.grad
                 if g is None:
                     continue
-                if g.is_sparse:
-                    raise RuntimeError("FusedAdam does not support sparse gradients")
-                st = self.state[p]
-                if len(st) == 0:
+                st = state[p]
+                if not st:
                     st["step"] = torch.tensor(0.0, dtype=torch.float32)
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                work.append((group, p, g, st))
-        if not work:
-            return loss
-        cache = self._step_cache
-        if len(cache) > 4 * len(work) + 64:  # states of parameters no longer optimised
-            live = {id(w[3]["step"]) for w in work}
-            for k in [k for k in cache if k not in live]:
-                del cache[k]
-        by_hyper = {}
-        for group, p, g, st in work:
-            t = st["step"]
-            if t.device.type != "cpu":  # a step tensor moved off the host (not torch's default): plain update
-                t += 1
-                step = t.item()
-            else:
+                t = st["step"]
                 e = cache.get(id(t))
-                # reload when the tensor is new to the cache or was edited in place since the last step
-                # (zero_(), copy_(), a manual reset): a host read through the numpy view, no sync
-                if e is None or e[0] is not t or float(e[1][()]) != e[2]:
-                    e = cache[id(t)] = [t, t.numpy(), t.item()]  # CPU float32 0-d tensor, as torch's Adam keeps it
-                e[2] += 1.0
-                e[1][()] = e[2]
-                step = e[2]
-            beta1, beta2 = group["betas"]
-            lists = by_hyper.get((beta1, beta2, group["eps"]))
-            if lists is None:
-                lists = by_hyper[(beta1, beta2, group["eps"])] = ([], [], [], [], [], [])
-            lists[0].append(p)
-            lists[1].append(g if g.is_contiguous() else g.contiguous())
-            lists[2].append(st["exp_avg"])
-            lists[3].append(st["exp_avg_sq"])
-            lists[4].append((group["lr"] / (1 - beta1 ** step)) * -1)
-            lists[5].append((1 - beta2 ** step) ** 0.5)
+                # the cached count holds while the tensor is the one cached and was not edited in place since
+                # the last step (zero_(), copy_(), a manual reset): a host read through the numpy view, no sync
+                if e is None or e[0] is not t or e[1][()] != e[2]:
+                    if g.is_sparse:
+                        raise RuntimeError("FusedAdam does not support sparse gradients")
+                    if t.device.type != "cpu":  # a step tensor moved off the host (not torch's default)
+                        t += 1
+                        step = t.item()
+                        e = None
+                    else:  # CPU float32 0-d tensor, as torch's Adam keeps it
+                        e = cache[id(t)] = [t, t.numpy(), t.item()]
+                if e is not None:
+                    step = e[2] = e[2] + 1.0
+                    e[1][()] = step
+                if lists is None:
+                    key = (beta1, beta2, group["eps"])
+                    lists = by_hyper.get(key)
+                    if lists is None:
+                        lists = by_hyper[key] = ([], [], [], [], [], [])
+                    ps, gs, ms, vs, ss, bs = lists
+                ps.append(p)
+                gs.append(g)
+                ms.append(st["exp_avg"])
+                vs.append(st["exp_avg_sq"])
+                ss.append((lr / (1 - beta1 ** step)) * -1)
+                bs.append((1 - beta2 ** step) ** 0.5)
+                live += 1
+        if not live:
+            return loss
+        if len(cache) > 4 * live + 64:  # states of parameters no longer optimised
+            keep = {id(state[p]["step"]) for ps in (l[0] for l in by_hyper.values()) for p in ps}
+            for k in [k for k in cache if k not in keep]:
+                del cache[k]
         for (beta1, beta2, eps), (ps, gs, ms, vs, ss, bs) in by_hyper.items():
             _C.adam_step(ps, gs, ms, vs, ss, bs, beta1, beta2, eps)
         return loss

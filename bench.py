@@ -455,12 +455,12 @@ def train_step_timing(P, W, H, dev, world, rank, steps, warmup, dist, unfused=Tr
                      "opacity+SH deform), fused libgs4d HexPlane field + regularisers / L1 / densification stats / Adam kernels, deformation heads as one GEMM block with their second-layer backward in HIP (gs4d_heads_backward)"}
     # BASELINE C3's "bf16/fp32": the same step with the deformation heads on bf16 operands (opt-in,
     # deformation.py _DeformHeadsBF16: the heads block forward on the bf16 MFMA, the second-layer backward on
-    # bf16 a / da, the two W x 5W GEMMs as bf16 rocBLAS GEMMs with f32 output; the rasterizer, feature_out,
-    # parameters, gradients and the heads' outputs stay fp32)
+    # bf16 a / da, the two W x 5W GEMMs of the backward as hand-written bf16-MFMA passes (dW1 with fp32 sums,
+    # dh); the rasterizer, feature_out, parameters, gradients and the heads' outputs stay fp32)
     bms, bloss = run(True, steps, warmup, mlp_dtype="bf16")
     res["bf16_mlp"] = {"ms": round(bms, 3), "loss": round(bloss, 6),
                        "config": "as above, hyper.mlp_dtype = 'bf16' (gs4d_heads_block_forward_bf16, "
-                                 "gs4d_heads_backward_bf16, bf16 rocBLAS dW1 / dh)"}
+                                 "gs4d_heads_backward_bf16, gs4d_mlp_dw_bf16 / gs4d_mlp_dx_bf16)"}
     if unfused and world == 1:
         ums, _ = run(False, max(3, steps // 4), 2)
         res["reference_torch_tail_ms"] = round(ums, 3)

@@ -328,6 +328,40 @@ def test_fused_adam_host_step_counts(monkeypatch):
     assert check(1)
 
 
+def test_fused_adam_hooks_and_profiler_take_the_wrapped_step(monkeypatch):
+    """FusedAdam's instance step skips torch's profiler/hook wrapper only while nothing is registered: step
+    pre/post hooks (per optimizer and global) still fire, a profiler still sees the "Optimizer.step#..." range,
+    an LR scheduler still wraps it, and parameters of groups with different betas go out in separate batches."""
+    from gs4d_train import kernels as K
+    calls = []
+    monkeypatch.setattr(K, "_C", type("Fake", (), {"adam_step": staticmethod(lambda *a: calls.append(a))}))
+    ps = [torch.nn.Parameter(torch.randn(3)) for _ in range(3)]
+    for p in ps:
+        p.grad = torch.randn(3)
+    ps[2].grad = None  # no gradient: skipped, no state
+    opt = K.FusedAdam([{"params": ps[:1], "lr": 0.1}, {"params": ps[1:], "lr": 0.2, "betas": (0.8, 0.9)}])
+    seen = []
+    h1 = opt.register_step_pre_hook(lambda o, a, k: seen.append("pre"))
+    h2 = opt.register_step_post_hook(lambda o, a, k: seen.append("post"))
+    from torch.optim.optimizer import register_optimizer_step_pre_hook
+    h3 = register_optimizer_step_pre_hook(lambda o, a, k: seen.append("global"))
+    opt.step()
+    assert seen == ["global", "pre", "post"]
+    for h in (h1, h2, h3):
+        h.remove()
+    opt.step()
+    assert seen == ["global", "pre", "post"] and len(calls) == 4
+    assert [len(c[0]) for c in calls[-2:]] == [1, 1] and {c[6] for c in calls[-2:]} == {0.9, 0.8}
+    assert ps[2] not in opt.state and float(opt.state[ps[1]]["step"]) == 2.0
+    with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU]) as prof:
+        opt.step()
+    assert any(e.name == "Optimizer.step#FusedAdam.step" for e in prof.events())
+    sched = torch.optim.lr_scheduler.StepLR(opt, step_size=1, gamma=0.5)
+    opt.step()
+    sched.step()
+    assert opt.param_groups[0]["lr"] == 0.05 and float(opt.state[ps[0]]["step"]) == 4.0
+
+
 def test_ssim_restatement():
     """utils/loss_utils.py:26-66: window taps, ssim(x, x) = 1, and a direct float64 evaluation of the
     same formula (zero-padded 11x11 Gaussian window) on a small image."""
