@@ -3,8 +3,11 @@
 #include <ATen/ATen.h>
 #include <c10/hip/HIPGuard.h>
 #include <c10/hip/HIPStream.h>
+#define ROCBLAS_BETA_FEATURES_API  // rocblas_gemm*_get_solutions: the candidates of the GEMM tuner
 #include <rocblas/rocblas.h>
 
+#include <map>
+#include <mutex>
 #include <unordered_map>
 #include <torch/extension.h>
 
@@ -653,32 +656,76 @@ torch::Tensor hexplane_points_backward(const torch::Tensor &dpts_, const torch::
     return dxyz;
 }
 
-// ---- plain f32 GEMMs of the deformation MLP on rocBLAS with a chosen kernel ---------------------------
+// ---- plain f32 GEMMs of the deformation MLP on rocBLAS with a tuned kernel ------------------------------
 // torch dispatches these f32 GEMMs to hipBLASLt, whose heuristic pick for the MLP's shapes runs at
-// 100-125 TF/s of the 157 TF/s f32 peak.  TunableOp (tools/tunableop_probe.sh: every hipBLASLt and rocBLAS
-// solution timed for the P = 100k shapes on this image) found rocBLAS kernels 20-40 % faster; they are
-// called here by their solution index (rocblas_gemm_algo_solution_index) for any P.  An index rocBLAS
-// rejects for a shape falls back to rocBLAS's own choice; the return value says which ran.
+// 100-125 TF/s of the 157 TF/s f32 peak; some rocBLAS (Tensile) kernels are 20-40 % faster on them
+// (tools/tunableop_probe.sh, profiles/r03_tunableop_results.csv).  Which kernels exist, and their solution
+// indices, depend on the rocBLAS build, so nothing is hard-coded: on the first call for a shape class,
+// gemm_f32 asks rocBLAS for every solution that serves the problem (rocblas_gemm_ex_get_solutions /
+// rocblas_gemm_strided_batched_ex_get_solutions), times each on the caller's stream (hipEvents; the library's
+// own pick included as solution 0) and keeps the fastest for that class.  A class is the shape with its one
+// large dimension (the point count, which densification changes every few hundred steps) rounded up to a
+// 1/8-octave bucket, so a new point count reuses its bucket's kernel instead of re-tuning.  A cached kernel
+// rocBLAS rejects for an exact shape is re-tuned for it.  Each choice is logged once (stderr) and readable
+// through gemm_tuned().
 // Column-major semantics: C (m x n) [+ i * sC] = op(A) op(B) for batch i, f32 inputs, f32 accumulation.
-// One handle per (host thread, stream): the forward and the autograd engine's backward thread may both call
-// in (rocblas_set_stream on a shared handle would race), and GEMMs queued on two streams must not share a
-// handle's workspace.  A stream belongs to one device, so the stream keys the device too.  Handles live for
-// the process (a handful: one per thread and stream that ever ran a GEMM).
-static rocblas_handle rocblas_for(const torch::Tensor &t) {
-    static thread_local std::unordered_map<hipStream_t, rocblas_handle> handles;
+// One handle per (host thread, device, stream): the forward and the autograd engine's backward thread may both
+// call in (rocblas_set_stream on a shared handle would race), GEMMs queued on two streams must not share a
+// handle's workspace, and a default stream is the null handle on every device, so the device is part of the
+// key.  Handles live for the process (a handful: one per thread and stream that ever ran a GEMM).
+namespace {
+struct HandleKey {
+    int dev;
+    hipStream_t st;
+    bool operator==(const HandleKey &o) const { return dev == o.dev && st == o.st; }
+};
+struct HandleKeyHash {
+    size_t operator()(const HandleKey &k) const {
+        return std::hash<const void *>()((const void *)k.st) * 31u + (size_t)k.dev;
+    }
+};
+rocblas_handle rocblas_for(const torch::Tensor &t) {
+    static thread_local std::unordered_map<HandleKey, rocblas_handle, HandleKeyHash> handles;
+    const int dev = t.device().index();
     const hipStream_t st = stream_of(t);
-    auto it = handles.find(st);
+    const HandleKey key{dev, st};
+    auto it = handles.find(key);
     if (it != handles.end()) return it->second;
     rocblas_handle h = nullptr;
     TORCH_CHECK(rocblas_create_handle(&h) == rocblas_status_success, "rocblas_create_handle");
     TORCH_CHECK(rocblas_set_stream(h, st) == rocblas_status_success, "rocblas_set_stream");
-    handles.emplace(st, h);
+    handles.emplace(key, h);
     return h;
 }
+// 1/8-octave bucket of a dimension: its upper end (so every size in a bucket maps to the same class)
+int64_t dim_bucket(int64_t v) {
+    if (v <= 64) return v;
+    int e = 63 - __builtin_clzll((unsigned long long)v);  // 2^e <= v < 2^(e+1)
+    const int64_t step = (int64_t)1 << (e - 3);
+    return (v + step - 1) / step * step;
+}
+struct TunedGemm {
+    int32_t solution = 0;  // 0: rocBLAS's own pick
+    double us = 0, default_us = 0;
+    int candidates = 0;
+};
+std::mutex g_tune_mu;
+std::map<std::string, TunedGemm> g_tuned;  // class key -> choice (and exact keys of re-tuned shapes)
+}  // namespace
+
+std::vector<std::tuple<std::string, int64_t, double, double, int64_t>> gemm_tuned() {
+    std::lock_guard<std::mutex> lk(g_tune_mu);
+    std::vector<std::tuple<std::string, int64_t, double, double, int64_t>> out;
+    for (const auto &kv : g_tuned)
+        out.emplace_back(kv.first, kv.second.solution, kv.second.us, kv.second.default_us, kv.second.candidates);
+    return out;
+}
+
 // A and B may instead both be bf16 (the bf16 MLP path): bf16 products, f32 accumulation, f32 C.
-bool gemm_f32(torch::Tensor A, torch::Tensor B, torch::Tensor C, bool ta, bool tb, int64_t m, int64_t n, int64_t k,
-              int64_t lda, int64_t ldb, int64_t ldc, int64_t batch, int64_t sA, int64_t sB, int64_t sC,
-              int64_t solution) {
+// tune: true = the tuned kernel for the shape's class (first call of a class tunes it), false = rocBLAS's
+// own pick.  Returns the solution index that ran (0 = rocBLAS's own pick).
+int64_t gemm_f32(torch::Tensor A, torch::Tensor B, torch::Tensor C, bool ta, bool tb, int64_t m, int64_t n, int64_t k,
+                 int64_t lda, int64_t ldb, int64_t ldc, int64_t batch, int64_t sA, int64_t sB, int64_t sC, bool tune) {
     const bool bf = A.scalar_type() == torch::kBFloat16;
     const auto ab_type = bf ? torch::kBFloat16 : torch::kFloat32;
     TORCH_CHECK(A.is_cuda() && B.is_cuda() && C.is_cuda() && A.scalar_type() == ab_type && B.scalar_type() == ab_type &&
@@ -698,29 +745,116 @@ bool gemm_f32(torch::Tensor A, torch::Tensor B, torch::Tensor C, bool ta, bool t
                 "gemm_f32: operands exceed their tensors");
     const c10::hip::HIPGuard guard(A.device().index());
     rocblas_handle h = rocblas_for(A);
+    const hipStream_t stream = stream_of(A);
     const float one = 1.f, zero = 0.f;
     const rocblas_operation oa = ta ? rocblas_operation_transpose : rocblas_operation_none;
     const rocblas_operation ob = tb ? rocblas_operation_transpose : rocblas_operation_none;
-    auto run = [&](rocblas_gemm_algo algo, int32_t sol) {
+    const uint32_t flags = rocblas_gemm_flags_check_solution_index;
+    auto run = [&](int32_t sol) {
+        const rocblas_gemm_algo algo = sol ? rocblas_gemm_algo_solution_index : rocblas_gemm_algo_standard;
         if (batch == 1)
             return rocblas_gemm_ex(h, oa, ob, (int)m, (int)n, (int)k, &one, A.data_ptr(), abt, (int)lda, B.data_ptr(),
-                                   abt, (int)ldb, &zero,
-                                   C.data_ptr<float>(), rocblas_datatype_f32_r, (int)ldc, C.data_ptr<float>(),
-                                   rocblas_datatype_f32_r, (int)ldc, rocblas_datatype_f32_r, algo, sol, 0);
+                                   abt, (int)ldb, &zero, C.data_ptr<float>(), rocblas_datatype_f32_r, (int)ldc,
+                                   C.data_ptr<float>(), rocblas_datatype_f32_r, (int)ldc, rocblas_datatype_f32_r, algo,
+                                   sol, sol ? flags : 0);
         return rocblas_gemm_strided_batched_ex(h, oa, ob, (int)m, (int)n, (int)k, &one, A.data_ptr(), abt, (int)lda,
                                                sA, B.data_ptr(), abt, (int)ldb, sB, &zero, C.data_ptr<float>(),
                                                rocblas_datatype_f32_r, (int)ldc, sC, C.data_ptr<float>(),
                                                rocblas_datatype_f32_r, (int)ldc, sC, (int)batch, rocblas_datatype_f32_r,
-                                               algo, sol, 0);
+                                               algo, sol, sol ? flags : 0);
     };
-    if (solution != 0) {
-        if (run(rocblas_gemm_algo_solution_index, (int32_t)solution) == rocblas_status_success) return true;
-        TORCH_WARN_ONCE("gemm_f32: rocBLAS rejected solution ", solution, " for m=", m, " n=", n, " k=", k,
-                        "; using rocBLAS's default kernel");
+    auto run_default = [&]() {
+        const rocblas_status st = run(0);
+        TORCH_CHECK(st == rocblas_status_success, "gemm_f32: rocBLAS status ", (int)st);
+        return (int64_t)0;
+    };
+    if (!tune) return run_default();
+
+    // the shape class: the large dimension (> 4096: the point count) bucketed, the others exact
+    auto key_of = [&](bool exact) {
+        auto d = [&](int64_t v) { return exact || v <= 4096 ? v : dim_bucket(v); };
+        std::string key = std::string(bf ? "bf16" : "f32") + (ta ? " t" : " n") + (tb ? "t" : "n") + " m=" +
+                          std::to_string(d(m)) + " n=" + std::to_string(d(n)) + " k=" + std::to_string(d(k)) +
+                          " lda=" + std::to_string(d(lda)) + " ldb=" + std::to_string(d(ldb)) + " ldc=" +
+                          std::to_string(d(ldc)) + " batch=" + std::to_string(batch) + " dev=" +
+                          std::to_string(A.device().index());
+        return exact ? key + " (exact)" : key;
+    };
+    const std::string ckey = key_of(false), xkey = key_of(true);
+    {
+        std::lock_guard<std::mutex> lk(g_tune_mu);
+        auto it = g_tuned.find(xkey);
+        if (it == g_tuned.end()) it = g_tuned.find(ckey);
+        if (it != g_tuned.end()) {
+            const int32_t sol = it->second.solution;
+            if (sol == 0) return run_default();
+            if (run(sol) == rocblas_status_success) return sol;
+            // rejected for this exact shape: tune it below under its exact key
+        }
     }
-    const rocblas_status st = run(rocblas_gemm_algo_standard, 0);
-    TORCH_CHECK(st == rocblas_status_success, "gemm_f32: rocBLAS status ", (int)st);
-    return false;
+    // the candidates: every solution rocBLAS has for this exact problem
+    std::vector<rocblas_int> sols;
+    rocblas_int count = 0;
+    auto list = [&](rocblas_int *arr, rocblas_int *sz) {
+        if (batch == 1)
+            return rocblas_gemm_ex_get_solutions(h, oa, ob, (int)m, (int)n, (int)k, &one, A.data_ptr(), abt, (int)lda,
+                                                 B.data_ptr(), abt, (int)ldb, &zero, C.data_ptr<float>(),
+                                                 rocblas_datatype_f32_r, (int)ldc, C.data_ptr<float>(),
+                                                 rocblas_datatype_f32_r, (int)ldc, rocblas_datatype_f32_r,
+                                                 rocblas_gemm_algo_solution_index, flags, arr, sz);
+        return rocblas_gemm_strided_batched_ex_get_solutions(
+            h, oa, ob, (int)m, (int)n, (int)k, &one, A.data_ptr(), abt, (int)lda, sA, B.data_ptr(), abt, (int)ldb, sB,
+            &zero, C.data_ptr<float>(), rocblas_datatype_f32_r, (int)ldc, sC, C.data_ptr<float>(),
+            rocblas_datatype_f32_r, (int)ldc, sC, (int)batch, rocblas_datatype_f32_r, rocblas_gemm_algo_solution_index,
+            flags, arr, sz);
+    };
+    if (list(nullptr, &count) == rocblas_status_success && count > 0) {
+        sols.resize((size_t)count);
+        if (list(sols.data(), &count) != rocblas_status_success) count = 0;
+        sols.resize((size_t)std::max<rocblas_int>(count, 0));
+    }
+    sols.insert(sols.begin(), 0);  // rocBLAS's own pick competes too
+    hipEvent_t e0, e1;
+    TORCH_CHECK(hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess, "gemm_f32: hipEventCreate");
+    auto time_of = [&](int32_t sol, int reps) -> double {
+        if (run(sol) != rocblas_status_success) return -1.0;  // warm-up (and the validity check)
+        (void)hipEventRecord(e0, stream);
+        for (int r = 0; r < reps; r++) run(sol);
+        (void)hipEventRecord(e1, stream);
+        (void)hipEventSynchronize(e1);
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        return 1e3 * ms / reps;
+    };
+    TunedGemm best;
+    best.solution = 0;
+    best.us = 1e30;
+    for (const rocblas_int sol : sols) {
+        double us = time_of(sol, 1);
+        if (us < 0) continue;
+        if (us < 1.5 * best.us) us = std::min(us, time_of(sol, 3));  // a contender: a steadier measurement
+        if (sol == 0) best.default_us = us;
+        if (us < best.us) {
+            best.us = us;
+            best.solution = sol;
+        }
+        best.candidates++;
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    TORCH_CHECK(best.candidates > 0, "gemm_f32: no rocBLAS solution ran for ", xkey);
+    bool rejected;
+    {
+        std::lock_guard<std::mutex> lk(g_tune_mu);
+        rejected = g_tuned.count(ckey) != 0;  // the class's kernel did not serve this exact shape
+        g_tuned[rejected ? xkey : ckey] = best;
+    }
+    fprintf(stderr, "gs4d gemm_f32: tuned %s: solution %d at %.1f us (rocBLAS's own pick %.1f us; %d candidates)\n",
+            (rejected ? xkey : ckey).c_str(), best.solution, best.us, best.default_us, best.candidates);
+    // the result of the chosen kernel (the timing runs wrote C too, but leave no doubt which one did last)
+    if (best.solution == 0) return run_default();
+    TORCH_CHECK(run(best.solution) == rocblas_status_success, "gemm_f32: tuned solution failed");
+    return best.solution;
 }
 
 // out[i] = sum over s of parts[s][i], s in order (a split-K GEMM's partials)
@@ -748,6 +882,7 @@ PYBIND11_MODULE(_C, m) {
     m.def("heads_backward", &heads_backward);
     m.def("linear_dw", &linear_dw);
     m.def("gemm_f32", &gemm_f32);
+    m.def("gemm_tuned", &gemm_tuned);
     m.def("sum_slices", &sum_slices);
     m.def("hexplane_reg_forward", &hexplane_reg_forward);
     m.def("hexplane_reg_backward", &hexplane_reg_backward);

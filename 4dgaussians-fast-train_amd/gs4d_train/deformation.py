@@ -155,14 +155,11 @@ class Linear(nn.Linear):
         return F.linear(x, self.weight, self.bias)
 
 
-# rocBLAS kernels (solution indices) for the MLP's f32 GEMMs, found by TunableOp on this image for the
-# P = 100k train step (tools/tunableop_probe.sh, profiles/r03_tunableop_results.csv): hipBLASLt's heuristic
-# picks took 129 (split-K dW, 97 chunks of 1024 rows), 14 (its 672-row remainder) and 158 us (the input
-# gradient da @ W1); these take 121, 8.7 and 126 us.  train_glue.cpp's gemm_f32 falls back to rocBLAS's own
-# choice for a shape a kernel does not serve.
-_SOL_DW_BATCHED = -624952225  # nt, batched: (K x N) chunk partials of dW^T
-_SOL_DW = -624951956          # nt: the remainder rows
-_SOL_DX = -624952408          # nn: dx = dy @ W (P x K) from (P x N) (N x K)
+# The MLP's GEMMs run on rocBLAS kernels chosen at run time: gemm_f32(..., tune=True) times every solution
+# rocBLAS has for a shape class on its first call and keeps the fastest (train_glue.cpp).  On the r03 image
+# the chosen kernels took 121 (split-K dW, 97 chunks of 1024 rows), 8.7 (its 672-row remainder) and 126 us
+# (the input gradient da @ W1) where hipBLASLt's heuristic picks took 129, 14 and 158 us
+# (tools/tunableop_probe.sh, profiles/r03_tunableop_results.csv).  _C.gemm_tuned() lists the choices.
 
 
 _USE_ROCBLAS = os.environ.get("GS4D_MLP_ROCBLAS", "1") != "0"  # 0: torch's GEMMs (A/B runs)
@@ -177,7 +174,7 @@ def _rocblas_ok(*ts):
 def _splitk_dw(dy, x):
     """dW = dy^T x reduced over the P rows as a split-K batched GEMM (see _LinearSplitK); x may be a
     column slice of a wider row-major tensor (its rows are then strided).  On the GPU: the chunks' partials
-    and the remainder's on rocBLAS (gemm_f32, the TunableOp kernels above) into one (S + 1, N, K) buffer,
+    and the remainder's on rocBLAS (gemm_f32, the tuned kernels above) into one (S + 1, N, K) buffer,
     summed in chunk order by one pass (gs4d_sum_slices) -- the bmm, its .sum(0), the remainder GEMM and
     the add of the torch form in three launches."""
     P, c = x.shape[0], _LinearSplitK.kChunk
@@ -189,17 +186,16 @@ def _splitk_dw(dy, x):
         N, K = dy.shape[1], x.shape[1]
         if S < 2:  # one GEMM, f32 out (a bf16 torch GEMM would round the result to bf16)
             out = torch.empty(N, K, device=dy.device)
-            _C.gemm_f32(x, dy, out, False, True, K, N, P, x.stride(0), dy.stride(0), K, 1, 0, 0, 0, 0)
+            _C.gemm_f32(x, dy, out, False, True, K, N, P, x.stride(0), dy.stride(0), K, 1, 0, 0, 0, True)
             return out
         rem = P - S * c
-        f32 = x.dtype == torch.float32  # the tuned solutions are f32 kernels; bf16 takes rocBLAS's choice
         parts = torch.empty(S + (1 if rem else 0), N, K, device=dy.device)
         # column-major: part_s^T (K x N) = x_s^T (K x c) . dy_s (c x N)
         _C.gemm_f32(x, dy, parts, False, True, K, N, c, x.stride(0), dy.stride(0), K, S, c * x.stride(0),
-                    c * dy.stride(0), N * K, _SOL_DW_BATCHED if f32 else 0)
+                    c * dy.stride(0), N * K, True)
         if rem:
             _C.gemm_f32(x[S * c:], dy[S * c:], parts[S], False, True, K, N, rem, x.stride(0), dy.stride(0), K, 1,
-                        0, 0, 0, _SOL_DW if f32 else 0)
+                        0, 0, 0, True)
         return _C.sum_slices(parts)
     xs = x[:S * c].unflatten(0, (S, c))
     dw = torch.bmm(dy[:S * c].unflatten(0, (S, c)).transpose(1, 2), xs).sum(0)
@@ -209,14 +205,13 @@ def _splitk_dw(dy, x):
 
 
 def _mm_dx(dy, w):
-    """dy @ w (P x N)(N x K): the MLP's input gradient; on the GPU rocBLAS with the TunableOp kernel."""
+    """dy @ w (P x N)(N x K): the MLP's input gradient; on the GPU rocBLAS with the tuned kernel."""
     if _rocblas_ok(dy, w) and w.is_contiguous() and dy.shape[0] > 0:
         from . import _C
         P, N, K = dy.shape[0], dy.shape[1], w.shape[1]
         out = torch.empty(P, K, device=dy.device)
         # column-major: out^T (K x P) = w^T (K x N) . dy^T (N x P)
-        _C.gemm_f32(w, dy, out, False, False, K, P, N, K, dy.stride(0), K, 1, 0, 0, 0,
-                    _SOL_DX if w.dtype == torch.float32 else 0)
+        _C.gemm_f32(w, dy, out, False, False, K, P, N, K, dy.stride(0), K, 1, 0, 0, 0, True)
         return out
     return (dy @ w).float()
 

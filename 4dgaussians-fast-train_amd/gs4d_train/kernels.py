@@ -74,17 +74,25 @@ class FusedAdam(torch.optim.Optimizer):
         # fresh state, load_state_dict) is read once.
         self._step_cache = {}
         # torch.optim.Optimizer wraps step() in a profiler range plus the step-hook loops (~25 us of host time
-        # per call).  The instance-level step below skips that wrapper while no hook is registered and no
-        # profiler runs, and takes the wrapped class method otherwise (hooks and profiler ranges behave as
-        # with torch's optimizers).
-        self.step = self._step_unwrapped
+        # per call).  The class's step (set once per class, after Optimizer.__init__ has wrapped it) skips that
+        # wrapper while no hook is registered and no profiler runs, and takes the wrapped method otherwise (hooks
+        # and profiler ranges behave as with torch's optimizers).  It lives on the class, not the instance, so
+        # an optimizer holds no reference to itself and is freed with its last reference.
+        cls = type(self)
+        if not getattr(cls.step, "_gs4d_fast", False):
+            wrapped = cls.step
 
-    def _step_unwrapped(self, closure=None):
-        if (_optim_mod._global_optimizer_pre_hooks or _optim_mod._global_optimizer_post_hooks
-                or self._optimizer_step_pre_hooks or self._optimizer_step_post_hooks
-                or torch.autograd.profiler._is_profiler_enabled):
-            return type(self).step(self, closure)
-        return self._step(closure)
+            def step(self, closure=None):
+                if (_optim_mod._global_optimizer_pre_hooks or _optim_mod._global_optimizer_post_hooks
+                        or self._optimizer_step_pre_hooks or self._optimizer_step_post_hooks
+                        or torch.autograd.profiler._is_profiler_enabled):
+                    return wrapped(self, closure)
+                return self._step(closure)
+
+            step.hooked = True  # Optimizer._patch_step_function: already wrapped
+            step._gs4d_fast = True
+            step.__doc__ = wrapped.__doc__
+            cls.step = step
 
     def step(self, closure=None):
         return self._step(closure)
@@ -101,6 +109,7 @@ class FusedAdam(torch.optim.Optimizer):
         # take the slow branch.  Non-contiguous gradients are made contiguous by the extension.
         state, cache = self.state, self._step_cache
         by_hyper = {}
+        pending = []
         live = 0
         for group in self.param_groups:
             lists = None
@@ -123,14 +132,15 @@ class FusedAdam(torch.optim.Optimizer):
                     if g.is_sparse:
                         raise RuntimeError("FusedAdam does not support sparse gradients")
                     if t.device.type != "cpu":  # a step tensor moved off the host (not torch's default)
-                        t += 1
-                        step = t.item()
+                        step = t.item() + 1.0
                         e = None
                     else:  # CPU float32 0-d tensor, as torch's Adam keeps it
                         e = cache[id(t)] = [t, t.numpy(), t.item()]
                 if e is not None:
-                    step = e[2] = e[2] + 1.0
-                    e[1][()] = step
+                    step = e[2] + 1.0
+                # the counts advance only once every update below has been accepted (a rejected tensor
+                # leaves every step count as it was)
+                pending.append((e, t, step))
                 if lists is None:
                     key = (beta1, beta2, group["eps"])
                     lists = by_hyper.get(key)
@@ -152,6 +162,12 @@ class FusedAdam(torch.optim.Optimizer):
                 del cache[k]
         for (beta1, beta2, eps), (ps, gs, ms, vs, ss, bs) in by_hyper.items():
             _C.adam_step(ps, gs, ms, vs, ss, bs, beta1, beta2, eps)
+        for e, t, step in pending:
+            if e is None:
+                t.fill_(step)
+            else:
+                e[2] = step
+                e[1][()] = step
         return loss
 
 

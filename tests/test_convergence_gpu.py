@@ -25,7 +25,7 @@ grid gradients of both are summed with float atomics).  Measured over seeds at K
 (tools/probes/conv_diag.py, conv_ablate.py); at 300 + 300 iterations without densification the two
 runs already differ by ~0.1 dB.  Hence two tests:
   * short horizon (no densification, 200 + 200 iterations, 6 seeds): the formulations' mean held-out
-    PSNR within 0.1 dB, each seed's two runs within 0.25 dB (single seeds measured 0.02-0.16 dB apart,
+    PSNR within 0.1 dB, each seed's two runs within 0.2 dB (single seeds measured 0.02-0.16 dB apart,
     so one pair, or the mean of three, sits at the noise of a 0.1 dB bar) and their last-50-iteration
     mean losses within 1 %;
   * long horizon (the full miniature schedule, 5 seeds each): every run converges (above RUN_FLOOR and
@@ -53,7 +53,8 @@ PSNR_GAIN = 15.0      # dB over the initial random point cloud (8.5-8.7 dB)
 PSNR_DELTA = 1.0      # dB between the medians of the fused and the unfused runs
 SEEDS = 5
 SHORT_DELTA = 0.1     # dB between the two formulations' mean short-horizon PSNR over SHORT_SEEDS seeds
-SHORT_RUN_DELTA = 0.25  # dB between the two runs of any one seed (measured up to 0.104 on one seed)
+SHORT_RUN_DELTA = 0.2   # dB between the two runs of any one seed (per-seed gaps measured 0.02-0.16 dB over the
+                        # round-4 6-seed runs; the 6-seed mean bar SHORT_DELTA holds the formulations together)
 SHORT_SEEDS = 6
 
 

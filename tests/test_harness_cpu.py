@@ -328,6 +328,44 @@ def test_fused_adam_host_step_counts(monkeypatch):
     assert check(1)
 
 
+def test_fused_adam_rejected_update_keeps_step_counts_and_frees_without_gc(monkeypatch):
+    """A launch the extension rejects (a wrong dtype, size or device) leaves every step count as it was, so the
+    bias corrections of the next accepted step are those of the right step; and an optimizer holds no reference
+    to itself, so dropping the last reference frees it (and its moment buffers) without the cyclic GC."""
+    import gc
+    import weakref
+    from gs4d_train import kernels as K
+    calls = []
+
+    def adam_step(*a):
+        if any(p.numel() == 5 for p in a[0]):
+            raise RuntimeError("adam_step: rejected")
+        calls.append(a)
+    monkeypatch.setattr(K, "_C", type("Fake", (), {"adam_step": staticmethod(adam_step)}))
+    ps = [torch.nn.Parameter(torch.randn(4)) for _ in range(2)]
+    for p in ps:
+        p.grad = torch.randn(4)
+    opt = K.FusedAdam([{"params": ps, "lr": 0.1}])
+    opt.step()
+    bad = torch.nn.Parameter(torch.randn(5))
+    bad.grad = torch.randn(5)
+    opt.param_groups[0]["params"].append(bad)
+    with pytest.raises(RuntimeError):
+        opt.step()
+    assert [float(opt.state[p]["step"]) for p in ps] == [1.0, 1.0]
+    opt.param_groups[0]["params"].pop()
+    opt.step()
+    assert [float(opt.state[p]["step"]) for p in ps] == [2.0, 2.0]
+    assert abs(calls[-1][4][0] + 0.1 / (1 - 0.9 ** 2)) < 1e-12
+    gc.disable()
+    try:
+        ref = weakref.ref(opt)
+        del opt
+        assert ref() is None, "FusedAdam must be freed by reference counting alone"
+    finally:
+        gc.enable()
+
+
 def test_fused_adam_hooks_and_profiler_take_the_wrapped_step(monkeypatch):
     """FusedAdam's instance step skips torch's profiler/hook wrapper only while nothing is registered: step
     pre/post hooks (per optimizer and global) still fire, a profiler still sees the "Optimizer.step#..." range,

@@ -324,7 +324,8 @@ def test_mlp_gemms_match_fp64(P, N, K, col0):
     """The deformation MLP's GPU GEMMs on rocBLAS (deformation._splitk_dw: split-K chunk partials + their
     remainder + gs4d_sum_slices; deformation._mm_dx: dy @ W) vs fp64 torch, to 1e-5 of each result's largest
     |term| sum; P a multiple of the 1024-row chunk and not, x a column block of a wider matrix (col0 > 0),
-    W 64/128/256.  Also the library-choice fallback (solution 0) of gemm_f32 and gs4d_sum_slices' scalar form."""
+    W 64/128/256.  The tuned kernel of each shape class is the one that runs (gemm_tuned), rocBLAS's own
+    pick (tune=False) computes the same product, and gs4d_sum_slices' scalar form."""
     from gs4d_train import _C, deformation as D
     torch.manual_seed(P + N)
     dy = torch.randn(P, N, device="cuda")
@@ -339,23 +340,34 @@ def test_mlp_gemms_match_fp64(P, N, K, col0):
     dx = D._mm_dx(dy, w)
     refx = dy.double() @ w.double()
     assert dx.shape == (P, K)
-    if (N, K) == (640, 128) and col0 == 0:
-        # the tuned kernels (TunableOp solution indices) are the ones that run at the train step's shapes
-        from gs4d_train import _C
-        o = torch.empty(P, K, device="cuda")
-        assert _C.gemm_f32(w, dy, o, False, False, K, P, N, K, N, K, 1, 0, 0, 0, D._SOL_DX) is True
+    assert float(((dx.double() - refx).abs() - 1e-5 * (dy.double().abs() @ w.double().abs())).max()) <= 0
+    # the kernel chosen for a shape class (gemm_f32 tune=True) is the one that runs at the train step's shapes:
+    # a second call reports the cached choice, and every tuned class has a record (no rejected index)
+    o = torch.empty(P, K, device="cuda")
+    sol = _C.gemm_f32(w, dy, o, False, False, K, P, N, K, N, K, 1, 0, 0, 0, True)
+    tuned = {k: v for k, v, *_ in _C.gemm_tuned()}
+    def bucket(v):  # train_glue.cpp dim_bucket: sizes above 4096 by 1/8-octave classes
+        if v <= 4096:
+            return v
+        step = 1 << (v.bit_length() - 4)
+        return -(-v // step) * step
+    key = f"f32 nn m={K} n={bucket(P)} k={N} lda={K} ldb={N} ldc={K} batch=1 dev={o.device.index}"
+    assert tuned.get(key) == sol, (key, sol, tuned)
+    assert float(((o.double() - refx).abs() - 1e-5 * (dy.double().abs() @ w.double().abs())).max()) <= 0
+    if P >= 4096:
         S = P // 1024
         parts = torch.empty(S, N, K, device="cuda")
-        assert _C.gemm_f32(x, dy, parts, False, True, K, N, 1024, x.stride(0), N, K, S, 1024 * x.stride(0),
-                           1024 * N, N * K, D._SOL_DW_BATCHED) is True
-    assert float(((dx.double() - refx).abs() - 1e-5 * (dy.double().abs() @ w.double().abs())).max()) <= 0
+        sol_b = _C.gemm_f32(x, dy, parts, False, True, K, N, 1024, x.stride(0), N, K, S, 1024 * x.stride(0),
+                            1024 * N, N * K, True)
+        tuned = {k: v for k, v, *_ in _C.gemm_tuned()}
+        assert any(v == sol_b and f"batch={S} " in k for k, v in tuned.items()), (sol_b, tuned)
     # the library's own kernel (solution 0) computes the same product
     out = torch.empty(P, K, device="cuda")
-    assert _C.gemm_f32(w, dy, out, False, False, K, P, N, K, N, K, 1, 0, 0, 0, 0) is False
+    assert _C.gemm_f32(w, dy, out, False, False, K, P, N, K, N, K, 1, 0, 0, 0, False) == 0
     assert float(((out.double() - refx).abs() - 1e-5 * (dy.double().abs() @ w.double().abs())).max()) <= 0
     # an operand that does not fit its tensor is refused before any launch
     with pytest.raises(RuntimeError):
-        _C.gemm_f32(w, dy, out, False, False, K, P + 1, N, K, N, K, 1, 0, 0, 0, 0)
+        _C.gemm_f32(w, dy, out, False, False, K, P + 1, N, K, N, K, 1, 0, 0, 0, True)
     parts = torch.randn(5, 7, 3, device="cuda")  # n = 21: the scalar form
     assert torch.equal(_C.sum_slices(parts), (((parts[0] + parts[1]) + parts[2]) + parts[3]) + parts[4])
 
