@@ -214,6 +214,15 @@ int gs4d_last_timings(const char **names, float *ms, int max_entries) {
     return n;
 }
 
+int gs4d_debug_pair_alpha(int P, int width, int height, const char *geometry_buffer, int n, const int *gid,
+                          const int *px, const int *py, float *og, float *pw, void *stream_) {
+    if (P <= 0 || width <= 0 || height <= 0 || n < 0 || !geometry_buffer || (n > 0 && (!gid || !px || !py || !og || !pw)))
+        return fail(GS4D_ERR_ARG, "debug_pair_alpha: bad args");
+    const int T = ((width + kBlockX - 1) / kBlockX) * ((height + kBlockY - 1) / kBlockY);
+    GeomState g = GeomState::carve(const_cast<char *>(geometry_buffer), P, T);
+    GS4D_HIP(launch_pair_alpha(g, n, gid, px, py, og, pw, (hipStream_t)stream_));
+    return GS4D_OK;
+}
 int gs4d_mark_visible_ex(int P, const float *means3D, const float *viewmatrix, const float *projmatrix,
                          uint8_t *present, void *stream_, int view_transposed) {
     hipStream_t stream = (hipStream_t)stream_;

@@ -196,6 +196,8 @@ hipError_t launch_binning(const Args &a, GeomState g, const int *radii, BinningS
                           hipStream_t s);
 hipError_t launch_render_forward(const Args &a, GeomState g, BinningState b, ImageState img, float *out_color,
                                  float *out_depth, hipStream_t s);  // also sorts runs <= kWaveSortMax
+hipError_t launch_pair_alpha(GeomState g, int n, const int *gid, const int *px, const int *py, float *og, float *pw,
+                             hipStream_t s);
 hipError_t launch_render_backward(const Args &a, GeomState g, const uint32_t *gid_by_e, const uint32_t *upos, ImageState img,
                                   const float *colors, const float *dL_dpix, float *contrib, hipStream_t s);
 size_t contrib_scratch_bytes(int R, int P);

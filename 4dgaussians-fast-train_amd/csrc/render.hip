@@ -431,6 +431,33 @@ hipError_t launch_render_forward(const Args &a, GeomState g, BinningState b, Ima
     return hipGetLastError();
 }
 
+// Diagnostic (test infrastructure's view of the blend arithmetic): o G and the base-2 exponent of given
+// (Gaussian, pixel) pairs, by the exact sequence both blend kernels evaluate (read_raw_lds's row shift,
+// falloff()), so the parity tests can measure how far the blend's alpha lies from the oracle's near the
+// 1/255 threshold and size the near-threshold band from that measurement.
+__global__ void pair_alpha_kernel(const float4 *__restrict__ splat, int n, const int *__restrict__ gid,
+                                  const int *__restrict__ px, const int *__restrict__ py, float *__restrict__ og,
+                                  float *__restrict__ pw) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float4 *rec = splat + 3 * (size_t)gid[i];
+    const float4 s0 = rec[0], s1 = rec[1];
+    const int ty = py[i] / kBlockY;
+    const float yc = (float)(ty * kBlockY) + 7.5f;
+    const float yl = (float)(py[i] - ty * kBlockY) - 7.5f;
+    const float4 geo = make_float4(s0.x, s0.y - yc, s0.z, s0.w);
+    const float4 opc = make_float4(s1.x, s1.y, s1.z, 0.f);
+    const float dx = geo.x - (float)px[i];
+    const Falloff f = falloff<false>(geo, opc, geo.z * dx * dx, geo.w * dx, f2{yl, yl});
+    og[i] = f.alpha.x;
+    pw[i] = f.pw.x;
+}
+hipError_t launch_pair_alpha(GeomState g, int n, const int *gid, const int *px, const int *py, float *og, float *pw,
+                             hipStream_t s) {
+    if (n > 0) hipLaunchKernelGGL(pair_alpha_kernel, dim3((n + 255) / 256), dim3(256), 0, s, g.splat, n, gid, px, py, og, pw);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------------------------
 // lanes 0-31 of the result hold a's half-wave sums, lanes 32-63 b's (v_permlane32_swap)
 __device__ __forceinline__ float swap32_add(float a, float b) {

@@ -201,8 +201,31 @@ static std::vector<std::tuple<std::string, float>> last_timings() {
 }
 
 // ext.cpp:15-18 plus three introspection helpers used by bench.py
+// parity-test diagnostic: (o G, log2 G) of (Gaussian, pixel) pairs by the blend kernels' arithmetic
+std::tuple<torch::Tensor, torch::Tensor> DebugPairAlpha(const torch::Tensor &geomBuffer, int P, int W, int H,
+                                                        const torch::Tensor &gid_, const torch::Tensor &px_,
+                                                        const torch::Tensor &py_) {
+    TORCH_CHECK(geomBuffer.is_cuda() && gid_.is_cuda(), "debug_pair_alpha: device tensors");
+    const c10::hip::HIPGuard guard(geomBuffer.device().index());
+    auto gid = gid_.to(torch::kInt32).contiguous(), px = px_.to(torch::kInt32).contiguous(),
+         py = py_.to(torch::kInt32).contiguous();
+    TORCH_CHECK(gid.numel() == px.numel() && gid.numel() == py.numel(), "debug_pair_alpha: pair arrays differ");
+    TORCH_CHECK(gid.numel() == 0 || (gid.min().item<int>() >= 0 && gid.max().item<int>() < P &&
+                                     px.min().item<int>() >= 0 && py.min().item<int>() >= 0),
+                "debug_pair_alpha: pair out of range");
+    auto og = torch::empty({gid.numel()}, geomBuffer.options().dtype(torch::kFloat32));
+    auto pw = torch::empty_like(og);
+    const int st = gs4d_debug_pair_alpha(P, W, H, (const char *)geomBuffer.data_ptr(), (int)gid.numel(),
+                                         gid.data_ptr<int>(), px.data_ptr<int>(), py.data_ptr<int>(),
+                                         og.data_ptr<float>(), pw.data_ptr<float>(),
+                                         c10::hip::getCurrentHIPStream(geomBuffer.device().index()).stream());
+    TORCH_CHECK(st == 0, "debug_pair_alpha: ", gs4d_last_error());
+    return {og, pw};
+}
+
 PYBIND11_MODULE(_C, m) {
     m.def("rasterize_gaussians", &RasterizeGaussians);
+    m.def("debug_pair_alpha", &DebugPairAlpha);
     m.def("rasterize_gaussians_backward", &RasterizeGaussiansBackward);
     m.def("mark_visible", &MarkVisible);
     m.def("set_profiling", [](int level) { gs4d_set_profiling(level); });

@@ -111,6 +111,13 @@ int gs4d_backward_ex(int P, int D, int M, int R, const float *background, int wi
 int gs4d_knn_mean_dist(int P, const float *points, float *mean_dists, gs4d_alloc_fn scratch_alloc, void *scratch_ctx,
                        void *stream);
 
+/* Diagnostic for the parity tests (no reference counterpart): for n (Gaussian, pixel) pairs, o G (the
+ * blend's alpha before the 0.99 cap) and the base-2 exponent log2(G), evaluated by the exact arithmetic
+ * of the blend kernels from the packed splat records a gs4d_forward left in geometry_buffer (P Gaussians,
+ * a width x height image).  gid/px/py: n int32 device arrays; og/pw: n fp32 device outputs. */
+int gs4d_debug_pair_alpha(int P, int width, int height, const char *geometry_buffer, int n, const int *gid,
+                          const int *px, const int *py, float *og, float *pw, void *stream);
+
 /* Human-readable message for the last error on this thread (never NULL). */
 const char *gs4d_last_error(void);
 

@@ -612,6 +612,70 @@ static void cov3d_backward(int idx, const float *scale, float mod, const float *
     dL_drots[4 * idx + 0] = q0; dL_drots[4 * idx + 1] = q1; dL_drots[4 * idx + 2] = q2; dL_drots[4 * idx + 3] = q3;
 }
 
+/* One pixel of K7 (renderCUDA backward, backward.cu:399-557): the reverse walk over the tile list
+ * [rs, re) from T_final / last_contributor, adding each pair's 9 terms (dL_dmean2D x/y, dL_dconic
+ * x/y/w, dL_dopacity, dL_dcolor rgb) in double to cb[(k - cb_off) * 9 + q].  flip_kind 1 inverts the
+ * alpha test (backward.cu:486-490) of list position flip_k: the walk the near-threshold bounds replay
+ * for a blend that took the other side of 1/255 (termination is not tested by the backward; its flip
+ * enters through T_final and last_contributor). */
+#define NO_FLIP 0xffffffffu
+static void pixel_backward(const gs4d_oracle_state *s, const float *color_ptr, const float *background,
+                           const float *dL_dpixel, uint32_t rs, uint32_t re, float pfx, float pfy, float T_final,
+                           uint32_t last_contributor, uint32_t flip_k, int flip_kind, double *cb_base, uint32_t cb_off) {
+    const float ddelx_dx = 0.5f * s->W, ddely_dy = 0.5f * s->H; /* backward.cu:460-461 (0.5 * W is exact) */
+    float Tr = T_final;
+    float accum_rec[NCH] = {0, 0, 0}, last_color[NCH] = {0, 0, 0};
+    float last_alpha = 0;
+    float bg_dot_dpixel = 0;
+    for (int i = 0; i < NCH; i++) bg_dot_dpixel += background[i] * dL_dpixel[i];
+    for (uint32_t k = re; k-- > rs;) {
+        const uint32_t contributor = k - rs; /* 0-based position in the tile list */
+        if (contributor >= last_contributor) continue;
+        const uint32_t g = s->point_list[k];
+        const float dx = s->means2D[2 * g] - pfx, dy = s->means2D[2 * g + 1] - pfy;
+        const float *co = s->conic_opacity + 4 * (size_t)g;
+        const float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+        if (power > 0.0f) continue;
+        const float G = expf(power);
+        const float alpha = fminf_(0.99f, co[3] * G);
+        int pass = alpha >= 1.0f / 255.0f;
+        if (k == flip_k && flip_kind == 1) pass = !pass;
+        if (!pass) continue;
+        Tr = Tr / (1.f - alpha);
+        const float dchannel_dcolor = alpha * Tr;
+        float dL_dalpha = 0.0f;
+        double *cb = cb_base + (size_t)(k - cb_off) * 9;
+        for (int ch = 0; ch < NCH; ch++) {
+            const float c = color_ptr[(size_t)g * NCH + ch];
+            accum_rec[ch] = last_alpha * last_color[ch] + (1.f - last_alpha) * accum_rec[ch];
+            last_color[ch] = c;
+            const float dL_dchannel = dL_dpixel[ch];
+            dL_dalpha += (c - accum_rec[ch]) * dL_dchannel;
+            cb[6 + ch] += (double)(dchannel_dcolor * dL_dchannel);
+        }
+        dL_dalpha *= Tr;
+        last_alpha = alpha;
+        dL_dalpha += (-T_final / (1.f - alpha)) * bg_dot_dpixel;
+        const float dL_dG = co[3] * dL_dalpha;
+        const float gdx = G * dx, gdy = G * dy;
+        const float dG_ddelx = -gdx * co[0] - gdy * co[1];
+        const float dG_ddely = -gdy * co[2] - gdx * co[1];
+        cb[0] += (double)(dL_dG * dG_ddelx * ddelx_dx);
+        cb[1] += (double)(dL_dG * dG_ddely * ddely_dy);
+        cb[2] += (double)(-0.5f * gdx * dx * dL_dG);
+        cb[3] += (double)(-0.5f * gdx * dy * dL_dG);
+        cb[4] += (double)(-0.5f * gdy * dy * dL_dG);
+        cb[5] += (double)(G * dL_dalpha);
+    }
+}
+
+void gs4d_oracle_backward_tail(const gs4d_oracle_state *s, const float *means3D, const float *shs, const float *scales,
+                               float scale_modifier, const float *rotations, const float *cov3D_precomp,
+                               const float *viewmatrix, const float *projmatrix, const float *campos, float tan_fovx,
+                               float tan_fovy, const int *radii_in, const float *dL_dmean2D, const float *dL_dconic,
+                               const float *dL_dcolor, float *dL_dmean3D, float *dL_dcov3D, float *dL_dsh,
+                               float *dL_dscale, float *dL_drot);
+
 /* Rasterizer::backward (rasterizer_impl.cu:343-437).  Output arrays must be zero-initialised by
  * the caller, exactly like RasterizeGaussiansBackwardCUDA (rasterize_points.cu:153-161).
  * Layouts: dL_dmean2D (P,3), dL_dconic (P,4), dL_dopacity (P), dL_dcolor (P,3), dL_dmean3D (P,3),
@@ -623,11 +687,8 @@ void gs4d_oracle_backward(const gs4d_oracle_state *s, const float *background, c
                           const int *radii_in, const float *dL_dpix, float *dL_dmean2D, float *dL_dconic,
                           float *dL_dopacity, float *dL_dcolor, float *dL_dmean3D, float *dL_dcov3D, float *dL_dsh,
                           float *dL_dscale, float *dL_drot) {
-    const int P = s->P, D = s->D, M = s->M, W = s->W, H = s->H, gx = s->gx, gy = s->gy, L = s->L;
+    const int P = s->P, W = s->W, H = s->H, gx = s->gx, gy = s->gy, L = s->L;
     const int T = gx * gy;
-    const int *radii = radii_in ? radii_in : s->radii;
-    const float focal_y = H / (2.0f * tan_fovy);
-    const float focal_x = W / (2.0f * tan_fovx);
     const float *color_ptr = colors_precomp ? colors_precomp : s->rgb;
 
     /* K7: renderCUDA backward (backward.cu:399-557).  Each (tile, Gaussian) pair's contributions
@@ -639,58 +700,15 @@ void gs4d_oracle_backward(const gs4d_oracle_state *s, const float *background, c
         const int bx = tile % gx, by = tile / gx;
         const uint32_t rs = s->ranges[2 * tile], re = s->ranges[2 * tile + 1];
         if (re <= rs) continue;
-        const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H; /* backward.cu:460-461 (double lits in ref: 0.5 * W is exact) */
         for (int ty = 0; ty < BLOCK_Y; ty++)
             for (int tx = 0; tx < BLOCK_X; tx++) {
                 const int pxi = bx * BLOCK_X + tx, pyi = by * BLOCK_Y + ty;
                 if (!(pxi < W && pyi < H)) continue;
                 const size_t pix = (size_t)W * pyi + pxi;
-                const float pfx = (float)pxi, pfy = (float)pyi;
-                const float T_final = s->final_T[pix];
-                float Tr = T_final;
-                const uint32_t last_contributor = s->n_contrib[pix];
-                float accum_rec[NCH] = {0, 0, 0}, dL_dpixel[NCH], last_color[NCH] = {0, 0, 0};
-                float last_alpha = 0;
+                float dL_dpixel[NCH];
                 for (int i = 0; i < NCH; i++) dL_dpixel[i] = dL_dpix[(size_t)i * H * W + pix];
-                float bg_dot_dpixel = 0;
-                for (int i = 0; i < NCH; i++) bg_dot_dpixel += background[i] * dL_dpixel[i];
-                for (uint32_t k = re; k-- > rs;) {
-                    const uint32_t contributor = k - rs; /* 0-based position in the tile list */
-                    if (contributor >= last_contributor) continue;
-                    const uint32_t g = s->point_list[k];
-                    const float dx = s->means2D[2 * g] - pfx, dy = s->means2D[2 * g + 1] - pfy;
-                    const float *co = s->conic_opacity + 4 * (size_t)g;
-                    const float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
-                    if (power > 0.0f) continue;
-                    const float G = expf(power);
-                    const float alpha = fminf_(0.99f, co[3] * G);
-                    if (alpha < 1.0f / 255.0f) continue;
-                    Tr = Tr / (1.f - alpha);
-                    const float dchannel_dcolor = alpha * Tr;
-                    float dL_dalpha = 0.0f;
-                    double *cb = contrib + (size_t)k * NG;
-                    for (int ch = 0; ch < NCH; ch++) {
-                        const float c = color_ptr[(size_t)g * NCH + ch];
-                        accum_rec[ch] = last_alpha * last_color[ch] + (1.f - last_alpha) * accum_rec[ch];
-                        last_color[ch] = c;
-                        const float dL_dchannel = dL_dpixel[ch];
-                        dL_dalpha += (c - accum_rec[ch]) * dL_dchannel;
-                        cb[6 + ch] += (double)(dchannel_dcolor * dL_dchannel);
-                    }
-                    dL_dalpha *= Tr;
-                    last_alpha = alpha;
-                    dL_dalpha += (-T_final / (1.f - alpha)) * bg_dot_dpixel;
-                    const float dL_dG = co[3] * dL_dalpha;
-                    const float gdx = G * dx, gdy = G * dy;
-                    const float dG_ddelx = -gdx * co[0] - gdy * co[1];
-                    const float dG_ddely = -gdy * co[2] - gdx * co[1];
-                    cb[0] += (double)(dL_dG * dG_ddelx * ddelx_dx);
-                    cb[1] += (double)(dL_dG * dG_ddely * ddely_dy);
-                    cb[2] += (double)(-0.5f * gdx * dx * dL_dG);
-                    cb[3] += (double)(-0.5f * gdx * dy * dL_dG);
-                    cb[4] += (double)(-0.5f * gdy * dy * dL_dG);
-                    cb[5] += (double)(G * dL_dalpha);
-                }
+                pixel_backward(s, color_ptr, background, dL_dpixel, rs, re, (float)pxi, (float)pyi, s->final_T[pix],
+                               s->n_contrib[pix], NO_FLIP, 0, contrib, 0);
             }
     }
     /* per-Gaussian reduction in unsorted-instance order (deterministic) */
@@ -716,6 +734,26 @@ void gs4d_oracle_backward(const gs4d_oracle_state *s, const float *background, c
     free(inv);
     free(contrib);
 
+    gs4d_oracle_backward_tail(s, means3D, shs, scales, scale_modifier, rotations, cov3D_precomp, viewmatrix,
+                              projmatrix, campos, tan_fovx, tan_fovy, radii_in, dL_dmean2D, dL_dconic, dL_dcolor,
+                              dL_dmean3D, dL_dcov3D, dL_dsh, dL_dscale, dL_drot);
+}
+
+/* K8 (computeCov2DCUDA, backward.cu:144-274) + K9 (preprocessCUDA backward, backward.cu:346-396) of every
+ * Gaussian from its K7 totals dL_dmean2D (P,3), dL_dconic (P,4) and dL_dcolor (P,3) (dL_dopacity is final
+ * after K7).  Outputs as gs4d_oracle_backward's, zero-initialised by the caller.  Linear in the K7 totals
+ * for a fixed forward state, which the near-threshold bounds use to carry the K7 terms' intervals to the
+ * final gradients. */
+void gs4d_oracle_backward_tail(const gs4d_oracle_state *s, const float *means3D, const float *shs, const float *scales,
+                               float scale_modifier, const float *rotations, const float *cov3D_precomp,
+                               const float *viewmatrix, const float *projmatrix, const float *campos, float tan_fovx,
+                               float tan_fovy, const int *radii_in, const float *dL_dmean2D, const float *dL_dconic,
+                               const float *dL_dcolor, float *dL_dmean3D, float *dL_dcov3D, float *dL_dsh,
+                               float *dL_dscale, float *dL_drot) {
+    const int P = s->P, D = s->D, M = s->M, W = s->W, H = s->H;
+    const int *radii = radii_in ? radii_in : s->radii;
+    const float focal_y = H / (2.0f * tan_fovy);
+    const float focal_x = W / (2.0f * tan_fovx);
     const float *cov3Ds = cov3D_precomp ? cov3D_precomp : s->cov3D;
     /* K8: computeCov2DCUDA (backward.cu:144-274) */
 #pragma omp parallel for schedule(static)
@@ -843,4 +881,220 @@ void gs4d_oracle_state_export(const gs4d_oracle_state *s, float *depths, float *
 void gs4d_oracle_sh_forward(int P, int D, int M, const float *means, const float *campos, const float *shs,
                             float *rgb_out, uint8_t *clamped_out) {
     for (int i = 0; i < P; i++) sh_forward(i, D, M, means, campos, shs, clamped_out, rgb_out + 3 * (size_t)i);
+}
+
+/* ---------------------------------------------------------------------------------------------- */
+/* Near-threshold bounds for the parity tests.
+ *
+ * The blend's two discrete decisions, alpha >= 1/255 (forward.cu:346-348, backward.cu:486-490) and
+ * T(1 - alpha) >= 1e-4 (forward.cu:350-354), can go either way between two correct float
+ * implementations when their operand lies within rounding of the threshold.  For every pixel this
+ * replays the forward walk, finds those decisions (|255 alpha - 1| <= band_alpha before the pixel's
+ * termination; |T(1 - alpha) / 1e-4 - 1| <= band_T for a splat that passed the alpha test), and for EACH
+ * of them replays the pixel's forward and backward with that one decision taken the other way.  The
+ * differences bound what a flip can change:
+ *   pix_rad[p]      sum over the pixel's near decisions of max_ch |colour(flipped) - colour(oracle)|
+ *   depth_rad[p]    the same for the depth
+ *   rad9[g * 9 + q] sum over all near decisions of all pixels of |term_q(flipped) - term_q(oracle)| of
+ *                   Gaussian g's K7 totals (q: dL_dmean2D x/y, dL_dconic x/y/w, dL_dopacity, dL_dcolor
+ *                   rgb), i.e. the flipping splat's own term and the T / accum_rec changes it causes in
+ *                   every other splat of the pixel
+ * pix_flag / gauss_flag: bit 0 = a near-1/255 decision (at the pixel / of the Gaussian), bit 1 = a
+ * near-termination one.  Several near decisions of one pixel are bounded by the sum of their single
+ * flips (their joint effect differs from that sum only at second order).  rad9 is linear-mapped to the
+ * final gradients by the caller (gs4d_oracle_backward_tail is linear in the K7 totals).
+ * Returns the number of flagged pixels. */
+typedef struct {
+    float T;
+    uint32_t n_contrib;
+    float C[NCH];
+    float D;
+} pixwalk_t;
+
+/* forward.cu:309-367 for one pixel, with the decision of list position flip_k inverted (flip_kind 1:
+ * the alpha test, 2: the termination test) */
+static void pixel_forward(const gs4d_oracle_state *s, const float *features, uint32_t rs, uint32_t re, float pfx,
+                          float pfy, uint32_t flip_k, int flip_kind, pixwalk_t *o) {
+    float Tr = 1.0f, C[NCH] = {0, 0, 0}, Dp = 0;
+    uint32_t contributor = 0, last_contributor = 0;
+    for (uint32_t k = rs; k < re; k++) {
+        contributor++;
+        const uint32_t g = s->point_list[k];
+        const float dx = s->means2D[2 * g] - pfx, dy = s->means2D[2 * g + 1] - pfy;
+        const float *co = s->conic_opacity + 4 * (size_t)g;
+        float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+        if (power > 0.0f) continue;
+        float alpha = fminf_(0.99f, co[3] * expf(power));
+        int pass = alpha >= 1.0f / 255.0f;
+        if (k == flip_k && flip_kind == 1) pass = !pass;
+        if (!pass) continue;
+        float test_T = Tr * (1 - alpha);
+        int term = test_T < 0.0001f;
+        if (k == flip_k && flip_kind == 2) term = !term;
+        if (term) break;
+        for (int ch = 0; ch < NCH; ch++) C[ch] += features[(size_t)g * NCH + ch] * alpha * Tr;
+        Dp += s->depths[g] * alpha * Tr;
+        Tr = test_T;
+        last_contributor = contributor;
+    }
+    o->T = Tr;
+    o->n_contrib = last_contributor;
+    for (int ch = 0; ch < NCH; ch++) o->C[ch] = C[ch];
+    o->D = Dp;
+}
+
+int gs4d_oracle_flip_bounds(const gs4d_oracle_state *s, const float *background, const float *colors_precomp,
+                            const float *dL_dpix, float band_alpha, float band_T, uint8_t *pix_flag,
+                            uint8_t *gauss_flag, float *pix_rad, float *depth_rad, double *rad9) {
+    const int W = s->W, H = s->H, gx = s->gx, T = s->gx * s->gy;
+    const float *features = colors_precomp ? colors_precomp : s->rgb;
+    const float a_thr = 1.0f / 255.0f;
+    int nflag = 0;
+    memset(gauss_flag, 0, (size_t)(s->P > 0 ? s->P : 0));
+    memset(rad9, 0, sizeof(double) * 9 * (size_t)(s->P > 0 ? s->P : 0));
+    memset(pix_rad, 0, sizeof(float) * (size_t)W * H);
+    memset(depth_rad, 0, sizeof(float) * (size_t)W * H);
+    memset(pix_flag, 0, (size_t)W * H);
+#pragma omp parallel for schedule(dynamic, 1) reduction(+ : nflag)
+    for (int tile = 0; tile < T; tile++) {
+        const int bx = tile % gx, by = tile / gx;
+        const uint32_t rs = s->ranges[2 * tile], re = s->ranges[2 * tile + 1];
+        if (re <= rs) continue;
+        const size_t n = re - rs;
+        double *ref9 = NULL, *alt9 = NULL;
+        uint32_t *near_k = NULL;
+        uint8_t *near_kind = NULL;
+        size_t near_cap = 0;
+        for (int ty = 0; ty < BLOCK_Y; ty++)
+            for (int tx = 0; tx < BLOCK_X; tx++) {
+                const int pxi = bx * BLOCK_X + tx, pyi = by * BLOCK_Y + ty;
+                if (!(pxi < W && pyi < H)) continue;
+                const float pfx = (float)pxi, pfy = (float)pyi;
+                const size_t pix = (size_t)W * pyi + pxi;
+                /* the near decisions of the oracle's own walk (as gs4d_oracle_flip_flags finds them) */
+                size_t nn = 0;
+                float Tr = 1.0f;
+                uint8_t f = 0;
+                for (uint32_t k = rs; k < re; k++) {
+                    const uint32_t g = s->point_list[k];
+                    const float dx = s->means2D[2 * g] - pfx, dy = s->means2D[2 * g + 1] - pfy;
+                    const float *co = s->conic_opacity + 4 * (size_t)g;
+                    float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+                    if (power > 0.0f) continue;
+                    float alpha = fminf_(0.99f, co[3] * expf(power));
+                    int kinds = 0;
+                    if (fabsf(alpha * 255.0f - 1.0f) <= band_alpha) kinds |= 1;
+                    float test_T = Tr * (1 - alpha);
+                    if (alpha >= a_thr && fabsf(test_T * 1e4f - 1.0f) <= band_T) kinds |= 2;
+                    for (int kind = 1; kind <= 2; kind++) {
+                        if (!(kinds & kind)) continue;
+                        if (nn == near_cap) {
+                            near_cap = near_cap ? 2 * near_cap : 16;
+                            near_k = (uint32_t *)realloc(near_k, 4 * near_cap);
+                            near_kind = (uint8_t *)realloc(near_kind, near_cap);
+                        }
+                        near_k[nn] = k;
+                        near_kind[nn] = (uint8_t)kind;
+                        nn++;
+                        f |= (uint8_t)kind;
+                        __atomic_fetch_or(&gauss_flag[g], (uint8_t)kind, __ATOMIC_RELAXED);
+                    }
+                    if (alpha < a_thr) continue;
+                    if (test_T < 0.0001f) break;
+                    Tr = test_T;
+                }
+                pix_flag[pix] = f;
+                if (!nn) continue;
+                nflag++;
+                if (!ref9) {
+                    ref9 = (double *)malloc(sizeof(double) * 9 * n);
+                    alt9 = (double *)malloc(sizeof(double) * 9 * n);
+                }
+                float dL_dpixel[NCH];
+                for (int i = 0; i < NCH; i++) dL_dpixel[i] = dL_dpix[(size_t)i * H * W + pix];
+                pixwalk_t pr, pa;
+                pixel_forward(s, features, rs, re, pfx, pfy, NO_FLIP, 0, &pr);
+                memset(ref9, 0, sizeof(double) * 9 * n);
+                pixel_backward(s, features, background, dL_dpixel, rs, re, pfx, pfy, pr.T, pr.n_contrib, NO_FLIP, 0,
+                               ref9, rs);
+                float prad = 0, drad = 0;
+                for (size_t d = 0; d < nn; d++) {
+                    pixel_forward(s, features, rs, re, pfx, pfy, near_k[d], near_kind[d], &pa);
+                    memset(alt9, 0, sizeof(double) * 9 * n);
+                    pixel_backward(s, features, background, dL_dpixel, rs, re, pfx, pfy, pa.T, pa.n_contrib, near_k[d],
+                                   near_kind[d], alt9, rs);
+                    float cmax = 0;
+                    for (int ch = 0; ch < NCH; ch++) {
+                        const float a = pa.C[ch] + pa.T * background[ch], b = pr.C[ch] + pr.T * background[ch];
+                        cmax = fmaxf_(cmax, fabsf(a - b));
+                    }
+                    prad += cmax;
+                    drad += fabsf(pa.D - pr.D);
+                    for (size_t k = 0; k < n; k++) {
+                        const double *x = alt9 + 9 * k, *y = ref9 + 9 * k;
+                        const uint32_t g = s->point_list[rs + k];
+                        for (int q = 0; q < 9; q++) {
+                            const double dq = fabs(x[q] - y[q]);
+                            if (dq != 0.0) {
+#pragma omp atomic
+                                rad9[9 * (size_t)g + q] += dq;
+                            }
+                        }
+                    }
+                }
+                pix_rad[pix] = prad;
+                depth_rad[pix] = drad;
+            }
+        free(ref9);
+        free(alt9);
+        free(near_k);
+        free(near_kind);
+    }
+    return nflag;
+}
+
+/* The (Gaussian, pixel) pairs of the forward walks whose alpha lies within band of 1/255 (relative; before
+ * each pixel's termination): gid / px / py and the oracle's o G = co[3] * expf(power) (alpha before the
+ * 0.99 cap), for measuring the blend kernels' operand against it.  Writes at most max_n; returns the count
+ * found (which may exceed max_n). */
+int gs4d_oracle_near_pairs(const gs4d_oracle_state *s, float band, int max_n, int *gid, int *px, int *py, float *og) {
+    const int W = s->W, H = s->H, gx = s->gx, T = s->gx * s->gy;
+    int count = 0;
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int tile = 0; tile < T; tile++) {
+        const int bx = tile % gx, by = tile / gx;
+        const uint32_t rs = s->ranges[2 * tile], re = s->ranges[2 * tile + 1];
+        for (int ty = 0; ty < BLOCK_Y; ty++)
+            for (int tx = 0; tx < BLOCK_X; tx++) {
+                const int pxi = bx * BLOCK_X + tx, pyi = by * BLOCK_Y + ty;
+                if (!(pxi < W && pyi < H)) continue;
+                const float pfx = (float)pxi, pfy = (float)pyi;
+                float Tr = 1.0f;
+                for (uint32_t k = rs; k < re; k++) {
+                    const uint32_t g = s->point_list[k];
+                    const float dx = s->means2D[2 * g] - pfx, dy = s->means2D[2 * g + 1] - pfy;
+                    const float *co = s->conic_opacity + 4 * (size_t)g;
+                    float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+                    if (power > 0.0f) continue;
+                    const float o_g = co[3] * expf(power);
+                    float alpha = fminf_(0.99f, o_g);
+                    if (fabsf(alpha * 255.0f - 1.0f) <= band) {
+                        int i;
+#pragma omp atomic capture
+                        i = count++;
+                        if (i < max_n) {
+                            gid[i] = (int)g;
+                            px[i] = pxi;
+                            py[i] = pyi;
+                            og[i] = o_g;
+                        }
+                    }
+                    if (alpha < 1.0f / 255.0f) continue;
+                    float test_T = Tr * (1 - alpha);
+                    if (test_T < 0.0001f) break;
+                    Tr = test_T;
+                }
+            }
+    }
+    return count;
 }

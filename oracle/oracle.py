@@ -59,6 +59,15 @@ def _load():
     lib.gs4d_oracle_knn.argtypes = [ctypes.c_int, _f32p, _f32p]
     lib.gs4d_oracle_flip_flags.argtypes = [ctypes.c_void_p, ctypes.c_float, ctypes.c_float, _u8p, _u8p]
     lib.gs4d_oracle_flip_flags.restype = ctypes.c_int
+    lib.gs4d_oracle_flip_bounds.argtypes = [ctypes.c_void_p, _f32p, _f32p, _f32p, ctypes.c_float, ctypes.c_float, _u8p,
+                                            _u8p, _f32p, _f32p, ctypes.POINTER(ctypes.c_double)]
+    lib.gs4d_oracle_flip_bounds.restype = ctypes.c_int
+    lib.gs4d_oracle_near_pairs.argtypes = [ctypes.c_void_p, ctypes.c_float, ctypes.c_int, _i32p, _i32p, _i32p, _f32p]
+    lib.gs4d_oracle_near_pairs.restype = ctypes.c_int
+    lib.gs4d_oracle_backward_tail.restype = None
+    lib.gs4d_oracle_backward_tail.argtypes = [
+        ctypes.c_void_p, _f32p, _f32p, _f32p, ctypes.c_float, _f32p, _f32p, _f32p, _f32p, _f32p, ctypes.c_float,
+        ctypes.c_float, _i32p, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p]
     lib.gs4d_oracle_set_threads.argtypes = [ctypes.c_int]
     lib.gs4d_oracle_get_threads.restype = ctypes.c_int
     _lib = lib
@@ -194,6 +203,105 @@ def flip_flags(state, band_alpha, band_T):
         lib.gs4d_oracle_flip_flags(state.handle, float(band_alpha), float(band_T), pix.ctypes.data_as(_u8p),
                                    gau.ctypes.data_as(_u8p))
     return pix, gau[:state.P]
+
+
+def backward_tail(state, means3D, radii, scales, rotations, scale_modifier, cov3D_precomp, viewmatrix, projmatrix,
+                  tanfovx, tanfovy, sh, degree, campos, dL_dmean2D, dL_dconic, dL_dcolor):
+    """K8 + K9 (backward.cu:144-274, 346-396) from given K7 totals: dL_dmean2D (P,3), dL_dconic (P,4),
+    dL_dcolor (P,3) -> (dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations).  Linear in the totals."""
+    lib = _load()
+    means3D = np.ascontiguousarray(np.asarray(means3D, np.float32))
+    P = means3D.shape[0]
+    sh_a, sh_p = _arr(sh)
+    M = sh_a.shape[1] if sh_a is not None else 0
+    out = dict(m=np.zeros((P, 3), np.float32), c=np.zeros((P, 6), np.float32), sh=np.zeros((P, M, 3), np.float32),
+               s=np.zeros((P, 3), np.float32), r=np.zeros((P, 4), np.float32))
+    if P:
+        keep = [_arr(x) for x in (scales, rotations, cov3D_precomp, viewmatrix, projmatrix, campos, dL_dmean2D,
+                                  dL_dconic, dL_dcolor)]
+        (sc_a, sc_p), (ro_a, ro_p), (c3_a, c3_p), (vm_a, vm_p), (pm_a, pm_p), (cam_a, cam_p), (m2_a, m2_p), \
+            (cn_a, cn_p), (cl_a, cl_p) = keep
+        ra, rp = _arr(radii, np.int32)
+        q = lambda k: out[k].ctypes.data_as(_f32p)
+        lib.gs4d_oracle_backward_tail(state.handle, means3D.ctypes.data_as(_f32p), sh_p, sc_p, float(scale_modifier),
+                                      ro_p, c3_p, vm_p, pm_p, cam_p, float(tanfovx), float(tanfovy), rp, m2_p, cn_p,
+                                      cl_p, q("m"), q("c"), out["sh"].ctypes.data_as(_f32p) if M > 0 else None, q("s"),
+                                      q("r"))
+    return out["m"], out["c"], out["sh"], out["s"], out["r"]
+
+
+def flip_bounds(state, band_alpha, band_T, bg, means3D, radii, colors_precomp, scales, rotations, scale_modifier,
+                cov3D_precomp, viewmatrix, projmatrix, tanfovx, tanfovy, dL_dout_color, sh, degree, campos):
+    """Near-threshold flags AND bounds (gs4d_oracle_flip_bounds): every decision of the forward within
+    band_alpha of 1/255 or band_T of 1e-4 (relative) is replayed the other way, pixel by pixel, and the
+    differences it makes are summed.  The arguments after the bands are rasterize_backward's.  Returns a dict:
+      pflag (H, W) / gflag (P,)  bit 0 near-1/255, bit 1 near-termination (pixels; the Gaussians whose own
+                                 decision it is)
+      pix_rad, depth_rad (H, W)  bound on |colour| (max over channels) and |depth| changes at the pixel
+      grad_rad                   8-tuple aligned with rasterize_backward's outputs: per-element bounds on the
+                                 gradient changes, the K7 terms' bounds carried through the (linear) K8 + K9
+                                 by their absolute values (sum_j |M e_j| r_j >= |M r| for every r in the box)."""
+    lib = _load()
+    means3D = np.ascontiguousarray(np.asarray(means3D, np.float32))
+    P = means3D.shape[0]
+    H, W = state.H, state.W
+    pflag = np.zeros((H, W), np.uint8)
+    gflag = np.zeros(max(P, 1), np.uint8)
+    pix_rad = np.zeros((H, W), np.float32)
+    depth_rad = np.zeros((H, W), np.float32)
+    rad9 = np.zeros((max(P, 1), 9), np.float64)
+    if state is not None and state.handle:
+        bg_a, bg_p = _arr(bg)
+        cp_a, cp_p = _arr(colors_precomp)
+        dl_a, dl_p = _arr(dL_dout_color)
+        lib.gs4d_oracle_flip_bounds(state.handle, bg_p, cp_p, dl_p, float(band_alpha), float(band_T),
+                                    pflag.ctypes.data_as(_u8p), gflag.ctypes.data_as(_u8p),
+                                    pix_rad.ctypes.data_as(_f32p), depth_rad.ctypes.data_as(_f32p),
+                                    rad9.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+    rad9 = rad9[:P]
+    gflag = gflag[:P]
+    sh_a = None if sh is None else np.asarray(sh)
+    M = sh_a.shape[1] if sh_a is not None and sh_a.size else 0
+    r_m2 = np.zeros((P, 3), np.float32)
+    r_m2[:, :2] = rad9[:, :2]
+    r_col = rad9[:, 6:9].astype(np.float32)
+    r_op = rad9[:, 5:6].astype(np.float32)
+    r_m3, r_c3, r_sh, r_s, r_r = (np.zeros((P, 3)), np.zeros((P, 6)), np.zeros((P, M, 3)), np.zeros((P, 3)),
+                                  np.zeros((P, 4)))
+    live = rad9.any(1)
+    if live.any():
+        rad_in = np.where(live, np.asarray(radii, np.int32), 0).astype(np.int32)  # the tail skips radius-0 rows
+        for j in (0, 1, 2, 3, 4, 6, 7, 8):
+            col = rad9[:, j].astype(np.float32)
+            if not col.any():
+                continue
+            m2, cn, cl = np.zeros((P, 3), np.float32), np.zeros((P, 4), np.float32), np.zeros((P, 3), np.float32)
+            if j < 2:
+                m2[:, j] = col
+            elif j < 5:
+                cn[:, (0, 1, 3)[j - 2]] = col
+            else:
+                cl[:, j - 6] = col
+            outs = backward_tail(state, means3D, rad_in, scales, rotations, scale_modifier, cov3D_precomp, viewmatrix,
+                                 projmatrix, tanfovx, tanfovy, sh, degree, campos, m2, cn, cl)
+            for acc, o in zip((r_m3, r_c3, r_sh, r_s, r_r), outs):
+                acc += np.abs(o.astype(np.float64)).reshape(acc.shape)
+    grad_rad = (r_m2, r_col, r_op, r_m3.astype(np.float32), r_c3.astype(np.float32), r_sh.astype(np.float32),
+                r_s.astype(np.float32), r_r.astype(np.float32))
+    return dict(pflag=pflag, gflag=gflag, pix_rad=pix_rad, depth_rad=depth_rad, grad_rad=grad_rad)
+
+
+def near_pairs(state, band, max_n=1 << 22):
+    """(gid, px, py, o G) of every forward-walk pair whose alpha lies within `band` (relative) of 1/255
+    (gs4d_oracle_near_pairs), in no particular order."""
+    lib = _load()
+    gid, px, py = (np.zeros(max_n, np.int32) for _ in range(3))
+    og = np.zeros(max_n, np.float32)
+    n = lib.gs4d_oracle_near_pairs(state.handle, float(band), int(max_n), gid.ctypes.data_as(_i32p),
+                                   px.ctypes.data_as(_i32p), py.ctypes.data_as(_i32p), og.ctypes.data_as(_f32p))
+    if n > max_n:
+        raise RuntimeError(f"near_pairs: {n} pairs, more than max_n = {max_n}")
+    return gid[:n], px[:n], py[:n], og[:n]
 
 
 def sh_forward(degree, means, campos, shs):

@@ -46,6 +46,24 @@ def o_backward(O, s, st, radii, grad, colors=None, cov3D=None, use_sh=True, degr
         s["campos"])[0]
 
 
+def o_bounds(O, s, st, radii, grad, colors=None, cov3D=None, use_sh=True, degree=None):
+    """oracle.flip_bounds for the scene (near-threshold flags and the per-pixel / per-element flip bounds the
+    parity bars widen by); an all-culled scene (no oracle state) has none."""
+    from oracle import parity as PAR
+    if st is None:
+        P, H, W = len(radii), s["H"], s["W"]
+        M = np.asarray(s["shs"]).shape[1] if use_sh else 0
+        z = np.zeros
+        return dict(pflag=z((H, W), np.uint8), gflag=z(P, np.uint8), pix_rad=z((H, W), np.float32),
+                    depth_rad=z((H, W), np.float32),
+                    grad_rad=(z((P, 3)), z((P, 3)), z((P, 1)), z((P, 3)), z((P, 6)), z((P, M, 3)), z((P, 3)), z((P, 4))))
+    return O.flip_bounds(
+        st, PAR.FLIP_BAND_ALPHA, PAR.FLIP_BAND_T, s["bg"], s["means3D"], radii, colors,
+        None if cov3D is not None else s["scales"], None if cov3D is not None else s["rotations"], s["scale_modifier"],
+        cov3D, s["viewmatrix"], s["projmatrix"], s["tanfovx"], s["tanfovy"], grad, s["shs"] if use_sh else None,
+        s["sh_degree"] if degree is None else degree, s["campos"])
+
+
 def image_parity(a, b, atol=1e-4):
     """(max abs error, fraction of elements above atol)."""
     err = np.abs(np.asarray(a, np.float64) - np.asarray(b, np.float64))

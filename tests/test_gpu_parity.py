@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 import torch
 
-from gpu_helpers import c_backward, c_forward, o_backward, o_forward, to_dev
+from gpu_helpers import c_backward, c_forward, o_backward, o_bounds, o_forward, to_dev
 from gs4d_train.synthetic import make_scene, make_upstream_grad
 from oracle import parity as PAR
 
@@ -45,16 +45,15 @@ def _check(C, O, s, dev, colors=None, cov3D=None, use_sh=True, degree=None, repo
     nr, color, depth, radii, st = o_forward(O, s, colors=colors, cov3D=cov3D, use_sh=use_sh, degree=degree)
     assert fwd[0] == nr, f"num_rendered {fwd[0]} != oracle {nr}"
     assert np.array_equal(fwd[3].cpu().numpy(), radii), "radii differ"
-    pflag, gflag = O.flip_flags(st, PAR.FLIP_BAND_ALPHA, PAR.FLIP_BAND_T) if st is not None else (
-        np.zeros((s["H"], s["W"]), np.uint8), np.zeros(len(radii), np.uint8))
     g, _ = make_upstream_grad(color)
     g = g * (3 * s["W"] * s["H"])
     grads_c = c_backward(C, s, d, fwd, torch.tensor(g, device=dev), colors=col_t, cov3D=cov_t, use_sh=use_sh,
                          degree=degree)
     torch.cuda.synchronize()
     grads_o = o_backward(O, s, st, radii, g, colors=colors, cov3D=cov3D, use_sh=use_sh, degree=degree)
+    bounds = o_bounds(O, s, st, radii, g, colors=colors, cov3D=cov3D, use_sh=use_sh, degree=degree)
     res = PAR.check(fwd[1].cpu().numpy(), fwd[2].cpu().numpy(), [a.cpu().numpy() for a in grads_c], color, depth,
-                    grads_o, pflag, gflag, pix_frac=pix_frac, gauss_frac=gauss_frac)
+                    grads_o, bounds, pix_frac=pix_frac, gauss_frac=gauss_frac)
     res["L"] = nr
     if report is not None:
         report.append(res)
@@ -262,13 +261,15 @@ def test_autograd_api(dev, oracle):
     (img * torch.tensor(g, device=dev)).sum().backward()
     nr, color, depth_o, radii_o, st = o_forward(oracle, s)
     go = o_backward(oracle, s, st, radii_o, g)
-    pflag, gflag = oracle.flip_flags(st, PAR.FLIP_BAND_ALPHA, PAR.FLIP_BAND_T)
+    bounds = o_bounds(oracle, s, st, radii_o, g)
+    rad = bounds["grad_rad"]
     # the Python API's gradients: (means3D, shs, opacities, scales, rotations, means2D) against the
     # oracle's (dL_dmeans3D, dL_dsh, dL_dopacity, dL_dscales, dL_drotations, dL_dmeans2D)
     res = PAR.check(img.detach().cpu().numpy(), depth.detach().cpu().numpy(),
                     [leaves[k].grad.cpu().numpy() for k in ("means3D", "shs", "opacities", "scales", "rotations")]
                     + [screenspace.grad.cpu().numpy()], color, depth_o,
-                    [go[3], go[5], go[2], go[6], go[7], go[0]], pflag, gflag,
+                    [go[3], go[5], go[2], go[6], go[7], go[0]], bounds,
+                    o_rads=[rad[3], rad[5], rad[2], rad[6], rad[7], rad[0]],
                     names=["means3D", "shs", "opacities", "scales", "rotations", "means2D"])
     vis = raster.markVisible(leaves["means3D"].detach())
     assert vis.dtype == torch.bool and vis.shape == (3000,)
@@ -346,10 +347,63 @@ def test_grid_of_2pow20_tiles(C, oracle, dev):
     torch.cuda.synchronize()
     nr, color, depth, radii, st = o_forward(oracle, s)
     assert fwd[0] == nr and np.array_equal(fwd[3].cpu().numpy(), radii)
-    pflag, gflag = oracle.flip_flags(st, PAR.FLIP_BAND_ALPHA, PAR.FLIP_BAND_T)
     g = np.sign(color - 0.5).astype(np.float32)
     grads_c = c_backward(C, s, d, fwd, torch.tensor(g, device=dev))
     torch.cuda.synchronize()
     grads_o = o_backward(oracle, s, st, radii, g)
+    bounds = o_bounds(oracle, s, st, radii, g)
     res = PAR.check(fwd[1].cpu().numpy(), fwd[2].cpu().numpy(), [a.cpu().numpy() for a in grads_c], color, depth,
-                    grads_o, pflag, gflag, gauss_frac=GRID_GAUSS_FRAC)
+                    grads_o, bounds, gauss_frac=GRID_GAUSS_FRAC)
+
+
+def _final_T(ib, W, H):
+    """final_T carved from the forward's image buffer (capi.hip ImageState::carve: first array)."""
+    base = (ib.data_ptr() + 255) // 256 * 256 - ib.data_ptr()
+    raw = ib.cpu().numpy().view(np.uint8)
+    return raw[base:base + 4 * W * H].view(np.float32).reshape(H, W)
+
+
+@pytest.mark.parametrize("cfg", ["metric", "c2_800", "train_like", "opaque"])
+def test_flip_bands_cover_measured_operands(C, oracle, dev, cfg):
+    """The near-threshold bands of oracle/parity.py are set from this measurement, not guessed:
+      * alpha: for every (pixel, splat) pair of the oracle's walks with 255 alpha within 1e-3 of 1, the blend
+        kernels' own o G (gs4d_debug_pair_alpha: the exact arithmetic of both blend kernels) differs from the
+        oracle's by at most FLIP_BAND_ALPHA / 2, relative to 1/255;
+      * termination: T(1 - alpha) is a product of the walk's (1 - alpha) factors, so its relative difference
+        is bounded by the final transmittance's (every pixel whose decisions the oracle does not flag) plus
+        the last factor's share (alpha's relative difference times alpha / (1 - alpha) <= 99); that sum is at
+        most FLIP_BAND_T / 2.
+    Prints the measured maxima (DESIGN.md §5 quotes them)."""
+    from gs4d_train.synthetic import CONFIGS, make_train_like_scene
+    if cfg == "metric":
+        s = make_scene(100_000, 1352, 1014, seed=0)
+    elif cfg == "c2_800":
+        P, W, H = CONFIGS[cfg]
+        s = make_scene(P, W, H, seed=21)
+    elif cfg == "train_like":
+        s = make_train_like_scene(100_000, 1352, 1014, seed=0)
+    else:  # many terminations
+        s = make_scene(6000, 128, 128, seed=13, log_scale=math.log(0.1))
+        s["opacities"] = np.full_like(s["opacities"], 0.995)
+    d = to_dev(s, dev)
+    fwd = c_forward(C, s, d)
+    torch.cuda.synchronize()
+    nr, color, depth, radii, st = o_forward(oracle, s)
+    gid, px, py, og = oracle.near_pairs(st, 1e-3)
+    assert len(gid) > 0
+    t = lambda a: torch.tensor(a, device=dev)
+    og_gpu, _ = C.debug_pair_alpha(fwd[4], len(radii), s["W"], s["H"], t(gid), t(px), t(py))
+    d_alpha = float(np.abs(255.0 * og_gpu.cpu().numpy().astype(np.float64) - 255.0 * og.astype(np.float64)).max())
+    T_gpu = _final_T(fwd[6], s["W"], s["H"])
+    T_o = st.export()["final_T"]
+    pflag, _ = oracle.flip_flags(st, PAR.FLIP_BAND_ALPHA, PAR.FLIP_BAND_T)
+    ok = (pflag == 0) & (T_o > 0)
+    d_T = float((np.abs(T_gpu.astype(np.float64) - T_o) / T_o)[ok].max())
+    # T(1 - alpha): the last factor adds alpha's relative difference (d_alpha, measured at 1/255) times
+    # alpha / (1 - alpha) <= 99 (alpha <= 0.99)
+    d_test_T = d_T + 99.0 * d_alpha
+    print(f"{cfg}: {len(gid)} pairs within 1e-3 of 1/255: max |255 alpha_gpu - 255 alpha_oracle| = {d_alpha:.3g} "
+          f"(band {PAR.FLIP_BAND_ALPHA:.3g}); final T max relative difference {d_T:.3g}, test_T bound "
+          f"{d_test_T:.3g} (band {PAR.FLIP_BAND_T:.3g})", flush=True)
+    assert d_alpha <= PAR.FLIP_BAND_ALPHA / 2
+    assert d_test_T <= PAR.FLIP_BAND_T / 2

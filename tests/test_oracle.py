@@ -257,3 +257,51 @@ def test_threads_deterministic(oracle):
     oracle.set_threads(os.cpu_count())
     for a, b in zip(*res):
         assert np.array_equal(a, b)
+
+
+def _flip_bounds(O, s, st, radii, g, band):
+    return O.flip_bounds(st, band, 0.0, s["bg"], s["means3D"], radii, None, s["scales"], s["rotations"],
+                         s["scale_modifier"], None, s["viewmatrix"], s["projmatrix"], s["tanfovx"], s["tanfovy"], g,
+                         s["shs"], s["sh_degree"], s["campos"])
+
+
+def test_flip_bounds_single_splat_near_threshold(oracle):
+    """oracle.flip_bounds on one Gaussian whose alpha at one pixel sits just above 1/255, with the upstream
+    gradient on that pixel only: flipping that decision removes exactly that pixel's term, so the K7-level
+    bounds (dL_dmeans2D, dL_dcolors, dL_dopacity) equal the magnitudes of the oracle's own gradients, the
+    bounds carried through K8 + K9 cover the final gradients, and the pixel's colour bound is the splat's
+    whole weight there (forward.cu:346-348 taken the other way)."""
+    O = oracle
+    s = make_scene(1, 64, 48, seed=3, log_scale=math.log(0.1))
+    s["means3D"][0] = (0.0123, 0.0071, 4.0)  # off the pixel grid's symmetry: one near pixel
+    n, color, depth, radii, st = _fwd(O, s)
+    ex = st.export()
+    (mx, my), co = ex["means2D"][0], ex["conic_opacity"][0]
+    px, py = int(mx) + 4, int(my) + 2  # a few pixels off the centre
+    dx, dy = np.float32(mx - px), np.float32(my - py)
+    power = -0.5 * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy
+    assert power < -0.5
+    for delta in (2e-6, 4e-6, 8e-6):
+        s["opacities"][0, 0] = np.float32((1.0 / 255.0) * (1 + delta) / math.exp(float(power)))
+        n, color, depth, radii, st = _fwd(O, s)
+        if st.export()["n_contrib"][py, px] == 1:  # the oracle blends it (alpha >= 1/255 in its arithmetic)
+            break
+    else:
+        pytest.fail("no opacity put the pixel just above 1/255")
+    g = np.zeros((3, s["H"], s["W"]), np.float32)
+    g[:, py, px] = (0.3, -0.2, 0.5)
+    grads = _bwd(O, s, st, radii, g)[0]
+    b = _flip_bounds(O, s, st, radii, g, 1e-4)
+    assert b["gflag"][0] == 1 and b["pflag"][py, px] == 1 and b["pflag"].sum() == 1
+    rad = b["grad_rad"]
+    for i in (0, 1, 2):  # dL_dmeans2D, dL_dcolors, dL_dopacity: the pixel's term itself
+        np.testing.assert_allclose(rad[i], np.abs(grads[i]), rtol=1e-6, atol=0)
+    assert np.abs(grads[0][0, :2]).min() > 0 and rad[3].max() > 0
+    for i in (3, 4, 5, 6, 7):  # carried through K8 + K9: they cover the final gradients
+        assert np.all(np.abs(grads[i]) <= rad[i] * (1 + 1e-5) + 1e-12), i
+    s0 = dict(s, opacities=np.zeros_like(s["opacities"]))
+    _, color0, _, _, _ = _fwd(O, s0)
+    np.testing.assert_allclose(b["pix_rad"][py, px], np.abs(color[:, py, px] - color0[:, py, px]).max(), rtol=1e-6)
+    # outside the band nothing is flagged and every bound is zero
+    b = _flip_bounds(O, s, st, radii, g, 1e-7)
+    assert not b["pflag"].any() and not b["gflag"].any() and all(not r.any() for r in b["grad_rad"])
