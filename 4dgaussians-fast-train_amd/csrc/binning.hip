@@ -179,13 +179,9 @@ __global__ __launch_bounds__(256) void emit_instances_kernel(Args a, GeomState g
     // look-back words start at zero: both cleared here instead of by memset launches of their own
     for (int i = blockIdx.x * 256 + threadIdx.x; i < T; i += gridDim.x * 256) ranges[i] = make_uint2(0u, 0u);
     for (int i = blockIdx.x * 256 + threadIdx.x; i < nlook; i += gridDim.x * 256) look[i] = 0u;
-    // s_own (the owner marks, dead after the owner scan) and s_n (kept candidates before each candidate of
-    // the chunk, written after the compaction's barriers) share one array: 20 KiB per workgroup instead of
-    // 28, eight workgroups per CU, so a launch of up to 2048 chunks is resident at once (the kernel is
-    // latency-bound: 26 % VALU busy)
-    __shared__ uint32_t s_own_n[kEmitChunk + 1];
-    uint32_t *const s_own = s_own_n, *const s_n = s_own_n;
+    __shared__ uint32_t s_own[kEmitChunk];
     __shared__ uint32_t s_off[kEmitChunk + 2];
+    __shared__ uint32_t s_n[kEmitChunk + 1];  // kept candidates before each candidate of the chunk
     __shared__ uint32_t s_hist[kMaxPasses][256];
     __shared__ uint32_t s_w[4], s_tmp[4];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;

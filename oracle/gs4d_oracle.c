@@ -1053,11 +1053,13 @@ int gs4d_oracle_flip_bounds(const gs4d_oracle_state *s, const float *background,
     return nflag;
 }
 
-/* The (Gaussian, pixel) pairs of the forward walks whose alpha lies within band of 1/255 (relative; before
- * each pixel's termination): gid / px / py and the oracle's o G = co[3] * expf(power) (alpha before the
- * 0.99 cap), for measuring the blend kernels' operand against it.  Writes at most max_n; returns the count
- * found (which may exceed max_n). */
-int gs4d_oracle_near_pairs(const gs4d_oracle_state *s, float band, int max_n, int *gid, int *px, int *py, float *og) {
+/* The (Gaussian, pixel) pairs of the forward walks near one of the blend's thresholds: kind 1, alpha within
+ * band of 1/255 (relative; before each pixel's termination); kind 2, a splat passing the alpha test whose
+ * T(1 - alpha) lies within band of 1e-4 (relative).  gid / px / py and the oracle's o G = co[3] * expf(power)
+ * (alpha before the 0.99 cap), for measuring the blend kernels' operands against them.  Writes at most
+ * max_n; returns the count found (which may exceed max_n). */
+int gs4d_oracle_near_pairs(const gs4d_oracle_state *s, int kind, float band, int max_n, int *gid, int *px, int *py,
+                           float *og) {
     const int W = s->W, H = s->H, gx = s->gx, T = s->gx * s->gy;
     int count = 0;
 #pragma omp parallel for schedule(dynamic, 1)
@@ -1078,7 +1080,10 @@ int gs4d_oracle_near_pairs(const gs4d_oracle_state *s, float band, int max_n, in
                     if (power > 0.0f) continue;
                     const float o_g = co[3] * expf(power);
                     float alpha = fminf_(0.99f, o_g);
-                    if (fabsf(alpha * 255.0f - 1.0f) <= band) {
+                    const float test_T = Tr * (1 - alpha);
+                    const int near = kind == 1 ? fabsf(alpha * 255.0f - 1.0f) <= band
+                                               : alpha >= 1.0f / 255.0f && fabsf(test_T * 1e4f - 1.0f) <= band;
+                    if (near) {
                         int i;
 #pragma omp atomic capture
                         i = count++;
@@ -1090,7 +1095,6 @@ int gs4d_oracle_near_pairs(const gs4d_oracle_state *s, float band, int max_n, in
                         }
                     }
                     if (alpha < 1.0f / 255.0f) continue;
-                    float test_T = Tr * (1 - alpha);
                     if (test_T < 0.0001f) break;
                     Tr = test_T;
                 }
