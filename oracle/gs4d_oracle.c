@@ -51,6 +51,17 @@ typedef struct { float m[3][3]; } mat3; /* m[col][row], glm convention */
 static inline float fminf_(float a, float b) { return a < b ? a : b; }
 static inline float fmaxf_(float a, float b) { return a > b ? a : b; }
 
+/* The alpha test's near-threshold band at one (pixel, splat) pair.  Two float evaluations of
+ * power = -0.5 (a dx^2 + c dy^2) - b dx dy (forward.cu:336-338) in different operation orders (the blend
+ * kernels: base 2, pre-scaled conic, FMA) differ by a few roundings of the terms' magnitudes, and alpha = o
+ * exp(power) inherits that absolute difference as a relative one.  So the band scales with
+ * 1 + 0.5 (|a| dx^2 + |c| dy^2) + |b dx dy|: band_alpha is the allowance per unit of it (set from the
+ * measured differences, oracle/parity.py). */
+static inline int near_alpha(float alpha, const float *co, float dx, float dy, float band_alpha) {
+    const float mag = 1.0f + 0.5f * (fabsf(co[0]) * dx * dx + fabsf(co[2]) * dy * dy) + fabsf(co[1] * dx * dy);
+    return fabsf(alpha * 255.0f - 1.0f) <= band_alpha * mag;
+}
+
 /* glm::mat3(a0..a8): columns (a0,a1,a2), (a3,a4,a5), (a6,a7,a8) */
 static inline mat3 mat3_cols(float a0, float a1, float a2, float a3, float a4, float a5, float a6,
                              float a7, float a8) {
@@ -454,7 +465,7 @@ gs4d_oracle_state *gs4d_oracle_forward(int P, int D, int M, const float *backgro
  * (forward.cu:346-348, backward.cu:486-490) and T(1 - alpha) >= 1e-4 (forward.cu:350-354), flip
  * between two correct float implementations when their operand lies within rounding of the
  * threshold.  This replays the K6 walk of every pixel and flags:
- *   pix_flag bit 0   some splat before the pixel's termination has |255 alpha - 1| <= band_alpha
+ *   pix_flag bit 0   some splat before the pixel's termination has |255 alpha - 1| within its near_alpha band
  *   pix_flag bit 1   some blended splat has |test_T / 1e-4 - 1| <= band_T (termination may flip)
  *   gauss_flag bit 0 the Gaussian is such a near-1/255 splat at some pixel
  *   gauss_flag bit 1 the Gaussian is such a near-termination splat at some pixel
@@ -488,7 +499,7 @@ int gs4d_oracle_flip_flags(const gs4d_oracle_state *s, float band_alpha, float b
                     float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
                     if (power > 0.0f) continue;
                     float alpha = fminf_(0.99f, co[3] * expf(power));
-                    if (fabsf(alpha * 255.0f - 1.0f) <= band_alpha) {
+                    if (near_alpha(alpha, co, dx, dy, band_alpha)) {
                         f |= 1;
                         __atomic_fetch_or(&gauss_flag[g], (uint8_t)1, __ATOMIC_RELAXED);
                     }
@@ -889,7 +900,7 @@ void gs4d_oracle_sh_forward(int P, int D, int M, const float *means, const float
  * The blend's two discrete decisions, alpha >= 1/255 (forward.cu:346-348, backward.cu:486-490) and
  * T(1 - alpha) >= 1e-4 (forward.cu:350-354), can go either way between two correct float
  * implementations when their operand lies within rounding of the threshold.  For every pixel this
- * replays the forward walk, finds those decisions (|255 alpha - 1| <= band_alpha before the pixel's
+ * replays the forward walk, finds those decisions (|255 alpha - 1| within near_alpha's band before the pixel's
  * termination; |T(1 - alpha) / 1e-4 - 1| <= band_T for a splat that passed the alpha test), and for EACH
  * of them replays the pixel's forward and backward with that one decision taken the other way.  The
  * differences bound what a flip can change:
@@ -983,7 +994,7 @@ int gs4d_oracle_flip_bounds(const gs4d_oracle_state *s, const float *background,
                     if (power > 0.0f) continue;
                     float alpha = fminf_(0.99f, co[3] * expf(power));
                     int kinds = 0;
-                    if (fabsf(alpha * 255.0f - 1.0f) <= band_alpha) kinds |= 1;
+                    if (near_alpha(alpha, co, dx, dy, band_alpha)) kinds |= 1;
                     float test_T = Tr * (1 - alpha);
                     if (alpha >= a_thr && fabsf(test_T * 1e4f - 1.0f) <= band_T) kinds |= 2;
                     for (int kind = 1; kind <= 2; kind++) {
@@ -1055,11 +1066,12 @@ int gs4d_oracle_flip_bounds(const gs4d_oracle_state *s, const float *background,
 
 /* The (Gaussian, pixel) pairs of the forward walks near one of the blend's thresholds: kind 1, alpha within
  * band of 1/255 (relative; before each pixel's termination); kind 2, a splat passing the alpha test whose
- * T(1 - alpha) lies within band of 1e-4 (relative).  gid / px / py and the oracle's o G = co[3] * expf(power)
- * (alpha before the 0.99 cap), for measuring the blend kernels' operands against them.  Writes at most
+ * T(1 - alpha) lies within band of 1e-4 (relative).  gid / px / py, the oracle's o G = co[3] * expf(power)
+ * (alpha before the 0.99 cap) and near_alpha's magnitude factor, for measuring the blend kernels' operands
+ * against them.  Writes at most
  * max_n; returns the count found (which may exceed max_n). */
 int gs4d_oracle_near_pairs(const gs4d_oracle_state *s, int kind, float band, int max_n, int *gid, int *px, int *py,
-                           float *og) {
+                           float *og, float *mag) {
     const int W = s->W, H = s->H, gx = s->gx, T = s->gx * s->gy;
     int count = 0;
 #pragma omp parallel for schedule(dynamic, 1)
@@ -1081,7 +1093,7 @@ int gs4d_oracle_near_pairs(const gs4d_oracle_state *s, int kind, float band, int
                     const float o_g = co[3] * expf(power);
                     float alpha = fminf_(0.99f, o_g);
                     const float test_T = Tr * (1 - alpha);
-                    const int near = kind == 1 ? fabsf(alpha * 255.0f - 1.0f) <= band
+                    const int near = kind == 1 ? near_alpha(alpha, co, dx, dy, band)
                                                : alpha >= 1.0f / 255.0f && fabsf(test_T * 1e4f - 1.0f) <= band;
                     if (near) {
                         int i;
@@ -1092,6 +1104,8 @@ int gs4d_oracle_near_pairs(const gs4d_oracle_state *s, int kind, float band, int
                             px[i] = pxi;
                             py[i] = pyi;
                             og[i] = o_g;
+                            mag[i] = 1.0f + 0.5f * (fabsf(co[0]) * dx * dx + fabsf(co[2]) * dy * dy) +
+                                     fabsf(co[1] * dx * dy);
                         }
                     }
                     if (alpha < 1.0f / 255.0f) continue;

@@ -62,7 +62,8 @@ def _load():
     lib.gs4d_oracle_flip_bounds.argtypes = [ctypes.c_void_p, _f32p, _f32p, _f32p, ctypes.c_float, ctypes.c_float, _u8p,
                                             _u8p, _f32p, _f32p, ctypes.POINTER(ctypes.c_double)]
     lib.gs4d_oracle_flip_bounds.restype = ctypes.c_int
-    lib.gs4d_oracle_near_pairs.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_int, _i32p, _i32p, _i32p, _f32p]
+    lib.gs4d_oracle_near_pairs.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_int, _i32p, _i32p, _i32p,
+                                           _f32p, _f32p]
     lib.gs4d_oracle_near_pairs.restype = ctypes.c_int
     lib.gs4d_oracle_backward_tail.restype = None
     lib.gs4d_oracle_backward_tail.argtypes = [
@@ -292,17 +293,19 @@ def flip_bounds(state, band_alpha, band_T, bg, means3D, radii, colors_precomp, s
 
 
 def near_pairs(state, band, kind=1, max_n=1 << 22):
-    """(gid, px, py, o G) of every forward-walk pair near a threshold (gs4d_oracle_near_pairs), in no
-    particular order: kind 1, alpha within `band` (relative) of 1/255; kind 2, a blended splat whose
-    T(1 - alpha) lies within `band` (relative) of 1e-4."""
+    """(gid, px, py, o G, mag) of every forward-walk pair near a threshold (gs4d_oracle_near_pairs), in no
+    particular order: kind 1, alpha within `band` x mag (relative) of 1/255, mag = 1 + the magnitude of the
+    power's terms (near_alpha); kind 2, a blended splat whose T(1 - alpha) lies within `band` (relative) of
+    1e-4."""
     lib = _load()
     gid, px, py = (np.zeros(max_n, np.int32) for _ in range(3))
-    og = np.zeros(max_n, np.float32)
+    og, mag = np.zeros(max_n, np.float32), np.zeros(max_n, np.float32)
     n = lib.gs4d_oracle_near_pairs(state.handle, int(kind), float(band), int(max_n), gid.ctypes.data_as(_i32p),
-                                   px.ctypes.data_as(_i32p), py.ctypes.data_as(_i32p), og.ctypes.data_as(_f32p))
+                                   px.ctypes.data_as(_i32p), py.ctypes.data_as(_i32p), og.ctypes.data_as(_f32p),
+                                   mag.ctypes.data_as(_f32p))
     if n > max_n:
         raise RuntimeError(f"near_pairs: {n} pairs, more than max_n = {max_n}")
-    return gid[:n], px[:n], py[:n], og[:n]
+    return gid[:n], px[:n], py[:n], og[:n], mag[:n]
 
 
 def sh_forward(degree, means, campos, shs):
