@@ -143,21 +143,28 @@ __global__ __launch_bounds__(kHexThreads) void hexplane_forward_kernel(int N, co
     }
 }
 
-// Backward.  A workgroup serves NPW consecutive points of the Morton order (hex_points_per_wg: 2048 / F,
-// at least one chunk of 256 / (F/4) points, at most 128), so they cover a small box of the field.  Per
-// level:
-//   1. each point's reverse pass (F/4 lanes) writes its 6 plane gradients dv (F floats each), its
-//      bilinear anchor cell (x0, y0) and unnormalised coordinates (ix, iy) to LDS, and reduces its
-//      coordinate gradient with shuffles;
-//   2. per plane, the points' <= 4 taps (weights as make_tap forms them) are counting-sorted by cell
-//      in LDS over the touched box, and every (cell, 4 features) of it sums its taps' w * dv with
-//      plain LDS reads and adds the sums to HBM with no-return float atomics.  A plane whose box
-//      exceeds kHexMaxCells scatters its points' taps with direct float atomics instead.
-// gfx950 executes LDS float atomics (ds_add_f32) at well under one lane per clock per CU: the previous
-// version, which summed the taps into LDS windows with them, spent 280 of its 620 us in those atomics.
-constexpr int kHexMaxCells = 1024;
+// Backward, deterministic by construction.  A workgroup serves NPW consecutive points of the Morton order
+// (hex_points_per_wg: 2048 / F, at least one chunk of 256 / (F/4) points, at most 128), so they cover a small
+// box of the field.  Per level:
+//   1. each point's reverse pass (F/4 lanes) writes its 6 plane gradients dv (F floats each), its bilinear
+//      anchor cell (x0, y0) and unnormalised coordinates (ix, iy) to LDS, and reduces its coordinate
+//      gradient with shuffles;
+//   2. per plane: the anchors' box; every (point, tap, feature) term w * dv (make_tap's weights) is rounded
+//      ONCE to a 64-bit fixed-point integer at the plane's power-of-two scale (hex_plane_scale) and added into
+//      an LDS window over the box's cells with ds_add_u64; the window's nonzero sums then go to the packed
+//      gradient's 64-bit accumulators with one no-return integer atomic each, and hex_fix_to_float_kernel
+//      turns them into floats.  Integer sums are exact, so neither the order of the LDS adds nor that of the
+//      workgroups' atomics changes a bit: the gradients are bitwise reproducible with no ordering work at all.
+//      A box too large for the window at F features is covered in feature slices (F/2, F/4 per pass); beyond
+//      that its terms go straight to the global accumulators (still exact).
+// Measured on this chip (tools/bench/lds_atomics.hip, global_atomics.hip): ds_add_u64 ~7.4 lane-ops per clock
+// per CU, as fast as a plain LDS read-modify-write (ds_add_f32: 0.33); global u64 atomics as fast as f32 ones
+// (2x faster on 4096 hot addresses).  The previous design counting-sorted each plane's taps by cell in LDS
+// and gathered them (float atomics across workgroups; a fixed-point mode that ranked taps by ballots was
+// ~300 us against 225).
 constexpr int kHexDvFloats = 2048;   // NPW * F
 constexpr int kHexLdsWords = 20480;  // 80 KiB: two workgroups per CU, as the registers allow
+constexpr int kHexNanWord = 63;      // scale words: [0] max|dfeat|, [1 + p] max|param| of plane p, [63] non-finite flag
 
 __host__ __device__ __forceinline__ int hex_points_per_wg(int F) {
     const int ppc = kHexThreads / (F / 4);
@@ -165,105 +172,118 @@ __host__ __device__ __forceinline__ int hex_points_per_wg(int F) {
     const int want = fit < 128 ? fit : 128;
     return ppc > want ? ppc : want;  // a whole number of chunks
 }
-// LDS words of the backward's layout (hexplane_backward_kernel); <= kHexLdsWords for every valid F
-__host__ __device__ __forceinline__ int hex_bwd_lds_words(int F) {
+// LDS words of the backward's fixed arrays (s_dv, s_anc, s_ixy, boxes); the rest of kHexLdsWords is the
+// 64-bit window
+__host__ __device__ __forceinline__ int hex_bwd_fixed_words(int F) {
     const int npw = hex_points_per_wg(F);
-    return 6 * npw * F + 6 * npw * 3 + (kHexMaxCells + 1) + kHexMaxCells / 2 + (kHexMaxCells + 2) / 2 + 4 * npw +
-           2 * npw + 6 * 4 + 4 * 6 * 4 + 8;
+    return (6 * npw * F + 6 * npw * 3 + 6 * 4 + 4 * 6 * 4 + 8 + 1) & ~1;
 }
+__host__ __device__ __forceinline__ int hex_bwd_window(int F) { return (kHexLdsWords - hex_bwd_fixed_words(F)) / 2; }
 
-// exclusive prefix sum over the workgroup (256 threads), `tot` = the sum; s_tmp holds 4 ints
-__device__ __forceinline__ int block_excl_scan(int v, int *s_tmp, int &tot) {
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    int x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
-    if (lane == 63) s_tmp[wv] = x;
-    __syncthreads();
-    int base = 0;
-    tot = 0;
-#pragma unroll
-    for (int w = 0; w < kHexThreads / 64; w++) {
-        const int t = s_tmp[w];
-        if (w < wv) base += t;
-        tot += t;
-    }
-    __syncthreads();
-    return base + x - v;
-}
-
-// The fixed-point scale 2^e with e chosen so that N max|dfeat| max|param|^5 * 2^e <= 2^61 (mx[0] =
-// max|dfeat|, mx[1] = max|param| as float bits, hex_max_kernel); 1 when the bound is 0 or not finite.
-__device__ __forceinline__ float hex_scale_of(int N, const uint32_t *mx) {
-    const float a = __uint_as_float(mx[0]), m = __uint_as_float(mx[1]);
-    const float m2 = m * m;
-    const float bound = (float)N * a * (m2 * m2 * m);
-    if (!(bound > 0.f) || !(bound < 3.0e38f)) return 1.f;
+// The fixed-point scale of plane p (of level l): 2^e with e chosen so that the largest possible cell sum fits
+// 2^61.  A term is w dv with w <= 1 and dv = dfeat * the product of the level's 5 other plane values, each a
+// convex combination of its plane's parameters, and a cell takes at most one tap per point, so
+//   |sum| <= N max|dfeat| prod_{q != p} max|param_q|
+// (computed in double: no overflow).  A zero bound (every term is 0) takes 1; a bound beyond the float
+// exponent range clamps e to its minimum, -126 (the largest term is a float, < 2^128, so N of them scaled by
+// 2^-126 still fit); non-finite inputs are flagged separately (kHexNanWord).
+__device__ __forceinline__ float hex_plane_scale(int N, const uint32_t *mx, int l, int p) {
+    double b = (double)N * (double)__uint_as_float(mx[0]);
+    for (int q = 0; q < 6; q++)
+        if (q != p) b *= (double)__uint_as_float(mx[1 + 6 * l + q]);
+    if (!(b > 0.0)) return 1.f;
     int ex;
-    (void)frexpf(bound, &ex);  // bound < 2^ex
+    (void)frexp(b, &ex);  // b < 2^ex
     return ldexpf(1.f, max(-126, min(127, 61 - ex)));
 }
 __device__ __forceinline__ unsigned long long hex_fix(float v, float scale) {
     return (unsigned long long)__float2ll_rn(v * scale);  // scale is a power of two: v * scale is exact
 }
-// max |x| over n floats into *mx (float bits of a non-negative value order like unsigned integers)
-__global__ __launch_bounds__(256) void hex_max_kernel(int64_t n, const float *__restrict__ x, uint32_t *__restrict__ mx) {
+// Maxima of |x| for the scales: blockIdx.y = r selects range r of `rg` (n_r floats at x_r) and its word
+// mx[w_r]; a non-finite element sets mx[kHexNanWord] (fmaxf would skip a NaN).  Float bits of a
+// non-negative value order like unsigned integers.
+struct HexMaxRanges {
+    const float *x[1 + 6 * GS4D_HEXPLANE_MAX_LEVELS];
+    int64_t n[1 + 6 * GS4D_HEXPLANE_MAX_LEVELS];
+    int first[2 + 6 * GS4D_HEXPLANE_MAX_LEVELS];  // first block of each range (blocks in proportion to its size)
+    int nr;
+};
+__global__ __launch_bounds__(256) void hex_max_kernel(HexMaxRanges rg, uint32_t *__restrict__ mx) {
+    int r = 0;
+    while (r + 1 < rg.nr && (int)blockIdx.x >= rg.first[r + 1]) r++;
+    const float4 *x = reinterpret_cast<const float4 *>(rg.x[r]);  // every range is float4-aligned, n % 4 == 0
+    const int64_t n = rg.n[r] / 4;
+    const int b = (int)blockIdx.x - rg.first[r], nb = rg.first[r + 1] - rg.first[r];
     float m = 0.f;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) m = fmaxf(m, fabsf(x[i]));
+    bool bad = false;
+    // four loads in flight per thread per round (the range is split over few blocks: each block's maximum is
+    // one atomicMax on the range's word, and those serialise)
+    for (int64_t i0 = (int64_t)b * 1024 + threadIdx.x; i0 < n; i0 += (int64_t)nb * 1024) {
+        float4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) v[u] = i0 + u * 256 < n ? x[i0 + u * 256] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const float a = fmaxf(fmaxf(fabsf(v[u].x), fabsf(v[u].y)), fmaxf(fabsf(v[u].z), fabsf(v[u].w)));
+            bad |= !(a <= 3.4028235e38f) || v[u].x != v[u].x || v[u].y != v[u].y || v[u].z != v[u].z ||
+                   v[u].w != v[u].w;
+            m = fmaxf(m, a);
+        }
+    }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+    const bool any_bad = __builtin_amdgcn_ballot_w64(bad) != 0;
     __shared__ float s_m[4];
-    if ((threadIdx.x & 63) == 0) s_m[threadIdx.x >> 6] = m;
+    __shared__ int s_bad[4];
+    if ((threadIdx.x & 63) == 0) {
+        s_m[threadIdx.x >> 6] = m;
+        s_bad[threadIdx.x >> 6] = any_bad;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         m = fmaxf(fmaxf(s_m[0], s_m[1]), fmaxf(s_m[2], s_m[3]));
-        if (m > 0.f) atomicMax(mx, __float_as_uint(m));
+        if (m > 0.f) atomicMax(mx + r, __float_as_uint(m));
+        if (s_bad[0] | s_bad[1] | s_bad[2] | s_bad[3]) atomicOr(mx + kHexNanWord, 1u);
     }
 }
-// the fixed-point sums back to floats (channels-last packed layout)
-__global__ __launch_bounds__(256) void hex_fix_to_float_kernel(int64_t n, int N, const uint32_t *__restrict__ mx,
-                                                               const long long *__restrict__ acc,
-                                                               float *__restrict__ out) {
-    const float inv = 1.f / hex_scale_of(N, mx);
+// the fixed-point sums to floats in the packed layout, plane by plane (blockIdx.y), for callers that want the
+// packed buffer (the glue writes the planes directly: the unpack's FIX load)
+__global__ __launch_bounds__(256) void hex_fix_to_packed_kernel(gs4d_hexplane_layout lay, int N,
+                                                                const uint32_t *__restrict__ mx,
+                                                                const long long *__restrict__ acc,
+                                                                float *__restrict__ out) {
+    const int pg = blockIdx.y, l = pg / 6, p = pg - 6 * l;
+    const gs4d_hexplane_plane pl = lay.plane[pg];
+    const int64_t n = (int64_t)pl.W * pl.H * lay.F;
+    const float inv = 1.f / hex_plane_scale(N, mx, l, p);
+    const bool nan = mx[kHexNanWord] != 0;
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
-        out[i] = (float)acc[i] * inv;
+        out[pl.offset + i] = nan ? __builtin_nanf("") : (float)acc[pl.offset + i] * inv;
 }
 
-// DET: the deterministic sums (fixed rank order in the workgroup, 64-bit fixed-point atomics across
-// workgroups, dacc = the fixed-point accumulators); otherwise the reference's kind of sum -- float
-// atomics straight into the packed float gradients (dacc), LDS-atomic tap ranks -- which is faster.
-template <bool DET>
 __global__ __launch_bounds__(kHexThreads) void hexplane_backward_kernel(int N, const float *__restrict__ pts,
                                                                         const uint32_t *__restrict__ order,
                                                                         gs4d_hexplane_layout lay,
                                                                         const float *__restrict__ packed,
                                                                         const float *__restrict__ dfeat,
                                                                         const uint32_t *__restrict__ mx,
-                                                                        void *__restrict__ dacc,
+                                                                        unsigned long long *__restrict__ dfix,
                                                                         float *__restrict__ dpts) {
-    const float scale = DET ? hex_scale_of(N, mx) : 1.f;
-    unsigned long long *const dfix = (unsigned long long *)dacc;
-    float *const dflt = (float *)dacc;
-    __shared__ float smem[kHexLdsWords];
+    __shared__ unsigned long long smem64[kHexLdsWords / 2];
+    float *const smem = reinterpret_cast<float *>(smem64);
     const int F = lay.F, G = F / 4, ppc = kHexThreads / G;
     const int npw = hex_points_per_wg(F), cpw = npw / ppc;
+    const int fixed = hex_bwd_fixed_words(F), wcap = hex_bwd_window(F);
     float *s_dv = smem;                                            // [6][npw][F]
     int *s_anc = (int *)(s_dv + 6 * npw * F);                      // [6][npw]: y0 << 16 | x0, -1: none
     float2 *s_ixy = (float2 *)(s_anc + 6 * npw);                   // [6][npw]
-    int *s_off = (int *)(s_ixy + 6 * npw);                         // [kHexMaxCells + 1]: cell -> first tap
-    uint16_t *s_cells = (uint16_t *)(s_off + kHexMaxCells + 1);    // [kHexMaxCells]: touched cells
-    uint16_t *s_cstart = s_cells + kHexMaxCells;                   // [kHexMaxCells + 1]: their first taps
-    float *s_pw = (float *)(s_off + kHexMaxCells + 1 + kHexMaxCells / 2 + (kHexMaxCells + 2) / 2);  // [4 npw]
-    uint16_t *s_pj = (uint16_t *)(s_pw + 4 * npw);                 // [4 npw]: point
-    int *s_box = (int *)(s_pj + 4 * npw);                          // [6][4]: ax0, ay0, aw, ah
+    int *s_box = (int *)(s_ixy + 6 * npw);                         // [6][4]: ax0, ay0, aw, ah
     int *s_wbox = s_box + 24;                                      // [waves][6][4]
-    int *s_tmp = s_wbox + 4 * 24;                                  // [8]
+    unsigned long long *s_win = smem64 + fixed / 2;                // [wcap]: the fixed-point window
     const int q = threadIdx.x % G, slot = threadIdx.x / G;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t first = (int64_t)blockIdx.x * npw;
+    for (int e = threadIdx.x; e < wcap; e += kHexThreads) s_win[e] = 0ull;  // flushes leave it zeroed
     for (int l = 0; l < lay.levels; l++) {
         // 1. reverse passes
         for (int c = 0; c < cpw; c++) {
@@ -381,19 +401,23 @@ __global__ __launch_bounds__(kHexThreads) void hexplane_backward_kernel(int N, c
             s_box[p * 4 + 3] = y1 >= y0 ? y1 - y0 + 1 : 0;
         }
         __syncthreads();
-        // 2b. per plane: bucket the points by anchor, gather each touched (cell, feature)
+        // 2b. per plane: fixed-point terms into the LDS window over the box's cells, then to HBM
         for (int p = 0; p < 6; p++) {
             const gs4d_hexplane_plane pl = lay.plane[6 * l + p];
             const int ax0 = s_box[p * 4 + 0], ay0 = s_box[p * 4 + 1], aw = s_box[p * 4 + 2], ah = s_box[p * 4 + 3];
-            const int na = aw * ah;
-            if (na == 0) continue;  // uniform
+            if (aw * ah == 0) continue;  // uniform
+            const float scale = hex_plane_scale(N, mx, l, p);
             const float *dvp = s_dv + p * npw * F;
             const int *ancp = s_anc + p * npw;
             const float2 *ixyp = s_ixy + p * npw;
             unsigned long long *dpl = dfix + pl.offset;
-            float *dplf = dflt + pl.offset;
-            if ((min(ax0 + aw, pl.W - 1) - ax0 + 1) * (min(ay0 + ah, pl.H - 1) - ay0 + 1) > kHexMaxCells) {
-                // uniform: a box too large for the cell offsets -- direct atomics per (point, feature)
+            // the touched cells: the anchors' box and its +1 neighbours inside the plane
+            const int cw = min(ax0 + aw, pl.W - 1) - ax0 + 1, ch = min(ay0 + ah, pl.H - 1) - ay0 + 1;
+            const int nc = cw * ch;
+            int fp = F;  // features per pass (uniform)
+            while (nc * fp > wcap && fp > 4) fp >>= 1;
+            if (nc * fp > wcap) {
+                // uniform: a box too large even at 4 features per pass -- terms straight to the accumulators
                 for (int e = threadIdx.x; e < npw * F; e += kHexThreads) {
                     const int j = e / F, f = e - j * F;
                     const int a = ancp[j];
@@ -404,144 +428,50 @@ __global__ __launch_bounds__(kHexThreads) void hexplane_backward_kernel(int N, c
                     const float xa = (float)(x0 + 1) - ixy.x, xb = ixy.x - (float)x0;
                     const float ya = (float)(y0 + 1) - ixy.y, yb = ixy.y - (float)y0;
                     const bool in_x1 = x0 + 1 < pl.W, in_y1 = y0 + 1 < pl.H;
-                    const size_t i0 = ((size_t)y0 * pl.W + x0) * F + f;
-                    if (DET) {
-                        unsigned long long *b0 = dpl + i0;
-                        atomicAdd(b0, hex_fix((xa * ya) * d, scale));
-                        if (in_x1) atomicAdd(b0 + F, hex_fix((xb * ya) * d, scale));
-                        if (in_y1) atomicAdd(b0 + (size_t)pl.W * F, hex_fix((xa * yb) * d, scale));
-                        if (in_x1 && in_y1) atomicAdd(b0 + (size_t)(pl.W + 1) * F, hex_fix((xb * yb) * d, scale));
-                    } else {
-                        float *b0 = dplf + i0;
-                        unsafeAtomicAdd(b0, (xa * ya) * d);
-                        if (in_x1) unsafeAtomicAdd(b0 + F, (xb * ya) * d);
-                        if (in_y1) unsafeAtomicAdd(b0 + (size_t)pl.W * F, (xa * yb) * d);
-                        if (in_x1 && in_y1) unsafeAtomicAdd(b0 + (size_t)(pl.W + 1) * F, (xb * yb) * d);
-                    }
+                    unsigned long long *b0 = dpl + ((size_t)y0 * pl.W + x0) * F + f;
+                    atomicAdd(b0, hex_fix((xa * ya) * d, scale));
+                    if (in_x1) atomicAdd(b0 + F, hex_fix((xb * ya) * d, scale));
+                    if (in_y1) atomicAdd(b0 + (size_t)pl.W * F, hex_fix((xa * yb) * d, scale));
+                    if (in_x1 && in_y1) atomicAdd(b0 + (size_t)(pl.W + 1) * F, hex_fix((xb * yb) * d, scale));
                 }
                 continue;
             }
-            // the touched cells' box; each point's <= 4 taps counting-sorted by cell: s_off <- counts,
-            // the taps' ranks within their cells kept in registers
-            const int cw = min(ax0 + aw, pl.W - 1) - ax0 + 1, ch = min(ay0 + ah, pl.H - 1) - ay0 + 1;
-            const int nc = cw * ch;
-            for (int e = threadIdx.x; e <= nc; e += kHexThreads) s_off[e] = 0;
-            __syncthreads();
-            int tc[4] = {-1, -1, -1, -1}, tr[4] = {0, 0, 0, 0};
-            float tw[4] = {0.f, 0.f, 0.f, 0.f};
-            if (threadIdx.x < npw) {
-                const int a = ancp[threadIdx.x];
-                if (a >= 0) {
-                    const int x0 = a & 0xFFFF, y0 = a >> 16, lx = x0 - ax0, ly = y0 - ay0;
-                    const float2 ixy = ixyp[threadIdx.x];
-                    // make_tap's weights: w00, w10, w01, w11
-                    const float xa = (float)(x0 + 1) - ixy.x, xb = ixy.x - (float)x0;
-                    const float ya = (float)(y0 + 1) - ixy.y, yb = ixy.y - (float)y0;
-                    const bool in_x1 = x0 + 1 < pl.W, in_y1 = y0 + 1 < pl.H;
-                    tc[0] = ly * cw + lx;
-                    tw[0] = xa * ya;
-                    if (in_x1) tc[1] = tc[0] + 1, tw[1] = xb * ya;
-                    if (in_y1) tc[2] = tc[0] + cw, tw[2] = xa * yb;
-                    if (in_x1 && in_y1) tc[3] = tc[0] + cw + 1, tw[3] = xb * yb;
+            const int gp = fp / 4, lg = __builtin_ctz(gp), lf = __builtin_ctz(fp);  // powers of two
+            const float inv_cw = 1.f / (float)cw;
+            for (int f0 = 0; f0 < F; f0 += fp) {
+                // items (point j, tap t, group b): consecutive lanes take a tap's consecutive feature groups
+                for (int e = threadIdx.x; e < npw * 4 * gp; e += kHexThreads) {
+                    const int b = e & (gp - 1), t = (e >> lg) & 3, j = e >> (lg + 2);
+                    const int a = ancp[j];
+                    if (a < 0) continue;
+                    const int x0 = a & 0xFFFF, y0 = a >> 16, tx = t & 1, ty = t >> 1;
+                    if ((tx && x0 + 1 >= pl.W) || (ty && y0 + 1 >= pl.H)) continue;
+                    const float2 ixy = ixyp[j];
+                    // make_tap's weights: w00 = xa ya, w10 = xb ya, w01 = xa yb, w11 = xb yb
+                    const float wx = tx ? ixy.x - (float)x0 : (float)(x0 + 1) - ixy.x;
+                    const float wy = ty ? ixy.y - (float)y0 : (float)(y0 + 1) - ixy.y;
+                    const float w = wx * wy;
+                    const float4 d = *reinterpret_cast<const float4 *>(dvp + j * F + f0 + 4 * b);
+                    unsigned long long *c = s_win + ((y0 + ty - ay0) * cw + (x0 + tx - ax0)) * fp + 4 * b;
+                    atomicAdd(c + 0, hex_fix(w * d.x, scale));
+                    atomicAdd(c + 1, hex_fix(w * d.y, scale));
+                    atomicAdd(c + 2, hex_fix(w * d.z, scale));
+                    atomicAdd(c + 3, hex_fix(w * d.w, scale));
                 }
-            }
-            // deterministic ranks of the taps within their cells: tap slot by tap slot, wave by wave in
-            // order, lane by lane (peer lanes of a cell found by ballots over its 10 bits), so a cell's taps
-            // are summed in the same order on every run
-            if (!DET) {
-                if (threadIdx.x < npw)
-#pragma unroll
-                    for (int t = 0; t < 4; t++)
-                        if (tc[t] >= 0) tr[t] = atomicAdd(&s_off[tc[t]], 1);
+                __syncthreads();
+                // flush the nonzero sums (and leave the window zeroed for the next pass)
+                for (int e = threadIdx.x; e < nc * fp; e += kHexThreads) {
+                    const unsigned long long v = s_win[e];
+                    if (v == 0ull) continue;
+                    s_win[e] = 0ull;
+                    const int cell = e >> lf, f = e & (fp - 1);
+                    // cell / cw by a float reciprocal: (cell + 0.5) / cw lies >= 0.5 / cw >= 2^-11 from an
+                    // integer, far beyond the float quotient's error (cell < 2^16)
+                    const int ry = (int)(((float)cell + 0.5f) * inv_cw), rx = cell - ry * cw;
+                    atomicAdd(dpl + ((size_t)(ay0 + ry) * pl.W + ax0 + rx) * F + f0 + f, v);
+                }
                 __syncthreads();
             }
-            const uint64_t lt_mask = ((threadIdx.x & 63) == 0) ? 0ull : (~0ull >> (64 - (threadIdx.x & 63)));
-            for (int t = 0; t < 4 && DET; t++) {
-                for (int w = 0; w * 64 < npw; w++) {
-                    if ((int)(threadIdx.x >> 6) == w) {
-                        const int c = tc[t];
-                        uint64_t peers = __builtin_amdgcn_ballot_w64(c >= 0);
-#pragma unroll
-                        for (int bit = 0; bit < 10; bit++) {
-                            const bool set = (c >> bit) & 1;
-                            const uint64_t m = __builtin_amdgcn_ballot_w64(set);
-                            peers &= set ? m : ~m;
-                        }
-                        const int old = c >= 0 ? s_off[c] : 0;
-                        __builtin_amdgcn_wave_barrier();
-                        if (c >= 0 && (peers & lt_mask) == 0) s_off[c] = old + __popcll(peers);
-                        tr[t] = old + __popcll(peers & lt_mask);
-                    }
-                    __syncthreads();
-                }
-            }
-            int ntouched;
-            {
-                // exclusive scan of s_off[0, nc) (four entries per thread, nc <= kHexMaxCells), the tap
-                // counts in the low 16 bits and the touched-cell flags in the high 16: the cells' first
-                // taps and the compact list of touched cells from one scan
-                const int e0 = 4 * threadIdx.x;
-                int c[4], v = 0;
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    c[u] = e0 + u < nc ? s_off[e0 + u] : 0;
-                    v += c[u] + (c[u] > 0 ? 0x10000 : 0);
-                }
-                int tot;
-                int ex = block_excl_scan(v, s_tmp, tot);
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    if (e0 + u < nc) {
-                        s_off[e0 + u] = ex & 0xFFFF;
-                        if (c[u] > 0) {
-                            s_cells[ex >> 16] = (uint16_t)(e0 + u);
-                            s_cstart[ex >> 16] = (uint16_t)(ex & 0xFFFF);
-                        }
-                    }
-                    ex += c[u] + (c[u] > 0 ? 0x10000 : 0);
-                }
-                ntouched = tot >> 16;
-                if (threadIdx.x == 0) s_cstart[ntouched] = (uint16_t)(tot & 0xFFFF);
-            }
-            __syncthreads();
-#pragma unroll
-            for (int t = 0; t < 4; t++)
-                if (tc[t] >= 0) {
-                    const int k = s_off[tc[t]] + tr[t];
-                    s_pj[k] = (uint16_t)threadIdx.x;
-                    s_pw[k] = tw[t];
-                }
-            __syncthreads();
-            // gather: (touched cell, 4 features) per item, over the cell's taps in LDS
-            const int nb = F / 4;
-            for (int e = threadIdx.x; e < ntouched * nb; e += kHexThreads) {
-                const int r = e / nb, b4 = e - r * nb;
-                const int cell = s_cells[r], k0 = s_cstart[r], k1 = s_cstart[r + 1];
-                // the cell's taps in their deterministic rank order, then one exact fixed-point atomic
-                float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-                for (int k = k0; k < k1; k++) {
-                    const int j = s_pj[k];
-                    const float w = s_pw[k];
-                    const float4 d = *reinterpret_cast<const float4 *>(dvp + j * F + 4 * b4);
-                    acc.x += w * d.x; acc.y += w * d.y; acc.z += w * d.z; acc.w += w * d.w;
-                }
-                const int ry = cell / cw, rx = cell - ry * cw;
-                const size_t i0 = ((size_t)(ay0 + ry) * pl.W + ax0 + rx) * F + 4 * b4;
-                if (DET) {
-                    unsigned long long *dst = dpl + i0;
-                    if (acc.x != 0.f) atomicAdd(dst + 0, hex_fix(acc.x, scale));
-                    if (acc.y != 0.f) atomicAdd(dst + 1, hex_fix(acc.y, scale));
-                    if (acc.z != 0.f) atomicAdd(dst + 2, hex_fix(acc.z, scale));
-                    if (acc.w != 0.f) atomicAdd(dst + 3, hex_fix(acc.w, scale));
-                } else {
-                    float *dst = dplf + i0;
-                    if (acc.x != 0.f) unsafeAtomicAdd(dst + 0, acc.x);
-                    if (acc.y != 0.f) unsafeAtomicAdd(dst + 1, acc.y);
-                    if (acc.z != 0.f) unsafeAtomicAdd(dst + 2, acc.z);
-                    if (acc.w != 0.f) unsafeAtomicAdd(dst + 3, acc.w);
-                }
-            }
-            __syncthreads();
         }
     }
 }
@@ -601,14 +531,30 @@ __device__ __forceinline__ int repack_plane(const gs4d_hexplane_layout &lay, int
     }
     return p;
 }
-template <bool PACK, int FC>  // FC: the feature count when known at compile time (all loads in flight), else 0
+// FIX (unpack only): the source is the backward's 64-bit fixed-point sums `fix` (same layout), turned into
+// floats at the plane's scale on the way (NaN everywhere when an input was not finite: a float sum would
+// have propagated it)
+template <bool PACK, int FC, bool FIX = false>  // FC: the feature count when known at compile time (all loads in flight), else 0
 __global__ __launch_bounds__(kRepackThreads) void hexplane_repack_kernel(gs4d_hexplane_layout lay,
-                                                                         float *__restrict__ packed) {
+                                                                         float *__restrict__ packed,
+                                                                         const long long *__restrict__ fix = nullptr,
+                                                                         const uint32_t *__restrict__ mx = nullptr,
+                                                                         int N = 0) {
     extern __shared__ float s_tile[];  // F x (TC + 1)
     int64_t tile = blockIdx.x;
     const int p = repack_plane(lay, tile);
     if (p >= 6 * lay.levels) return;
     const gs4d_hexplane_plane pl = lay.plane[p];
+    float inv = 1.f;
+    bool nan = false;
+    if (FIX) {
+        inv = 1.f / hex_plane_scale(N, mx, p / 6, p % 6);
+        nan = mx[kHexNanWord] != 0;
+    }
+    auto src = [&](int64_t i) -> float {  // element i of the plane's packed block
+        if (!FIX) return packed[pl.offset + i];
+        return nan ? __builtin_nanf("") : (float)fix[pl.offset + i] * inv;
+    };
     const int F = FC ? FC : lay.F, TC = repack_cells(F), TS = TC + 1, t = threadIdx.x;
     const int64_t HW = (int64_t)pl.W * pl.H, c0 = tile * TC;
     const int nc = (int)min((int64_t)TC, HW - c0);
@@ -632,7 +578,7 @@ __global__ __launch_bounds__(kRepackThreads) void hexplane_repack_kernel(gs4d_he
 #pragma unroll
             for (int j = 0; j < FC; j++) {
                 const int k = t + j * kRepackThreads;
-                v[j] = k < nc * FC ? dst[k] : 0.f;
+                v[j] = k < nc * FC ? src(c0 * F + k) : 0.f;
             }
 #pragma unroll
             for (int j = 0; j < FC; j++) {
@@ -655,7 +601,7 @@ __global__ __launch_bounds__(kRepackThreads) void hexplane_repack_kernel(gs4d_he
         __syncthreads();
         for (int k = t; k < nc * F; k += kRepackThreads) dst[k] = s_tile[(k % F) * TS + k / F];
     } else {
-        for (int k = t; k < nc * F; k += kRepackThreads) s_tile[(k % F) * TS + k / F] = dst[k];
+        for (int k = t; k < nc * F; k += kRepackThreads) s_tile[(k % F) * TS + k / F] = src(c0 * F + k);
         __syncthreads();
         for (int e = t; e < F * nc; e += kRepackThreads) {
             const int f = e / nc, c = e % nc;
@@ -769,7 +715,7 @@ int gs4d_hexplane_forward(int N, const float *pts, const uint32_t *order, const 
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
-// backward scratch (deterministic mode): the max words and the 64-bit fixed-point accumulators
+// backward scratch: the scale words and the 64-bit fixed-point accumulators of the packed buffer
 size_t gs4d_hexplane_backward_scratch_bytes(int N, const gs4d_hexplane_layout *lay) {
     (void)N;
     if (!lay) return 256;
@@ -779,30 +725,65 @@ size_t gs4d_hexplane_backward_scratch_bytes(int N, const gs4d_hexplane_layout *l
 int gs4d_hexplane_backward(int N, const float *pts, const uint32_t *order, const gs4d_hexplane_layout *lay,
                            const float *packed, const float *dfeat, float *dpacked, float *dpts, void *scratch,
                            int deterministic, void *stream) {
-    if (N < 0 || !lay || (N > 0 && (!pts || !packed || !dfeat || !dpacked || !dpts))) return 1;
-    if (deterministic && N > 0 && !scratch) return 1;
+    (void)deterministic;  // always deterministic (fixed-point sums); kept for the ABI
+    if (N < 0 || !lay || (N > 0 && (!pts || !packed || !dfeat || !dpts || !scratch))) return 1;
     if (((size_t)pts & 15) || ((size_t)packed & 15) || ((size_t)dfeat & 15) || ((size_t)dpts & 15)) return 1;
+    if (lay->levels < 1 || lay->levels > GS4D_HEXPLANE_MAX_LEVELS) return 1;
     hipStream_t s = (hipStream_t)stream;
-    if (N == 0) return hipMemsetAsync(dpacked, 0, 4 * (size_t)lay->total, s) == hipSuccess ? 0 : 3;
+    if (N == 0) {
+        bool direct = true;
+        for (int p = 0; p < 6 * lay->levels; p++) direct = direct && lay->plane[p].grad;
+        if (direct) {
+            for (int p = 0; p < 6 * lay->levels; p++)
+                if (hipMemsetAsync(lay->plane[p].grad, 0, 4 * (size_t)lay->plane[p].W * lay->plane[p].H * lay->F, s) !=
+                    hipSuccess)
+                    return 3;
+            return 0;
+        }
+        return dpacked && hipMemsetAsync(dpacked, 0, 4 * (size_t)lay->total, s) == hipSuccess ? 0 : 3;
+    }
     const int64_t per_wg = hex_points_per_wg(lay->F);
     const int64_t nwg = ((int64_t)N + per_wg - 1) / per_wg;
-    if (hex_bwd_lds_words(lay->F) > kHexLdsWords) return 1;
-    if (!deterministic) {
-        if (hipMemsetAsync(dpacked, 0, 4 * (size_t)lay->total, s) != hipSuccess) return 3;
-        hipLaunchKernelGGL(hexplane_backward_kernel<false>, dim3((unsigned)nwg), dim3(kHexThreads), 0, s, N, pts, order,
-                           *lay, packed, dfeat, nullptr, (void *)dpacked, dpts);
-        return hipGetLastError() == hipSuccess ? 0 : 3;
-    }
+    if (hex_bwd_window(lay->F) < 4 * 4) return 1;
+    const int np = 6 * lay->levels;
     uint32_t *mx = (uint32_t *)align_up((size_t)scratch, 256);
     unsigned long long *dfix = (unsigned long long *)(mx + 64);
     if (hipMemsetAsync(mx, 0, 256 + 8 * (size_t)lay->total, s) != hipSuccess) return 3;
-    const int64_t nfeat = (int64_t)N * lay->levels * lay->F;
-    hipLaunchKernelGGL(hex_max_kernel, dim3(256), dim3(256), 0, s, nfeat, dfeat, mx);
-    hipLaunchKernelGGL(hex_max_kernel, dim3(256), dim3(256), 0, s, lay->total, packed, mx + 1);
-    hipLaunchKernelGGL(hexplane_backward_kernel<true>, dim3((unsigned)nwg), dim3(kHexThreads), 0, s, N, pts, order,
-                       *lay, packed, dfeat, mx, (void *)dfix, dpts);
-    hipLaunchKernelGGL(hex_fix_to_float_kernel, dim3(1024), dim3(256), 0, s, lay->total, N, mx,
-                       (const long long *)dfix, dpacked);
+    HexMaxRanges rg;
+    rg.nr = 1 + np;
+    rg.x[0] = dfeat;
+    rg.n[0] = (int64_t)N * lay->levels * lay->F;
+    for (int p = 0; p < np; p++) {
+        rg.x[1 + p] = packed + lay->plane[p].offset;
+        rg.n[1 + p] = (int64_t)lay->plane[p].W * lay->plane[p].H * lay->F;
+    }
+    rg.first[0] = 0;
+    for (int r = 0; r < rg.nr; r++)  // >= 4 float4 per thread, at most 128 blocks per range
+        rg.first[r + 1] = rg.first[r] + (int)std::min<int64_t>(128, std::max<int64_t>(1, (rg.n[r] + 4095) / 4096));
+    hipLaunchKernelGGL(hex_max_kernel, dim3(rg.first[rg.nr]), dim3(256), 0, s, rg, mx);
+    hipLaunchKernelGGL(hexplane_backward_kernel, dim3((unsigned)nwg), dim3(kHexThreads), 0, s, N, pts, order, *lay,
+                       packed, dfeat, mx, dfix, dpts);
+    // the fixed-point sums to floats: straight into the (1, F, H, W) gradients when the caller set them (the
+    // unpack transpose with the conversion on its load), else into the packed buffer
+    bool direct = true;
+    for (int p = 0; p < np; p++) direct = direct && lay->plane[p].grad;
+    const dim3 grid((unsigned)repack_tiles(*lay));
+    const size_t lds = 4 * (size_t)lay->F * (repack_cells(lay->F) + 1);
+    const long long *fx = (const long long *)dfix;
+    if (direct) {
+        if (lay->F == 16)
+            hipLaunchKernelGGL((hexplane_repack_kernel<false, 16, true>), grid, dim3(kRepackThreads), lds, s, *lay,
+                               nullptr, fx, mx, N);
+        else if (lay->F == 32)
+            hipLaunchKernelGGL((hexplane_repack_kernel<false, 32, true>), grid, dim3(kRepackThreads), lds, s, *lay,
+                               nullptr, fx, mx, N);
+        else
+            hipLaunchKernelGGL((hexplane_repack_kernel<false, 0, true>), grid, dim3(kRepackThreads), lds, s, *lay,
+                               nullptr, fx, mx, N);
+    } else {
+        if (!dpacked) return 1;
+        hipLaunchKernelGGL(hex_fix_to_packed_kernel, dim3(64, np), dim3(256), 0, s, *lay, N, mx, fx, dpacked);
+    }
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 

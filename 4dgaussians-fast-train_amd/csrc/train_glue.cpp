@@ -6,7 +6,10 @@
 #define ROCBLAS_BETA_FEATURES_API  // rocblas_gemm*_get_solutions: the candidates of the GEMM tuner
 #include <rocblas/rocblas.h>
 
+#include <cmath>
+#include <limits>
 #include <map>
+#include <set>
 #include <mutex>
 #include <unordered_map>
 #include <torch/extension.h>
@@ -82,7 +85,10 @@ void densify_stats(const torch::Tensor &vs_grad, const torch::Tensor &visible, c
     gpu_f32(denom, "denom");
     const int P = (int)vs_grad.size(0);
     need(vs_grad.dim() == 2 && vs_grad.size(1) == 3, "viewspace grad must be (P, 3)");
-    need(visible.scalar_type() == torch::kBool && visible.numel() == P && visible.is_cuda(), "visibility must be bool (P)");
+    // an empty visibility mask: radii > 0 filters (train.py's definition of the mask; radii required then)
+    need(visible.numel() == 0 || (visible.scalar_type() == torch::kBool && visible.numel() == P && visible.is_cuda()),
+         "visibility must be bool (P) or empty");
+    need(visible.numel() || radii.numel(), "densify_stats: an empty visibility mask needs the radii");
     need(grad_accum.numel() == P && denom.numel() == P, "accumulators must have P elements");
     c10::hip::HIPGuard guard(vs_grad.device().index());
     torch::Tensor vis = visible.contiguous();
@@ -92,7 +98,8 @@ void densify_stats(const torch::Tensor &vs_grad, const torch::Tensor &visible, c
         gpu_f32(max_radii, "max_radii2D");
         r = radii.to(torch::kInt32).contiguous();
     }
-    check(gs4d_densify_stats(P, vs_grad.data_ptr<float>(), reinterpret_cast<const uint8_t *>(vis.data_ptr<bool>()),
+    check(gs4d_densify_stats(P, vs_grad.data_ptr<float>(),
+                             vis.numel() ? reinterpret_cast<const uint8_t *>(vis.data_ptr<bool>()) : nullptr,
                              r.defined() ? r.data_ptr<int>() : nullptr, grad_accum.data_ptr<float>(),
                              denom.data_ptr<float>(), r.defined() ? max_radii.data_ptr<float>() : nullptr,
                              stream_of(vs_grad)),
@@ -215,8 +222,8 @@ std::tuple<torch::Tensor, std::vector<torch::Tensor>> hexplane_backward(const to
     const int N = (int)pts.size(0);
     need(packed.numel() == lay.total, "hexplane backward: packed buffer size");
     need(dfeat.dim() == 2 && dfeat.size(0) == N && dfeat.size(1) == (int64_t)lay.levels * lay.F, "hexplane backward: dfeat shape");
-    torch::Tensor dpacked = torch::empty({lay.total}, pts.options());  // every element written
-    torch::Tensor scratch = torch::empty({deterministic ? (int64_t)gs4d_hexplane_backward_scratch_bytes(N, &lay) : 0},
+    (void)deterministic;  // the backward is always deterministic (fixed-point sums)
+    torch::Tensor scratch = torch::empty({(int64_t)gs4d_hexplane_backward_scratch_bytes(N, &lay)},
                                          pts.options().dtype(torch::kUInt8));
     torch::Tensor dpts = torch::empty({N, 4}, pts.options());
     std::vector<torch::Tensor> grads;
@@ -227,11 +234,9 @@ std::tuple<torch::Tensor, std::vector<torch::Tensor>> hexplane_backward(const to
     hipStream_t s = stream_of(pts);
     need(order.numel() == N && order.scalar_type() == torch::kInt32 && order.is_contiguous(), "hexplane backward: order");
     check(gs4d_hexplane_backward(N, pts.data_ptr<float>(), (const uint32_t *)order.data_ptr<int>(), &lay,
-                                 packed.data_ptr<float>(), dfeat.data_ptr<float>(), dpacked.data_ptr<float>(),
-                                 dpts.data_ptr<float>(), deterministic ? scratch.data_ptr() : nullptr,
-                                 deterministic ? 1 : 0, (void *)s),
-          "hexplane backward");
-    check(gs4d_hexplane_unpack(&lay, dpacked.data_ptr<float>(), (void *)s), "hexplane unpack");
+                                 packed.data_ptr<float>(), dfeat.data_ptr<float>(), nullptr,
+                                 dpts.data_ptr<float>(), scratch.data_ptr(), 1, (void *)s),
+          "hexplane backward");  // the plane gradients are written directly (grad pointers set)
     return {dpts, grads};
 }
 
@@ -631,7 +636,9 @@ torch::Tensor feature_relu_forward(const torch::Tensor &x, const torch::Tensor &
 // ---- the field's input points: (pts (N, 4)) from xyz (N, 3+), t (N, 1+), aabb (2, 3); backward dxyz
 torch::Tensor hexplane_points(const torch::Tensor &xyz, const torch::Tensor &t, const torch::Tensor &aabb_) {
     gpu_f32(xyz, "xyz");
-    gpu_f32(t, "timestamps");
+    // t: (N, 1) float32 on the device, rows ld_t apart -- contiguous, or one value broadcast (stride 0)
+    need(t.is_cuda() && t.scalar_type() == torch::kFloat32 && (t.is_contiguous() || t.stride(0) == 0),
+         "hexplane_points: timestamps must be a float32 GPU tensor, contiguous or broadcast");
     need(xyz.dim() == 2 && xyz.size(1) >= 3 && xyz.stride(1) == 1 && t.dim() == 2 && t.size(0) == xyz.size(0),
          "hexplane_points: xyz (N, 3) with unit column stride, t (N, 1)");
     c10::hip::HIPGuard guard(xyz.device().index());
@@ -694,6 +701,10 @@ rocblas_handle rocblas_for(const torch::Tensor &t) {
     rocblas_handle h = nullptr;
     TORCH_CHECK(rocblas_create_handle(&h) == rocblas_status_success, "rocblas_create_handle");
     TORCH_CHECK(rocblas_set_stream(h, st) == rocblas_status_success, "rocblas_set_stream");
+    // no kernel that sums split-K partials with atomics: the train step stays bitwise reproducible whichever
+    // solution the tuner picks (rocBLAS leaves such kernels out of the candidates and its own choice)
+    TORCH_CHECK(rocblas_set_atomics_mode(h, rocblas_atomics_not_allowed) == rocblas_status_success,
+                "rocblas_set_atomics_mode");
     handles.emplace(key, h);
     return h;
 }
@@ -711,6 +722,7 @@ struct TunedGemm {
 };
 std::mutex g_tune_mu;
 std::map<std::string, TunedGemm> g_tuned;  // class key -> choice (and exact keys of re-tuned shapes)
+std::set<std::string> g_verified;          // exact shapes whose kernel's product was checked
 }  // namespace
 
 std::vector<std::tuple<std::string, int64_t, double, double, int64_t>> gemm_tuned() {
@@ -723,7 +735,8 @@ std::vector<std::tuple<std::string, int64_t, double, double, int64_t>> gemm_tune
 
 // A and B may instead both be bf16 (the bf16 MLP path): bf16 products, f32 accumulation, f32 C.
 // tune: true = the tuned kernel for the shape's class (first call of a class tunes it), false = rocBLAS's
-// own pick.  Returns the solution index that ran (0 = rocBLAS's own pick).
+// own pick.  Returns the solution index that ran (0 = rocBLAS's own pick).  The handles disallow atomics, so
+// every candidate is deterministic.
 int64_t gemm_f32(torch::Tensor A, torch::Tensor B, torch::Tensor C, bool ta, bool tb, int64_t m, int64_t n, int64_t k,
                  int64_t lda, int64_t ldb, int64_t ldc, int64_t batch, int64_t sA, int64_t sB, int64_t sC, bool tune) {
     const bool bf = A.scalar_type() == torch::kBFloat16;
@@ -782,14 +795,38 @@ int64_t gemm_f32(torch::Tensor A, torch::Tensor B, torch::Tensor C, bool ta, boo
     };
     const std::string ckey = key_of(false), xkey = key_of(true);
     {
-        std::lock_guard<std::mutex> lk(g_tune_mu);
-        auto it = g_tuned.find(xkey);
-        if (it == g_tuned.end()) it = g_tuned.find(ckey);
-        if (it != g_tuned.end()) {
-            const int32_t sol = it->second.solution;
-            if (sol == 0) return run_default();
-            if (run(sol) == rocblas_status_success) return sol;
-            // rejected for this exact shape: tune it below under its exact key
+        int32_t sol = -1;
+        bool verified = false;
+        {
+            std::lock_guard<std::mutex> lk(g_tune_mu);
+            auto it = g_tuned.find(xkey);
+            if (it == g_tuned.end()) it = g_tuned.find(ckey);
+            if (it != g_tuned.end()) {
+                sol = it->second.solution;
+                verified = g_verified.count(xkey) != 0;
+            }
+        }
+        if (sol == 0) return run_default();
+        if (sol != -1) {
+            if (verified) {
+                if (run(sol) == rocblas_status_success) return sol;
+            } else {
+                // the class's kernel on a shape it was not tuned on: checked once against rocBLAS's own pick
+                run_default();
+                const torch::Tensor ref = torch::from_blob(C.data_ptr<float>(), {batch, n, m},
+                                                           {batch > 1 ? sC : 0, ldc, 1}, C.options()).clone();
+                if (run(sol) == rocblas_status_success) {
+                    const torch::Tensor got =
+                        torch::from_blob(C.data_ptr<float>(), {batch, n, m}, {batch > 1 ? sC : 0, ldc, 1}, C.options());
+                    const float err = (got - ref).abs().max().item<float>();
+                    if (std::isfinite(err) && err <= 1e-4f * ref.abs().max().item<float>()) {
+                        std::lock_guard<std::mutex> lk(g_tune_mu);
+                        g_verified.insert(xkey);
+                        return sol;
+                    }
+                }
+            }
+            // rejected or wrong for this exact shape: tune it below under its exact key
         }
     }
     // the candidates: every solution rocBLAS has for this exact problem
@@ -814,6 +851,19 @@ int64_t gemm_f32(torch::Tensor A, torch::Tensor B, torch::Tensor C, bool ta, boo
         sols.resize((size_t)std::max<rocblas_int>(count, 0));
     }
     sols.insert(sols.begin(), 0);  // rocBLAS's own pick competes too
+    // Every candidate's product is checked against rocBLAS's own pick: an index the library accepts for the
+    // shape is not always a kernel that computes it (on the r05 image some returned in ~2 us having written
+    // nothing), so a candidate counts only when its result matches to 1e-4 of the product's largest entry.
+    auto view = [&]() {
+        return torch::from_blob(C.data_ptr<float>(), {batch, n, m}, {batch > 1 ? sC : 0, ldc, 1}, C.options());
+    };
+    TORCH_CHECK(run(0) == rocblas_status_success, "gemm_f32: rocBLAS's own kernel failed");
+    const torch::Tensor ref = view().clone();
+    const float ref_max = ref.abs().max().item<float>();
+    auto matches = [&]() {
+        const float err = (view() - ref).abs().max().item<float>();
+        return std::isfinite(err) && err <= 1e-4f * ref_max;
+    };
     hipEvent_t e0, e1;
     TORCH_CHECK(hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess, "gemm_f32: hipEventCreate");
     auto time_of = [&](int32_t sol, int reps) -> double {
@@ -829,9 +879,15 @@ int64_t gemm_f32(torch::Tensor A, torch::Tensor B, torch::Tensor C, bool ta, boo
     TunedGemm best;
     best.solution = 0;
     best.us = 1e30;
+    int wrong = 0;
     for (const rocblas_int sol : sols) {
+        if (sol != 0) view().fill_(std::numeric_limits<float>::quiet_NaN());  // a kernel that writes nothing fails
         double us = time_of(sol, 1);
         if (us < 0) continue;
+        if (sol != 0 && !matches()) {
+            wrong++;
+            continue;
+        }
         if (us < 1.5 * best.us) us = std::min(us, time_of(sol, 3));  // a contender: a steadier measurement
         if (sol == 0) best.default_us = us;
         if (us < best.us) {
@@ -848,9 +904,12 @@ int64_t gemm_f32(torch::Tensor A, torch::Tensor B, torch::Tensor C, bool ta, boo
         std::lock_guard<std::mutex> lk(g_tune_mu);
         rejected = g_tuned.count(ckey) != 0;  // the class's kernel did not serve this exact shape
         g_tuned[rejected ? xkey : ckey] = best;
+        g_verified.insert(xkey);
     }
-    fprintf(stderr, "gs4d gemm_f32: tuned %s: solution %d at %.1f us (rocBLAS's own pick %.1f us; %d candidates)\n",
-            (rejected ? xkey : ckey).c_str(), best.solution, best.us, best.default_us, best.candidates);
+    fprintf(stderr,
+            "gs4d gemm_f32: tuned %s: solution %d at %.1f us (rocBLAS's own pick %.1f us; %d candidates, %d with a "
+            "wrong product)\n",
+            (rejected ? xkey : ckey).c_str(), best.solution, best.us, best.default_us, best.candidates, wrong);
     // the result of the chosen kernel (the timing runs wrote C too, but leave no doubt which one did last)
     if (best.solution == 0) return run_default();
     TORCH_CHECK(run(best.solution) == rocblas_status_success, "gemm_f32: tuned solution failed");
@@ -891,7 +950,7 @@ PYBIND11_MODULE(_C, m) {
     m.def("deform_tail_backward", &deform_tail_backward);
     m.def("hexplane_forward", &hexplane_forward, py::arg("pts"), py::arg("planes"), py::arg("order") = py::none());
     m.def("hexplane_backward", &hexplane_backward, py::arg("pts"), py::arg("planes"), py::arg("packed"),
-          py::arg("dfeat"), py::arg("order"), py::arg("deterministic") = false);
+          py::arg("dfeat"), py::arg("order"), py::arg("deterministic") = true);
     m.def("l1_forward", &l1_forward);
     m.def("l1_backward", &l1_backward);
     m.def("l1_loss_grad", &l1_loss_grad);

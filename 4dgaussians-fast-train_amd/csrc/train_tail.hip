@@ -150,7 +150,10 @@ __global__ __launch_bounds__(kTailThreads) void densify_stats_kernel(int P, cons
                                                                      float *__restrict__ denom,
                                                                      float *__restrict__ max_radii) {
     const int i = blockIdx.x * kTailThreads + threadIdx.x;
-    if (i >= P || !visible[i]) return;
+    if (i >= P) return;
+    // without a visibility mask the filter is train.py's own definition of it, radii > 0 (:229-232; for a batch,
+    // max over views of radii > 0 is any over views of visibility)
+    if (visible ? !visible[i] : !(radii[i] > 0)) return;
     if (radii) max_radii[i] = fmaxf(max_radii[i], (float)radii[i]);  // train.py:348
     const float gx = vs_grad[3 * (size_t)i], gy = vs_grad[3 * (size_t)i + 1];
     grad_accum[i] += sqrtf(gx * gx + gy * gy);  // gaussian_model.py:522 torch.norm(grad[:, :2])
@@ -2347,7 +2350,8 @@ int gs4d_sum_slices(const float *parts, int S, int64_t n, float *out, void *stre
 
 int gs4d_densify_stats(int P, const float *viewspace_grad, const uint8_t *visible, const int *radii, float *grad_accum,
                        float *denom, float *max_radii, void *stream) {
-    if (P < 0 || (P > 0 && (!viewspace_grad || !visible || !grad_accum || !denom || (radii && !max_radii)))) return 1;
+    if (P < 0 || (P > 0 && (!viewspace_grad || (!visible && !radii) || !grad_accum || !denom || (radii && !max_radii))))
+        return 1;
     if (P == 0) return 0;
     hipLaunchKernelGGL(densify_stats_kernel, dim3((P + kTailThreads - 1) / kTailThreads), dim3(kTailThreads), 0,
                        (hipStream_t)stream, P, viewspace_grad, visible, radii, grad_accum, denom, max_radii);

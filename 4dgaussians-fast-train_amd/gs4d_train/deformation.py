@@ -230,6 +230,39 @@ def _block_forward_unavailable(dev, err):
     warnings.warn(f"heads block forward unavailable on {dev} ({err}); using the GEMM formulation")
 
 
+class _Stacked(torch.autograd.Function):
+    """torch.cat of tensors that already lie back to back in one storage, without the copy: the forward
+    returns one view over all of them, the backward hands each its slice of the gradient (views: no
+    kernel).  Deformation._pack_heads keeps the heads' first-layer weights and biases so (the parameters
+    stay the reference's separate tensors, for state dicts and optimizers)."""
+
+    @staticmethod
+    def forward(ctx, *ts):
+        ctx.rows = [t.shape[0] for t in ts]
+        n = sum(ctx.rows)
+        shape = (n,) + tuple(ts[0].shape[1:])
+        stride = ts[0].stride()
+        return ts[0].as_strided(shape, stride)
+
+    @staticmethod
+    def backward(ctx, g):
+        return tuple(g.split(ctx.rows, 0))
+
+
+def _stacked(ts):
+    """cat(ts, 0) as a view when the tensors are contiguous and consecutive in one storage, else None."""
+    t0 = ts[0]
+    if not t0.is_contiguous():
+        return None
+    off = t0.storage_offset()
+    for t in ts:
+        if not t.is_contiguous() or t.dtype != t0.dtype or t.device != t0.device or t.shape[1:] != t0.shape[1:] \
+                or t.untyped_storage().data_ptr() != t0.untyped_storage().data_ptr() or t.storage_offset() != off:
+            return None
+        off += t.numel()
+    return _Stacked.apply(*ts)
+
+
 class _DeformHeads(torch.autograd.Function):
     """The deformation heads (scene/deformation.py:73-78, each nn.Sequential(ReLU, Linear(W, W), ReLU,
     Linear(W, n)) applied to the same hidden features) evaluated together: one ReLU of the shared
@@ -519,10 +552,38 @@ class Deformation(nn.Module):
         else:
             h = torch.relu(self.feature_out(feat))  # every head starts with ReLU (scene/deformation.py:73-78)
         heads = [getattr(self, name) for name in active]
-        w1 = torch.cat([hd[1].weight for hd in heads], 0)
-        b1 = torch.cat([hd[1].bias for hd in heads], 0)
+        w1, b1 = self._first_layers(heads)
         second = [t for hd in heads for t in (hd[3].weight, hd[3].bias)]
         return dict(zip(active, _DeformHeadsBF16.apply(h.contiguous(), w1, b1, *second)))
+
+    def _pack_heads(self):
+        """Lay the heads' first-layer weights (and biases) back to back in one storage, each parameter a view
+        of its slice (same Parameter objects, so optimizers and state dicts are untouched): the heads block then
+        takes them as one (kW x W) operand with no per-step cat (_stacked).  Re-done whenever a move, load or
+        surgery has given a parameter its own storage again."""
+        heads = [getattr(self, name) for name in ("pos_deform", "scales_deform", "rotations_deform",
+                                                  "opacity_deform", "shs_deform")]
+        for attr in ("weight", "bias"):
+            ps = [hd[1].__getattr__(attr) for hd in heads]
+            with torch.no_grad():
+                big = torch.cat([p.data for p in ps], 0)
+                o = 0
+                for p in ps:
+                    n = p.shape[0]
+                    p.data = big[o:o + n]
+                    o += n
+
+    def _first_layers(self, heads):
+        """(cat of the heads' first-layer weights, of their biases): views when the storage is packed."""
+        ws = [hd[1].weight for hd in heads]
+        bs = [hd[1].bias for hd in heads]
+        w1, b1 = _stacked(ws), _stacked(bs)
+        if (w1 is None or b1 is None) and ws[0].is_cuda:
+            self._pack_heads()
+            w1, b1 = _stacked(ws), _stacked(bs)
+        if w1 is None or b1 is None:
+            return torch.cat(ws, 0), torch.cat(bs, 0)
+        return w1, b1
 
     def _heads(self, feat, active):
         """{name: head output} of the active heads on the field features (feature_out, then the heads)."""
@@ -530,8 +591,7 @@ class Deformation(nn.Module):
             return self._heads_bf16(feat, active)
         if self.fused_heads and feat.is_cuda and torch.is_grad_enabled() and active:
             heads = [getattr(self, name) for name in active]
-            w1 = torch.cat([hd[1].weight for hd in heads], 0)
-            b1 = torch.cat([hd[1].bias for hd in heads], 0)
+            w1, b1 = self._first_layers(heads)
             second = [t for hd in heads for t in (hd[3].weight, hd[3].bias)]
             lin = self.feature_out[0]
             if len(self.feature_out) == 1 and (feat.shape[1], self.W) in _FeatureReLU.shapes:

@@ -218,11 +218,13 @@ class GaussianModel:
     # ---- densification statistics (gaussian_model.py:521-523, train.py:346-349)
     def add_densification_stats(self, viewspace_grad, update_filter, radii=None):
         """xyz_gradient_accum[f] += |grad[f, :2]|, denom[f] += 1 and (when radii is given, train.py:348)
-        max_radii2D[f] = max(max_radii2D[f], radii[f])."""
+        max_radii2D[f] = max(max_radii2D[f], radii[f]).  update_filter None: f = radii > 0 (train.py:229-232)."""
         if self.fused:
             from .kernels import densify_stats
             densify_stats(viewspace_grad, update_filter, radii, self.xyz_gradient_accum, self.denom, self.max_radii2D)
             return
+        if update_filter is None:
+            update_filter = radii > 0
         if radii is not None:
             self.max_radii2D[update_filter] = torch.max(self.max_radii2D[update_filter], radii[update_filter])
         self.xyz_gradient_accum[update_filter] += torch.norm(viewspace_grad[update_filter, :2], dim=-1, keepdim=True)

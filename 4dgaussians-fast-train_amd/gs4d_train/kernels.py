@@ -49,9 +49,12 @@ def l1_loss_and_grad(network_output, gt, dloss=1.0):
 
 @torch.no_grad()
 def densify_stats(viewspace_grad, visibility, radii, grad_accum, denom, max_radii2D):
-    """train.py:346-349 + gaussian_model.py:521-523 in one launch, in place."""
-    r = radii if radii is not None else torch.empty(0, dtype=torch.int32, device=viewspace_grad.device)
-    _C.densify_stats(viewspace_grad.contiguous(), visibility, r, grad_accum, denom, max_radii2D)
+    """train.py:346-349 + gaussian_model.py:521-523 in one launch, in place.  visibility None: the mask is
+    radii > 0 (train.py's definition of it), evaluated inside the launch."""
+    e = torch.empty(0, dtype=torch.int32, device=viewspace_grad.device)
+    r = radii if radii is not None else e
+    v = visibility if visibility is not None else e.bool()
+    _C.densify_stats(viewspace_grad.contiguous(), v, r, grad_accum, denom, max_radii2D)
 
 
 class FusedAdam(torch.optim.Optimizer):
@@ -227,10 +230,6 @@ class _HexPlane(torch.autograd.Function):
     order_refresh = 100
     _order = None
     _calls = 0
-    # set_deterministic(True): bitwise-reproducible plane gradients (gs4d_hexplane_backward's fixed-point
-    # mode, ~0.1 ms slower per step at 100k points); default: float atomics, as the reference's
-    # grid_sampler backward sums
-    deterministic = False
 
     @staticmethod
     def forward(ctx, pts, *planes):
@@ -248,7 +247,7 @@ class _HexPlane(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dfeat):
         pts, packed, order, *planes = ctx.saved_tensors
-        dpts, dplanes = _C.hexplane_backward(pts, planes, packed, dfeat, order, _HexPlane.deterministic)
+        dpts, dplanes = _C.hexplane_backward(pts, planes, packed, dfeat, order)
         return (dpts, *dplanes)
 
 
@@ -269,9 +268,10 @@ class _HexPoints(torch.autograd.Function):
 
 
 def set_deterministic(flag=True):
-    """Bitwise-reproducible training steps: the one kernel whose sums are schedule-dependent by default
-    is the HexPlane field's backward (float atomics); every other kernel of the step is deterministic."""
-    _HexPlane.deterministic = bool(flag)
+    """Kept for callers of the round-4 API: every kernel of the fused train step is now deterministic (the
+    HexPlane field's backward sums exact 64-bit fixed-point terms; the rasterizer reduces in fixed order),
+    so the step is bitwise reproducible whatever `flag` says."""
+    del flag
 
 
 def hexplane_points(xyz, t, aabb):
@@ -336,8 +336,15 @@ def hexplane_regulation_accumulate_grad(ms_grids, time_smoothness_weight, l1_tim
     for p in planes:
         if p.grad is None:
             p.grad = torch.zeros_like(p)
-    dloss = torch.full((1,), float(scale), device=planes[0].device)
+    # the upstream scale as a device scalar, made once per (device, value): no fill launch per step
+    key = (planes[0].device, float(scale))
+    dloss = _DLOSS.get(key)
+    if dloss is None:
+        dloss = _DLOSS[key] = torch.full((1,), float(scale), device=planes[0].device)
     _C.hexplane_reg_accumulate([p.detach() for p in planes], [p.grad for p in planes], ws, wl, dloss)
+
+
+_DLOSS = {}
 
 
 def hexplane_regulation(ms_grids, time_smoothness_weight, l1_time_planes_weight, plane_tv_weight):

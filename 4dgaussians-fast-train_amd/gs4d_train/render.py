@@ -12,6 +12,69 @@ import torch
 import diff_gaussian_rasterization as dgr
 
 
+_TIMES = {}
+
+
+def _time_value(t, dev):
+    """a (1, 1) float32 device tensor holding t, cached per (device, t)"""
+    key = (str(dev), t)
+    v = _TIMES.get(key)
+    if v is None:
+        if len(_TIMES) > 4096:
+            _TIMES.clear()
+        v = _TIMES[key] = torch.full((1, 1), t, dtype=torch.float32, device=dev)
+    return v
+
+
+class RenderPackage(dict):
+    """render()'s dict (gaussian_renderer/__init__.py:130-138) with "visibility_filter" = radii > 0 formed on
+    first use: the fused train step filters the densification statistics by radii > 0 inside their kernel,
+    so a step that never reads the mask launches no compare for it.  Every key the reference returns is
+    there for any reader (in, keys(), items() and indexing all see it)."""
+
+    def __init__(self, **kw):
+        super().__init__(**kw)
+        self._lazy_vis = True
+
+    def _vis(self):
+        if self._lazy_vis:
+            self._lazy_vis = False
+            dict.__setitem__(self, "visibility_filter", dict.__getitem__(self, "radii") > 0)
+
+    def __getitem__(self, k):
+        if k == "visibility_filter":
+            self._vis()
+        return dict.__getitem__(self, k)
+
+    def get(self, k, default=None):
+        if k == "visibility_filter":
+            self._vis()
+        return dict.get(self, k, default)
+
+    def __contains__(self, k):
+        return k == "visibility_filter" or dict.__contains__(self, k)
+
+    def keys(self):
+        self._vis()
+        return dict.keys(self)
+
+    def items(self):
+        self._vis()
+        return dict.items(self)
+
+    def values(self):
+        self._vis()
+        return dict.values(self)
+
+    def __iter__(self):
+        self._vis()
+        return dict.__iter__(self)
+
+    def __len__(self):
+        self._vis()
+        return dict.__len__(self)
+
+
 def render(viewpoint_camera, pc, pipe_debug, bg_color, scaling_modifier=1.0, stage="fine"):
     xyz = pc.get_xyz
     # the rasterizer's means2D gradient sink (:24-29 builds zeros + 0 and retains its grad; a zero leaf
@@ -28,8 +91,9 @@ def render(viewpoint_camera, pc, pipe_debug, bg_color, scaling_modifier=1.0, sta
         tanfovx=math.tan(viewpoint_camera.FoVx * 0.5), tanfovy=math.tan(viewpoint_camera.FoVy * 0.5),
         bg=bg_color, scale_modifier=scaling_modifier, viewmatrix=view_m, projmatrix=proj_m,
         sh_degree=pc.active_sh_degree, campos=cam_c, prefiltered=False, debug=pipe_debug)
-    # torch.tensor(time).to(dev).repeat(P, 1) (:52): the same float32 column, filled on the device
-    time = torch.full((xyz.shape[0], 1), float(torch.tensor(viewpoint_camera.time)), device=dev)
+    # torch.tensor(time).to(dev).repeat(P, 1) (:52): the same float32 column, as one device value broadcast
+    # over the P rows (made once per (device, time); no fill per call)
+    time = _time_value(float(torch.tensor(viewpoint_camera.time)), dev).expand(xyz.shape[0], 1)
     rasterizer = dgr.GaussianRasterizer(raster_settings=settings)
     if "coarse" not in stage and "fine" not in stage:
         raise NotImplementedError(stage)
@@ -51,5 +115,4 @@ def render(viewpoint_camera, pc, pipe_debug, bg_color, scaling_modifier=1.0, sta
         op = pc.opacity_activation(op)
     image, radii, depth = rasterizer(means3D=m3, means2D=screenspace_points, shs=sh, colors_precomp=None,
                                      opacities=op, scales=sc, rotations=rot, cov3D_precomp=None)
-    return {"render": image, "viewspace_points": screenspace_points, "visibility_filter": radii > 0,
-            "radii": radii, "depth": depth}
+    return RenderPackage(render=image, viewspace_points=screenspace_points, radii=radii, depth=depth)

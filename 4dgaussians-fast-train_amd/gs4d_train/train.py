@@ -37,7 +37,7 @@ def train_step(gaussians, views, opt, hyper, iteration, background, stage="fine"
         images.append(pkg["render"].unsqueeze(0))
         gts.append(gt.unsqueeze(0))
         radii_list.append(pkg["radii"].unsqueeze(0))
-        vis_list.append(pkg["visibility_filter"].unsqueeze(0))
+        vis_list.append(pkg)  # its visibility_filter (radii > 0) is read only where needed below
         vs_list.append(pkg["viewspace_points"])
     P = gaussians.get_xyz.shape[0]
     dev = gaussians.get_xyz.device
@@ -45,8 +45,11 @@ def train_step(gaussians, views, opt, hyper, iteration, background, stage="fine"
     # per rank those are the view's own tensors (no copies, no reductions)
     one = len(mine) == 1
     if one:
-        radii, visibility_filter = radii_list[0][0], vis_list[0][0]
+        # the fused statistics filter by radii > 0 inside their kernel (visibility_filter's definition)
+        radii = radii_list[0][0]
+        visibility_filter = None if (gaussians.fused and not data_parallel) else vis_list[0]["visibility_filter"]
     else:
+        vis_list = [pk["visibility_filter"].unsqueeze(0) for pk in vis_list]
         radii = torch.cat(radii_list, 0).max(dim=0).values if radii_list else torch.zeros(P, dtype=torch.int32,
                                                                                        device=dev)
         visibility_filter = torch.cat(vis_list).any(dim=0) if vis_list else torch.zeros(P, dtype=torch.bool,
@@ -80,7 +83,9 @@ def train_step(gaussians, views, opt, hyper, iteration, background, stage="fine"
         if fused:
             # the regulariser depends only on the planes: its value joins the reported loss and its
             # gradient is added to the planes' gradients after the backward, in one launch
-            reg_deferred = gaussians.regulation_value(*reg_w) * reg_scale
+            reg_deferred = gaussians.regulation_value(*reg_w)
+            if reg_scale != 1.0:
+                reg_deferred = reg_deferred * reg_scale
         else:
             reg = gaussians.compute_regulation(*reg_w)
             loss = loss + reg * reg_scale
@@ -105,7 +110,10 @@ def train_step(gaussians, views, opt, hyper, iteration, background, stage="fine"
         for t in vs_list:
             if t.grad is not None:
                 viewspace_grad = viewspace_grad + t.grad
-    loss_out = loss.detach().reshape(1).clone()
+    # the returned loss: a view when nothing writes it later (the data-parallel all-reduce sums in place)
+    loss_out = loss.detach().reshape(1)
+    if data_parallel:
+        loss_out = loss_out.clone()
     if data_parallel and dp.world() > 1:
         # a parameter gets a gradient on every replica iff some rank produced one (a rank without views
         # produces none); parameters no rank touched keep grad None, so the optimizer skips them as the

@@ -56,7 +56,8 @@ int gs4d_sum_slices(const float *parts, int S, int64_t n, float *out, void *stre
 
 /* ---- densification statistics: train.py:346-349 and scene/gaussian_model.py:521-523.
  * For every i with visible[i]: max_radii[i] = max(max_radii[i], radii[i]) (skipped when radii is
- * NULL), grad_accum[i] += |viewspace_grad[i, 0:2]|, denom[i] += 1.  viewspace_grad is (P, 3). */
+ * NULL), grad_accum[i] += |viewspace_grad[i, 0:2]|, denom[i] += 1.  viewspace_grad is (P, 3).  visible may
+ * be NULL when radii is given: the mask is then radii[i] > 0, train.py:229-232's own definition of it. */
 int gs4d_densify_stats(int P, const float *viewspace_grad, const uint8_t *visible, const int *radii, float *grad_accum,
                        float *denom, float *max_radii, void *stream);
 
@@ -94,10 +95,12 @@ int gs4d_adam_step(const gs4d_adam_batch *batch, void *stream);
  * parameter tensor with W = reso[c0], H = reso[c1]; the kernels read a packed channels-last copy
  * of all planes (gs4d_hexplane_pack); the backward writes the plane gradients (every element: no zero
  * fill needed) into a packed buffer that gs4d_hexplane_unpack writes back to (1, F, H, W) gradient
- * tensors.  dpts receives the gradient w.r.t. pts (all 4 columns).  deterministic != 0: the plane
- * gradients are bitwise reproducible (each workgroup's sum in a fixed order, exact 64-bit fixed-point
- * integer atomics across workgroups; needs the scratch); 0: float atomics (the reference's kind of sum,
- * faster; scratch may be NULL). */
+ * tensors.  dpts receives the gradient w.r.t. pts (all 4 columns).  The plane gradients are always bitwise
+ * reproducible: every term is rounded once to a 64-bit fixed-point integer and the integer sums (LDS windows
+ * per workgroup, integer atomics across workgroups) are exact; `deterministic` is accepted and ignored (the
+ * round-4 ABI's float-atomic mode is gone).  scratch: gs4d_hexplane_backward_scratch_bytes, required.  When
+ * every lay->plane[p].grad is set, the gradients are written straight to those (1, F, H, W) tensors and
+ * dpacked may be NULL (no packed round trip, no unpack call); otherwise dpacked receives them. */
 #define GS4D_HEXPLANE_MAX_LEVELS 4
 typedef struct {
     int W, H;
@@ -121,7 +124,7 @@ size_t gs4d_hexplane_order_scratch_bytes(int N);
 int gs4d_hexplane_order(int N, const float *pts, uint32_t *order, void *scratch, void *stream);
 int gs4d_hexplane_forward(int N, const float *pts, const uint32_t *order, const gs4d_hexplane_layout *lay,
                           const float *packed, float *feat, void *stream);
-/* scratch of gs4d_hexplane_backward's deterministic mode: 64-bit accumulators for the packed buffer */
+/* scratch of gs4d_hexplane_backward: the scale words and 64-bit accumulators for the packed buffer */
 size_t gs4d_hexplane_backward_scratch_bytes(int N, const gs4d_hexplane_layout *lay);
 int gs4d_hexplane_backward(int N, const float *pts, const uint32_t *order, const gs4d_hexplane_layout *lay,
                            const float *packed, const float *dfeat, float *dpacked, float *dpts, void *scratch,

@@ -80,6 +80,12 @@ def analyse(s):
         tot["bwd_eval"] += 128 * int(half[walked].sum())
         tot["bwd_half_steps"] = tot.get("bwd_half_steps", 0) + int(half[walked].sum())
         tot["bwd_full_half_steps"] = tot.get("bwd_full_half_steps", 0) + int(full[walked].sum())
+        # the same walk with each half skipped past the largest n_contrib of ITS pixels
+        for h in range(2):
+            lh = int(last.reshape(2, 128)[h].max())
+            lim_h = int(epos[lh - 1]) if lh > 0 else 0
+            tot["bwd_half_steps_perhalf"] = tot.get("bwd_half_steps_perhalf", 0) + int(
+                half[emit & (epos <= lim_h), h].sum())
         # forward: per half, splats reaching it until every live pixel of the half terminated (or the end)
         for h in range(2):
             lh = last.reshape(2, 128)[h]
