@@ -26,7 +26,8 @@ struct GeomState {
     float2 *xy;               // P   pixel-space centre (forward.cu:233)
     float4 *conic_opacity;    // P   (conic.a, conic.b, conic.c, opacity) (forward.cu:254)
     float4 *splat;            // 3P  packed blend record per Gaussian (render.hip): (x, y, -a/2 log2e, -b log2e),
-                              //     (-c/2 log2e, opacity, 1/opacity, depth), (r, g, b, 0)
+                              //     (-c/2 log2e, m, 1/opacity, depth), (r, g, b, lo): m = 1 and lo = log2 opacity
+                              //     for a positive-definite conic (o G = 2^(power2 + lo)), else m = opacity, lo = 0
     float *cov3D;             // 6P  world covariance (forward.cu:211)
     uint8_t *clamped;         // P   bit c set when channel c was clamped (forward.cu:67-69)
     uint32_t *tiles_touched;  // P   3-sigma rect area (the reference's tiles_touched, forward.cu:255)

@@ -89,11 +89,17 @@ __global__ __launch_bounds__(kPreprocessBlock) void preprocess_kernel(
                     g.xy[idx] = point_image;
                     g.conic_opacity[idx] = co;
                     // the blend kernels' packed record: log2(e) folded into the conic (forward.cu:340-342 in
-                    // base 2), 1/o for the backward's per-record division, colour and view depth
+                    // base 2), 1/o for the backward's per-record division, colour and view depth.  For a
+                    // positive-definite conic (the blend kernels' conic_pd on these same stored values) the
+                    // opacity is folded into the exponent too: o G = 2^(power2 + log2 o), the record's
+                    // multiplier is 1 and the blend's common path skips the o * G multiply; any other conic
+                    // keeps multiplier o and exponent offset 0 (its power test needs the bare exponent).
                     float4 *rec = g.splat + 3 * (size_t)idx;
-                    rec[0] = make_float4(point_image.x, point_image.y, (-0.5f * co.x) * kLog2e, (-co.y) * kLog2e);
-                    rec[1] = make_float4((-0.5f * co.z) * kLog2e, co.w, co.w > 0.f ? 1.0f / co.w : 0.f, p_view.z);
-                    rec[2] = make_float4(rgb.x, rgb.y, rgb.z, 0.f);
+                    const float ga = (-0.5f * co.x) * kLog2e, gb = (-co.y) * kLog2e, gc = (-0.5f * co.z) * kLog2e;
+                    const bool pd = ga < 0.f && 4.f * ga * gc - gb * gb > 0.f;
+                    rec[0] = make_float4(point_image.x, point_image.y, ga, gb);
+                    rec[1] = make_float4(gc, pd ? 1.f : co.w, co.w > 0.f ? 1.0f / co.w : 0.f, p_view.z);
+                    rec[2] = make_float4(rgb.x, rgb.y, rgb.z, pd ? log2f(co.w) : 0.f);
                     my_r = (int)my_radius;
                     touched = area;
                 }

@@ -41,8 +41,9 @@ __device__ __forceinline__ float hsum(f2 v) {
 }
 
 
-// Blend-ready splat constants.  geo = (x, y - yc, -a/2 log2e, -b log2e), opc = (-c/2 log2e, opacity, -, -),
-// col = (r, g, b, depth).  power2 = log2(e) * power (forward.cu:340-342) at offset d = mean - pixel.
+// Blend-ready splat constants.  geo = (x, y - yc, -a/2 log2e, -b log2e), opc = (-c/2 log2e, m, 1/o, lo),
+// col = (r, g, b, depth): o G = m 2^(power2 + lo) with m = 1, lo = log2 o for a positive-definite conic (the
+// opacity folded into the exponent: the common path has no o * G multiply) and m = o, lo = 0 otherwise.  power2 = log2(e) * power (forward.cu:340-342) at offset d = mean - pixel.
 // Rows are measured from the tile's centre row yc = 16 ty + 7.5 (pixel row py = yc + yl, yl a
 // half-integer in [-7.5, 7.5]): dy = (my - yc) - yl, the same two roundings in both kernels.
 struct SplatLDS {
@@ -88,7 +89,7 @@ __device__ __forceinline__ void read_raw_lds(SplatRegs &s, const RawLDS &r, int 
     if (valid) {
         const float4 s0 = r.s0[lane], s1 = r.s1[lane], s2 = r.s2[lane];
         s.geo = make_float4(s0.x, s0.y - yc, s0.z, s0.w);
-        s.opc = make_float4(s1.x, s1.y, s1.z, 0.f);
+        s.opc = make_float4(s1.x, s1.y, s1.z, s2.w);  // -c/2 log2e, multiplier m, 1/o, exponent offset lo
         s.col = make_float4(s2.x, s2.y, s2.z, s1.w);  // rgb, view depth
     } else {
         s.geo = s.opc = s.col = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -100,16 +101,19 @@ __device__ __forceinline__ void read_raw_lds(SplatRegs &s, const RawLDS &r, int 
 // alpha = min(0.99, o G) caps nothing for opacities at or below kCapFree: G = 2^power <= 1 wherever the
 // power test passes (up to an ulp), so o G <= 0.98 (1 + ulp) < 0.99.
 constexpr float kCapFree = 0.98f;
+constexpr float kInvCapFree = 1.f / kCapFree;  // the record holds 1/o: o > kCapFree <=> 1/o < kInvCapFree
 struct Falloff {
     f2 dy, pw, G, alpha;
 };
-template <bool CAP = true>
+// pa = geo.z dx^2 + lo (lane constant per splat: fmaf(geo.z dx, dx, lo)); FOLD: every splat of the walk has a
+// positive-definite conic, so m = 1 and o G is the exponential itself
+template <bool CAP = true, bool FOLD = false>
 __device__ __forceinline__ Falloff falloff(const float4 &geo, const float4 &opc, float pa, float pb, f2 yl) {
     Falloff f;
     f.dy = bc2(geo.y) - yl;
     f.pw = fma2(f.dy, fma2(bc2(opc.x), f.dy, bc2(pb)), bc2(pa));
     f.G = f2{__builtin_amdgcn_exp2f(f.pw.x), __builtin_amdgcn_exp2f(f.pw.y)};
-    const f2 al = bc2(opc.y) * f.G;
+    const f2 al = FOLD ? f.G : bc2(opc.y) * f.G;
     // without CAP every splat of the batch has opacity <= kCapFree: min(0.99, o G) = o G
     f.alpha = CAP ? f2{fminf(0.99f, al.x), fminf(0.99f, al.y)} : al;
     return f;
@@ -121,9 +125,10 @@ __device__ __forceinline__ bool lane_bit(uint64_t m) { return __builtin_amdgcn_i
 // ---------------------------------------------------------------------------------------------
 // A splat whose conic is positive definite has power <= 0 at every pixel (up to rounding at its
 // centre), so the power test of forward.cu:341 is only evaluated in batches holding another splat.
+// The same float operations, uncontracted, as preprocess.hip's choice of the record's opacity form.
 __device__ __forceinline__ bool conic_pd(const float4 &geo, const float4 &opc) {
     // geo.z = -a/2 k, geo.w = -b k, opc.x = -c/2 k (k = log2 e > 0): a > 0 and ac - b^2 > 0
-    return geo.z < 0.f && 4.f * geo.z * opc.x - geo.w * geo.w > 0.f;
+    return geo.z < 0.f && __fsub_rn(__fmul_rn(__fmul_rn(4.f, geo.z), opc.x), __fmul_rn(geo.w, geo.w)) > 0.f;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -343,7 +348,7 @@ __global__ __launch_bounds__(128) void render_forward_kernel(Args a, const uint2
         nxt.reach = valid ? rnxt : 0u;
         const uint64_t reach = ballot((nxt.reach >> h) & 1u);
         const uint64_t nonpd = ballot(!conic_pd(nxt.geo, nxt.opc));
-        const bool cap = ballot(valid && nxt.opc.y > kCapFree) != 0;  // wave-uniform: a splat the 0.99 cap can bind
+        const bool cap = ballot(valid && nxt.opc.z < kInvCapFree) != 0;  // wave-uniform: a splat the 0.99 cap can bind
         // one wave writes and reads its own staging area: LDS operations of a wave complete in order
         __builtin_amdgcn_wave_barrier();
         s_sp[lane].geo = nxt.geo;
@@ -380,7 +385,7 @@ __global__ __launch_bounds__(128) void render_forward_kernel(Args a, const uint2
             T = tT;
         };
         auto walk = [&](auto capc, auto pwc) {
-            constexpr bool CAP = decltype(capc)::value;
+            constexpr bool CAP = decltype(capc)::value, FOLD = !decltype(pwc)::value;
             for (uint64_t todo = reach; todo != 0;) {
                 const uint32_t j0 = (uint32_t)__builtin_ctzll(todo);
                 todo &= todo - 1;
@@ -390,8 +395,8 @@ __global__ __launch_bounds__(128) void render_forward_kernel(Args a, const uint2
                 const float4 geo0 = s_sp[j0].geo, opc0 = s_sp[j0].opc, col0 = s_sp[j0].col;
                 const float4 geo1 = s_sp[j1].geo, opc1 = s_sp[j1].opc, col1 = s_sp[j1].col;
                 const float dx0 = geo0.x - pfx, dx1 = geo1.x - pfx;
-                const Falloff f0 = falloff<CAP>(geo0, opc0, geo0.z * dx0 * dx0, geo0.w * dx0, yl);
-                const Falloff f1 = falloff<CAP>(geo1, opc1, geo1.z * dx1 * dx1, geo1.w * dx1, yl);
+                const Falloff f0 = falloff<CAP, FOLD>(geo0, opc0, fmaf(geo0.z * dx0, dx0, opc0.w), geo0.w * dx0, yl);
+                const Falloff f1 = falloff<CAP, FOLD>(geo1, opc1, fmaf(geo1.z * dx1, dx1, opc1.w), geo1.w * dx1, yl);
                 blend(f0, col0, j0, pwc);
                 if (two) blend(f1, col1, j1, pwc);
             }
@@ -446,9 +451,9 @@ __global__ void pair_alpha_kernel(const float4 *__restrict__ splat, int n, const
     const float yc = (float)(ty * kBlockY) + 7.5f;
     const float yl = (float)(py[i] - ty * kBlockY) - 7.5f;
     const float4 geo = make_float4(s0.x, s0.y - yc, s0.z, s0.w);
-    const float4 opc = make_float4(s1.x, s1.y, s1.z, 0.f);
+    const float4 opc = make_float4(s1.x, s1.y, s1.z, rec[2].w);
     const float dx = geo.x - (float)px[i];
-    const Falloff f = falloff<false>(geo, opc, geo.z * dx * dx, geo.w * dx, f2{yl, yl});
+    const Falloff f = falloff<false>(geo, opc, fmaf(geo.z * dx, dx, opc.w), geo.w * dx, f2{yl, yl});
     og[i] = f.alpha.x;
     pw[i] = f.pw.x;
 }
@@ -560,7 +565,9 @@ __device__ __forceinline__ HalfAlpha half_alpha(const f2 Y2, const f2 C2, const 
     const f2 dy = Y2 - yl;  // Y2 = my - yc
     const f2 pw = fma2(dy, fma2(C2, dy, pb2), pa2);
     const f2 G = f2{__builtin_amdgcn_exp2f(pw.x), __builtin_amdgcn_exp2f(pw.y)};
-    const f2 al = O2 * G;  // o G: min(0.99, o G) >= 1/255 iff o G >= 1/255
+    // o G: min(0.99, o G) >= 1/255 iff o G >= 1/255.  Without GEN every splat of the pair has a positive-
+    // definite conic, whose record folds o into the exponent (O2 = m = 1)
+    const f2 al = GEN ? O2 * G : G;
     // backward.cu:486-497: contributor test, alpha < 1/255 and power > 0 skip -- the forward's decisions
     bool k0 = al.x >= kAlphaMin, k1 = al.y >= kAlphaMin;
     if (!ALL) {
@@ -757,7 +764,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
         read_raw_lds(nxt, s_raw, lane, lane < n, yc, true);  // my - yc, as the forward stages it
         // per-splat wave masks (the staged zero splats past n are neither)
         const uint64_t nonpd = ballot(lane < n && !conic_pd(nxt.geo, nxt.opc));
-        const uint64_t hiop = ballot(nxt.opc.y > kCapFree);
+        const uint64_t hiop = ballot(lane < n && nxt.opc.z < kInvCapFree);
         __syncthreads();
         s_sp[lane].geo = nxt.geo;
         s_sp[lane].opc = nxt.opc;
@@ -781,7 +788,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
             for (int i = 0; i < 2; i++) {
                 geo[i] = s_sp[j + i].geo; opc[i] = s_sp[j + i].opc; col[i] = s_sp[j + i].col;
                 dxs[i] = geo[i].x - pfx;
-                pa[i] = geo[i].z * dxs[i] * dxs[i];  // forward: geo.z * dx * dx, geo.w * dx
+                pa[i] = fmaf(geo[i].z * dxs[i], dxs[i], opc[i].w);  // forward: fmaf(geo.z dx, dx, lo), geo.w dx
                 pb[i] = geo[i].w * dxs[i];
             }
             f2 U[2][6];
