@@ -762,7 +762,9 @@ int64_t gemm_f32(torch::Tensor A, torch::Tensor B, torch::Tensor C, bool ta, boo
     const float one = 1.f, zero = 0.f;
     const rocblas_operation oa = ta ? rocblas_operation_transpose : rocblas_operation_none;
     const rocblas_operation ob = tb ? rocblas_operation_transpose : rocblas_operation_none;
-    const uint32_t flags = rocblas_gemm_flags_check_solution_index;
+    // no flags: rocblas_gemm_flags_check_solution_index would make the call only validate the index and return
+    // without computing (an earlier tuner passed it and timed kernels that never ran)
+    const uint32_t flags = rocblas_gemm_flags_none;
     auto run = [&](int32_t sol) {
         const rocblas_gemm_algo algo = sol ? rocblas_gemm_algo_solution_index : rocblas_gemm_algo_standard;
         if (batch == 1)
@@ -851,18 +853,21 @@ int64_t gemm_f32(torch::Tensor A, torch::Tensor B, torch::Tensor C, bool ta, boo
         sols.resize((size_t)std::max<rocblas_int>(count, 0));
     }
     sols.insert(sols.begin(), 0);  // rocBLAS's own pick competes too
-    // Every candidate's product is checked against rocBLAS's own pick: an index the library accepts for the
-    // shape is not always a kernel that computes it (on the r05 image some returned in ~2 us having written
-    // nothing), so a candidate counts only when its result matches to 1e-4 of the product's largest entry.
+    // Every candidate's product is checked against rocBLAS's own pick: a candidate counts only when its result
+    // matches to 1e-4 of the product's largest entry (a guard against a kernel that skips work or writes
+    // nothing; an earlier version ran candidates with the check-only flag and timed calls that never computed).
     auto view = [&]() {
         return torch::from_blob(C.data_ptr<float>(), {batch, n, m}, {batch > 1 ? sC : 0, ldc, 1}, C.options());
     };
     TORCH_CHECK(run(0) == rocblas_status_success, "gemm_f32: rocBLAS's own kernel failed");
     const torch::Tensor ref = view().clone();
     const float ref_max = ref.abs().max().item<float>();
+    float first_wrong = 0.f;  // the first rejected candidate's error (the log line's diagnostic)
     auto matches = [&]() {
         const float err = (view() - ref).abs().max().item<float>();
-        return std::isfinite(err) && err <= 1e-4f * ref_max;
+        const bool ok = std::isfinite(err) && err <= 1e-4f * ref_max;
+        if (!ok && first_wrong == 0.f) first_wrong = std::isfinite(err) ? err : INFINITY;
+        return ok;
     };
     hipEvent_t e0, e1;
     TORCH_CHECK(hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess, "gemm_f32: hipEventCreate");
@@ -881,7 +886,8 @@ int64_t gemm_f32(torch::Tensor A, torch::Tensor B, torch::Tensor C, bool ta, boo
     best.us = 1e30;
     int wrong = 0;
     for (const rocblas_int sol : sols) {
-        if (sol != 0) view().fill_(std::numeric_limits<float>::quiet_NaN());  // a kernel that writes nothing fails
+        // a kernel that writes nothing fails (a finite poison, so the log can report by how much)
+        if (sol != 0) view().fill_(3.0e38f);
         double us = time_of(sol, 1);
         if (us < 0) continue;
         if (sol != 0 && !matches()) {
@@ -908,8 +914,9 @@ int64_t gemm_f32(torch::Tensor A, torch::Tensor B, torch::Tensor C, bool ta, boo
     }
     fprintf(stderr,
             "gs4d gemm_f32: tuned %s: solution %d at %.1f us (rocBLAS's own pick %.1f us; %d candidates, %d with a "
-            "wrong product)\n",
-            (rejected ? xkey : ckey).c_str(), best.solution, best.us, best.default_us, best.candidates, wrong);
+            "wrong product, first error %.3g of max %.3g)\n",
+            (rejected ? xkey : ckey).c_str(), best.solution, best.us, best.default_us, best.candidates, wrong,
+            (double)first_wrong, (double)ref_max);
     // the result of the chosen kernel (the timing runs wrote C too, but leave no doubt which one did last)
     if (best.solution == 0) return run_default();
     TORCH_CHECK(run(best.solution) == rocblas_status_success, "gemm_f32: tuned solution failed");

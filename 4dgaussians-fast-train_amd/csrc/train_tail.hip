@@ -2621,7 +2621,7 @@ int gs4d_hexplane_points(int N, const float *xyz, int64_t ld_xyz, const float *t
                          float *pts, void *stream) {
     if (N < 0 || !aabb) return 1;
     if (N == 0) return 0;
-    if (!xyz || !t || !pts || ((size_t)pts & 15) != 0 || ld_xyz < 3 || ld_t < 1) return 1;
+    if (!xyz || !t || !pts || ((size_t)pts & 15) != 0 || ld_xyz < 3 || ld_t < 0) return 1;
     hipLaunchKernelGGL(hex_points_kernel, dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream, N, xyz, ld_xyz, t,
                        ld_t, aabb, (float4 *)pts);
     return hipGetLastError() == hipSuccess ? 0 : 3;

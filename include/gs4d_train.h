@@ -133,7 +133,7 @@ int gs4d_hexplane_backward(int N, const float *pts, const uint32_t *order, const
 /* ---- The field's input points, scene/hexplane.py:20-21 (normalize_aabb with aabb = (max corner, min corner))
  * + :166 (torch.cat((pts, timestamps), -1)) in one pass: pts (N, 4) = ((xyz - aabb[0]) * s - 1, t) with
  * s = (1 / (aabb[1] - aabb[0])) * 2, the reference's float operations; xyz rows ld_xyz floats apart, t rows
- * ld_t apart, aabb (2, 3) on the device, pts 16-byte aligned.  backward: dxyz (N, 3) = dpts[:, :3] * s. */
+ * ld_t apart (ld_t 0: one time for every point), aabb (2, 3) on the device, pts 16-byte aligned.  backward: dxyz (N, 3) = dpts[:, :3] * s. */
 int gs4d_hexplane_points(int N, const float *xyz, int64_t ld_xyz, const float *t, int64_t ld_t, const float *aabb,
                          float *pts, void *stream);
 int gs4d_hexplane_points_backward(int N, const float *dpts, const float *aabb, float *dxyz, void *stream);

@@ -384,6 +384,10 @@ def test_mlp_gemms_match_fp64(P, N, K, col0):
         return -(-v // step) * step
     key = f"f32 nn m={K} n={bucket(P)} k={N} lda={K} ldb={N} ldc={K} batch=1 dev={o.device.index}"
     assert tuned.get(key) == sol, (key, sol, tuned)
+    # the tuner compared real kernels: rocBLAS's own pick and at least one more whose product matched (a check
+    # that rejects every candidate leaves the library's pick alone, silently)
+    cands = {k: c for k, _, _, _, c in _C.gemm_tuned()}
+    assert cands[key] >= 2, (key, cands[key])
     assert float(((o.double() - refx).abs() - 1e-5 * (dy.double().abs() @ w.double().abs())).max()) <= 0
     if P >= 4096:
         S = P // 1024
