@@ -41,7 +41,7 @@ __device__ __forceinline__ float hsum(f2 v) {
 }
 
 
-// Blend-ready splat constants.  geo = (x, y - yc, -a/2 log2e, -b log2e), opc = (-c/2 log2e, m, 1/o, lo),
+// Blend-ready splat constants.  geo = (x, y - yc, -a/2 log2e, -b log2e), opc = (-c/2 log2e, lo, 1/o, m),
 // col = (r, g, b, depth): o G = m 2^(power2 + lo) with m = 1, lo = log2 o for a positive-definite conic (the
 // opacity folded into the exponent: the common path has no o * G multiply) and m = o, lo = 0 otherwise.  power2 = log2(e) * power (forward.cu:340-342) at offset d = mean - pixel.
 // Rows are measured from the tile's centre row yc = 16 ty + 7.5 (pixel row py = yc + yl, yl a
@@ -89,7 +89,8 @@ __device__ __forceinline__ void read_raw_lds(SplatRegs &s, const RawLDS &r, int 
     if (valid) {
         const float4 s0 = r.s0[lane], s1 = r.s1[lane], s2 = r.s2[lane];
         s.geo = make_float4(s0.x, s0.y - yc, s0.z, s0.w);
-        s.opc = make_float4(s1.x, s1.y, s1.z, s2.w);  // -c/2 log2e, multiplier m, 1/o, exponent offset lo
+        s.opc = make_float4(s1.x, s2.w, s1.z, s1.y);  // -c/2 log2e, exponent offset lo, 1/o, multiplier m
+        // (the walks read c and lo as one 8-byte LDS load)
         s.col = make_float4(s2.x, s2.y, s2.z, s1.w);  // rgb, view depth
     } else {
         s.geo = s.opc = s.col = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -113,12 +114,18 @@ __device__ __forceinline__ Falloff falloff(const float4 &geo, const float4 &opc,
     f.dy = bc2(geo.y) - yl;
     f.pw = fma2(f.dy, fma2(bc2(opc.x), f.dy, bc2(pb)), bc2(pa));
     f.G = f2{__builtin_amdgcn_exp2f(f.pw.x), __builtin_amdgcn_exp2f(f.pw.y)};
-    const f2 al = FOLD ? f.G : bc2(opc.y) * f.G;
+    const f2 al = FOLD ? f.G : bc2(opc.w) * f.G;
     // without CAP every splat of the batch has opacity <= kCapFree: min(0.99, o G) = o G
     f.alpha = CAP ? f2{fminf(0.99f, al.x), fminf(0.99f, al.y)} : al;
     return f;
 }
 __device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+// a wave-uniform 64-bit mask kept in scalar registers (the compiler's divergence analysis may otherwise move a
+// loop-carried mask to VGPRs and turn its bit scans into vector code)
+__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
+    return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+           __builtin_amdgcn_readfirstlane((uint32_t)v);
+}
 // this lane's bit of a wave mask, used directly as the select condition (no VALU shift)
 __device__ __forceinline__ bool lane_bit(uint64_t m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
 
@@ -395,8 +402,8 @@ __global__ __launch_bounds__(128) void render_forward_kernel(Args a, const uint2
                 const float4 geo0 = s_sp[j0].geo, opc0 = s_sp[j0].opc, col0 = s_sp[j0].col;
                 const float4 geo1 = s_sp[j1].geo, opc1 = s_sp[j1].opc, col1 = s_sp[j1].col;
                 const float dx0 = geo0.x - pfx, dx1 = geo1.x - pfx;
-                const Falloff f0 = falloff<CAP, FOLD>(geo0, opc0, fmaf(geo0.z * dx0, dx0, opc0.w), geo0.w * dx0, yl);
-                const Falloff f1 = falloff<CAP, FOLD>(geo1, opc1, fmaf(geo1.z * dx1, dx1, opc1.w), geo1.w * dx1, yl);
+                const Falloff f0 = falloff<CAP, FOLD>(geo0, opc0, fmaf(geo0.z * dx0, dx0, opc0.y), geo0.w * dx0, yl);
+                const Falloff f1 = falloff<CAP, FOLD>(geo1, opc1, fmaf(geo1.z * dx1, dx1, opc1.y), geo1.w * dx1, yl);
                 blend(f0, col0, j0, pwc);
                 if (two) blend(f1, col1, j1, pwc);
             }
@@ -451,9 +458,9 @@ __global__ void pair_alpha_kernel(const float4 *__restrict__ splat, int n, const
     const float yc = (float)(ty * kBlockY) + 7.5f;
     const float yl = (float)(py[i] - ty * kBlockY) - 7.5f;
     const float4 geo = make_float4(s0.x, s0.y - yc, s0.z, s0.w);
-    const float4 opc = make_float4(s1.x, s1.y, s1.z, rec[2].w);
+    const float4 opc = make_float4(s1.x, rec[2].w, s1.z, s1.y);
     const float dx = geo.x - (float)px[i];
-    const Falloff f = falloff<false>(geo, opc, fmaf(geo.z * dx, dx, opc.w), geo.w * dx, f2{yl, yl});
+    const Falloff f = falloff<false>(geo, opc, fmaf(geo.z * dx, dx, opc.y), geo.w * dx, f2{yl, yl});
     og[i] = f.alpha.x;
     pw[i] = f.pw.x;
 }
@@ -788,7 +795,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
             for (int i = 0; i < 2; i++) {
                 geo[i] = s_sp[j + i].geo; opc[i] = s_sp[j + i].opc; col[i] = s_sp[j + i].col;
                 dxs[i] = geo[i].x - pfx;
-                pa[i] = fmaf(geo[i].z * dxs[i], dxs[i], opc[i].w);  // forward: fmaf(geo.z dx, dx, lo), geo.w dx
+                pa[i] = fmaf(geo[i].z * dxs[i], dxs[i], opc[i].y);  // forward: fmaf(geo.z dx, dx, lo), geo.w dx
                 pb[i] = geo[i].w * dxs[i];
             }
             f2 U[2][6];
@@ -799,7 +806,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
             SplatOps so[2];
 #pragma unroll
             for (int i = 0; i < 2; i++)
-                so[i] = SplatOps{bc2(geo[i].y), bc2(opc[i].x), bc2(opc[i].y), bc2(col[i].x), bc2(col[i].y),
+                so[i] = SplatOps{bc2(geo[i].y), bc2(opc[i].x), bc2(opc[i].w), bc2(col[i].x), bc2(col[i].y),
                                  bc2(col[i].z), bc2(pa[i]), bc2(pb[i]), ((nonpd >> (j + i)) & 1) != 0,
                                  (uint32_t)(end - 1 - (j + i))};
 #pragma unroll

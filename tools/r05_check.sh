@@ -18,5 +18,5 @@ PROBE_ARGS="metric --bf16" TAG=${TAG}_bf16 bash tools/train_seq.sh | tail -1 || 
 timeout -k 10 400 python3 bench.py --no-cpu-baseline > $OUT/bench.log 2>&1 || { echo "bench rc=$?"; tail -5 $OUT/bench.log; exit 1; }
 grep '^{' $OUT/bench.log | tail -1 | python3 -c "
 import json,sys; j=json.loads(sys.stdin.read()); t=j.get('train_step',{})
-print('value', j['value'], 'ms', j['ms_per_step'], 'train fp32', t.get('ms_per_step'), 'bf16', t.get('bf16_mlp'))
+print('value', j['value'], 'ms', j['ms_per_step'], 'train fp32', t.get('ms'), 'bf16', t.get('bf16_mlp',{}).get('ms'))
 "
