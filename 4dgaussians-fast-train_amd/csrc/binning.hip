@@ -39,6 +39,7 @@
 namespace gs4d {
 
 constexpr int kEmitPer = kEmitChunk / 256;  // candidates per lane in the emission pass
+constexpr int kEmitStage = 256;             // Gaussians per emission chunk staged in LDS (see the kernel)
 constexpr int kSortThreads = 1024;          // radix-sort workgroup: 16 waves rank one chunk together
 constexpr int kItemsL = 8;                  // keys per lane for the instance sort (8192 per workgroup)
 constexpr int kSortCap = 2048;              // tile runs sorted in LDS by one workgroup (see tile_sort_kernel)
@@ -181,7 +182,14 @@ __global__ __launch_bounds__(256) void emit_instances_kernel(Args a, GeomState g
     for (int i = blockIdx.x * 256 + threadIdx.x; i < nlook; i += gridDim.x * 256) look[i] = 0u;
     __shared__ uint32_t s_own[kEmitChunk];
     __shared__ uint32_t s_off[kEmitChunk + 2];
-    __shared__ uint32_t s_n[kEmitChunk + 1];  // kept candidates before each candidate of the chunk
+    // s_n: kept candidates before each candidate of the chunk (after the tests); during the tests the same
+    // words hold the chunk's Gaussians' attributes when there are at most kEmitStage of them (the common
+    // case: each candidate then reads its Gaussian from LDS, not by two dependent global gathers)
+    __shared__ __attribute__((aligned(16))) uint32_t s_n[kEmitChunk + 4];
+    __shared__ uint32_t s_ggid[kEmitStage];
+    float4 *s_gco = reinterpret_cast<float4 *>(s_n);                  // [kEmitStage]
+    float2 *s_gxy = reinterpret_cast<float2 *>(s_gco + kEmitStage);   // [kEmitStage]
+    int *s_grad = reinterpret_cast<int *>(s_gxy + kEmitStage);        // [kEmitStage]
     __shared__ uint32_t s_hist[kMaxPasses][256];
     __shared__ uint32_t s_w[4], s_tmp[4];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -194,6 +202,7 @@ __global__ __launch_bounds__(256) void emit_instances_kernel(Args a, GeomState g
     // chunk's run to V.  Visible Gaussians starting at or after c1 are ignored.
     const int rhi = c1 < (uint32_t)L ? (int)g.first_vis[b + 1] + 1 : V;
     const int nr = min(rhi - rlo, kEmitChunk + 1);
+    const bool staged = nr <= kEmitStage;  // workgroup-uniform
     for (int i = tid; i < kEmitChunk; i += 256) s_own[i] = 0;
     for (int i = tid; i < kMaxPasses * 256; i += 256) (&s_hist[0][0])[i] = 0;
     __syncthreads();
@@ -201,6 +210,13 @@ __global__ __launch_bounds__(256) void emit_instances_kernel(Args a, GeomState g
         const uint32_t st = g.cand_off[rlo + i];
         s_off[i] = st;
         if (st > c0 && st < c1) s_own[st - c0] = (uint32_t)i;
+        if (staged) {
+            const uint32_t gi = g.vis_gid[rlo + i];
+            s_ggid[i] = gi;
+            s_gxy[i] = g.xy[gi];
+            s_gco[i] = g.conic_opacity[gi];
+            s_grad[i] = radii[gi];
+        }
     }
     if (tid == 0) s_off[nr] = g.cand_off[rlo + nr];
     __syncthreads();
@@ -226,12 +242,23 @@ __global__ __launch_bounds__(256) void emit_instances_kernel(Args a, GeomState g
     float4 co[kEmitPer];
     int rad[kEmitPer];
     uint32_t gid[kEmitPer];
+    if (staged) {
 #pragma unroll
-    for (int k = 0; k < kEmitPer; k++) {
-        gid[k] = g.vis_gid[min(rlo + (int)own[k], V - 1)];
-        xy[k] = g.xy[gid[k]];
-        co[k] = g.conic_opacity[gid[k]];
-        rad[k] = radii[gid[k]];
+        for (int k = 0; k < kEmitPer; k++) {
+            const int i = min((int)own[k], nr - 1);
+            gid[k] = s_ggid[i];
+            xy[k] = s_gxy[i];
+            co[k] = s_gco[i];
+            rad[k] = s_grad[i];
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < kEmitPer; k++) {
+            gid[k] = g.vis_gid[min(rlo + (int)own[k], V - 1)];
+            xy[k] = g.xy[gid[k]];
+            co[k] = g.conic_opacity[gid[k]];
+            rad[k] = radii[gid[k]];
+        }
     }
     uint32_t tile[kEmitPer], reach[kEmitPer];
     uint32_t keep = 0;
@@ -306,7 +333,7 @@ __global__ __launch_bounds__(256) void emit_instances_kernel(Args a, GeomState g
     for (int i = tid; i < nr; i += 256) {
         const uint32_t lo = max(s_off[i], c0) - c0, hi = min(s_off[i + 1], c1) - c0;
         const uint32_t n = hi > lo ? s_n[hi] - s_n[lo] : 0u;
-        if (n) atomicAdd(&g.n_inst[g.vis_gid[rlo + i]], n);
+        if (n) atomicAdd(&g.n_inst[staged ? s_ggid[i] : g.vis_gid[rlo + i]], n);
     }
     uint32_t *hist = g.zero + geom_hist_off(a.P) + (b % kHistShards) * (kMaxPasses * 256);
     for (int p = 0; p < npass; p++)
@@ -547,7 +574,7 @@ __device__ __forceinline__ void wave_sort256(uint64_t key[4], int lane) {
 
 __device__ void merge_sort_run(uint32_t *__restrict__ seg, int n, const uint32_t *__restrict__ gid_by_e,
                                const float *__restrict__ depths, uint64_t *__restrict__ s_x) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, w = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     int total = 512;
     while (total < n) total <<= 1;  // 512, 1024 or 2048
     uint64_t *src = s_x, *dst = s_x + 2048;

@@ -281,7 +281,7 @@ __global__ __launch_bounds__(kHexThreads) void hexplane_backward_kernel(int N, c
     int *s_wbox = s_box + 24;                                      // [waves][6][4]
     unsigned long long *s_win = smem64 + fixed / 2;                // [wcap]: the fixed-point window
     const int q = threadIdx.x % G, slot = threadIdx.x / G;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wv = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t first = (int64_t)blockIdx.x * npw;
     for (int e = threadIdx.x; e < wcap; e += kHexThreads) s_win[e] = 0ull;  // flushes leave it zeroed
     for (int l = 0; l < lay.levels; l++) {

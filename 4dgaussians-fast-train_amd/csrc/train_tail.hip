@@ -898,7 +898,7 @@ __global__ __launch_bounds__(256) void heads_bwd_wide_mfma_kernel(HbArgs A, cons
         s_w2t[col * WS + r] = w2[e];
     }
     __syncthreads();
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, q = lane >> 4, c = lane & 15;
+    const int lane = threadIdx.x & 63, wv = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6), q = lane >> 4, c = lane & 15;
     const int half = wv & 1, cb = half * (W / 2);  // this wave's first column
     f4v accw[MT][CT];
 #pragma unroll
@@ -1102,7 +1102,7 @@ __global__ __launch_bounds__(kFbThreads) void feature_bwd_kernel(int P, const fl
     constexpr int PER = FOUT * FIN + FOUT;  // one partial: dW (row-major) then db
     __shared__ float s_w[FOUT * FIN + FOUT];
     __shared__ float s_t[NW][kFbRows * TS];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wv = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     for (int i = threadIdx.x; i < FOUT * FIN / 4; i += kFbThreads)
         reinterpret_cast<float4 *>(s_w)[i] = reinterpret_cast<const float4 *>(w)[i];
     __syncthreads();
@@ -1294,7 +1294,7 @@ __global__ __launch_bounds__(kHfThreads) void heads_fwd_kernel(HfArgs A, const f
                 reinterpret_cast<const float4 *>(A.w2[i] + (size_t)row * W)[c4];
         }
     __syncthreads();
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, q = lane >> 4, c = lane & 15;
+    const int lane = threadIdx.x & 63, wv = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6), q = lane >> 4, c = lane & 15;
     const int nblk = (A.P + 15) / 16;
     for (int blk = blockIdx.x * (kHfThreads / 64) + wv; blk < nblk; blk += gridDim.x * (kHfThreads / 64)) {
         const int r0 = blk * 16, ra = r0 + c;
@@ -1389,7 +1389,7 @@ __global__ __launch_bounds__(kHbfThreads) void heads_block_fwd_kernel(HfArgs A, 
     }
     for (int e = threadIdx.x; e < npad; e += kHbfThreads) s_b2[e] = e < n ? A.b2[head][e] : 0.f;
     __syncthreads();
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, q = lane >> 4, c = lane & 15;
+    const int lane = threadIdx.x & 63, wv = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6), q = lane >> 4, c = lane & 15;
     const int nblk = (A.P + 15) / 16;
     const int stride = gridDim.x * NW;
     float *out = A.out[head];
@@ -1524,7 +1524,7 @@ __global__ __launch_bounds__(kHbfThreads) void heads_block_fwd_bf16_kernel(HfArg
             *reinterpret_cast<bf8v *>(w1t + (size_t)col * A.kW + head * W + 8 * r8) = v;
         }
     }
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, q = lane >> 4, c = lane & 15;
+    const int lane = threadIdx.x & 63, wv = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6), q = lane >> 4, c = lane & 15;
     const int nblk = (A.P + 15) / 16;
     const int stride = gridDim.x * NW;
     float *out = A.out[head];
@@ -1624,7 +1624,7 @@ __global__ __launch_bounds__(kDxThreads) void mlp_dx_bf16_kernel(int P, int KW, 
     constexpr int NT = W / 16, RB = kDxRowsPerWave / 16;
     constexpr int kPieces = W * kDxChunk / 8 / kDxThreads;  // 16-byte pieces of a chunk per thread (W = 128: 2)
     __shared__ __attribute__((aligned(16))) __bf16 s_a[2][W * kDxLdsStride];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, q = lane >> 4, c = lane & 15;
+    const int lane = threadIdx.x & 63, wv = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6), q = lane >> 4, c = lane & 15;
     const int64_t row0 = (int64_t)blockIdx.x * (kDxThreads / 64) * kDxRowsPerWave + (int64_t)wv * kDxRowsPerWave;
     const __bf16 *brow[RB];
 #pragma unroll
@@ -1731,7 +1731,7 @@ __global__ __launch_bounds__(kDwbThreads) void mlp_dw_bf16_kernel(int P, int KW,
     const int head = blockIdx.y;
     const int64_t r0 = (int64_t)blockIdx.x * kDwbChunkRows;
     const int nst = (int)((min((int64_t)P, r0 + kDwbChunkRows) - r0 + kDwbStepRows - 1) / kDwbStepRows);
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4, li = lane & 15;
+    const int lane = threadIdx.x & 63, wv = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6), g = lane >> 4, li = lane & 15;
     f4v acc[MW][NT];
 #pragma unroll
     for (int m = 0; m < MW; m++)
@@ -1815,7 +1815,7 @@ __global__ __launch_bounds__(256) void heads_bwd_wide_bf16_kernel(HbArgs A, cons
     __shared__ float4 s_red[192];
     const int ld = A.k * W, h = A.h0;
     const float *__restrict__ w2 = A.w2[h];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, q = lane >> 4, c = lane & 15;
+    const int lane = threadIdx.x & 63, wv = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6), q = lane >> 4, c = lane & 15;
     for (int e = threadIdx.x; e < W * 64; e += 256) {
         const int n = e / 64, k = e % 64;
         s_w2t[n * KS + k] = (__bf16)(k < N ? w2[k * W + n] : 0.f);
@@ -1950,7 +1950,7 @@ __global__ __launch_bounds__(kFbThreads) void feature_fwd_kernel(int P, const fl
         reinterpret_cast<float4 *>(s_w + row * WS)[c4] = reinterpret_cast<const float4 *>(w + (size_t)row * FIN)[c4];
     }
     __syncthreads();
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, q = lane >> 4, c = lane & 15;
+    const int lane = threadIdx.x & 63, wv = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6), q = lane >> 4, c = lane & 15;
     float bias[NT];
 #pragma unroll
     for (int t = 0; t < NT; t++) bias[t] = b[16 * t + c];

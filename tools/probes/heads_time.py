@@ -50,6 +50,8 @@ def main():
         ("dh bf16 (rocBLAS)", lambda: D._mm_dx(dabf, w1b)),
         ("dh bf16 (mlp_dx_bf16)", lambda: _C.mlp_dx_bf16(dabf, w1t)),
     ]
+    if "--fwd32" in sys.argv:  # only the fp32 block forward (PMC passes: tools/hfpmc.sh)
+        rows = rows[:1]
     for name, fn in rows:
         print(f"{name:24s} {timed(fn):8.1f} us", flush=True)
 

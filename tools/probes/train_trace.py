@@ -76,8 +76,48 @@ def op_profile(cfg="metric", steps=5):
         print(prof.key_averages().table(sort_by=key, row_limit=45, max_name_column_width=60))
 
 
+def py_profile(cfg="metric", steps=30):
+    """cProfile of a few train steps (host cost by Python function; the GPU runs asynchronously, so a C
+    entry point's time is its launch path, and a wait shows up in whatever call synchronises)."""
+    import cProfile
+    import pstats
+    P, W, H = CONFIGS[cfg]
+    dev = torch.device("cuda:0")
+    hyper, opt = config.dynerf()
+    if "--bf16" in sys.argv:
+        hyper.mlp_dtype = "bf16"
+    torch.manual_seed(0)
+    g = GaussianModel(3, hyper, fused=True)
+    pts, cols = make_point_cloud(P, seed=0)
+    g.create_from_pcd(pts, cols, spatial_lr_scale=1.0, device=dev)
+    g._deformation.deformation_net.grid.fused = True
+    g._deformation.deformation_net.fused_heads = True
+    g.training_setup(opt)
+    g.active_sh_degree = 3
+    views = make_training_views(1, W, H, seed=1, device=dev)
+    bg = torch.ones(3, device=dev)
+    for i in range(5):
+        train_step(g, views, opt, hyper, 3001 + i, bg)
+    torch.cuda.synchronize()
+    pr = cProfile.Profile()
+    t0 = time.perf_counter()
+    pr.enable()
+    for i in range(steps):
+        train_step(g, views, opt, hyper, 3006 + i, bg)
+    pr.disable()
+    t1 = time.perf_counter()
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    print(f"host {1e3 * (t1 - t0) / steps:.3f} ms/step under cProfile, drain {1e3 * (t2 - t1):.3f} ms")
+    st = pstats.Stats(pr)
+    st.sort_stats("tottime").print_stats(45)
+    st.sort_stats("cumulative").print_stats(45)
+
+
 if __name__ == "__main__":
-    if "--ops" in sys.argv:
+    if "--pyprof" in sys.argv:
+        py_profile()
+    elif "--ops" in sys.argv:
         op_profile()
     else:
         args = [a for a in sys.argv[1:] if not a.startswith("--")]
