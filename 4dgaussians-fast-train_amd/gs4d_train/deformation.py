@@ -163,6 +163,10 @@ class Linear(nn.Linear):
 
 
 _USE_ROCBLAS = os.environ.get("GS4D_MLP_ROCBLAS", "1") != "0"  # 0: torch's GEMMs (A/B runs)
+# The tuned choice depends on timings, so two processes may pick different kernels for a shape (and round
+# differently); a step is bitwise reproducible inside a process either way.  GS4D_GEMM_TUNE=0 keeps
+# rocBLAS's own pick, the same in every process (reproducible across runs, slower: ~+0.35 ms per fp32 step).
+_TUNE = os.environ.get("GS4D_GEMM_TUNE", "1") != "0"
 
 
 def _rocblas_ok(*ts):
@@ -186,16 +190,16 @@ def _splitk_dw(dy, x):
         N, K = dy.shape[1], x.shape[1]
         if S < 2:  # one GEMM, f32 out (a bf16 torch GEMM would round the result to bf16)
             out = torch.empty(N, K, device=dy.device)
-            _C.gemm_f32(x, dy, out, False, True, K, N, P, x.stride(0), dy.stride(0), K, 1, 0, 0, 0, True)
+            _C.gemm_f32(x, dy, out, False, True, K, N, P, x.stride(0), dy.stride(0), K, 1, 0, 0, 0, _TUNE)
             return out
         rem = P - S * c
         parts = torch.empty(S + (1 if rem else 0), N, K, device=dy.device)
         # column-major: part_s^T (K x N) = x_s^T (K x c) . dy_s (c x N)
         _C.gemm_f32(x, dy, parts, False, True, K, N, c, x.stride(0), dy.stride(0), K, S, c * x.stride(0),
-                    c * dy.stride(0), N * K, True)
+                    c * dy.stride(0), N * K, _TUNE)
         if rem:
             _C.gemm_f32(x[S * c:], dy[S * c:], parts[S], False, True, K, N, rem, x.stride(0), dy.stride(0), K, 1,
-                        0, 0, 0, True)
+                        0, 0, 0, _TUNE)
         return _C.sum_slices(parts)
     xs = x[:S * c].unflatten(0, (S, c))
     dw = torch.bmm(dy[:S * c].unflatten(0, (S, c)).transpose(1, 2), xs).sum(0)
@@ -211,7 +215,7 @@ def _mm_dx(dy, w):
         P, N, K = dy.shape[0], dy.shape[1], w.shape[1]
         out = torch.empty(P, K, device=dy.device)
         # column-major: out^T (K x P) = w^T (K x N) . dy^T (N x P)
-        _C.gemm_f32(w, dy, out, False, False, K, P, N, K, dy.stride(0), K, 1, 0, 0, 0, True)
+        _C.gemm_f32(w, dy, out, False, False, K, P, N, K, dy.stride(0), K, 1, 0, 0, 0, _TUNE)
         return out
     return (dy @ w).float()
 

@@ -53,8 +53,11 @@ PSNR_GAIN = 15.0      # dB over the initial random point cloud (8.5-8.7 dB)
 PSNR_DELTA = 1.0      # dB between the medians of the fused and the unfused runs
 SEEDS = 5
 SHORT_DELTA = 0.1     # dB between the two formulations' mean short-horizon PSNR over SHORT_SEEDS seeds
-SHORT_RUN_DELTA = 0.2   # dB between the two runs of any one seed (per-seed gaps measured 0.02-0.16 dB over the
-                        # round-4 6-seed runs; the 6-seed mean bar SHORT_DELTA holds the formulations together)
+SHORT_RUN_DELTA = 0.35  # dB between the two runs of any one seed.  Measured (round 5, 6 seeds): per-seed gaps
+                        # 0.02-0.19 dB in one run and 0.33 dB at seed 2 in another -- the reference formulation
+                        # alone moved 0.17 dB at that seed between two runs (21.776 vs 21.943 dB: torch's
+                        # atomic-order backward), so one run of each formulation can differ by ~2x that.  The
+                        # 6-seed mean bar SHORT_DELTA (0.1 dB) is what holds the formulations together.
 SHORT_SEEDS = 6
 
 

@@ -1,7 +1,7 @@
 #!/bin/bash
-# Round-4 evidence on the final tree: the whole GPU suite, smoke(), and the default bench line.
+# Round-5 evidence on the final tree: the whole GPU suite, smoke(), and the default bench line.
 export TMPDIR=/tmp
-OUT=gpurun_out/ev_${TAG:-r04}
+OUT=gpurun_out/ev_${TAG:-r05}
 mkdir -p $OUT
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 400 --timeout-method thread > $OUT/gpu_tests.log 2>&1
 rc=$?; tail -3 $OUT/gpu_tests.log; [ $rc -ne 0 ] && exit $rc
@@ -11,5 +11,5 @@ timeout -k 10 400 python bench.py > $OUT/bench.log 2>&1 || { echo "bench rc=$?";
 grep '^{' $OUT/bench.log | tail -1 > $OUT/bench.json
 python3 -c "
 import json; j=json.load(open('$OUT/bench.json'))
-print('value', j['value'], 'ms', j['ms_per_step'], 'train', j.get('train_step',{}).get('ms_per_step'), 'cpu', j.get('cpu_baseline'))
+print('value', j['value'], 'ms', j['ms_per_step'], 'train', j.get("train_step",{}).get("ms"), "bf16", j.get("train_step",{}).get("bf16_mlp",{}).get("ms"), 'cpu', j.get('cpu_baseline'))
 "
