@@ -20,20 +20,16 @@
 //   - points are visited in a 3-D Morton order (gs4d_hexplane_order: 24-bit codes of the normalised
 //     coordinates, the library's onesweep sort), so the ~128 points of a backward workgroup cover a
 //     small box of the field and each plane sees only a small window of cells;
-//   - grid gradients are gathered, not scattered: the workgroup's points are bucketed by bilinear
-//     anchor cell in LDS and each touched (cell, feature) sums its neighbouring buckets with plain LDS
-//     reads, then goes to HBM with one no-return atomic per workgroup; a plane whose anchor box is too
-//     large falls back to direct atomics.  The channels-last gradient buffer is repacked to the
-//     (1, F, H, W) parameter layout by one launch;
-//   - deterministic mode (opt-in; the default sums with float atomics like the reference's
-//     grid_sampler backward, and is faster): inside a workgroup a cell's taps are summed in a fixed rank order
-//     (tap slot, wave, lane: ballot-matched peers, no LDS atomics), and each workgroup's sum is
-//     converted to a 64-bit fixed-point integer (round to nearest, a power-of-two scale) and added
-//     across workgroups by integer atomics -- exact, so no schedule changes a bit.  The scale
-//     (hex_scale_of) bounds every cell's sum by 2^61: |dv| <= max|dfeat| max|param|^5 (a product of
-//     5 bilinear samples, each a convex combination of parameters) and a cell takes at most one tap per
-//     point, so |sum| <= N max|dfeat| max|param|^5; the resolution is that bound times 2^-61 (~1e-13
-//     of the largest possible sum at 10^5 points, below fp32 rounding of any sum it can affect).
+//   - grid gradients are summed per workgroup, then across workgroups, in exact integer arithmetic: every
+//     (point, tap, feature) term is rounded once to 64-bit fixed point at its plane's power-of-two scale
+//     and added into an LDS window over the plane's anchor box (ds_add_u64), whose nonzero cells go to the
+//     packed gradient's 64-bit accumulators by one no-return integer atomic each.  Integer sums are
+//     exact, so no schedule changes a bit: the backward is deterministic by construction (there is no
+//     float-atomic mode).  The per-plane scale bounds every cell's sum: |term| <= max|dfeat| times the
+//     product of the other five planes' max|param| (each bilinear sample is a convex combination of its
+//     plane's parameters), a cell takes at most one tap per point, so |sum| <= N |term|max < 2^62 at the
+//     chosen scale (hex_plane_scale; details at hexplane_backward_kernel).  One launch unpacks the
+//     accumulators to floats in the (1, F, H, W) parameter layout.
 #include <algorithm>
 #include <climits>
 

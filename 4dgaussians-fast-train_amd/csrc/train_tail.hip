@@ -173,11 +173,8 @@ __global__ __launch_bounds__(kTailThreads) void adam_kernel(gs4d_adam_batch batc
     const float b1 = batch.beta1, omb1 = batch.one_minus_beta1, b2 = batch.beta2, omb2 = batch.one_minus_beta2;
     const float eps = batch.eps, step_size = d.neg_step_size, bc2 = d.bias_correction2_sqrt;
     (void)b1;
-    for (int k = threadIdx.x; k < kAdamChunk; k += kTailThreads) {
-        const int64_t i = base + k;
-        if (i >= d.n) break;
-        const float g = d.grad[i];
-        float m = d.exp_avg[i], v = d.exp_avg_sq[i];
+    // one element: exactly the scalar sequence below, whichever width the loop loads at
+    auto upd = [&](float g, float &p, float &m, float &v) {
         // exp_avg.lerp_(grad, 1 - beta1): weight < 0.5 -> self + weight * (end - self)
         m = fmaf(omb1, g - m, m);
         // exp_avg_sq.mul_(beta2).addcmul_(grad, grad, value=1 - beta2)
@@ -185,7 +182,44 @@ __global__ __launch_bounds__(kTailThreads) void adam_kernel(gs4d_adam_batch batc
         v = fmaf(omb2, g * g, v);
         // denom = exp_avg_sq.sqrt() / bias_correction2_sqrt + eps; param.addcdiv_(exp_avg, denom, -step_size)
         const float den = sqrtf(v) / bc2 + eps;
-        d.param[i] = fmaf(step_size, m / den, d.param[i]);
+        p = fmaf(step_size, m / den, p);
+    };
+    const bool vec = (((uintptr_t)d.param | (uintptr_t)d.grad | (uintptr_t)d.exp_avg | (uintptr_t)d.exp_avg_sq) & 15) == 0;
+    if (vec) {
+        // 16-byte loads and stores (the chunk base is a multiple of 4); the tensor's last n % 4 elements by the
+        // chunk that holds them
+        const int64_t n4 = d.n >> 2;
+        for (int k = threadIdx.x; k < kAdamChunk / 4; k += kTailThreads) {
+            const int64_t i4 = (base >> 2) + k;
+            if (i4 >= n4) break;
+            const float4 g = reinterpret_cast<const float4 *>(d.grad)[i4];
+            float4 p = reinterpret_cast<float4 *>(d.param)[i4];
+            float4 m = reinterpret_cast<float4 *>(d.exp_avg)[i4];
+            float4 v = reinterpret_cast<float4 *>(d.exp_avg_sq)[i4];
+            upd(g.x, p.x, m.x, v.x);
+            upd(g.y, p.y, m.y, v.y);
+            upd(g.z, p.z, m.z, v.z);
+            upd(g.w, p.w, m.w, v.w);
+            reinterpret_cast<float4 *>(d.param)[i4] = p;
+            reinterpret_cast<float4 *>(d.exp_avg)[i4] = m;
+            reinterpret_cast<float4 *>(d.exp_avg_sq)[i4] = v;
+        }
+        const int64_t i = 4 * n4 + threadIdx.x;
+        if (i < d.n && i >= base && i < base + kAdamChunk) {
+            float p = d.param[i], m = d.exp_avg[i], v = d.exp_avg_sq[i];
+            upd(d.grad[i], p, m, v);
+            d.param[i] = p;
+            d.exp_avg[i] = m;
+            d.exp_avg_sq[i] = v;
+        }
+        return;
+    }
+    for (int k = threadIdx.x; k < kAdamChunk; k += kTailThreads) {
+        const int64_t i = base + k;
+        if (i >= d.n) break;
+        float p = d.param[i], m = d.exp_avg[i], v = d.exp_avg_sq[i];
+        upd(d.grad[i], p, m, v);
+        d.param[i] = p;
         d.exp_avg[i] = m;
         d.exp_avg_sq[i] = v;
     }
@@ -227,7 +261,8 @@ __global__ __launch_bounds__(kTailThreads) void deform_tail_fwd_kernel(
     const int64_t e = (int64_t)(blockIdx.x - nb_g) * kTailThreads + threadIdx.x;
     const int64_t n = (int64_t)P * 3 * K;
     if (e >= n) return;
-    const int64_t g = e / (3 * K), k = e - g * 3 * K;
+    // 32-bit quotient (a 64-bit division is a long software sequence): e < P * 3K < 2^32 by the host check
+    const int64_t g = (int64_t)((uint32_t)e / (uint32_t)(3 * K)), k = e - g * 3 * K;
     const float base = k < 3 ? f_dc[3 * g + k] : f_rest[g * 3 * (K - 1) + (k - 3)];
     shs[e] = dshs ? base + dshs[e] : base;
 }
@@ -279,7 +314,7 @@ __global__ __launch_bounds__(kTailThreads) void deform_tail_bwd_kernel(
     const int64_t e = (int64_t)(blockIdx.x - nb_g) * kTailThreads + threadIdx.x;
     const int64_t n = (int64_t)P * 3 * K;
     if (e >= n) return;
-    const int64_t gi = e / (3 * K), k = e - gi * 3 * K;
+    const int64_t gi = (int64_t)((uint32_t)e / (uint32_t)(3 * K)), k = e - gi * 3 * K;  // e < 2^32: host check
     const float v = g_shs ? g_shs[e] : 0.f;
     if (k < 3) d_fdc[3 * gi + k] = v;
     else d_frest[gi * 3 * (K - 1) + (k - 3)] = v;
@@ -313,7 +348,7 @@ __global__ __launch_bounds__(kTailThreads) void reg_forward_kernel(gs4d_reg_batc
         const int64_t i = (blk - d.first_block) * kRegBlock + (int64_t)k * kTailThreads + threadIdx.x;
         if (i >= n) break;
         const float t = d.data[i];
-        const int y = (int)((i % hw) / d.W);
+        const int y = (int)(((uint32_t)i % (uint32_t)hw) / (uint32_t)d.W);  // 32-bit: a plane < 2^31 elements
         if (y <= d.H - 3) {
             const float s2 = second_diff(d.data + (i - (int64_t)y * d.W), y, d.W);
             acc += cs * (double)(s2 * s2);
@@ -354,7 +389,7 @@ __global__ __launch_bounds__(kTailThreads) void reg_backward_kernel(gs4d_reg_bat
     for (int k = 0; k < kRegPerThread; k++) {
         const int64_t i = (blk - d.first_block) * kRegBlock + (int64_t)k * kTailThreads + threadIdx.x;
         if (i >= n) break;
-        const int y = (int)((i % hw) / d.W);
+        const int y = (int)(((uint32_t)i % (uint32_t)hw) / (uint32_t)d.W);  // 32-bit: a plane < 2^31 elements
         const float *col = d.data + (i - (int64_t)y * d.W);
         float ds[3];  // ds[y-2], ds[y-1], ds[y]
 #pragma unroll
@@ -2223,6 +2258,7 @@ static int reg_check(const gs4d_reg_batch *b, int64_t *nblk) {
     for (int i = 0; i < b->count; i++) {
         const gs4d_reg_plane &p = b->p[i];
         if (!p.data || p.C < 1 || p.H < 3 || p.W < 1 || p.first_block != blocks) return 1;
+        if ((int64_t)p.C * p.H * p.W > INT32_MAX) return 1;  // the kernels index a plane in 32 bits
         blocks += gs4d_reg_blocks(p.C, p.H, p.W);
     }
     *nblk = blocks;
@@ -2311,6 +2347,7 @@ int gs4d_deform_tail_forward(int P, int K, const float *xyz, const float *s, con
                                      !rot || !opac || !shs)))
         return 1;
     if (P == 0) return 0;
+    if ((int64_t)P * 3 * K > UINT32_MAX) return 1;  // the SH range is indexed in 32 bits
     const int nb_g = (P + kTailThreads - 1) / kTailThreads;
     const int64_t nb_s = ((int64_t)P * 3 * K + kTailThreads - 1) / kTailThreads;
     hipLaunchKernelGGL(deform_tail_fwd_kernel, dim3((unsigned)(nb_g + nb_s)), dim3(kTailThreads), 0, (hipStream_t)stream,
@@ -2326,6 +2363,7 @@ int gs4d_deform_tail_backward(int P, int K, const float *scales, const float *r,
                                      (K > 1 && !d_frest))))
         return 1;
     if (P == 0) return 0;
+    if ((int64_t)P * 3 * K > UINT32_MAX) return 1;  // the SH range is indexed in 32 bits
     const int nb_g = (P + kTailThreads - 1) / kTailThreads;
     const int64_t nb_s = ((int64_t)P * 3 * K + kTailThreads - 1) / kTailThreads;
     hipLaunchKernelGGL(deform_tail_bwd_kernel, dim3((unsigned)(nb_g + nb_s)), dim3(kTailThreads), 0, (hipStream_t)stream,

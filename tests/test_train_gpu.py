@@ -100,6 +100,30 @@ def test_fused_adam_matches_torch_adam():
         assert float(sb["step"]) == float(sa["step"])
 
 
+def test_fused_adam_vector_and_scalar_paths_agree_bitwise():
+    """adam_kernel loads 16-byte aligned tensors as float4 and others element by element: the same float
+    sequence either way, so a parameter stored 4 bytes off alignment gets bitwise the same update."""
+    from gs4d_train.kernels import FusedAdam
+    torch.manual_seed(4)
+    n = 10_003
+    p0 = torch.randn(n, device="cuda")
+    store = torch.zeros(n + 1, device="cuda")
+    store[1:] = p0
+    qa = torch.nn.Parameter(p0.clone())               # aligned: the float4 path (+ 3 tail elements)
+    qb = torch.nn.Parameter(store[1:])                # 4 bytes past alignment: the scalar path
+    assert qa.data_ptr() % 16 == 0 and qb.data_ptr() % 16 == 4
+    oa = FusedAdam([{"params": [qa], "lr": 1e-3}], lr=1e-3, eps=1e-15)
+    ob = FusedAdam([{"params": [qb], "lr": 1e-3}], lr=1e-3, eps=1e-15)
+    for it in range(3):
+        g = torch.randn(n, device="cuda")
+        qa.grad, qb.grad = g.clone(), g.clone()
+        oa.step()
+        ob.step()
+    assert torch.equal(qa, qb)
+    assert torch.equal(oa.state[qa]["exp_avg"], ob.state[qb]["exp_avg"])
+    assert torch.equal(oa.state[qa]["exp_avg_sq"], ob.state[qb]["exp_avg_sq"])
+
+
 def _field(F=16, reso=(64, 64, 64, 150), multires=(1, 2)):
     from gs4d_train.deformation import HexPlaneField
     torch.manual_seed(3)
