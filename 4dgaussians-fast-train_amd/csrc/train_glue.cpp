@@ -547,9 +547,12 @@ std::vector<torch::Tensor> heads_block_forward(const torch::Tensor &h, const tor
 }
 
 // ---- heads block forward on bf16 operands: (a bf16, hb bf16, W1^T bf16, [out_i fp32]); same operands as above
+// hb_in (optional): h already rounded to bf16 by feature_relu_forward(..., with_hb=True); the kernel then reads it
+// instead of h and the returned hb is hb_in
 std::vector<torch::Tensor> heads_block_forward_bf16(const torch::Tensor &h, const torch::Tensor &w1,
                                                     const torch::Tensor &b1, const std::vector<torch::Tensor> &w2s,
-                                                    const std::vector<torch::Tensor> &b2s) {
+                                                    const std::vector<torch::Tensor> &b2s,
+                                                    const c10::optional<torch::Tensor> &hb_in) {
     const int k = (int)w2s.size();
     need(k >= 1 && k <= GS4D_HEADS_MAX && (int)b2s.size() == k, "heads_block_forward_bf16: 1-8 heads");
     for (const torch::Tensor *t : std::initializer_list<const torch::Tensor *>{&h, &w1, &b1})
@@ -563,11 +566,26 @@ std::vector<torch::Tensor> heads_block_forward_bf16(const torch::Tensor &h, cons
     const int64_t rows = (h.size(0) + 15) / 16 * 16;
     auto bopt = h.options().dtype(torch::kBFloat16);
     auto a_pad = torch::empty({rows, w1.size(0)}, bopt);
-    auto hb_pad = torch::empty({rows, h.size(1)}, bopt);
     auto w1t = torch::empty({w1.size(1), w1.size(0)}, bopt);  // W1^T (W, kW)
-    b.h = h.data_ptr<float>(), b.w1 = w1.data_ptr<float>(), b.b1 = b1.data_ptr<float>();
-    b.a = (uint16_t *)a_pad.data_ptr(), b.hb = (uint16_t *)hb_pad.data_ptr(), b.w1t = (uint16_t *)w1t.data_ptr();
-    std::vector<torch::Tensor> out{a_pad.narrow(0, 0, h.size(0)), hb_pad.narrow(0, 0, h.size(0)), w1t}, keep;
+    b.w1 = w1.data_ptr<float>(), b.b1 = b1.data_ptr<float>();
+    b.a = (uint16_t *)a_pad.data_ptr(), b.w1t = (uint16_t *)w1t.data_ptr();
+    torch::Tensor hb_out;
+    if (hb_in.has_value() && hb_in->defined()) {
+        const torch::Tensor &hb = *hb_in;
+        need(hb.is_cuda() && hb.scalar_type() == torch::kBFloat16 && hb.dim() == 2 && hb.size(0) == h.size(0) &&
+                 hb.size(1) == h.size(1) && hb.stride(1) == 1 && hb.stride(0) == hb.size(1) &&
+                 ((size_t)hb.data_ptr() & 15) == 0,
+             "heads_block_forward_bf16: hb (P, W) bf16, contiguous rows, 16-byte aligned");
+        b.h = nullptr;  // the kernel reads hb (only rows < P)
+        b.hb = (uint16_t *)hb.data_ptr();
+        hb_out = hb;
+    } else {
+        auto hb_pad = torch::empty({rows, h.size(1)}, bopt);
+        b.h = h.data_ptr<float>();
+        b.hb = (uint16_t *)hb_pad.data_ptr();
+        hb_out = hb_pad.narrow(0, 0, h.size(0));
+    }
+    std::vector<torch::Tensor> out{a_pad.narrow(0, 0, h.size(0)), hb_out, w1t}, keep;
     for (int i = 0; i < k; i++) {
         auto w2 = w2s[i].contiguous();
         auto b2 = b2s[i].contiguous();
@@ -619,7 +637,9 @@ torch::Tensor mlp_dw_bf16(const torch::Tensor &da, const torch::Tensor &hb) {
 }
 
 // ---- first deformation layer forward: h = relu(x W^T + b)
-torch::Tensor feature_relu_forward(const torch::Tensor &x, const torch::Tensor &w, const torch::Tensor &b) {
+// with_hb: also h rounded to bf16 ((P, W) view of a (ceil(P/16)*16, W) buffer) for the bf16 heads block
+std::vector<torch::Tensor> feature_relu_forward(const torch::Tensor &x, const torch::Tensor &w, const torch::Tensor &b,
+                                                bool with_hb) {
     for (const torch::Tensor *t : std::initializer_list<const torch::Tensor *>{&x, &w, &b})
         gpu_f32(*t, "feature_relu_forward operand");
     need(x.is_contiguous() && w.is_contiguous() && b.is_contiguous() && x.dim() == 2 && w.dim() == 2 &&
@@ -627,10 +647,14 @@ torch::Tensor feature_relu_forward(const torch::Tensor &x, const torch::Tensor &
          "feature_relu_forward: x (P, Fin), W (Fout, Fin), b (Fout), contiguous");
     c10::hip::HIPGuard guard(x.device().index());
     auto h = torch::empty({x.size(0), w.size(0)}, x.options());
-    check(gs4d_feature_relu_forward((int)x.size(0), (int)x.size(1), (int)w.size(0), x.data_ptr<float>(),
-                                    w.data_ptr<float>(), b.data_ptr<float>(), h.data_ptr<float>(), (void *)stream_of(x)),
+    torch::Tensor hb;
+    if (with_hb) hb = torch::empty({(x.size(0) + 15) / 16 * 16, w.size(0)}, x.options().dtype(torch::kBFloat16));
+    check(gs4d_feature_relu_forward_hb((int)x.size(0), (int)x.size(1), (int)w.size(0), x.data_ptr<float>(),
+                                       w.data_ptr<float>(), b.data_ptr<float>(), h.data_ptr<float>(),
+                                       with_hb ? (uint16_t *)hb.data_ptr() : nullptr, (void *)stream_of(x)),
           "feature_relu_forward");
-    return h;
+    if (with_hb) return {h, hb.narrow(0, 0, x.size(0))};
+    return {h};
 }
 
 // ---- the field's input points: (pts (N, 4)) from xyz (N, 3+), t (N, 1+), aabb (2, 3); backward dxyz
@@ -938,10 +962,12 @@ torch::Tensor sum_slices(torch::Tensor parts) {
 PYBIND11_MODULE(_C, m) {
     m.def("hexplane_points", &hexplane_points);
     m.def("hexplane_points_backward", &hexplane_points_backward);
-    m.def("feature_relu_forward", &feature_relu_forward);
+    m.def("feature_relu_forward", &feature_relu_forward, py::arg("x"), py::arg("w"), py::arg("b"),
+          py::arg("with_hb") = false);
     m.def("heads_forward", &heads_forward);
     m.def("heads_block_forward", &heads_block_forward);
-    m.def("heads_block_forward_bf16", &heads_block_forward_bf16);
+    m.def("heads_block_forward_bf16", &heads_block_forward_bf16, py::arg("h"), py::arg("w1"), py::arg("b1"),
+          py::arg("w2"), py::arg("b2"), py::arg("hb") = py::none());
     m.def("mlp_dx_bf16", &mlp_dx_bf16);
     m.def("mlp_dw_bf16", &mlp_dw_bf16);
     m.def("feature_relu_backward", &feature_relu_backward);

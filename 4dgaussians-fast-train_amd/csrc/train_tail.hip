@@ -1517,7 +1517,9 @@ __global__ __launch_bounds__(kHbfThreads) void heads_block_fwd_kernel(HfArgs A, 
 // that same feature order.
 typedef __attribute__((ext_vector_type(8))) __bf16 bf8v;
 typedef __attribute__((ext_vector_type(4))) __bf16 bf4v;
-template <int W>
+// HBIN: h arrives already rounded to bf16 in hb ((ceil(P / 16) * 16, W), gs4d_feature_relu_forward_hb), read as
+// 16-byte loads (half the fp32 bytes per head) and not written
+template <int W, bool HBIN>
 __global__ __launch_bounds__(kHbfThreads) void heads_block_fwd_bf16_kernel(HfArgs A, const float *__restrict__ h,
                                                                            const float *__restrict__ w1,
                                                                            const float *__restrict__ b1,
@@ -1565,14 +1567,21 @@ __global__ __launch_bounds__(kHbfThreads) void heads_block_fwd_bf16_kernel(HfArg
     float *out = A.out[head];
     const bool v4out = (n & 3) == 0 && ((size_t)out & 15) == 0;
     float4 hn[2 * NK];
+    bf8v hbn[NK];
     // unconditional loads (rows past P read row P - 1), as in heads_block_fwd_kernel
     auto load_h = [&](int blk) {
         const int pt = min(blk * 16 + c, A.P - 1);
-        const float4 *src = reinterpret_cast<const float4 *>(h + (size_t)pt * W + 8 * q);
+        if (HBIN) {
+            const bf8v *src = reinterpret_cast<const bf8v *>(hb + (size_t)pt * W + 8 * q);
 #pragma unroll
-        for (int t = 0; t < NK; t++) {
-            hn[2 * t] = src[8 * t];
-            hn[2 * t + 1] = src[8 * t + 1];
+            for (int t = 0; t < NK; t++) hbn[t] = src[4 * t];
+        } else {
+            const float4 *src = reinterpret_cast<const float4 *>(h + (size_t)pt * W + 8 * q);
+#pragma unroll
+            for (int t = 0; t < NK; t++) {
+                hn[2 * t] = src[8 * t];
+                hn[2 * t + 1] = src[8 * t + 1];
+            }
         }
     };
     int blk = blockIdx.x * NW + wv;
@@ -1581,12 +1590,16 @@ __global__ __launch_bounds__(kHbfThreads) void heads_block_fwd_bf16_kernel(HfArg
         bf8v hv[NK];
 #pragma unroll
         for (int t = 0; t < NK; t++) {
-            const float4 x = hn[2 * t], y = hn[2 * t + 1];
-            hv[t] = bf8v{(__bf16)x.x, (__bf16)x.y, (__bf16)x.z, (__bf16)x.w, (__bf16)y.x, (__bf16)y.y, (__bf16)y.z,
-                         (__bf16)y.w};
+            if (HBIN) {
+                hv[t] = hbn[t];
+            } else {
+                const float4 x = hn[2 * t], y = hn[2 * t + 1];
+                hv[t] = bf8v{(__bf16)x.x, (__bf16)x.y, (__bf16)x.z, (__bf16)x.w, (__bf16)y.x, (__bf16)y.y,
+                             (__bf16)y.z, (__bf16)y.w};
+            }
         }
         load_h(blk + stride);  // the next block's h loads fly while this one runs on the MFMA
-        if (hb && head == 0) {  // bf16 h for the backward's weight-gradient GEMM (ceil(P / 16) * 16 rows)
+        if (!HBIN && hb && head == 0) {  // bf16 h for the backward's weight-gradient GEMM (ceil(P / 16) * 16 rows)
             __bf16 *dst = hb + (size_t)(blk * 16 + c) * W + 8 * q;
 #pragma unroll
             for (int t = 0; t < NK; t++) *reinterpret_cast<bf8v *>(dst + 32 * t) = hv[t];
@@ -1974,10 +1987,13 @@ __global__ __launch_bounds__(256) void heads_bwd_wide_bf16_kernel(HbArgs A, cons
 // f32 MFMA.  Per 16-row block: lane group q = l >> 4 reads columns 4q..4q+3 of its row l & 15 of a 16-column
 // K chunk as one float4 (the MFMA's k index in step s is column 4q + s), the matching W rows (LDS, row stride
 // FIN + 4) are the B operand, FOUT / 16 accumulators; bias and ReLU on the way out.
+// hb (nullable): h rounded to bf16 as well, (ceil(P / 16) * 16, FOUT): the bf16 heads block reads it instead of
+// converting h once per head; its padding rows hold row P - 1's values (every x load reads row min(r, P - 1)).
 template <int FIN, int FOUT>
 __global__ __launch_bounds__(kFbThreads) void feature_fwd_kernel(int P, const float *__restrict__ x,
                                                                  const float *__restrict__ w,
-                                                                 const float *__restrict__ b, float *__restrict__ h) {
+                                                                 const float *__restrict__ b, float *__restrict__ h,
+                                                                 __bf16 *__restrict__ hb) {
     constexpr int WS = FIN + 4, NT = FOUT / 16, NW = kFbThreads / 64;
     __shared__ float s_w[FOUT * WS];
     for (int e = threadIdx.x; e < FOUT * FIN / 4; e += kFbThreads) {
@@ -1995,8 +2011,7 @@ __global__ __launch_bounds__(kFbThreads) void feature_fwd_kernel(int P, const fl
         float4 xv[FIN / 16];
 #pragma unroll
         for (int kc = 0; kc < FIN / 16; kc++)
-            xv[kc] = ra < P ? *reinterpret_cast<const float4 *>(x + (size_t)ra * FIN + 16 * kc + 4 * q)
-                            : make_float4(0.f, 0.f, 0.f, 0.f);
+            xv[kc] = *reinterpret_cast<const float4 *>(x + (size_t)min(ra, P - 1) * FIN + 16 * kc + 4 * q);
         f4v acc[NT];
 #pragma unroll
         for (int t = 0; t < NT; t++) acc[t] = f4v{0.f, 0.f, 0.f, 0.f};
@@ -2018,6 +2033,10 @@ __global__ __launch_bounds__(kFbThreads) void feature_fwd_kernel(int P, const fl
             if (r < P) {
 #pragma unroll
                 for (int t = 0; t < NT; t++) h[(size_t)r * FOUT + 16 * t + c] = fmaxf(acc[t][j] + bias[t], 0.f);
+            }
+            if (hb) {
+#pragma unroll
+                for (int t = 0; t < NT; t++) hb[(size_t)r * FOUT + 16 * t + c] = (__bf16)fmaxf(acc[t][j] + bias[t], 0.f);
             }
         }
     }
@@ -2518,7 +2537,7 @@ constexpr int kErrLds = 4;
 static bool raise_lds_limit(const void *k0, const void *k1, int set, size_t need) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
-    static int state[2][64] = {};  // 0 unknown, 1 raised, 2 unavailable
+    static int state[3][64] = {};  // [set][device]: 0 unknown, 1 raised, 2 unavailable
     int &st = state[set][dev];
     if (st == 0) {
         int maxlds = 0;
@@ -2583,7 +2602,9 @@ int gs4d_heads_block_forward_bf16(const gs4d_heads_block_fwd_bf16 *args, void *s
     }
     if (((size_t)b.w1 & 15) != 0 || ((size_t)b.b1 & 15) != 0) return 1;
     if (b.P == 0) return 0;
-    if (!b.h || !b.a || (((size_t)b.h | (size_t)b.a | (size_t)b.hb | (size_t)b.w1t) & 15) != 0) return 1;
+    // h NULL: hb is the input (h already rounded to bf16, gs4d_feature_relu_forward_hb)
+    const bool hbin = !b.h;
+    if ((hbin && !b.hb) || !b.a || (((size_t)b.h | (size_t)b.a | (size_t)b.hb | (size_t)b.w1t) & 15) != 0) return 1;
     const size_t lds = 2 * (size_t)(b.W + npad_max) * (b.W + 8) + 4 * (size_t)(b.W + npad_max);
     const int nblk = (b.P + 15) / 16;
     // two workgroups per CU (the bf16 kernel's VGPRs allow two 512-thread workgroups): one round of
@@ -2591,15 +2612,17 @@ int gs4d_heads_block_forward_bf16(const gs4d_heads_block_fwd_bf16 *args, void *s
     // heads, against the fp32 kernel's 1024 / k)
     const int per_head = std::max(1, std::min((nblk + 7) / 8, std::max(1, 2 * cu_count() / b.k)));
     hipStream_t s = (hipStream_t)stream;
-    if (!raise_lds_limit((const void *)heads_block_fwd_bf16_kernel<128>, (const void *)heads_block_fwd_bf16_kernel<64>,
-                         1, lds))
+    if (!raise_lds_limit((const void *)heads_block_fwd_bf16_kernel<128, false>,
+                         (const void *)heads_block_fwd_bf16_kernel<64, false>, 1, lds) ||
+        !raise_lds_limit((const void *)heads_block_fwd_bf16_kernel<128, true>,
+                         (const void *)heads_block_fwd_bf16_kernel<64, true>, 2, lds))
         return kErrLds;
-    if (b.W == 128)
-        hipLaunchKernelGGL(heads_block_fwd_bf16_kernel<128>, dim3(per_head, b.k), dim3(kHbfThreads), lds, s, A, b.h,
-                           b.w1, b.b1, (__bf16 *)b.a, (__bf16 *)b.hb, (__bf16 *)b.w1t);
-    else
-        hipLaunchKernelGGL(heads_block_fwd_bf16_kernel<64>, dim3(per_head, b.k), dim3(kHbfThreads), lds, s, A, b.h,
-                           b.w1, b.b1, (__bf16 *)b.a, (__bf16 *)b.hb, (__bf16 *)b.w1t);
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(per_head, b.k), dim3(kHbfThreads), lds, s, A, b.h, b.w1, b.b1, (__bf16 *)b.a,
+                           (__bf16 *)b.hb, (__bf16 *)b.w1t);
+    };
+    if (b.W == 128) hbin ? go(heads_block_fwd_bf16_kernel<128, true>) : go(heads_block_fwd_bf16_kernel<128, false>);
+    else hbin ? go(heads_block_fwd_bf16_kernel<64, true>) : go(heads_block_fwd_bf16_kernel<64, false>);
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
@@ -2638,21 +2661,26 @@ int gs4d_mlp_dw_bf16(int P, int KW, int W, const uint16_t *da, const uint16_t *h
     return gs4d_sum_slices(parts, S, (int64_t)KW * W, dw, stream);
 }
 
-int gs4d_feature_relu_forward(int P, int Fin, int Fout, const float *x, const float *w, const float *b, float *h,
-                              void *stream) {
+int gs4d_feature_relu_forward_hb(int P, int Fin, int Fout, const float *x, const float *w, const float *b, float *h,
+                                 uint16_t *hb, void *stream) {
     if (P < 0 || !w || !b) return 1;
     if (!((Fin == 32 && Fout == 128) || (Fin == 64 && Fout == 64) || (Fin == 32 && Fout == 64))) return 1;
     if (P == 0) return 0;
     if (!x || !h || (((size_t)x | (size_t)w) & 15) != 0) return 1;
     hipStream_t s = (hipStream_t)stream;
     const int nwg = std::max(1, std::min(1024, ((P + 15) / 16 + 3) / 4));
+    __bf16 *hbb = reinterpret_cast<__bf16 *>(hb);
     if (Fin == 32 && Fout == 128)
-        hipLaunchKernelGGL((feature_fwd_kernel<32, 128>), dim3(nwg), dim3(kFbThreads), 0, s, P, x, w, b, h);
+        hipLaunchKernelGGL((feature_fwd_kernel<32, 128>), dim3(nwg), dim3(kFbThreads), 0, s, P, x, w, b, h, hbb);
     else if (Fin == 64)
-        hipLaunchKernelGGL((feature_fwd_kernel<64, 64>), dim3(nwg), dim3(kFbThreads), 0, s, P, x, w, b, h);
+        hipLaunchKernelGGL((feature_fwd_kernel<64, 64>), dim3(nwg), dim3(kFbThreads), 0, s, P, x, w, b, h, hbb);
     else
-        hipLaunchKernelGGL((feature_fwd_kernel<32, 64>), dim3(nwg), dim3(kFbThreads), 0, s, P, x, w, b, h);
+        hipLaunchKernelGGL((feature_fwd_kernel<32, 64>), dim3(nwg), dim3(kFbThreads), 0, s, P, x, w, b, h, hbb);
     return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+int gs4d_feature_relu_forward(int P, int Fin, int Fout, const float *x, const float *w, const float *b, float *h,
+                              void *stream) {
+    return gs4d_feature_relu_forward_hb(P, Fin, Fout, x, w, b, h, nullptr, stream);
 }
 
 int gs4d_hexplane_points(int N, const float *xyz, int64_t ld_xyz, const float *t, int64_t ld_t, const float *aabb,

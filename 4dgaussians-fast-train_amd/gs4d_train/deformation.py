@@ -418,15 +418,16 @@ class _DeformHeadsBF16(torch.autograd.Function):
             all(t.shape[0] <= 16 or t.shape[0] == 48 for t in w2)
 
     @staticmethod
-    def forward(ctx, h, w1, b1, *second):
-        """h: relu already applied (every head starts with ReLU; _FeatureReLU)."""
+    def forward(ctx, h, hb_in, w1, b1, *second):
+        """h: relu already applied (every head starts with ReLU; _FeatureReLU).  hb_in: h rounded to bf16 by
+        _FeatureReLUHB, or None (the kernel then rounds h itself)."""
         ctx.W = h.shape[1]
         if _DeformHeadsBF16._fast(h, second):
             from . import _C
             try:
                 a, hb, w1t, *outs = _C.heads_block_forward_bf16(h.contiguous(), w1.contiguous(), b1.contiguous(),
                                                            [t.contiguous() for t in second[0::2]],
-                                                           [t.contiguous() for t in second[1::2]])
+                                                           [t.contiguous() for t in second[1::2]], hb=hb_in)
             except RuntimeError as e:
                 if "status 4" not in str(e):
                     raise
@@ -452,7 +453,7 @@ class _DeformHeadsBF16(torch.autograd.Function):
         dw1 = _C.mlp_dw_bf16(da, hb) if hb.shape[1] == 128 and da.shape[1] % 128 == 0 else _splitk_dw(da, hb)
         # (P, W) fp32: gs4d_mlp_dx_bf16 (bf16 MFMA) when KW is a multiple of its 64-wide k chunk
         dh = _C.mlp_dx_bf16(da, w1t) if da.shape[1] % 64 == 0 else _mm_dx(da, w1t.t().contiguous())
-        return tuple([dh, dw1, db1] + out[2:])
+        return tuple([dh, None, dw1, db1] + out[2:])
 
     @staticmethod
     def _torch_forward(ctx, h, w1, b1, *second):
@@ -486,7 +487,7 @@ class _DeformHeadsBF16(torch.autograd.Function):
         dw1 = _splitk_dw_bf16(da, hb)
         db1 = _colsum(da)
         dh = (da @ w1b).float()
-        return tuple([dh, dw1, db1] + grads2)
+        return tuple([dh, None, dw1, db1] + grads2)  # None: hb_in
 
 
 class _FeatureReLU(torch.autograd.Function):
@@ -500,7 +501,7 @@ class _FeatureReLU(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b):
         from . import _C
-        h = _C.feature_relu_forward(x, w.contiguous(), b.contiguous())  # one f32-MFMA pass, bias + ReLU fused
+        h = _C.feature_relu_forward(x, w.contiguous(), b.contiguous())[0]  # one f32-MFMA pass, bias + ReLU fused
         ctx.save_for_backward(x, w, h)
         return h
 
@@ -510,6 +511,23 @@ class _FeatureReLU(torch.autograd.Function):
         from . import _C
         dx, dw, db = _C.feature_relu_backward(g, h, x, w)
         return dx, dw, db
+
+
+class _FeatureReLUHB(_FeatureReLU):
+    """_FeatureReLU that also returns h rounded to bf16 (gs4d_feature_relu_forward_hb, the same pass): the bf16
+    heads block reads it instead of converting h once per head.  The bf16 copy carries no gradient."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        from . import _C
+        h, hb = _C.feature_relu_forward(x, w.contiguous(), b.contiguous(), with_hb=True)
+        ctx.save_for_backward(x, w, h)
+        ctx.mark_non_differentiable(hb)
+        return h, hb
+
+    @staticmethod
+    def backward(ctx, g, ghb):
+        return _FeatureReLU.backward(ctx, g)
 
 
 class Deformation(nn.Module):
@@ -551,14 +569,16 @@ class Deformation(nn.Module):
         cheap), then the heads block on bf16 operands (_DeformHeadsBF16).  The heads' outputs (the
         deltas) are fp32, as are all parameters and gradients."""
         lin = self.feature_out[0]
+        hb = None
         if len(self.feature_out) == 1 and (feat.shape[1], self.W) in _FeatureReLU.shapes and torch.is_grad_enabled():
-            h = _FeatureReLU.apply(feat.contiguous(), lin.weight, lin.bias)
+            # h and its bf16 copy in one pass; the heads block reads the copy (half the bytes per head)
+            h, hb = _FeatureReLUHB.apply(feat.contiguous(), lin.weight, lin.bias)
         else:
             h = torch.relu(self.feature_out(feat))  # every head starts with ReLU (scene/deformation.py:73-78)
         heads = [getattr(self, name) for name in active]
         w1, b1 = self._first_layers(heads)
         second = [t for hd in heads for t in (hd[3].weight, hd[3].bias)]
-        return dict(zip(active, _DeformHeadsBF16.apply(h.contiguous(), w1, b1, *second)))
+        return dict(zip(active, _DeformHeadsBF16.apply(h.contiguous(), hb, w1, b1, *second)))
 
     def _pack_heads(self):
         """Lay the heads' first-layer weights (and biases) back to back in one storage, each parameter a view

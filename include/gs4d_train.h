@@ -237,6 +237,10 @@ int gs4d_mlp_dw_bf16(int P, int KW, int W, const uint16_t *da, const uint16_t *h
  * (32, 64)}; contiguous; g, h, W 16-byte aligned; scratch of gs4d_feature_relu_backward_scratch_bytes. */
 int gs4d_feature_relu_forward(int P, int Fin, int Fout, const float *x, const float *w, const float *b, float *h,
                               void *stream);  /* h = relu(x W^T + b), f32 MFMA; same shapes; x, W 16-byte aligned */
+/* The same, also writing h rounded to bf16 into hb (uint16 bits, (ceil(P/16)*16, Fout); its padding rows hold row
+ * P - 1's values), the input gs4d_heads_block_forward_bf16 takes when its h is NULL.  hb NULL: as above. */
+int gs4d_feature_relu_forward_hb(int P, int Fin, int Fout, const float *x, const float *w, const float *b, float *h,
+                                 uint16_t *hb, void *stream);
 size_t gs4d_feature_relu_backward_scratch_bytes(int P, int Fin, int Fout);
 int gs4d_feature_relu_backward(int P, int Fin, int Fout, const float *g, const float *h, const float *x,
                                const float *w, float *dx, float *dw, float *db, void *scratch, void *stream);
@@ -277,7 +281,8 @@ int gs4d_heads_block_forward(const gs4d_heads_block_fwd *args, void *stream);
 /* The same block on bf16 operands (hyper.mlp_dtype = "bf16"): h, W1, W2 rounded to bf16, fp32 accumulation
  * (v_mfma_f32_16x16x32_bf16), a = relu(z + b1) stored as bf16 (uint16 bits, (ceil(P/16)*16, kW)), out_i fp32.
  * hb (nullable): h rounded to bf16, (ceil(P/16)*16, W), for the backward's weight-gradient GEMM; w1t (nullable):
- * W1^T rounded to bf16 (W, kW), for its input gradient (gs4d_mlp_dx_bf16).
+ * W1^T rounded to bf16 (W, kW), for its input gradient (gs4d_mlp_dx_bf16).  h NULL: hb is an INPUT instead, h
+ * already rounded to bf16 (gs4d_feature_relu_forward_hb): read as bf16, not converted per head, not written.
  * Returns 4 (GS4D_TRAIN_ERR_LDS) when the device cannot give the kernel its LDS (also for the fp32 form). */
 #define GS4D_TRAIN_ERR_LDS 4
 typedef struct gs4d_heads_block_fwd_bf16 {

@@ -553,6 +553,12 @@ def test_heads_block_forward_bf16_matches_fp64(P, W, ns):
         return
     bf = torch.bfloat16
     assert torch.equal(hb, h.to(bf))
+    # the same block fed h already rounded to bf16 (the train path's _FeatureReLUHB copy): bitwise the same
+    hbin = torch.empty((P + 15) // 16 * 16, W, device="cuda", dtype=bf)[:P]
+    hbin.copy_(h.to(bf))
+    a2, hb2, w1t2, *out2 = _C.heads_block_forward_bf16(h, w1, b1, w2, b2, hb=hbin)
+    assert hb2.data_ptr() == hbin.data_ptr() and torch.equal(a2, a) and torch.equal(w1t2, w1t)
+    assert all(torch.equal(x, y) for x, y in zip(out2, out))
     hd = h.to(bf).double()
     z = hd @ w1.to(bf).double().t() + b1.double()
     za = hd.abs() @ w1.to(bf).double().abs().t() + b1.double().abs()
@@ -696,7 +702,9 @@ def test_feature_relu_backward_matches_fp64(P, Fin, Fout):
     assert float((dw.double() - rw).abs().max() / sw) <= 1e-5
     assert float((db.double() - rb).abs().max() / sb) <= 1e-5
     # the forward kernel: h to 1e-5 of its |terms| sum (exact zeros where the ReLU clips)
-    hf = _C.feature_relu_forward(x, w, b)
+    hf = _C.feature_relu_forward(x, w, b)[0]
+    hf2, hbf = _C.feature_relu_forward(x, w, b, with_hb=True)  # + the bf16 copy the bf16 heads block reads
+    assert torch.equal(hf2, hf) and hbf.dtype == torch.bfloat16 and torch.equal(hbf, hf.to(torch.bfloat16))
     if P:
         ref_h = (x.double() @ w.double().t() + b.double())
         hscale = x.double().abs() @ w.double().abs().t() + b.double().abs()
