@@ -212,14 +212,15 @@ __global__ __launch_bounds__(256) void hex_max_kernel(HexMaxRanges rg, uint32_t 
     const int b = (int)blockIdx.x - rg.first[r], nb = rg.first[r + 1] - rg.first[r];
     float m = 0.f;
     bool bad = false;
-    // four loads in flight per thread per round (the range is split over few blocks: each block's maximum is
-    // one atomicMax on the range's word, and those serialise)
-    for (int64_t i0 = (int64_t)b * 1024 + threadIdx.x; i0 < n; i0 += (int64_t)nb * 1024) {
-        float4 v[4];
+    // sixteen 16-byte loads in flight per thread per round (the range is split over few blocks: each block's
+    // maximum is one atomicMax on the range's word, and those serialise; so the rounds must be few and wide)
+    constexpr int kU = 16;
+    for (int64_t i0 = (int64_t)b * (256 * kU) + threadIdx.x; i0 < n; i0 += (int64_t)nb * (256 * kU)) {
+        float4 v[kU];
 #pragma unroll
-        for (int u = 0; u < 4; u++) v[u] = i0 + u * 256 < n ? x[i0 + u * 256] : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int u = 0; u < kU; u++) v[u] = i0 + u * 256 < n ? x[i0 + u * 256] : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < kU; u++) {
             const float a = fmaxf(fmaxf(fabsf(v[u].x), fabsf(v[u].y)), fmaxf(fabsf(v[u].z), fabsf(v[u].w)));
             bad |= !(a <= 3.4028235e38f) || v[u].x != v[u].x || v[u].y != v[u].y || v[u].z != v[u].z ||
                    v[u].w != v[u].w;
@@ -754,8 +755,8 @@ int gs4d_hexplane_backward(int N, const float *pts, const uint32_t *order, const
         rg.n[1 + p] = (int64_t)lay->plane[p].W * lay->plane[p].H * lay->F;
     }
     rg.first[0] = 0;
-    for (int r = 0; r < rg.nr; r++)  // >= 4 float4 per thread, at most 128 blocks per range
-        rg.first[r + 1] = rg.first[r] + (int)std::min<int64_t>(128, std::max<int64_t>(1, (rg.n[r] + 4095) / 4096));
+    for (int r = 0; r < rg.nr; r++)  // >= 16 float4 per thread, at most 128 blocks per range
+        rg.first[r + 1] = rg.first[r] + (int)std::min<int64_t>(128, std::max<int64_t>(1, (rg.n[r] + 16383) / 16384));
     hipLaunchKernelGGL(hex_max_kernel, dim3(rg.first[rg.nr]), dim3(256), 0, s, rg, mx);
     hipLaunchKernelGGL(hexplane_backward_kernel, dim3((unsigned)nwg), dim3(kHexThreads), 0, s, N, pts, order, *lay,
                        packed, dfeat, mx, dfix, dpts);
