@@ -234,7 +234,7 @@ __global__ __launch_bounds__(kTailThreads) void deform_tail_fwd_kernel(
     const float *__restrict__ o, const float *__restrict__ f_dc, const float *__restrict__ f_rest,
     const float *__restrict__ dx, const float *__restrict__ ds, const float *__restrict__ dr,
     const float *__restrict__ d_o, const float *__restrict__ dshs, float *__restrict__ means,
-    float *__restrict__ scales, float *__restrict__ rot, float *__restrict__ opac, float *__restrict__ shs) {
+    float *__restrict__ scales, float *__restrict__ rot, float *__restrict__ opac, float *__restrict__ shs, int v4) {
     if ((int)blockIdx.x < nb_g) {
         const int i = blockIdx.x * kTailThreads + threadIdx.x;
         if (i >= P) return;
@@ -258,8 +258,24 @@ __global__ __launch_bounds__(kTailThreads) void deform_tail_fwd_kernel(
         opac[i] = 1.f / (1.f + expf(-x));
         return;
     }
-    const int64_t e = (int64_t)(blockIdx.x - nb_g) * kTailThreads + threadIdx.x;
     const int64_t n = (int64_t)P * 3 * K;
+    if (v4) {
+        // four consecutive values per thread (3K % 4 == 0: they share a Gaussian), dshs / shs as 16-byte accesses
+        const int64_t e0 = 4 * ((int64_t)(blockIdx.x - nb_g) * kTailThreads + threadIdx.x);
+        if (e0 >= n) return;
+        const int64_t g = (int64_t)((uint32_t)e0 / (uint32_t)(3 * K)), k0 = e0 - g * 3 * K;
+        const float4 d = dshs ? reinterpret_cast<const float4 *>(dshs)[e0 / 4] : make_float4(0.f, 0.f, 0.f, 0.f);
+        float b[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int64_t k = k0 + j;
+            b[j] = k < 3 ? f_dc[3 * g + k] : f_rest[g * 3 * (K - 1) + (k - 3)];
+        }
+        reinterpret_cast<float4 *>(shs)[e0 / 4] =
+            dshs ? make_float4(b[0] + d.x, b[1] + d.y, b[2] + d.z, b[3] + d.w) : make_float4(b[0], b[1], b[2], b[3]);
+        return;
+    }
+    const int64_t e = (int64_t)(blockIdx.x - nb_g) * kTailThreads + threadIdx.x;
     if (e >= n) return;
     // 32-bit quotient (a 64-bit division is a long software sequence): e < P * 3K < 2^32 by the host check
     const int64_t g = (int64_t)((uint32_t)e / (uint32_t)(3 * K)), k = e - g * 3 * K;
@@ -273,7 +289,7 @@ __global__ __launch_bounds__(kTailThreads) void deform_tail_bwd_kernel(
     const float *__restrict__ g_scales, const float *__restrict__ g_rot, const float *__restrict__ g_opac,
     const float *__restrict__ g_shs, float *__restrict__ d_xyz, float *__restrict__ d_s, float *__restrict__ d_r,
     float *__restrict__ d_o, float *__restrict__ d_fdc, float *__restrict__ d_frest, float *__restrict__ g_dx,
-    float *__restrict__ g_ds, float *__restrict__ g_dr, float *__restrict__ g_do) {
+    float *__restrict__ g_ds, float *__restrict__ g_dr, float *__restrict__ g_do, int v4) {
     if ((int)blockIdx.x < nb_g) {
         const int i = blockIdx.x * kTailThreads + threadIdx.x;
         if (i >= P) return;
@@ -311,8 +327,22 @@ __global__ __launch_bounds__(kTailThreads) void deform_tail_bwd_kernel(
         if (g_do) g_do[i] = go;
         return;
     }
-    const int64_t e = (int64_t)(blockIdx.x - nb_g) * kTailThreads + threadIdx.x;
     const int64_t n = (int64_t)P * 3 * K;
+    if (v4) {  // as in deform_tail_fwd_kernel: g_shs as 16-byte loads
+        const int64_t e0 = 4 * ((int64_t)(blockIdx.x - nb_g) * kTailThreads + threadIdx.x);
+        if (e0 >= n) return;
+        const int64_t gi = (int64_t)((uint32_t)e0 / (uint32_t)(3 * K)), k0 = e0 - gi * 3 * K;
+        const float4 v4v = g_shs ? reinterpret_cast<const float4 *>(g_shs)[e0 / 4] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float v[4] = {v4v.x, v4v.y, v4v.z, v4v.w};
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int64_t k = k0 + j;
+            if (k < 3) d_fdc[3 * gi + k] = v[j];
+            else d_frest[gi * 3 * (K - 1) + (k - 3)] = v[j];
+        }
+        return;
+    }
+    const int64_t e = (int64_t)(blockIdx.x - nb_g) * kTailThreads + threadIdx.x;
     if (e >= n) return;
     const int64_t gi = (int64_t)((uint32_t)e / (uint32_t)(3 * K)), k = e - gi * 3 * K;  // e < 2^32: host check
     const float v = g_shs ? g_shs[e] : 0.f;
@@ -2368,9 +2398,10 @@ int gs4d_deform_tail_forward(int P, int K, const float *xyz, const float *s, con
     if (P == 0) return 0;
     if ((int64_t)P * 3 * K > UINT32_MAX) return 1;  // the SH range is indexed in 32 bits
     const int nb_g = (P + kTailThreads - 1) / kTailThreads;
-    const int64_t nb_s = ((int64_t)P * 3 * K + kTailThreads - 1) / kTailThreads;
+    const int v4 = (3 * K) % 4 == 0 && (((size_t)dshs | (size_t)shs) & 15) == 0;
+    const int64_t nb_s = ((int64_t)P * 3 * K / (v4 ? 4 : 1) + kTailThreads - 1) / kTailThreads;
     hipLaunchKernelGGL(deform_tail_fwd_kernel, dim3((unsigned)(nb_g + nb_s)), dim3(kTailThreads), 0, (hipStream_t)stream,
-                       P, K, nb_g, xyz, s, r, o, f_dc, f_rest, dx, ds, dr, d_o, dshs, means, scales, rot, opac, shs);
+                       P, K, nb_g, xyz, s, r, o, f_dc, f_rest, dx, ds, dr, d_o, dshs, means, scales, rot, opac, shs, v4);
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
@@ -2384,10 +2415,11 @@ int gs4d_deform_tail_backward(int P, int K, const float *scales, const float *r,
     if (P == 0) return 0;
     if ((int64_t)P * 3 * K > UINT32_MAX) return 1;  // the SH range is indexed in 32 bits
     const int nb_g = (P + kTailThreads - 1) / kTailThreads;
-    const int64_t nb_s = ((int64_t)P * 3 * K + kTailThreads - 1) / kTailThreads;
+    const int v4 = (3 * K) % 4 == 0 && ((size_t)g_shs & 15) == 0;
+    const int64_t nb_s = ((int64_t)P * 3 * K / (v4 ? 4 : 1) + kTailThreads - 1) / kTailThreads;
     hipLaunchKernelGGL(deform_tail_bwd_kernel, dim3((unsigned)(nb_g + nb_s)), dim3(kTailThreads), 0, (hipStream_t)stream,
                        P, K, nb_g, scales, r, dr, opac, g_means, g_scales, g_rot, g_opac, g_shs, d_xyz, d_s, d_r, d_o,
-                       d_fdc, d_frest, g_dx, g_ds, g_dr, g_do);
+                       d_fdc, d_frest, g_dx, g_ds, g_dr, g_do, v4);
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
