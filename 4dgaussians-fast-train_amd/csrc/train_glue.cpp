@@ -357,9 +357,11 @@ std::vector<torch::Tensor> hexplane_reg_backward(std::vector<torch::Tensor> plan
     return grads;
 }
 
-// the regulariser's gradient added in place to the planes' existing gradients (one launch for all)
-void hexplane_reg_accumulate(std::vector<torch::Tensor> planes, std::vector<torch::Tensor> grads,
-                             std::vector<double> w_smooth, std::vector<double> w_l1, const torch::Tensor &dloss_) {
+// the regulariser's gradient added in place to the planes' existing gradients (one launch for all); with_value:
+// also its value (unscaled), from the same pass (a 0-dim tensor; else an undefined one)
+torch::Tensor hexplane_reg_accumulate(std::vector<torch::Tensor> planes, std::vector<torch::Tensor> grads,
+                                      std::vector<double> w_smooth, std::vector<double> w_l1, const torch::Tensor &dloss_,
+                                      bool with_value) {
     need(grads.size() == planes.size(), "hexplane_reg_accumulate: one gradient per plane");
     for (size_t i = 0; i < planes.size(); i++) {
         gpu_f32(grads[i], "hexplane_reg gradient");
@@ -370,7 +372,17 @@ void hexplane_reg_accumulate(std::vector<torch::Tensor> planes, std::vector<torc
     b.accumulate = 1;
     c10::hip::HIPGuard guard(planes[0].device().index());
     auto dloss = dloss_.to(planes[0].device(), torch::kFloat32).contiguous();
-    check(gs4d_hexplane_reg_backward(&b, dloss.data_ptr<float>(), (void *)stream_of(planes[0])), "hexplane_reg accumulate");
+    if (!with_value) {
+        check(gs4d_hexplane_reg_backward(&b, dloss.data_ptr<float>(), (void *)stream_of(planes[0])),
+              "hexplane_reg accumulate");
+        return torch::Tensor();
+    }
+    auto loss = torch::empty({}, planes[0].options());
+    auto scratch = torch::empty({(int64_t)gs4d_reg_scratch_bytes(&b)}, planes[0].options().dtype(torch::kUInt8));
+    check(gs4d_hexplane_reg_backward_value(&b, dloss.data_ptr<float>(), loss.data_ptr<float>(), scratch.data_ptr(),
+                                           (void *)stream_of(planes[0])),
+          "hexplane_reg accumulate");
+    return loss;
 }
 
 // ---- Linear weight gradients: [(dw (n, W), db (n))] for pairs dy (P, n), x (P, W) (row strides kept)
@@ -978,7 +990,8 @@ PYBIND11_MODULE(_C, m) {
     m.def("sum_slices", &sum_slices);
     m.def("hexplane_reg_forward", &hexplane_reg_forward);
     m.def("hexplane_reg_backward", &hexplane_reg_backward);
-    m.def("hexplane_reg_accumulate", &hexplane_reg_accumulate);
+    m.def("hexplane_reg_accumulate", &hexplane_reg_accumulate, py::arg("planes"), py::arg("grads"), py::arg("w_smooth"),
+          py::arg("w_l1"), py::arg("dloss"), py::arg("with_value") = false);
     m.def("deform_tail_forward", &deform_tail_forward);
     m.def("deform_tail_backward", &deform_tail_backward);
     m.def("hexplane_forward", &hexplane_forward, py::arg("pts"), py::arg("planes"), py::arg("order") = py::none());

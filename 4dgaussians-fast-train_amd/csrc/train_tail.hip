@@ -408,24 +408,32 @@ __global__ __launch_bounds__(kTailThreads) void reg_final_kernel(int nblk, const
 // d/dt of the batch loss, as autograd derives it from the reference's graph: mean -> g / N, square
 // -> 2 s g, second[y] = first[y+1] - first[y] -> dfirst[j] = ds[j-1] - ds[j], first[j] = t[j+1] - t[j]
 // -> dt[y] = dfirst[y-1] - dfirst[y] (out-of-range terms are 0); abs(1 - t) -> -sign(1 - t) g / N.
-__global__ __launch_bounds__(kTailThreads) void reg_backward_kernel(gs4d_reg_batch b, const float *__restrict__ dloss) {
+// part (nullable): also the value's per-workgroup partials, exactly as reg_forward_kernel forms them (same
+// workgroups, same per-thread order and terms: its second difference at row y is the ds[2] term below), for
+// reg_final_kernel -- the value and the gradient from one read of the planes.
+__global__ __launch_bounds__(kTailThreads) void reg_backward_kernel(gs4d_reg_batch b, const float *__restrict__ dloss,
+                                                                    double *__restrict__ part) {
     const int64_t blk = blockIdx.x;
     const gs4d_reg_plane d = b.p[reg_plane_of(b, blk)];
     const int64_t n = (int64_t)d.C * d.H * d.W, hw = (int64_t)d.H * d.W;
     const float g = *dloss;
     const float gs = (g * d.w_smooth) / (float)((int64_t)d.C * (d.H - 2) * d.W);
     const float gl = (g * d.w_l1) / (float)n;
+    const double cs = (double)d.w_smooth / ((double)d.C * (d.H - 2) * d.W), cl = (double)d.w_l1 / (double)n;
+    double acc = 0.0;
 #pragma unroll
     for (int k = 0; k < kRegPerThread; k++) {
         const int64_t i = (blk - d.first_block) * kRegBlock + (int64_t)k * kTailThreads + threadIdx.x;
         if (i >= n) break;
         const int y = (int)(((uint32_t)i % (uint32_t)hw) / (uint32_t)d.W);  // 32-bit: a plane < 2^31 elements
         const float *col = d.data + (i - (int64_t)y * d.W);
-        float ds[3];  // ds[y-2], ds[y-1], ds[y]
+        float ds[3], s2y = 0.f;  // ds[y-2], ds[y-1], ds[y]; s2y: the second difference at row y itself
 #pragma unroll
         for (int q = 0; q < 3; q++) {
             const int yy = y - 2 + q;
-            ds[q] = (yy >= 0 && yy <= d.H - 3) ? 2.f * second_diff(col, yy, d.W) * gs : 0.f;
+            const float s2 = (yy >= 0 && yy <= d.H - 3) ? second_diff(col, yy, d.W) : 0.f;
+            ds[q] = (yy >= 0 && yy <= d.H - 3) ? 2.f * s2 * gs : 0.f;
+            if (q == 2) s2y = s2;
         }
         const float df_prev = (y >= 1) ? ds[0] - ds[1] : 0.f;      // dfirst[y-1] = ds[y-2] - ds[y-1]
         const float df_cur = (y <= d.H - 2) ? ds[1] - ds[2] : 0.f;  // dfirst[y] = ds[y-1] - ds[y]
@@ -435,6 +443,18 @@ __global__ __launch_bounds__(kTailThreads) void reg_backward_kernel(gs4d_reg_bat
         const float v = (df_prev - df_cur) + (-sg) * gl;
         if (b.accumulate) d.grad[i] += v;
         else d.grad[i] = v;
+        if (part) {  // reg_forward_kernel's terms, in its order
+            if (y <= d.H - 3) acc += cs * (double)(s2y * s2y);
+            acc += cl * (double)fabsf(1.f - t);
+        }
+    }
+    if (part) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+        __shared__ double s_w[kTailThreads / 64];
+        if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = acc;
+        __syncthreads();
+        if (threadIdx.x == 0) part[blk] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
     }
 }
 
@@ -2336,7 +2356,20 @@ int gs4d_hexplane_reg_backward(const gs4d_reg_batch *batch, const float *dloss, 
     for (int i = 0; i < batch->count; i++)
         if (!batch->p[i].grad) return 1;
     hipLaunchKernelGGL(reg_backward_kernel, dim3((unsigned)nblk), dim3(kTailThreads), 0, (hipStream_t)stream, *batch,
-                       dloss);
+                       dloss, nullptr);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+int gs4d_hexplane_reg_backward_value(const gs4d_reg_batch *batch, const float *dloss, float *loss, void *scratch,
+                                     void *stream) {
+    int64_t nblk = 0;
+    if (reg_check(batch, &nblk) || !dloss || !loss || !scratch) return 1;
+    for (int i = 0; i < batch->count; i++)
+        if (!batch->p[i].grad) return 1;
+    double *part = (double *)align_up((size_t)scratch, 8);
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(reg_backward_kernel, dim3((unsigned)nblk), dim3(kTailThreads), 0, s, *batch, dloss, part);
+    hipLaunchKernelGGL(reg_final_kernel, dim3(1), dim3(kTailThreads), 0, s, (int)nblk, part, loss);
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 

@@ -379,13 +379,15 @@ class GaussianModel:
         return hexplane_regulation_value([list(g) for g in grids], time_smoothness_weight, l1_time_planes_weight,
                                          plane_tv_weight)
 
-    def add_regulation_grad(self, time_smoothness_weight, l1_time_planes_weight, plane_tv_weight, scale=1.0):
+    def add_regulation_grad(self, time_smoothness_weight, l1_time_planes_weight, plane_tv_weight, scale=1.0,
+                            with_value=False):
         """scale * d(compute_regulation)/d(plane) added to the planes' .grad in one launch: the gradient
-        the loss's regulariser term contributes, applied after the rest of the backward."""
+        the loss's regulariser term contributes, applied after the rest of the backward.  with_value: returns
+        compute_regulation's value too, from the same pass (regulation_value's number, bitwise)."""
         from .kernels import hexplane_regulation_accumulate_grad
         grids = self._deformation.deformation_net.grid.grids
-        hexplane_regulation_accumulate_grad([list(g) for g in grids], time_smoothness_weight, l1_time_planes_weight,
-                                            plane_tv_weight, scale)
+        return hexplane_regulation_accumulate_grad([list(g) for g in grids], time_smoothness_weight,
+                                                   l1_time_planes_weight, plane_tv_weight, scale, with_value)
 
     # ---- on-disk formats (gaussian_model.py:214-314 and scene/__init__.py:143-150)
     def save_ply(self, path):

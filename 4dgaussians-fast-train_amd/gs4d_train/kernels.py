@@ -326,13 +326,15 @@ def hexplane_regulation_value(ms_grids, time_smoothness_weight, l1_time_planes_w
 
 @torch.no_grad()
 def hexplane_regulation_accumulate_grad(ms_grids, time_smoothness_weight, l1_time_planes_weight, plane_tv_weight,
-                                        scale=1.0):
+                                        scale=1.0, with_value=False):
     """Adds scale * d(regulariser)/d(plane) to every plane's .grad in one launch: the gradient autograd
     would add to the field's plane gradients when the regulariser is part of the loss (train.py:251-254),
-    without autograd's separate add per plane.  A plane without a gradient yet gets one."""
+    without autograd's separate add per plane.  A plane without a gradient yet gets one.  with_value: also
+    returns the regulariser's (unscaled) value from the same pass over the planes, bitwise
+    hexplane_regulation_value's."""
     planes, ws, wl = _reg_batch(ms_grids, time_smoothness_weight, l1_time_planes_weight, plane_tv_weight)
     if not planes:
-        return
+        return torch.zeros((), device=ms_grids[0][0].device) if with_value else None
     for p in planes:
         if p.grad is None:
             p.grad = torch.zeros_like(p)
@@ -341,7 +343,9 @@ def hexplane_regulation_accumulate_grad(ms_grids, time_smoothness_weight, l1_tim
     dloss = _DLOSS.get(key)
     if dloss is None:
         dloss = _DLOSS[key] = torch.full((1,), float(scale), device=planes[0].device)
-    _C.hexplane_reg_accumulate([p.detach() for p in planes], [p.grad for p in planes], ws, wl, dloss)
+    v = _C.hexplane_reg_accumulate([p.detach() for p in planes], [p.grad for p in planes], ws, wl, dloss,
+                                   with_value=with_value)
+    return v if with_value else None
 
 
 _DLOSS = {}

@@ -78,14 +78,12 @@ def train_step(gaussians, views, opt, hyper, iteration, background, stage="fine"
         loss = torch.zeros((), device=dev)
     reg_w = (hyper.time_smoothness_weight, hyper.l1_time_planes, hyper.plane_tv_weight)
     reg_scale = 1.0 / dp.world() if data_parallel else 1.0
-    reg_deferred = None
+    reg_deferred = False
     if stage == "fine" and hyper.time_smoothness_weight != 0:
         if fused:
-            # the regulariser depends only on the planes: its value joins the reported loss and its
-            # gradient is added to the planes' gradients after the backward, in one launch
-            reg_deferred = gaussians.regulation_value(*reg_w)
-            if reg_scale != 1.0:
-                reg_deferred = reg_deferred * reg_scale
+            # the regulariser depends only on the planes: after the backward one pass over them adds its
+            # gradient to the planes' gradients and gives its value, which joins the reported loss
+            reg_deferred = True
         else:
             reg = gaussians.compute_regulation(*reg_w)
             loss = loss + reg * reg_scale
@@ -100,9 +98,11 @@ def train_step(gaussians, views, opt, hyper, iteration, background, stage="fine"
             image_tensor.backward(image_grad)
     elif loss.requires_grad:
         loss.backward()
-    if reg_deferred is not None:
-        gaussians.add_regulation_grad(*reg_w, scale=reg_scale)
-        loss = loss.detach() + reg_deferred
+    if reg_deferred:
+        reg_value = gaussians.add_regulation_grad(*reg_w, scale=reg_scale, with_value=True)
+        if reg_scale != 1.0:
+            reg_value = reg_value * reg_scale
+        loss = loss.detach() + reg_value
     if len(vs_list) == 1 and vs_list[0].grad is not None:
         viewspace_grad = vs_list[0].grad
     else:

@@ -166,6 +166,10 @@ int64_t gs4d_reg_blocks(int C, int H, int W);
 size_t gs4d_reg_scratch_bytes(const gs4d_reg_batch *batch);
 int gs4d_hexplane_reg_forward(const gs4d_reg_batch *batch, float *loss, void *scratch, void *stream);
 int gs4d_hexplane_reg_backward(const gs4d_reg_batch *batch, const float *dloss, void *stream);
+/* The backward and the value in one pass over the planes: the gradient as gs4d_hexplane_reg_backward, and *loss
+ * bitwise as gs4d_hexplane_reg_forward would give it (same partials, same order); scratch as for the forward. */
+int gs4d_hexplane_reg_backward_value(const gs4d_reg_batch *batch, const float *dloss, float *loss, void *scratch,
+                                     void *stream);
 
 /* ---- Linear-layer weight gradients over many rows: for each problem, dw (n, W) = dy^T x and db (n)
  * = column sums of dy (db may be NULL) -- the backward of F.linear as autograd forms it -- for dy (P, n)

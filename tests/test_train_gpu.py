@@ -318,6 +318,16 @@ def test_hexplane_regulation_fused_matches_torch():
     for a, b in zip([p for l in grids_f for p in l], [p for l in grids_t for p in l]):
         scale = max(float(b.grad.abs().max()), 1e-30)
         assert float((a.grad - b.grad).abs().max()) <= 1e-5 * scale
+    # the train step's form: value and gradient from one pass (accumulate_grad with_value) -- the value bitwise
+    # hexplane_regulation_value's, the gradient bitwise the accumulate-only pass's
+    from gs4d_train.kernels import hexplane_regulation_accumulate_grad, hexplane_regulation_value
+    ga = [[p.detach().clone().requires_grad_(True) for p in l] for l in grids_f]
+    gb = [[p.detach().clone().requires_grad_(True) for p in l] for l in grids_f]
+    v = hexplane_regulation_accumulate_grad(ga, *w, scale=2.5, with_value=True)
+    assert hexplane_regulation_accumulate_grad(gb, *w, scale=2.5) is None
+    assert torch.equal(v, hexplane_regulation_value(ga, *w))
+    for a, b in zip([p for l in ga for p in l], [p for l in gb for p in l]):
+        assert torch.equal(a.grad, b.grad)
 
 
 @pytest.mark.parametrize("P,W,ns", [(100_003, 128, [3, 3, 4, 1]), (777, 64, [2, 5, 8]), (3000, 256, [16, 7]),
