@@ -9,13 +9,13 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "4dgaussians-fast-train_amd"))
-from gs4d_train.synthetic import CONFIGS, make_scene  # noqa: E402
+from gs4d_train.synthetic import CONFIGS, make_scene, make_train_like_scene  # noqa: E402
 import diff_gaussian_rasterization as dgr  # noqa: E402
 
 
 def main():
     P, W, H = CONFIGS[sys.argv[1] if len(sys.argv) > 1 else "metric"]
-    s = make_scene(P, W, H, seed=0)
+    s = (make_train_like_scene if "--train-like" in sys.argv else make_scene)(P, W, H, seed=0)
     dev = torch.device("cuda", 0)
     t = lambda a: torch.tensor(np.asarray(a), device=dev)
     e = torch.empty(0, device=dev)
@@ -35,6 +35,9 @@ def main():
     q = lambda a: {p: int(np.percentile(a, p)) for p in (50, 90, 99, 100)}
     print("num_rendered", nr, "emitted", int(cnt.sum()), "tiles", T)
     print("instances/tile", q(cnt), "mean", float(cnt.mean()))
+    hist = {f"{lo}-{hi}": int(((cnt >= lo) & (cnt <= hi)).sum()) for lo, hi in
+            ((0, 128), (129, 256), (257, 512), (513, 1024), (1025, 2048), (2049, 1 << 30))}
+    print("tiles by run length", hist)
     order = np.sort(cnt)[::-1]
     print("top tiles", order[:16].tolist())
     print("n_contrib/pixel", q(ncontrib), "mean", float(ncontrib.mean()))
