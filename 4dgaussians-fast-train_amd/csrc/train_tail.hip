@@ -2170,10 +2170,13 @@ static bool hb_mfma(int W, int n) { return (W == 64 || W == 128) && n == 48; }  
 #define HB_WIDE_BF16 1
 #endif
 static const bool hb_wide_bf16 = HB_WIDE_BF16 != 0;  // the bf16 path's wide head on heads_bwd_wide_bf16_kernel
-static int hb_rows_per_wg(int P, bool wide) {
-    // narrow heads stream a: about two workgroups per CU; the wide head's waves are compute-heavy and
-    // its per-workgroup partials large: 256-row blocks
-    return wide ? 128 : std::max(64, (P + 511) / 512);
+static int hb_rows_per_wg(int P, bool wide, bool bf) {
+    // narrow heads stream a: about two (fp32) or four (bf16: half the bytes per row) workgroups per CU; the wide
+    // head's waves are compute-heavy and its per-workgroup partials large (9 KB per block of rows): 512-row
+    // blocks on the fp32 MFMA kernel, 256 on the bf16 one (tools/ab_heads.sh at P = 100k: the fp32 heads
+    // backward 160 -> 148 us, the bf16 one 106 -> 97 us against 128-row blocks and P / 512 narrow rows)
+    if (wide) return bf ? 256 : 512;
+    return bf ? std::max(64, (P + 1023) / 1024) : std::max(64, (P + 511) / 512);
 }
 extern "C++" {
 template <class Fn>
@@ -2193,7 +2196,8 @@ size_t gs4d_heads_backward_scratch_bytes(int P, int W, int k, const int *n) {
     hb_groups(k, n, [&](int h0, int hk) {
         size_t per = (size_t)hk * W;
         for (int i = h0; i < h0 + hk; i++) per += (size_t)std::max(n[i], 0) * (W + 1);
-        const int rows = hb_rows_per_wg(P, hb_wide(n[h0]));
+        // one size for both element types: the smaller row block (more workgroups, more partials)
+        const int rows = std::min(hb_rows_per_wg(P, hb_wide(n[h0]), false), hb_rows_per_wg(P, hb_wide(n[h0]), true));
         const size_t nwg = std::max<size_t>(1, ((size_t)P + rows - 1) / rows);
         total += align_up(4 * nwg * per, 256);
     });
@@ -2228,7 +2232,7 @@ static int heads_backward_t(const Args *args, void *scratch, void *stream) {
     int err = 0;
     hb_groups(b.k, b.n, [&](int h0, int hk) {
         A.h0 = h0, A.hk = hk;
-        A.rows_per_wg = hb_rows_per_wg(b.P, hb_wide(b.n[h0]));
+        A.rows_per_wg = hb_rows_per_wg(b.P, hb_wide(b.n[h0]), std::is_same<TA, __bf16>::value);
         A.poff[0] = hk * b.W;
         for (int i = 0; i < hk; i++) A.poff[i + 1] = A.poff[i] + b.n[h0 + i] * (b.W + 1);
         const int nwg = std::max(1, (int)(((int64_t)b.P + A.rows_per_wg - 1) / A.rows_per_wg));
