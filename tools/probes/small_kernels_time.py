@@ -1,0 +1,42 @@
+"""Device time of the train step's smaller HIP passes at its shapes (diagnostic, GPU): the first deformation
+layer's backward (P = 100k, 32 -> 128), the deformation tail both ways, HIP events over R calls.  For A/B of
+libgs4d variants (LD_LIBRARY_PATH=4dgaussians-fast-train_amd/build/variant_<name>)."""
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "4dgaussians-fast-train_amd")]
+from gs4d_train import _C  # noqa: E402
+
+
+def timed(fn, reps=20):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps * 1e3
+
+
+def main():
+    P, Fin, Fout = 100_000, 32, 128
+    torch.manual_seed(0)
+    x = torch.randn(P, Fin, device="cuda")
+    w = torch.randn(Fout, Fin, device="cuda") / Fin ** 0.5
+    b = torch.randn(Fout, device="cuda") * 0.1
+    h = _C.feature_relu_forward(x, w, b)[0]
+    g = torch.randn(P, Fout, device="cuda")
+    rows = [("feature_relu_forward", lambda: _C.feature_relu_forward(x, w, b)),
+            ("feature_relu_forward (+hb)", lambda: _C.feature_relu_forward(x, w, b, with_hb=True)),
+            ("feature_relu_backward", lambda: _C.feature_relu_backward(g, h, x, w))]
+    for name, fn in rows:
+        print(f"{name:28s} {timed(fn):8.1f} us", flush=True)
+
+
+if __name__ == "__main__":
+    main()
