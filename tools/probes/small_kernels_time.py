@@ -34,6 +34,16 @@ def main():
     rows = [("feature_relu_forward", lambda: _C.feature_relu_forward(x, w, b)),
             ("feature_relu_forward (+hb)", lambda: _C.feature_relu_forward(x, w, b, with_hb=True)),
             ("feature_relu_backward", lambda: _C.feature_relu_backward(g, h, x, w))]
+    # the HexPlane regulariser's gradient (+ value) at DyNeRF's planes (F = 16, [64, 64, 64, 150] x multires [1, 2])
+    from gs4d_train.kernels import hexplane_regulation_accumulate_grad
+    grids = []
+    for reso in ([64, 64, 64, 150], [128, 128, 128, 150]):
+        pairs = [(0, 1), (0, 2), (0, 3), (1, 2), (1, 3), (2, 3)]
+        grids.append([torch.rand(1, 16, reso[c1], reso[c0], device="cuda").requires_grad_(True) for c0, c1 in pairs])
+    for lvl in grids:
+        for q in lvl:
+            q.grad = torch.zeros_like(q)
+    rows.append(("reg accumulate + value", lambda: hexplane_regulation_accumulate_grad(grids, 1.0, 1e-4, 2e-4, 1.0, True)))
     for name, fn in rows:
         print(f"{name:28s} {timed(fn):8.1f} us", flush=True)
 
