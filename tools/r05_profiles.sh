@@ -2,7 +2,7 @@
 # Round-5 profiles on one box: kernel trace + PMC passes of the metric scene (tools/prof_valu.sh), the kernel
 # trace of the train-like scene, and the train step's kernel sequence (fp32 and bf16 MLP).
 export TMPDIR=/tmp
-T=${TAG:-r05a}
+T=${TAG:-r05b}
 TAG=$T bash tools/prof_valu.sh || exit $?
 OUT=gpurun_out/prof_$T
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $OUT/trace_tl -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-train-step --no-extras --scene train_like > $OUT/bench_trace_tl.log 2>&1 || { echo "trace_tl rc=$?"; exit 1; }
