@@ -15,6 +15,7 @@
 #include <torch/extension.h>
 
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "../../include/gs4d.h"
@@ -33,6 +34,28 @@ void gpu_f32(const torch::Tensor &t, const char *name) {
     need(t.is_contiguous(), std::string(name) + " must be contiguous");
 }
 hipStream_t stream_of(const torch::Tensor &t) { return c10::hip::getCurrentHIPStream(t.device().index()).stream(); }
+
+// Scratch for the last-workgroup totals (L1 loss, regulariser): its ticket word must be zero on entry and each
+// call leaves it zero, so one buffer is kept per (device, stream, user) -- zeroed when made or grown -- instead of
+// a fresh allocation (and a memset launch) per call.  Calls on one stream are ordered, so they may share it.
+void *ticket_scratch(const torch::Tensor &like, size_t bytes, int user) {
+    struct Key {
+        int dev;
+        hipStream_t s;
+        int user;
+        bool operator<(const Key &o) const {
+            return std::tie(dev, s, user) < std::tie(o.dev, o.s, o.user);
+        }
+    };
+    static std::mutex mu;
+    static auto *bufs = new std::map<Key, torch::Tensor>();  // never destroyed: no device frees at process exit
+    const Key k{(int)like.device().index(), stream_of(like), user};
+    std::lock_guard<std::mutex> lk(mu);
+    torch::Tensor &b = (*bufs)[k];
+    if (!b.defined() || (size_t)b.numel() < bytes)
+        b = torch::zeros({(int64_t)std::max<size_t>(bytes, 4096)}, like.options().dtype(torch::kUInt8));
+    return b.data_ptr();
+}
 }  // namespace
 
 // l1_loss forward: returns (loss (0-dim), sign (int8, x's shape))
@@ -44,9 +67,8 @@ std::tuple<torch::Tensor, torch::Tensor> l1_forward(const torch::Tensor &x_, con
     const int64_t n = x.numel();
     torch::Tensor sign = torch::empty(x.sizes(), x.options().dtype(torch::kInt8));
     torch::Tensor loss = torch::empty({}, x.options());
-    torch::Tensor scratch = torch::empty({(int64_t)gs4d_l1_scratch_bytes(n)}, x.options().dtype(torch::kUInt8));
     check(gs4d_l1_loss_forward(n, x.data_ptr<float>(), y.data_ptr<float>(), sign.data_ptr<int8_t>(),
-                               loss.data_ptr<float>(), scratch.data_ptr(), stream_of(x)),
+                               loss.data_ptr<float>(), ticket_scratch(x, gs4d_l1_scratch_bytes(n), 0), stream_of(x)),
           "l1_loss forward");
     return {loss, sign};
 }
@@ -61,9 +83,8 @@ std::tuple<torch::Tensor, torch::Tensor> l1_loss_grad(const torch::Tensor &x_, c
     need(n % 4 == 0, "l1_loss_grad: numel must be a multiple of 4");
     torch::Tensor grad = torch::empty(x.sizes(), x.options());
     torch::Tensor loss = torch::empty({}, x.options());
-    torch::Tensor scratch = torch::empty({(int64_t)gs4d_l1_scratch_bytes(n)}, x.options().dtype(torch::kUInt8));
     check(gs4d_l1_loss_grad(n, x.data_ptr<float>(), y.data_ptr<float>(), (float)dloss, loss.data_ptr<float>(),
-                            grad.data_ptr<float>(), scratch.data_ptr(), stream_of(x)),
+                            grad.data_ptr<float>(), ticket_scratch(x, gs4d_l1_scratch_bytes(n), 0), stream_of(x)),
           "l1_loss_grad");
     return {loss, grad};
 }
@@ -341,8 +362,9 @@ torch::Tensor hexplane_reg_forward(std::vector<torch::Tensor> planes, std::vecto
     c10::hip::HIPGuard guard(planes[0].device().index());
     hipStream_t s = stream_of(planes[0]);
     auto loss = torch::empty({}, planes[0].options());
-    auto scratch = torch::empty({(int64_t)gs4d_reg_scratch_bytes(&b)}, planes[0].options().dtype(torch::kUInt8));
-    check(gs4d_hexplane_reg_forward(&b, loss.data_ptr<float>(), scratch.data_ptr(), (void *)s), "hexplane_reg forward");
+    check(gs4d_hexplane_reg_forward(&b, loss.data_ptr<float>(), ticket_scratch(planes[0], gs4d_reg_scratch_bytes(&b), 1),
+                                    (void *)s),
+          "hexplane_reg forward");
     return loss;
 }
 
@@ -361,7 +383,7 @@ std::vector<torch::Tensor> hexplane_reg_backward(std::vector<torch::Tensor> plan
 // also its value (unscaled), from the same pass (a 0-dim tensor; else an undefined one)
 torch::Tensor hexplane_reg_accumulate(std::vector<torch::Tensor> planes, std::vector<torch::Tensor> grads,
                                       std::vector<double> w_smooth, std::vector<double> w_l1, const torch::Tensor &dloss_,
-                                      bool with_value) {
+                                      bool with_value, c10::optional<torch::Tensor> base) {
     need(grads.size() == planes.size(), "hexplane_reg_accumulate: one gradient per plane");
     for (size_t i = 0; i < planes.size(); i++) {
         gpu_f32(grads[i], "hexplane_reg gradient");
@@ -378,8 +400,14 @@ torch::Tensor hexplane_reg_accumulate(std::vector<torch::Tensor> planes, std::ve
         return torch::Tensor();
     }
     auto loss = torch::empty({}, planes[0].options());
-    auto scratch = torch::empty({(int64_t)gs4d_reg_scratch_bytes(&b)}, planes[0].options().dtype(torch::kUInt8));
-    check(gs4d_hexplane_reg_backward_value(&b, dloss.data_ptr<float>(), loss.data_ptr<float>(), scratch.data_ptr(),
+    const float *bp = nullptr;
+    if (base && base->defined()) {
+        gpu_f32(*base, "hexplane_reg base");
+        need(base->numel() == 1 && base->device() == planes[0].device(), "hexplane_reg base: one value on the planes' device");
+        bp = base->data_ptr<float>();
+    }
+    check(gs4d_hexplane_reg_backward_value(&b, dloss.data_ptr<float>(), loss.data_ptr<float>(), bp,
+                                           ticket_scratch(planes[0], gs4d_reg_scratch_bytes(&b), 1),
                                            (void *)stream_of(planes[0])),
           "hexplane_reg accumulate");
     return loss;
@@ -686,15 +714,25 @@ torch::Tensor hexplane_points(const torch::Tensor &xyz, const torch::Tensor &t, 
           "hexplane_points");
     return pts;
 }
-torch::Tensor hexplane_points_backward(const torch::Tensor &dpts_, const torch::Tensor &aabb_) {
+// add (optional): another (N, 3) gradient of xyz, summed in by the same pass
+torch::Tensor hexplane_points_backward(const torch::Tensor &dpts_, const torch::Tensor &aabb_,
+                                       const c10::optional<torch::Tensor> &add_) {
     auto dpts = dpts_.contiguous();
     gpu_f32(dpts, "dpts");
     need(dpts.dim() == 2 && dpts.size(1) == 4, "hexplane_points_backward: dpts (N, 4)");
     c10::hip::HIPGuard guard(dpts.device().index());
     auto aabb = aabb_.to(dpts.device(), torch::kFloat32).contiguous();
+    torch::Tensor add;
+    if (add_.has_value() && add_->defined()) {
+        add = add_->to(torch::kFloat32).contiguous();
+        need(add.is_cuda() && add.device() == dpts.device() && add.dim() == 2 && add.size(0) == dpts.size(0) &&
+                 add.size(1) == 3,
+             "hexplane_points_backward: add (N, 3) on dpts' device");
+    }
     auto dxyz = torch::empty({dpts.size(0), 3}, dpts.options());
-    check(gs4d_hexplane_points_backward((int)dpts.size(0), dpts.data_ptr<float>(), aabb.data_ptr<float>(),
-                                        dxyz.data_ptr<float>(), (void *)stream_of(dpts)),
+    check(gs4d_hexplane_points_backward_add((int)dpts.size(0), dpts.data_ptr<float>(), aabb.data_ptr<float>(),
+                                            add.defined() ? add.data_ptr<float>() : nullptr, dxyz.data_ptr<float>(),
+                                            (void *)stream_of(dpts)),
           "hexplane_points_backward");
     return dxyz;
 }
@@ -973,7 +1011,8 @@ torch::Tensor sum_slices(torch::Tensor parts) {
 
 PYBIND11_MODULE(_C, m) {
     m.def("hexplane_points", &hexplane_points);
-    m.def("hexplane_points_backward", &hexplane_points_backward);
+    m.def("hexplane_points_backward", &hexplane_points_backward, py::arg("dpts"), py::arg("aabb"),
+          py::arg("add") = py::none());
     m.def("feature_relu_forward", &feature_relu_forward, py::arg("x"), py::arg("w"), py::arg("b"),
           py::arg("with_hb") = false);
     m.def("heads_forward", &heads_forward);
@@ -991,7 +1030,7 @@ PYBIND11_MODULE(_C, m) {
     m.def("hexplane_reg_forward", &hexplane_reg_forward);
     m.def("hexplane_reg_backward", &hexplane_reg_backward);
     m.def("hexplane_reg_accumulate", &hexplane_reg_accumulate, py::arg("planes"), py::arg("grads"), py::arg("w_smooth"),
-          py::arg("w_l1"), py::arg("dloss"), py::arg("with_value") = false);
+          py::arg("w_l1"), py::arg("dloss"), py::arg("with_value") = false, py::arg("base") = py::none());
     m.def("deform_tail_forward", &deform_tail_forward);
     m.def("deform_tail_backward", &deform_tail_backward);
     m.def("hexplane_forward", &hexplane_forward, py::arg("pts"), py::arg("planes"), py::arg("order") = py::none());

@@ -32,9 +32,87 @@ constexpr int kTailThreads = 256;
 constexpr int kL1PerThread = 8;
 constexpr int kL1Chunk = kTailThreads * kL1PerThread;
 
+// ---- last-workgroup totals ------------------------------------------------------------------------
+// A sum over a grid's per-workgroup partials without a second launch.  Each workgroup publishes its partial
+// in its slot (agent-scope relaxed atomic store: coherent across the XCDs' L2s) and draws a ticket; the
+// workgroup that draws the last ticket reads every slot and sums them in a fixed order -- thread-strided, then
+// the wave tree, then the waves in order: the order of the separate one-workgroup final kernels these replace,
+// so totals are unchanged bit for bit -- then puts every slot and ticket back to 0 for the next call.
+// Tickets in two levels: workgroup b draws from sub-counter b % kTicketFan (each on its own 128-byte line),
+// the last drawer of a sub-counter from the top counter -- one counter drawn by ~2000 workgroups serialised
+// its atomics (~10 ns each, ~20 us per launch here).  No fences: an acquire/release pair at agent scope
+// writes back the whole L2 in every workgroup (buffer_wbl2; ~70 us per launch here).  Instead a slot holds
+// bits + 1 (never 0 for a partial: a double whose bits are all ones is not produced), and the last workgroup
+// waits on any slot still reading 0 (a store issued before its workgroup's ticket, not yet visible); the wait
+// is bounded.  Scratch layout: the counters at the 8-aligned start (kTicketWords words), the slots after them;
+// all zero on entry and again on return (the callers keep the scratch).
+constexpr int kTicketFan = 16, kTicketLine = 32;  // sub-counters; u32 words per counter (128 bytes)
+constexpr int kTicketWords = (kTicketFan + 1) * kTicketLine;
+struct TicketScratch {
+    uint32_t *ticket;  // [0] top, [(j + 1) * kTicketLine] sub-counter j
+    double *part;
+};
+__host__ __device__ inline TicketScratch ticket_scratch(void *scratch) {
+    uint32_t *t = (uint32_t *)(((size_t)scratch + 7) & ~(size_t)7);
+    return {t, (double *)(t + kTicketWords)};
+}
+
+// Thread 0 holds `t`, this workgroup's partial.  Returns true in every thread of the last workgroup, with
+// the total in *total (all threads); false elsewhere.
+__device__ __forceinline__ bool publish_and_total(double t, TicketScratch ts, int nblk, double *total) {
+    __shared__ uint32_t s_last;
+    __shared__ double s_w[kTailThreads / 64];
+    unsigned long long *slot = (unsigned long long *)ts.part;
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(slot + blockIdx.x, (unsigned long long)__double_as_longlong(t) + 1ull, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t j = blockIdx.x % kTicketFan, nj = ((uint32_t)nblk - j + kTicketFan - 1) / kTicketFan;
+        uint32_t *sub = ts.ticket + (j + 1) * kTicketLine;
+        bool last = false;
+        if (__hip_atomic_fetch_add(sub, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nj - 1u) {
+            __hip_atomic_store(sub, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // every draw on it is done
+            const uint32_t nsub = nblk < kTicketFan ? (uint32_t)nblk : (uint32_t)kTicketFan;
+            last = __hip_atomic_fetch_add(ts.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nsub - 1u;
+        }
+        s_last = last;
+    }
+    __syncthreads();
+    if (!s_last) return false;
+    // the slots in rounds of kRound per thread, all loads of a round in flight at once (then the rare waits)
+    constexpr int kRound = 8;
+    double s = 0.0;
+    for (int i0 = 0; i0 < nblk; i0 += kRound * kTailThreads) {
+        unsigned long long v[kRound];
+#pragma unroll
+        for (int k = 0; k < kRound; k++) {
+            const int i = i0 + k * kTailThreads + (int)threadIdx.x;
+            v[k] = i < nblk ? __hip_atomic_load(slot + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 1ull;  // 1: +0.0
+        }
+#pragma unroll
+        for (int k = 0; k < kRound; k++) {
+            const int i = i0 + k * kTailThreads + (int)threadIdx.x;
+            for (uint32_t spins = 0; v[k] == 0ull && spins < (1u << 22); spins++)
+                v[k] = __hip_atomic_load(slot + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (i < nblk) __hip_atomic_store(slot + i, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (i < nblk) s += __longlong_as_double((long long)(v[k] - 1ull));
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = s;
+    __syncthreads();
+    double sum = 0.0;
+#pragma unroll
+    for (int w = 0; w < kTailThreads / 64; w++) sum += s_w[w];
+    *total = sum;
+    if (threadIdx.x == 0) __hip_atomic_store(ts.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+}
+
 __global__ __launch_bounds__(kTailThreads) void l1_partial_kernel(int64_t n, const float *__restrict__ x,
                                                                   const float *__restrict__ y,
-                                                                  int8_t *__restrict__ sign, double *__restrict__ part) {
+                                                                  int8_t *__restrict__ sign, TicketScratch ts,
+                                                                  float *__restrict__ loss) {
     const int64_t base = (int64_t)blockIdx.x * kL1Chunk;
     float acc = 0.f;
 #pragma unroll
@@ -52,12 +130,11 @@ __global__ __launch_bounds__(kTailThreads) void l1_partial_kernel(int64_t n, con
     __shared__ double s_w[kTailThreads / 64];
     if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = s;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        double t = 0.0;
+    double t = 0.0;
 #pragma unroll
-        for (int w = 0; w < kTailThreads / 64; w++) t += s_w[w];
-        part[blockIdx.x] = t;
-    }
+    for (int w = 0; w < kTailThreads / 64; w++) t += s_w[w];
+    double total;
+    if (publish_and_total(t, ts, (int)gridDim.x, &total) && threadIdx.x == 0) *loss = (float)(total / (double)n);
 }
 
 // The same pass over 16-byte words (n % 4 == 0, 16-byte aligned x / y and 4-byte aligned sign): each
@@ -68,8 +145,8 @@ __global__ __launch_bounds__(kTailThreads) void l1_partial_kernel(int64_t n, con
 template <bool GRAD>
 __global__ __launch_bounds__(kTailThreads) void l1_partial_v4_kernel(int64_t n4, const float4 *__restrict__ x,
                                                                      const float4 *__restrict__ y,
-                                                                     char4 *__restrict__ sign,
-                                                                     double *__restrict__ part, float4 *__restrict__ grad,
+                                                                     char4 *__restrict__ sign, TicketScratch ts,
+                                                                     float *__restrict__ loss, float4 *__restrict__ grad,
                                                                      float scale) {
     const int64_t base = (int64_t)blockIdx.x * (kL1Chunk / 4);
     float acc = 0.f;
@@ -97,29 +174,11 @@ __global__ __launch_bounds__(kTailThreads) void l1_partial_v4_kernel(int64_t n4,
     __shared__ double s_w[kTailThreads / 64];
     if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = s;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        double t = 0.0;
+    double t = 0.0;
 #pragma unroll
-        for (int w = 0; w < kTailThreads / 64; w++) t += s_w[w];
-        part[blockIdx.x] = t;
-    }
-}
-
-__global__ __launch_bounds__(kTailThreads) void l1_final_kernel(int nblk, int64_t n, const double *__restrict__ part,
-                                                                float *__restrict__ loss) {
-    double s = 0.0;
-    for (int i = threadIdx.x; i < nblk; i += kTailThreads) s += part[i];
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
-    __shared__ double s_w[kTailThreads / 64];
-    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double t = 0.0;
-#pragma unroll
-        for (int w = 0; w < kTailThreads / 64; w++) t += s_w[w];
-        *loss = (float)(t / (double)n);
-    }
+    for (int w = 0; w < kTailThreads / 64; w++) t += s_w[w];
+    double total;
+    if (publish_and_total(t, ts, (int)gridDim.x, &total) && threadIdx.x == 0) *loss = (float)(total / (double)(4 * n4));
 }
 
 __global__ __launch_bounds__(kTailThreads) void l1_backward_kernel(int64_t n, const int8_t *__restrict__ sign,
@@ -367,20 +426,32 @@ __device__ __forceinline__ float second_diff(const float *__restrict__ col, int 
     return (t2 - t1) - (t1 - t0);
 }
 
-__global__ __launch_bounds__(kTailThreads) void reg_forward_kernel(gs4d_reg_batch b, double *__restrict__ part) {
+__global__ __launch_bounds__(kTailThreads) void reg_forward_kernel(gs4d_reg_batch b, TicketScratch ts, float *__restrict__ loss) {
     const int64_t blk = blockIdx.x;
     const gs4d_reg_plane d = b.p[reg_plane_of(b, blk)];
     const int64_t n = (int64_t)d.C * d.H * d.W, hw = (int64_t)d.H * d.W;
     const double cs = (double)d.w_smooth / ((double)d.C * (d.H - 2) * d.W), cl = (double)d.w_l1 / (double)n;
     double acc = 0.0;
+    // rows y .. y + 2 of every element first (indices clamped into the plane: all loads in flight at once, none
+    // behind the loop's exit), then the terms in element order
+    float r[kRegPerThread][3];
+    const int64_t i0 = (blk - d.first_block) * kRegBlock + threadIdx.x;
 #pragma unroll
     for (int k = 0; k < kRegPerThread; k++) {
-        const int64_t i = (blk - d.first_block) * kRegBlock + (int64_t)k * kTailThreads + threadIdx.x;
-        if (i >= n) break;
-        const float t = d.data[i];
+        const int64_t i = std::min<int64_t>(i0 + (int64_t)k * kTailThreads, n - 1);
         const int y = (int)(((uint32_t)i % (uint32_t)hw) / (uint32_t)d.W);  // 32-bit: a plane < 2^31 elements
+        const float *col = d.data + (i - (int64_t)y * d.W);
+#pragma unroll
+        for (int q = 0; q < 3; q++) r[k][q] = col[(size_t)std::min(y + q, d.H - 1) * d.W];
+    }
+#pragma unroll
+    for (int k = 0; k < kRegPerThread; k++) {
+        const int64_t i = i0 + (int64_t)k * kTailThreads;
+        if (i >= n) break;
+        const float t = r[k][0];
+        const int y = (int)(((uint32_t)i % (uint32_t)hw) / (uint32_t)d.W);
         if (y <= d.H - 3) {
-            const float s2 = second_diff(d.data + (i - (int64_t)y * d.W), y, d.W);
+            const float s2 = (r[k][2] - r[k][1]) - (r[k][1] - r[k][0]);  // second_diff at row y
             acc += cs * (double)(s2 * s2);
         }
         acc += cl * (double)fabsf(1.f - t);
@@ -390,29 +461,22 @@ __global__ __launch_bounds__(kTailThreads) void reg_forward_kernel(gs4d_reg_batc
     __shared__ double s_w[kTailThreads / 64];
     if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = acc;
     __syncthreads();
-    if (threadIdx.x == 0) part[blk] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
-}
-
-__global__ __launch_bounds__(kTailThreads) void reg_final_kernel(int nblk, const double *__restrict__ part,
-                                                                 float *__restrict__ loss) {
-    double s = 0.0;
-    for (int i = threadIdx.x; i < nblk; i += kTailThreads) s += part[i];
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
-    __shared__ double s_w[kTailThreads / 64];
-    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) *loss = (float)(s_w[0] + s_w[1] + s_w[2] + s_w[3]);
+    double total;
+    if (publish_and_total(s_w[0] + s_w[1] + s_w[2] + s_w[3], ts, (int)gridDim.x, &total) && threadIdx.x == 0)
+        *loss = (float)total;
 }
 
 // d/dt of the batch loss, as autograd derives it from the reference's graph: mean -> g / N, square
 // -> 2 s g, second[y] = first[y+1] - first[y] -> dfirst[j] = ds[j-1] - ds[j], first[j] = t[j+1] - t[j]
 // -> dt[y] = dfirst[y-1] - dfirst[y] (out-of-range terms are 0); abs(1 - t) -> -sign(1 - t) g / N.
-// part (nullable): also the value's per-workgroup partials, exactly as reg_forward_kernel forms them (same
-// workgroups, same per-thread order and terms: its second difference at row y is the ds[2] term below), for
-// reg_final_kernel -- the value and the gradient from one read of the planes.
+// loss (nullable): also the value, its per-workgroup partials exactly as reg_forward_kernel forms them (same
+// workgroups, same per-thread order and terms: its second difference at row y is the ds[2] term below) and
+// totalled by the last workgroup -- the value and the gradient from one read of the planes.  base (nullable):
+// *loss = *base + value instead, the fp32 add of a loss term the value joins.
 __global__ __launch_bounds__(kTailThreads) void reg_backward_kernel(gs4d_reg_batch b, const float *__restrict__ dloss,
-                                                                    double *__restrict__ part) {
+                                                                    TicketScratch ts, float *__restrict__ loss,
+                                                                    const float *__restrict__ base) {
+    const bool part = loss != nullptr;
     const int64_t blk = blockIdx.x;
     const gs4d_reg_plane d = b.p[reg_plane_of(b, blk)];
     const int64_t n = (int64_t)d.C * d.H * d.W, hw = (int64_t)d.H * d.W;
@@ -421,28 +485,40 @@ __global__ __launch_bounds__(kTailThreads) void reg_backward_kernel(gs4d_reg_bat
     const float gl = (g * d.w_l1) / (float)n;
     const double cs = (double)d.w_smooth / ((double)d.C * (d.H - 2) * d.W), cl = (double)d.w_l1 / (double)n;
     double acc = 0.0;
+    // rows y - 2 .. y + 2 of every element (and its gradient, when accumulating) first, indices clamped into the
+    // plane: all loads in flight at once, none behind the loop's exit; out-of-range rows only feed masked terms
+    float r[kRegPerThread][5], gv[kRegPerThread];
+    const int64_t i0 = (blk - d.first_block) * kRegBlock + threadIdx.x;
 #pragma unroll
     for (int k = 0; k < kRegPerThread; k++) {
-        const int64_t i = (blk - d.first_block) * kRegBlock + (int64_t)k * kTailThreads + threadIdx.x;
-        if (i >= n) break;
+        const int64_t i = std::min<int64_t>(i0 + (int64_t)k * kTailThreads, n - 1);
         const int y = (int)(((uint32_t)i % (uint32_t)hw) / (uint32_t)d.W);  // 32-bit: a plane < 2^31 elements
         const float *col = d.data + (i - (int64_t)y * d.W);
+#pragma unroll
+        for (int q = 0; q < 5; q++) r[k][q] = col[(size_t)std::min(std::max(y - 2 + q, 0), d.H - 1) * d.W];
+        gv[k] = b.accumulate ? d.grad[i] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < kRegPerThread; k++) {
+        const int64_t i = i0 + (int64_t)k * kTailThreads;
+        if (i >= n) break;
+        const int y = (int)(((uint32_t)i % (uint32_t)hw) / (uint32_t)d.W);
         float ds[3], s2y = 0.f;  // ds[y-2], ds[y-1], ds[y]; s2y: the second difference at row y itself
 #pragma unroll
         for (int q = 0; q < 3; q++) {
             const int yy = y - 2 + q;
-            const float s2 = (yy >= 0 && yy <= d.H - 3) ? second_diff(col, yy, d.W) : 0.f;
-            ds[q] = (yy >= 0 && yy <= d.H - 3) ? 2.f * s2 * gs : 0.f;
+            const bool in = yy >= 0 && yy <= d.H - 3;
+            const float s2 = in ? (r[k][q + 2] - r[k][q + 1]) - (r[k][q + 1] - r[k][q]) : 0.f;  // second_diff at yy
+            ds[q] = in ? 2.f * s2 * gs : 0.f;
             if (q == 2) s2y = s2;
         }
         const float df_prev = (y >= 1) ? ds[0] - ds[1] : 0.f;      // dfirst[y-1] = ds[y-2] - ds[y-1]
         const float df_cur = (y <= d.H - 2) ? ds[1] - ds[2] : 0.f;  // dfirst[y] = ds[y-1] - ds[y]
-        const float t = d.data[i];
+        const float t = r[k][2];
         const float one_m = 1.f - t;
         const float sg = (float)((one_m > 0.f) - (one_m < 0.f));
         const float v = (df_prev - df_cur) + (-sg) * gl;
-        if (b.accumulate) d.grad[i] += v;
-        else d.grad[i] = v;
+        d.grad[i] = b.accumulate ? gv[k] + v : v;
         if (part) {  // reg_forward_kernel's terms, in its order
             if (y <= d.H - 3) acc += cs * (double)(s2y * s2y);
             acc += cl * (double)fabsf(1.f - t);
@@ -454,7 +530,9 @@ __global__ __launch_bounds__(kTailThreads) void reg_backward_kernel(gs4d_reg_bat
         __shared__ double s_w[kTailThreads / 64];
         if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = acc;
         __syncthreads();
-        if (threadIdx.x == 0) part[blk] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+        double total;
+        if (publish_and_total(s_w[0] + s_w[1] + s_w[2] + s_w[3], ts, (int)gridDim.x, &total) && threadIdx.x == 0)
+            *loss = base ? *base + (float)total : (float)total;
     }
 }
 
@@ -1121,11 +1199,26 @@ struct HbOut {
 // 16 outputs per workgroup (16 interleaved sixteenths of the workgroups each, combined in a fixed order): the
 // ~2k outputs of a launch then fill ~120 CUs instead of ~60
 constexpr int kHbRedOut = 16, kHbRedSlices = 256 / kHbRedOut;
-__global__ __launch_bounds__(256) void heads_bwd_reduce_kernel(HbArgs A, HbOut O, int nwg, const float *__restrict__ part) {
+// One launch reduces the partials of up to kHbRedGroups launch groups (the narrow heads' and the wide head's):
+// group g owns workgroups [blk0[g], blk0[g + 1]).
+constexpr int kHbRedGroups = 2;
+struct HbRed {
+    HbArgs A[kHbRedGroups];
+    const float *part[kHbRedGroups];
+    int nwg[kHbRedGroups];
+    int blk0[kHbRedGroups + 1];
+    int count;
+};
+__global__ __launch_bounds__(256) void heads_bwd_reduce_kernel(HbRed R, HbOut O) {
     __shared__ float s_sum[kHbRedSlices][kHbRedOut];
+    int gi = 0;
+    while (gi + 1 < R.count && (int)blockIdx.x >= R.blk0[gi + 1]) gi++;
+    const HbArgs &A = R.A[gi];
+    const float *__restrict__ part = R.part[gi];
+    const int nwg = R.nwg[gi];
     const int per = A.poff[A.hk];
     const int o = threadIdx.x % kHbRedOut, q = threadIdx.x / kHbRedOut;
-    const int i = blockIdx.x * kHbRedOut + o;
+    const int i = ((int)blockIdx.x - R.blk0[gi]) * kHbRedOut + o;
     float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
     if (i < per) {
         int w = q;
@@ -2110,15 +2203,23 @@ __global__ __launch_bounds__(256) void hex_points_kernel(int N, const float *__r
     pts[n] = make_float4((x[0] - aabb[0]) * sc.x - 1.0f, (x[1] - aabb[1]) * sc.y - 1.0f, (x[2] - aabb[2]) * sc.z - 1.0f,
                          t[(size_t)n * ld_t]);
 }
+// add (nullable): another gradient of xyz, summed in (the add autograd would launch for xyz's two uses)
 __global__ __launch_bounds__(256) void hex_points_bwd_kernel(int N, const float4 *__restrict__ dpts,
-                                                             const float *__restrict__ aabb, float *__restrict__ dxyz) {
+                                                             const float *__restrict__ aabb,
+                                                             const float *__restrict__ add, float *__restrict__ dxyz) {
     const int n = blockIdx.x * 256 + threadIdx.x;
     if (n >= N) return;
     const float3 sc = hex_scale(aabb);
     const float4 d = dpts[n];
-    dxyz[3 * (size_t)n] = d.x * sc.x;
-    dxyz[3 * (size_t)n + 1] = d.y * sc.y;
-    dxyz[3 * (size_t)n + 2] = d.z * sc.z;
+    float g0 = d.x * sc.x, g1 = d.y * sc.y, g2 = d.z * sc.z;
+    if (add) {
+        g0 = add[3 * (size_t)n] + g0;
+        g1 = add[3 * (size_t)n + 1] + g1;
+        g2 = add[3 * (size_t)n + 2] + g2;
+    }
+    dxyz[3 * (size_t)n] = g0;
+    dxyz[3 * (size_t)n + 1] = g1;
+    dxyz[3 * (size_t)n + 2] = g2;
 }
 
 }  // namespace gs4d
@@ -2230,6 +2331,12 @@ static int heads_backward_t(const Args *args, void *scratch, void *stream) {
     hipStream_t s = (hipStream_t)stream;
     char *q = (char *)align_up((size_t)scratch, 256);
     int err = 0;
+    HbRed R{};
+    auto flush = [&]() {  // the pending groups' reduction, one launch
+        if (!R.count) return;
+        hipLaunchKernelGGL(heads_bwd_reduce_kernel, dim3(R.blk0[R.count]), dim3(256), 0, s, R, O);
+        R = HbRed{};
+    };
     hb_groups(b.k, b.n, [&](int h0, int hk) {
         A.h0 = h0, A.hk = hk;
         A.rows_per_wg = hb_rows_per_wg(b.P, hb_wide(b.n[h0]), std::is_same<TA, __bf16>::value);
@@ -2265,9 +2372,12 @@ static int heads_backward_t(const Args *args, void *scratch, void *stream) {
                 hipLaunchKernelGGL(heads_bwd_kernel<TA>, dim3(nwg), dim3(hk * b.W), 0, s, A, ba, bda, g[0], g[1], g[2],
                                    g[3], g[4], g[5], g[6], g[7], part);
         }
-        hipLaunchKernelGGL(heads_bwd_reduce_kernel, dim3((A.poff[hk] + kHbRedOut - 1) / kHbRedOut), dim3(256), 0, s, A, O, nwg,
-                           (const float *)part);
+        if (R.count == kHbRedGroups) flush();
+        R.A[R.count] = A, R.part[R.count] = part, R.nwg[R.count] = nwg;
+        R.blk0[R.count + 1] = R.blk0[R.count] + (A.poff[hk] + kHbRedOut - 1) / kHbRedOut;
+        R.count++;
     });
+    flush();
     if (err) return err;
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
@@ -2341,16 +2451,14 @@ static int reg_check(const gs4d_reg_batch *b, int64_t *nblk) {
 size_t gs4d_reg_scratch_bytes(const gs4d_reg_batch *batch) {
     int64_t nblk = 0;
     if (reg_check(batch, &nblk)) return 0;
-    return 8 * (size_t)nblk + 256;
+    return 8 * (size_t)nblk + 4 * kTicketWords + 256;
 }
 
 int gs4d_hexplane_reg_forward(const gs4d_reg_batch *batch, float *loss, void *scratch, void *stream) {
     int64_t nblk = 0;
     if (reg_check(batch, &nblk) || !loss || !scratch) return 1;
-    double *part = (double *)align_up((size_t)scratch, 8);
-    hipStream_t s = (hipStream_t)stream;
-    hipLaunchKernelGGL(reg_forward_kernel, dim3((unsigned)nblk), dim3(kTailThreads), 0, s, *batch, part);
-    hipLaunchKernelGGL(reg_final_kernel, dim3(1), dim3(kTailThreads), 0, s, (int)nblk, part, loss);
+    hipLaunchKernelGGL(reg_forward_kernel, dim3((unsigned)nblk), dim3(kTailThreads), 0, (hipStream_t)stream, *batch,
+                       ticket_scratch(scratch), loss);
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
@@ -2360,39 +2468,38 @@ int gs4d_hexplane_reg_backward(const gs4d_reg_batch *batch, const float *dloss, 
     for (int i = 0; i < batch->count; i++)
         if (!batch->p[i].grad) return 1;
     hipLaunchKernelGGL(reg_backward_kernel, dim3((unsigned)nblk), dim3(kTailThreads), 0, (hipStream_t)stream, *batch,
-                       dloss, nullptr);
+                       dloss, TicketScratch{nullptr, nullptr}, (float *)nullptr, (const float *)nullptr);
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
-int gs4d_hexplane_reg_backward_value(const gs4d_reg_batch *batch, const float *dloss, float *loss, void *scratch,
-                                     void *stream) {
+int gs4d_hexplane_reg_backward_value(const gs4d_reg_batch *batch, const float *dloss, float *loss, const float *base,
+                                     void *scratch, void *stream) {
     int64_t nblk = 0;
     if (reg_check(batch, &nblk) || !dloss || !loss || !scratch) return 1;
     for (int i = 0; i < batch->count; i++)
         if (!batch->p[i].grad) return 1;
-    double *part = (double *)align_up((size_t)scratch, 8);
-    hipStream_t s = (hipStream_t)stream;
-    hipLaunchKernelGGL(reg_backward_kernel, dim3((unsigned)nblk), dim3(kTailThreads), 0, s, *batch, dloss, part);
-    hipLaunchKernelGGL(reg_final_kernel, dim3(1), dim3(kTailThreads), 0, s, (int)nblk, part, loss);
+    hipLaunchKernelGGL(reg_backward_kernel, dim3((unsigned)nblk), dim3(kTailThreads), 0, (hipStream_t)stream, *batch,
+                       dloss, ticket_scratch(scratch), loss, base);
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
 
-size_t gs4d_l1_scratch_bytes(int64_t n) { return 8 * (size_t)((n + kL1Chunk - 1) / kL1Chunk) + 256; }
+size_t gs4d_l1_scratch_bytes(int64_t n) { return 8 * (size_t)((n + kL1Chunk - 1) / kL1Chunk) + 4 * kTicketWords + 256; }
 
 int gs4d_l1_loss_forward(int64_t n, const float *x, const float *y, int8_t *sign, float *loss, void *scratch,
                          void *stream) {
     if (n < 0 || (n > 0 && (!x || !y || !sign || !scratch)) || !loss) return 1;
     hipStream_t s = (hipStream_t)stream;
     if (n == 0) return hipMemsetAsync(loss, 0, 4, s) == hipSuccess ? 0 : 3;
-    const int nblk = (int)((n + kL1Chunk - 1) / kL1Chunk);
-    double *part = (double *)align_up((size_t)scratch, 8);
+    const int64_t nblk = (n + kL1Chunk - 1) / kL1Chunk;
+    if (nblk > INT32_MAX) return 1;
     if (n % 4 == 0 && (((size_t)x | (size_t)y) & 15) == 0 && ((size_t)sign & 3) == 0)
-        hipLaunchKernelGGL(l1_partial_v4_kernel<false>, dim3(nblk), dim3(kTailThreads), 0, s, n / 4, (const float4 *)x,
-                           (const float4 *)y, (char4 *)sign, part, (float4 *)nullptr, 0.f);
+        hipLaunchKernelGGL(l1_partial_v4_kernel<false>, dim3((unsigned)nblk), dim3(kTailThreads), 0, s, n / 4,
+                           (const float4 *)x, (const float4 *)y, (char4 *)sign, ticket_scratch(scratch), loss,
+                           (float4 *)nullptr, 0.f);
     else
-        hipLaunchKernelGGL(l1_partial_kernel, dim3(nblk), dim3(kTailThreads), 0, s, n, x, y, sign, part);
-    hipLaunchKernelGGL(l1_final_kernel, dim3(1), dim3(kTailThreads), 0, s, nblk, n, part, loss);
+        hipLaunchKernelGGL(l1_partial_kernel, dim3((unsigned)nblk), dim3(kTailThreads), 0, s, n, x, y, sign,
+                           ticket_scratch(scratch), loss);
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
@@ -2402,12 +2509,12 @@ int gs4d_l1_loss_grad(int64_t n, const float *x, const float *y, float dloss, fl
     hipStream_t s = (hipStream_t)stream;
     if (n == 0) return hipMemsetAsync(loss, 0, 4, s) == hipSuccess ? 0 : 3;
     if (n % 4 != 0 || (((size_t)x | (size_t)y | (size_t)grad) & 15) != 0) return 1;  // the float4 form only
-    const int nblk = (int)((n + kL1Chunk - 1) / kL1Chunk);
-    double *part = (double *)align_up((size_t)scratch, 8);
+    const int64_t nblk = (n + kL1Chunk - 1) / kL1Chunk;
+    if (nblk > INT32_MAX) return 1;
     const float scale = dloss * (1.0f / (float)n);  // torch's MeanBackward rounding, as l1_backward
-    hipLaunchKernelGGL(l1_partial_v4_kernel<true>, dim3(nblk), dim3(kTailThreads), 0, s, n / 4, (const float4 *)x,
-                       (const float4 *)y, (char4 *)nullptr, part, (float4 *)grad, scale);
-    hipLaunchKernelGGL(l1_final_kernel, dim3(1), dim3(kTailThreads), 0, s, nblk, n, part, loss);
+    hipLaunchKernelGGL(l1_partial_v4_kernel<true>, dim3((unsigned)nblk), dim3(kTailThreads), 0, s, n / 4,
+                       (const float4 *)x, (const float4 *)y, (char4 *)nullptr, ticket_scratch(scratch), loss,
+                       (float4 *)grad, scale);
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
@@ -2762,13 +2869,18 @@ int gs4d_hexplane_points(int N, const float *xyz, int64_t ld_xyz, const float *t
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
-int gs4d_hexplane_points_backward(int N, const float *dpts, const float *aabb, float *dxyz, void *stream) {
+int gs4d_hexplane_points_backward_add(int N, const float *dpts, const float *aabb, const float *add, float *dxyz,
+                                      void *stream) {
     if (N < 0 || !aabb) return 1;
     if (N == 0) return 0;
     if (!dpts || !dxyz || ((size_t)dpts & 15) != 0) return 1;
     hipLaunchKernelGGL(hex_points_bwd_kernel, dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream, N,
-                       (const float4 *)dpts, aabb, dxyz);
+                       (const float4 *)dpts, aabb, add, dxyz);
     return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+int gs4d_hexplane_points_backward(int N, const float *dpts, const float *aabb, float *dxyz, void *stream) {
+    return gs4d_hexplane_points_backward_add(N, dpts, aabb, nullptr, dxyz, stream);
 }
 
 }  // extern "C"

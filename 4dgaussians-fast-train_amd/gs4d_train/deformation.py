@@ -83,14 +83,16 @@ class HexPlaneField(nn.Module):
         self.aabb = nn.Parameter(torch.tensor([xyz_max, xyz_min], dtype=torch.float32, device=self.aabb.device),
                                  requires_grad=False)
 
-    def forward(self, pts, timestamps=None):
-        """get_density (scene/hexplane.py:160-177): normalised (x, y, z, t) -> per-level plane products."""
+    def forward(self, pts, timestamps=None, alias=None):
+        """get_density (scene/hexplane.py:160-177): normalised (x, y, z, t) -> per-level plane products.
+        alias (a list, fused path only): receives a pass-through view of pts for their other use, whose
+        gradient the points' backward then sums in (kernels.hexplane_points)."""
         # the fused field differentiates w.r.t. the points only: timestamps that need a gradient take
         # the grid_sample graph
         if (self.fused and pts.is_cuda and pts.dim() == 2 and timestamps is not None and timestamps.dim() == 2
                 and not timestamps.requires_grad):
             from .kernels import hexplane, hexplane_points
-            return hexplane(hexplane_points(pts, timestamps, self.aabb), [list(g) for g in self.grids])
+            return hexplane(hexplane_points(pts, timestamps, self.aabb, alias), [list(g) for g in self.grids])
         pts = normalize_aabb(pts, self.aabb)
         pts = torch.cat((pts, timestamps), dim=-1).reshape(-1, 4)
         if self.fused:
@@ -523,10 +525,13 @@ class _FeatureReLUHB(_FeatureReLU):
         h, hb = _C.feature_relu_forward(x, w.contiguous(), b.contiguous(), with_hb=True)
         ctx.save_for_backward(x, w, h)
         ctx.mark_non_differentiable(hb)
+        ctx.set_materialize_grads(False)  # no zero-filled (P, W) bf16 gradient for hb in the backward
         return h, hb
 
     @staticmethod
     def backward(ctx, g, ghb):
+        if g is None:
+            return None, None, None
         return _FeatureReLU.backward(ctx, g)
 
 
@@ -551,9 +556,10 @@ class Deformation(nn.Module):
         # "fp32" (default) is the reference's precision.
         self.mlp_dtype = getattr(args, "mlp_dtype", "fp32")
 
-    def deltas(self, xyz, time):
+    def deltas(self, xyz, time, alias=None):
         """The active heads' outputs {name: (P, n)} of forward_dynamic (scene/deformation.py:97-139),
-        before the residual adds (which gs4d_train.kernels.deform_tail fuses with the activations)."""
+        before the residual adds (which gs4d_train.kernels.deform_tail fuses with the activations).
+        alias (a list): may receive a pass-through view of xyz to use in those adds (HexPlaneField.forward)."""
         a = self.args
         if a.apply_rotation and not a.no_dr:
             raise NotImplementedError("apply_rotation (documented as unused in arguments/__init__.py:104)")
@@ -562,7 +568,7 @@ class Deformation(nn.Module):
         active = [name for name, flag in (("pos_deform", a.no_dx), ("scales_deform", a.no_ds),
                                           ("rotations_deform", a.no_dr), ("opacity_deform", a.no_do),
                                           ("shs_deform", a.no_dshs)) if not flag]
-        return self._heads(self.grid(xyz, time), active)
+        return self._heads(self.grid(xyz, time, alias) if alias is not None else self.grid(xyz, time), active)
 
     def _heads_bf16(self, feat, active):
         """The bf16 form of _heads: feature_out and its ReLU as on the fp32 path (a K = feat_dim layer,
@@ -677,8 +683,8 @@ class DeformNetwork(nn.Module):
     def forward(self, point, scales=None, rotations=None, opacity=None, shs=None, times_sel=None):
         return self.deformation_net(point, scales, rotations, opacity, shs, times_sel)
 
-    def deltas(self, point, times_sel):
-        return self.deformation_net.deltas(point, times_sel)
+    def deltas(self, point, times_sel, alias=None):
+        return self.deformation_net.deltas(point, times_sel, alias)
 
     def get_mlp_parameters(self):
         return self.deformation_net.get_mlp_parameters() + list(self.timenet.parameters())

@@ -380,14 +380,15 @@ class GaussianModel:
                                          plane_tv_weight)
 
     def add_regulation_grad(self, time_smoothness_weight, l1_time_planes_weight, plane_tv_weight, scale=1.0,
-                            with_value=False):
+                            with_value=False, base=None):
         """scale * d(compute_regulation)/d(plane) added to the planes' .grad in one launch: the gradient
         the loss's regulariser term contributes, applied after the rest of the backward.  with_value: returns
-        compute_regulation's value too, from the same pass (regulation_value's number, bitwise)."""
+        compute_regulation's value too, from the same pass (regulation_value's number, bitwise); with base (a
+        one-value device tensor), base + that value, added by the same launch."""
         from .kernels import hexplane_regulation_accumulate_grad
         grids = self._deformation.deformation_net.grid.grids
         return hexplane_regulation_accumulate_grad([list(g) for g in grids], time_smoothness_weight,
-                                                   l1_time_planes_weight, plane_tv_weight, scale, with_value)
+                                                   l1_time_planes_weight, plane_tv_weight, scale, with_value, base)
 
     # ---- on-disk formats (gaussian_model.py:214-314 and scene/__init__.py:143-150)
     def save_ply(self, path):

@@ -100,6 +100,15 @@ class FusedAdam(torch.optim.Optimizer):
     def step(self, closure=None):
         return self._step(closure)
 
+    def zero_grad(self, set_to_none: bool = True):
+        """torch's zero_grad.  set_to_none (the train step's call) while no profiler runs: the same loop without
+        torch's profiler range around it (host time every step, with the GPU idle behind it at a step's start)."""
+        if not set_to_none or torch.autograd.profiler._is_profiler_enabled:
+            return super().zero_grad(set_to_none)
+        for group in self.param_groups:
+            for p in group["params"]:
+                p.grad = None
+
     @torch.no_grad()
     def _step(self, closure=None):
         loss = None
@@ -267,6 +276,26 @@ class _HexPoints(torch.autograd.Function):
         return _C.hexplane_points_backward(dpts, aabb), None, None
 
 
+class _HexPointsAlias(torch.autograd.Function):
+    """_HexPoints that also passes xyz through (a view of it) for xyz's other use, the deformation tail's
+    xyz + dx: the backward then forms xyz's whole gradient -- the tail's plus the field's -- in its one pass
+    (gs4d_hexplane_points_backward_add), where autograd would sum the two with a separate add launch.  Same
+    sum (one fp32 add per element, which is commutative), one launch fewer."""
+
+    @staticmethod
+    def forward(ctx, xyz, t, aabb):
+        ctx.save_for_backward(aabb)
+        ctx.set_materialize_grads(False)  # a use without a gradient arrives as None, not as a zero fill
+        return _C.hexplane_points(xyz, t, aabb), xyz.view_as(xyz)
+
+    @staticmethod
+    def backward(ctx, dpts, dxyz):
+        (aabb,) = ctx.saved_tensors
+        if dpts is None:
+            return dxyz, None, None
+        return _C.hexplane_points_backward(dpts, aabb, add=dxyz), None, None
+
+
 def set_deterministic(flag=True):
     """Kept for callers of the round-4 API: every kernel of the fused train step is now deterministic (the
     HexPlane field's backward sums exact 64-bit fixed-point terms; the rasterizer reduces in fixed order),
@@ -274,8 +303,13 @@ def set_deterministic(flag=True):
     del flag
 
 
-def hexplane_points(xyz, t, aabb):
-    """(N, 4) = (normalize_aabb(xyz, aabb), t) for the field (gradient to xyz only)."""
+def hexplane_points(xyz, t, aabb, alias=None):
+    """(N, 4) = (normalize_aabb(xyz, aabb), t) for the field (gradient to xyz only).  alias (a list): also
+    append a pass-through view of xyz for its other differentiable use (_HexPointsAlias)."""
+    if alias is not None and torch.is_grad_enabled() and xyz.requires_grad:
+        pts, xa = _HexPointsAlias.apply(xyz, t.detach(), aabb.detach())
+        alias.append(xa)
+        return pts
     return _HexPoints.apply(xyz, t.detach(), aabb.detach())
 
 
@@ -326,15 +360,19 @@ def hexplane_regulation_value(ms_grids, time_smoothness_weight, l1_time_planes_w
 
 @torch.no_grad()
 def hexplane_regulation_accumulate_grad(ms_grids, time_smoothness_weight, l1_time_planes_weight, plane_tv_weight,
-                                        scale=1.0, with_value=False):
+                                        scale=1.0, with_value=False, base=None):
     """Adds scale * d(regulariser)/d(plane) to every plane's .grad in one launch: the gradient autograd
     would add to the field's plane gradients when the regulariser is part of the loss (train.py:251-254),
     without autograd's separate add per plane.  A plane without a gradient yet gets one.  with_value: also
     returns the regulariser's (unscaled) value from the same pass over the planes, bitwise
-    hexplane_regulation_value's."""
+    hexplane_regulation_value's.  base (a one-value fp32 device tensor, with_value only): returns base + value
+    instead, the add done by the same launch (bitwise torch's fp32 add of the two)."""
     planes, ws, wl = _reg_batch(ms_grids, time_smoothness_weight, l1_time_planes_weight, plane_tv_weight)
     if not planes:
-        return torch.zeros((), device=ms_grids[0][0].device) if with_value else None
+        if not with_value:
+            return None
+        z = torch.zeros((), device=ms_grids[0][0].device)
+        return z if base is None else base.reshape(()) + z
     for p in planes:
         if p.grad is None:
             p.grad = torch.zeros_like(p)
@@ -343,8 +381,14 @@ def hexplane_regulation_accumulate_grad(ms_grids, time_smoothness_weight, l1_tim
     dloss = _DLOSS.get(key)
     if dloss is None:
         dloss = _DLOSS[key] = torch.full((1,), float(scale), device=planes[0].device)
+    if base is not None and not (base.is_cuda and base.dtype == torch.float32 and base.numel() == 1
+                                 and base.device == planes[0].device):
+        v = hexplane_regulation_accumulate_grad(ms_grids, time_smoothness_weight, l1_time_planes_weight,
+                                                plane_tv_weight, scale, with_value)
+        return base.detach().reshape(()) + v if with_value else v
     v = _C.hexplane_reg_accumulate([p.detach() for p in planes], [p.grad for p in planes], ws, wl, dloss,
-                                   with_value=with_value)
+                                   with_value=with_value,
+                                   base=base.detach().contiguous() if (with_value and base is not None) else None)
     return v if with_value else None
 
 

@@ -26,6 +26,21 @@ def _time_value(t, dev):
     return v
 
 
+_ZERO_POINTS = {}
+
+
+def _zero_points(xyz):
+    """the means2D gradient sink: a fresh leaf (requires_grad, its own .grad) over a zero (P, 3) buffer kept per
+    (device, shape, dtype) -- its values are never written, so one fill serves every call (no fill per step)"""
+    key = (xyz.device, tuple(xyz.shape), xyz.dtype)
+    z = _ZERO_POINTS.get(key)
+    if z is None:
+        if len(_ZERO_POINTS) >= 4:
+            _ZERO_POINTS.clear()
+        z = _ZERO_POINTS[key] = torch.zeros_like(xyz, dtype=xyz.dtype, device=xyz.device)
+    return z.detach().requires_grad_(True)
+
+
 class RenderPackage(dict):
     """render()'s dict (gaussian_renderer/__init__.py:130-138) with "visibility_filter" = radii > 0 formed on
     first use: the fused train step filters the densification statistics by radii > 0 inside their kernel,
@@ -79,7 +94,7 @@ def render(viewpoint_camera, pc, pipe_debug, bg_color, scaling_modifier=1.0, sta
     xyz = pc.get_xyz
     # the rasterizer's means2D gradient sink (:24-29 builds zeros + 0 and retains its grad; a zero leaf
     # holds the same values and receives the same .grad)
-    screenspace_points = torch.zeros_like(xyz, dtype=xyz.dtype, requires_grad=True, device=xyz.device)
+    screenspace_points = _zero_points(xyz)
     dev = xyz.device
     if hasattr(viewpoint_camera, "on_device"):
         view_m, proj_m, cam_c = viewpoint_camera.on_device(dev)
@@ -100,8 +115,9 @@ def render(viewpoint_camera, pc, pipe_debug, bg_color, scaling_modifier=1.0, sta
     if getattr(pc, "fused", False) and getattr(pc, "fused_tail", True) and xyz.is_cuda:
         # the heads' residual adds, cat(f_dc, f_rest) and the activations as one HIP pass each way
         from .kernels import deform_tail
-        d = pc._deformation.deltas(xyz, time) if "fine" in stage else {}
-        m3, sc, rot, op, sh = deform_tail(xyz, pc._scaling, pc._rotation, pc._opacity, pc._features_dc,
+        alias = []  # xyz passed through the field's points op, which then sums in the tail's xyz gradient
+        d = pc._deformation.deltas(xyz, time, alias) if "fine" in stage else {}
+        m3, sc, rot, op, sh = deform_tail(alias[0] if alias else xyz, pc._scaling, pc._rotation, pc._opacity, pc._features_dc,
                                           pc._features_rest, d.get("pos_deform"), d.get("scales_deform"),
                                           d.get("rotations_deform"), d.get("opacity_deform"), d.get("shs_deform"))
     else:

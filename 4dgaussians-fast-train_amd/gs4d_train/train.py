@@ -99,10 +99,11 @@ def train_step(gaussians, views, opt, hyper, iteration, background, stage="fine"
     elif loss.requires_grad:
         loss.backward()
     if reg_deferred:
-        reg_value = gaussians.add_regulation_grad(*reg_w, scale=reg_scale, with_value=True)
-        if reg_scale != 1.0:
-            reg_value = reg_value * reg_scale
-        loss = loss.detach() + reg_value
+        if reg_scale == 1.0:
+            # loss.detach() + value, the add inside the regulariser's own launch
+            loss = gaussians.add_regulation_grad(*reg_w, scale=reg_scale, with_value=True, base=loss.detach())
+        else:
+            loss = loss.detach() + gaussians.add_regulation_grad(*reg_w, scale=reg_scale, with_value=True) * reg_scale
     if len(vs_list) == 1 and vs_list[0].grad is not None:
         viewspace_grad = vs_list[0].grad
     else:

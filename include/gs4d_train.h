@@ -17,7 +17,10 @@ extern "C" {
 
 /* ---- L1 loss: utils/loss_utils.py:20-21 l1_loss(x, y) = |x - y|.mean(), and its autograd gradient.
  * forward: *loss = mean |x - y| (fp64 partial sums in a fixed order), sign[i] = sign(x[i] - y[i]);
- * scratch must hold gs4d_l1_scratch_bytes(n) bytes.  backward: grad[i] = sign[i] * (*dloss) / n. */
+ * scratch must hold gs4d_l1_scratch_bytes(n) bytes and be all zero on entry (the completion counters and
+ * partial slots of the workgroup that finishes last: it sums the partials itself, no second launch); a call
+ * leaves it zero again, so a caller zeroes its scratch once and keeps it (one scratch per stream: two calls
+ * in flight at once must not share one).  backward: grad[i] = sign[i] * (*dloss) / n. */
 size_t gs4d_l1_scratch_bytes(int64_t n);
 int gs4d_l1_loss_forward(int64_t n, const float *x, const float *y, int8_t *sign, float *loss, void *scratch,
                          void *stream);
@@ -137,6 +140,10 @@ int gs4d_hexplane_backward(int N, const float *pts, const uint32_t *order, const
 int gs4d_hexplane_points(int N, const float *xyz, int64_t ld_xyz, const float *t, int64_t ld_t, const float *aabb,
                          float *pts, void *stream);
 int gs4d_hexplane_points_backward(int N, const float *dpts, const float *aabb, float *dxyz, void *stream);
+/* The same with add (nullable, (N, 3) contiguous): dxyz = add + the points' gradient -- xyz's other gradient
+ * (the deformation tail's, xyz + dx) summed in by this pass instead of a separate add. */
+int gs4d_hexplane_points_backward_add(int N, const float *dpts, const float *aabb, const float *add, float *dxyz,
+                                      void *stream);
 
 /* ---- HexPlane regularisers: scene/gaussian_model.py:538-577 (compute_regulation = plane_tv_weight *
  * _plane_regulation + time_smoothness_weight * _time_regulation + l1_time_planes * _l1_regulation) with
@@ -144,7 +151,8 @@ int gs4d_hexplane_points_backward(int N, const float *dpts, const float *aabb, f
  *   w_smooth * mean over (C, H-2, W) of ((t[y+2] - t[y+1]) - (t[y+1] - t[y]))^2  +  w_l1 * mean |1 - t|
  * (w_smooth: plane_tv_weight for the spatial planes, time_smoothness_weight for the time planes; w_l1:
  * l1_time_planes for the time planes, 0 otherwise).  H >= 3.  forward: *loss = the sum over the
- * batch (fp64 partials summed in a fixed order; scratch of gs4d_reg_scratch_bytes).  backward: grad
+ * batch (fp64 partials summed in a fixed order; scratch of gs4d_reg_scratch_bytes, all zero on entry and left
+ * zero, as the L1 loss's above).  backward: grad
  * (1, C, H, W) of each plane = dloss * d(loss)/d(t), the gradient autograd derives from the
  * reference's graph: assigned, or with accumulate = 1 added to what grad holds (the plane's .grad after
  * the field's backward: the sum autograd would form, without its extra add per plane).  first_block of
@@ -167,9 +175,10 @@ size_t gs4d_reg_scratch_bytes(const gs4d_reg_batch *batch);
 int gs4d_hexplane_reg_forward(const gs4d_reg_batch *batch, float *loss, void *scratch, void *stream);
 int gs4d_hexplane_reg_backward(const gs4d_reg_batch *batch, const float *dloss, void *stream);
 /* The backward and the value in one pass over the planes: the gradient as gs4d_hexplane_reg_backward, and *loss
- * bitwise as gs4d_hexplane_reg_forward would give it (same partials, same order); scratch as for the forward. */
-int gs4d_hexplane_reg_backward_value(const gs4d_reg_batch *batch, const float *dloss, float *loss, void *scratch,
-                                     void *stream);
+ * bitwise as gs4d_hexplane_reg_forward would give it (same partials, same order); scratch as for the forward.
+ * base (nullable): *loss = *base + value instead (one fp32 add: the loss term the value joins). */
+int gs4d_hexplane_reg_backward_value(const gs4d_reg_batch *batch, const float *dloss, float *loss, const float *base,
+                                     void *scratch, void *stream);
 
 /* ---- Linear-layer weight gradients over many rows: for each problem, dw (n, W) = dy^T x and db (n)
  * = column sums of dy (db may be NULL) -- the backward of F.linear as autograd forms it -- for dy (P, n)

@@ -328,6 +328,15 @@ def test_hexplane_regulation_fused_matches_torch():
     assert torch.equal(v, hexplane_regulation_value(ga, *w))
     for a, b in zip([p for l in ga for p in l], [p for l in gb for p in l]):
         assert torch.equal(a.grad, b.grad)
+    # with a base (the train step's L1 value): base + value from the same launch, bitwise torch's fp32 add; the
+    # last-workgroup total re-arms its ticket, so repeated calls agree
+    base = torch.full((), 0.0123456789, device="cuda")
+    for _ in range(3):
+        gc = [[p.detach().clone().requires_grad_(True) for p in l] for l in grids_f]
+        vb = hexplane_regulation_accumulate_grad(gc, *w, scale=2.5, with_value=True, base=base)
+        assert torch.equal(vb, base + v)
+        for a, b in zip([p for l in gc for p in l], [p for l in gb for p in l]):
+            assert torch.equal(a.grad, b.grad)
 
 
 @pytest.mark.parametrize("P,W,ns", [(100_003, 128, [3, 3, 4, 1]), (777, 64, [2, 5, 8]), (3000, 256, [16, 7]),
@@ -905,3 +914,44 @@ def test_heads_block_forward_lds_fallback(monkeypatch):
         assert float((a - b).abs().max()) <= 1e-4 * max(float(b.abs().max()), 1.0)
     for a, b in zip(grad, ref_grad):
         assert float((a - b).abs().max()) <= 1e-4 * max(float(b.abs().max()), 1e-20)
+
+
+def test_zero_points_sink_is_a_fresh_leaf():
+    """render()'s means2D gradient sink (gaussian_renderer/__init__.py:24-29): one kept zero buffer, but every
+    call a new leaf with its own .grad, so one step's viewspace gradient never leaks into another's."""
+    from gs4d_train.render import _zero_points
+    xyz = torch.rand(10, 3, device="cuda")
+    a, b = _zero_points(xyz), _zero_points(xyz)
+    assert a is not b and a.is_leaf and b.is_leaf and a.requires_grad and b.requires_grad
+    assert not bool(torch.any(a)) and a.shape == xyz.shape and a.dtype == xyz.dtype
+    (a * 2.0).sum().backward()
+    assert b.grad is None and torch.equal(a.grad, torch.full_like(a, 2.0))
+    (b * 3.0).sum().backward()
+    assert torch.equal(a.grad, torch.full_like(a, 2.0)) and torch.equal(b.grad, torch.full_like(b, 3.0))
+    assert not bool(torch.any(_zero_points(xyz)))
+
+
+def test_hexplane_points_alias_sums_xyz_gradient_bitwise():
+    """kernels.hexplane_points with alias: xyz's other use (the deformation tail's xyz + dx) reads the pass-through
+    view, and the points' backward sums that use's gradient into its own pass -- bitwise the gradient autograd
+    forms with its separate add.  A use of the view alone (no field gradient) still gets its gradient."""
+    from gs4d_train.kernels import hexplane_points
+    torch.manual_seed(11)
+    P = 5003
+    x0 = torch.randn(P, 3, device="cuda")
+    t = torch.full((1, 1), 0.3, device="cuda").expand(P, 1)
+    aabb = torch.tensor([[1.5, 1.2, 1.3], [-1.4, -1.1, -1.6]], device="cuda")
+    w, u = torch.randn(P, 4, device="cuda"), torch.randn(P, 3, device="cuda")
+    xa = x0.clone().requires_grad_(True)
+    ((hexplane_points(xa, t, aabb) * w).sum() + (xa * u).sum()).backward()
+    xb = x0.clone().requires_grad_(True)
+    alias = []
+    pts = hexplane_points(xb, t, aabb, alias)
+    assert len(alias) == 1 and alias[0].data_ptr() == xb.data_ptr()
+    ((pts * w).sum() + (alias[0] * u).sum()).backward()
+    assert torch.equal(xa.grad, xb.grad)
+    xc = x0.clone().requires_grad_(True)
+    alias = []
+    hexplane_points(xc, t, aabb, alias)
+    (alias[0] * u).sum().backward()
+    assert torch.equal(xc.grad, u)

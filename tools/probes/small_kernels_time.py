@@ -44,6 +44,10 @@ def main():
         for q in lvl:
             q.grad = torch.zeros_like(q)
     rows.append(("reg accumulate + value", lambda: hexplane_regulation_accumulate_grad(grids, 1.0, 1e-4, 2e-4, 1.0, True)))
+    rows.append(("reg accumulate", lambda: hexplane_regulation_accumulate_grad(grids, 1.0, 1e-4, 2e-4, 1.0, False)))
+    # the L1 value + gradient at the bench image (3 x 1014 x 1352)
+    img, gt = torch.rand(3, 1014, 1352, device="cuda"), torch.rand(3, 1014, 1352, device="cuda")
+    rows.append(("l1_loss_grad", lambda: _C.l1_loss_grad(img, gt, 1.0)))
     for name, fn in rows:
         print(f"{name:28s} {timed(fn):8.1f} us", flush=True)
 
