@@ -11,5 +11,6 @@ timeout -k 10 400 python bench.py > $OUT/bench.log 2>&1 || { echo "bench rc=$?";
 grep '^{' $OUT/bench.log | tail -1 > $OUT/bench.json
 python3 -c "
 import json; j=json.load(open('$OUT/bench.json'))
-print('value', j['value'], 'ms', j['ms_per_step'], 'train', j.get("train_step",{}).get("ms"), "bf16", j.get("train_step",{}).get("bf16_mlp",{}).get("ms"), 'cpu', j.get('cpu_baseline'))
+t=j.get('train_step',{})
+print('value', j['value'], 'ms', j['ms_per_step'], 'train', t.get('ms'), 'bf16', t.get('bf16_mlp',{}).get('ms'), 'cpu', j.get('cpu_baseline'))
 "
