@@ -177,6 +177,17 @@ def _rocblas_ok(*ts):
         all(t.is_cuda and t.dim() == 2 and t.stride(1) == 1 for t in ts)
 
 
+def _chunk_rows(P):
+    """The split-K chunk for P rows on rocBLAS: the largest multiple of 8 in [3/4, 2] x kChunk that divides P (no
+    remainder GEMM: at P = 100k, 50 chunks of 2000 rows took 162 us per dW where 97 of 1024 plus the 672-row
+    remainder took 172, tools/sk_probe.sh), else kChunk and a remainder."""
+    c0 = _LinearSplitK.kChunk
+    for c in range(2 * c0 - (2 * c0) % 8, (3 * c0) // 4 - 1, -8):
+        if P % c == 0:
+            return c
+    return c0
+
+
 def _splitk_dw(dy, x):
     """dW = dy^T x reduced over the P rows as a split-K batched GEMM (see _LinearSplitK); x may be a
     column slice of a wider row-major tensor (its rows are then strided).  On the GPU: the chunks' partials
@@ -184,6 +195,8 @@ def _splitk_dw(dy, x):
     summed in chunk order by one pass (gs4d_sum_slices) -- the bmm, its .sum(0), the remainder GEMM and
     the add of the torch form in three launches."""
     P, c = x.shape[0], _LinearSplitK.kChunk
+    if _rocblas_ok(dy, x):
+        c = _chunk_rows(P)
     S = P // c
     if S < 2 and not (_rocblas_ok(dy, x) and P > 0):
         return (dy.t() @ x).float()

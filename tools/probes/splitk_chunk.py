@@ -1,5 +1,5 @@
 """dW = dy^T x split-K chunk size sweep (diagnostic, GPU): _splitk_dw at the heads' first-layer shape (P = 100k,
-N = 640, K = 128, fp32 and bf16) for several _LinearSplitK.kChunk values, HIP events over R calls."""
+N = 640, K = 128, fp32) for several _LinearSplitK.kChunk values (argv, or a default list), HIP events over R calls."""
 import os
 import sys
 
@@ -28,11 +28,16 @@ def main():
     dy = torch.randn(P, N, device="cuda")
     x = torch.relu(torch.randn(P, K, device="cuda"))
     ref = (dy.double().t() @ x.double())
-    for c in (1024, 2048, 4096, 8192, 16384):
+    for c in [int(a) for a in sys.argv[1:]] or (1024, 2048, 4096, 8192, 16384):
         D._LinearSplitK.kChunk = c
         out = D._splitk_dw(dy, x)
         err = float((out.double() - ref).abs().max() / ref.abs().max())
         print(f"kChunk {c:6d}: {timed(lambda: D._splitk_dw(dy, x)):8.1f} us  rel err {err:.2e}", flush=True)
+        torch.cuda.synchronize()
+        torch.full((7,), 1.0, device="cuda")  # a marker launch: a trace's kernels after it are 10 steady calls
+        for _ in range(10):
+            D._splitk_dw(dy, x)
+        torch.cuda.synchronize()
 
 
 if __name__ == "__main__":
