@@ -138,14 +138,14 @@ __global__ __launch_bounds__(256) void contrib_segments_kernel(const uint32_t *_
 // Pass 2 (at the start of gaussian_backward, one thread per Gaussian): a Gaussian whose slots span
 // several waves sums its pieces in wave order -- part[w0][1] (its head piece) then part[w][0] of each
 // following wave up to the one holding its last slot -- and a Gaussian without instances gets zeros.
-__global__ __launch_bounds__(256) void gaussian_backward_kernel(
-    Args a, GeomState g, const int *__restrict__ radii, const float *__restrict__ means3D,
+// Then K8 + K9 without the SH part: dL/dcov3D, dL/dscale, dL/drot stored; dL/dmean3D's covariance +
+// projection terms returned (the caller adds the SH term, backward.cu:390, and stores it).
+__device__ __forceinline__ V3 gaussian_grads(
+    int idx, const Args &a, const GeomState &g, const int *__restrict__ radii, const float *__restrict__ means3D,
     const float *__restrict__ scales, const float *__restrict__ rotations, const float *__restrict__ cov3Ds,
-    const float *dL_dmean2D, const float4 *dL_dconic, float *__restrict__ dL_dmean3D,
-    float *__restrict__ dL_dcov3D, float *__restrict__ dL_dscale, float *__restrict__ dL_drot,
-    const uint32_t *__restrict__ e_first, const float4 *__restrict__ part, GradOut o) {
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= a.P) return;
+    const float *dL_dmean2D, const float4 *dL_dconic, float *__restrict__ dL_dcov3D, float *__restrict__ dL_dscale,
+    float *__restrict__ dL_drot, const uint32_t *__restrict__ e_first, const float4 *__restrict__ part,
+    const GradOut &o) {
     {
         const uint32_t ni = g.n_inst[idx];
         if (ni == 0) {
@@ -186,7 +186,7 @@ __global__ __launch_bounds__(256) void gaussian_backward_kernel(
         dm2.y = (proj[4] * m_w - proj[7] * mul1) * g2x + (proj[5] * m_w - proj[7] * mul2) * g2y;
         dm2.z = (proj[8] * m_w - proj[11] * mul1) * g2x + (proj[9] * m_w - proj[11] * mul2) * g2y;
         dmean = dmean + dm2;
-        // SH part (backward.cu:390-391): sh_backward_kernel, launched next
+        // SH part (backward.cu:390-391): added by the caller
         // cov3D part (backward.cu:394-395)
         if (scales) {
             V3 sc = v3(scales[3 * idx], scales[3 * idx + 1], scales[3 * idx + 2]);
@@ -194,35 +194,50 @@ __global__ __launch_bounds__(256) void gaussian_backward_kernel(
             cov3D_backward(sc, a.scale_modifier, rot, dcov, dscale, drot);
         }
     }
-    dL_dmean3D[3 * idx + 0] = dmean.x;
-    dL_dmean3D[3 * idx + 1] = dmean.y;
-    dL_dmean3D[3 * idx + 2] = dmean.z;
 #pragma unroll
     for (int i = 0; i < 6; i++) dL_dcov3D[6 * (size_t)idx + i] = dcov[i];
     dL_dscale[3 * idx + 0] = dscale.x;
     dL_dscale[3 * idx + 1] = dscale.y;
     dL_dscale[3 * idx + 2] = dscale.z;
     reinterpret_cast<float4 *>(dL_drot)[idx] = drot;
+    return dmean;
 }
 
-// K9's SH part (backward.cu:390-391 -> computeColorFromSH backward, :20-139), one thread per Gaussian
-// with the block's coefficient rows staged through LDS: the block reads its 128 rows of 3M floats
-// (one contiguous span, float4 when M = 16 and aligned) into a 49-float-stride tile (odd stride: a
-// wave's rows hit distinct banks), each thread takes its row into registers, writes its gradients back
-// into the same row (zeros past (D + 1)^2 and for culled Gaussians) and adds the view-direction term to
-// dL/dmean3D after gaussian_backward's covariance + projection terms (the reference's order, :390), and
-// the block stores the tile as one contiguous span.  A thread per Gaussian straight from global memory
-// (192-byte strided rows) took 12.6 us of gaussian_backward's 26 at P = 100k.
+// Without SH coefficients (colours precomputed): one thread per Gaussian, dL/dmean3D = the two terms.
+__global__ __launch_bounds__(256) void gaussian_backward_kernel(
+    Args a, GeomState g, const int *__restrict__ radii, const float *__restrict__ means3D,
+    const float *__restrict__ scales, const float *__restrict__ rotations, const float *__restrict__ cov3Ds,
+    const float *dL_dmean2D, const float4 *dL_dconic, float *__restrict__ dL_dmean3D,
+    float *__restrict__ dL_dcov3D, float *__restrict__ dL_dscale, float *__restrict__ dL_drot,
+    const uint32_t *__restrict__ e_first, const float4 *__restrict__ part, GradOut o) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= a.P) return;
+    const V3 dmean = gaussian_grads(idx, a, g, radii, means3D, scales, rotations, cov3Ds, dL_dmean2D, dL_dconic,
+                                    dL_dcov3D, dL_dscale, dL_drot, e_first, part, o);
+    dL_dmean3D[3 * idx + 0] = dmean.x;
+    dL_dmean3D[3 * idx + 1] = dmean.y;
+    dL_dmean3D[3 * idx + 2] = dmean.z;
+}
+
+// With SH coefficients: the same per-Gaussian work and K9's SH part (backward.cu:390-391 -> computeColorFromSH
+// backward, :20-139) in one launch, one thread per Gaussian.  The block's coefficient rows are staged through
+// LDS: the block reads its 128 rows of 3M floats (one contiguous span, float4 when M = 16 and aligned) into a
+// 49-float-stride tile (odd stride: a wave's rows hit distinct banks), each thread takes its row into
+// registers, writes its gradients back into the same row (zeros past (D + 1)^2 and for culled Gaussians), and
+// the block stores the tile as one contiguous span.  dL/dmean3D = (covariance + projection terms) + the
+// view-direction term, the reference's order (:390).  A thread per Gaussian straight from global memory
+// (192-byte strided rows) took 12.6 us of the old gaussian_backward's 26 at P = 100k; two launches (this
+// work split at the SH part) cost one launch more.
 constexpr int kShThreads = 128, kShRow = 49;
 
 template <bool kVec4>
-__global__ __launch_bounds__(kShThreads) void sh_backward_kernel(Args a, const int *__restrict__ radii,
-                                                                 const float *__restrict__ means3D,
-                                                                 const float *__restrict__ shs,
-                                                                 const uint8_t *__restrict__ clamped,
-                                                                 const float *__restrict__ dL_dcolor,
-                                                                 float *__restrict__ dL_dmean3D,
-                                                                 float *__restrict__ dL_dsh) {
+__global__ __launch_bounds__(kShThreads) void gaussian_sh_backward_kernel(
+    Args a, GeomState g, const int *__restrict__ radii, const float *__restrict__ means3D,
+    const float *__restrict__ scales, const float *__restrict__ rotations, const float *__restrict__ cov3Ds,
+    const float *dL_dmean2D, const float4 *dL_dconic, float *__restrict__ dL_dmean3D,
+    float *__restrict__ dL_dcov3D, float *__restrict__ dL_dscale, float *__restrict__ dL_drot,
+    const uint32_t *__restrict__ e_first, const float4 *__restrict__ part, GradOut o, const float *__restrict__ shs,
+    const uint8_t *__restrict__ clamped, const float *dL_dcolor, float *__restrict__ dL_dsh) {
     __shared__ float tile[kShThreads * kShRow];
     const int g0 = blockIdx.x * kShThreads;
     // rows of M > 16 coefficients: only the first 16 can be used (D <= 3); the rest get zeros
@@ -243,9 +258,13 @@ __global__ __launch_bounds__(kShThreads) void sh_backward_kernel(Args a, const i
             if (c < 48) tile[r * kShRow + c] = shs[base + i];
         }
     }
+    V3 dmean = v3(0, 0, 0);
+    const int idx = g0 + threadIdx.x;
+    if ((int)threadIdx.x < n)  // pass 2 writes this Gaussian's dL/dcolor (when it spans waves) before it is read
+        dmean = gaussian_grads(idx, a, g, radii, means3D, scales, rotations, cov3Ds, dL_dmean2D, dL_dconic, dL_dcov3D,
+                               dL_dscale, dL_drot, e_first, part, o);
     __syncthreads();
     if ((int)threadIdx.x < n) {
-        const int idx = g0 + threadIdx.x;
         float *trow = tile + threadIdx.x * kShRow;
         float shl[48];
 #pragma unroll
@@ -260,10 +279,11 @@ __global__ __launch_bounds__(kShThreads) void sh_backward_kernel(Args a, const i
                                dL_dcolor[3 * idx + 2] * ((cl & 4) ? 0.f : 1.f));
             const V3 m = v3(means3D[3 * idx], means3D[3 * idx + 1], means3D[3 * idx + 2]);
             const V3 dm = sh_backward(a.D, shl, m - load_v3(a.campos), dRGB, trow);
-            dL_dmean3D[3 * idx + 0] += dm.x;
-            dL_dmean3D[3 * idx + 1] += dm.y;
-            dL_dmean3D[3 * idx + 2] += dm.z;
+            dmean = dmean + dm;
         }
+        dL_dmean3D[3 * idx + 0] = dmean.x;
+        dL_dmean3D[3 * idx + 1] = dmean.y;
+        dL_dmean3D[3 * idx + 2] = dmean.z;
     }
     __syncthreads();
     if (kVec4) {
@@ -314,15 +334,17 @@ hipError_t launch_gaussian_backward(const Args &a, GeomState g, int R, char *scr
                                     const float *cov3D, float *dL_dmean2D, float4 *dL_dconic, float *dL_dopacity,
                                     float *dL_dcolor, float *dL_dmean3D, float *dL_dcov3D, float *dL_dsh,
                                     float *dL_dscale, float *dL_drot, hipStream_t s) {
-    hipLaunchKernelGGL(gaussian_backward_kernel, dim3((a.P + 255) / 256), dim3(256), 0, s, a, g, radii, means3D,
-                       scales, rotations, cov3D, dL_dmean2D, dL_dconic, dL_dmean3D, dL_dcov3D,
-                       dL_dscale, dL_drot, scratch_e_first(scratch, R), scratch_part(scratch),
-                       grad_out(a, g, dL_dmean2D, dL_dconic, dL_dopacity, dL_dcolor));
+    const GradOut o = grad_out(a, g, dL_dmean2D, dL_dconic, dL_dopacity, dL_dcolor);
     if (shs) {
         const bool vec4 = a.M == 16 && (((size_t)shs | (size_t)dL_dsh) & 15) == 0;
-        hipLaunchKernelGGL(vec4 ? sh_backward_kernel<true> : sh_backward_kernel<false>,
-                           dim3((a.P + kShThreads - 1) / kShThreads), dim3(kShThreads), 0, s, a, radii, means3D, shs,
-                           g.clamped, dL_dcolor, dL_dmean3D, dL_dsh);
+        hipLaunchKernelGGL(vec4 ? gaussian_sh_backward_kernel<true> : gaussian_sh_backward_kernel<false>,
+                           dim3((a.P + kShThreads - 1) / kShThreads), dim3(kShThreads), 0, s, a, g, radii, means3D,
+                           scales, rotations, cov3D, dL_dmean2D, dL_dconic, dL_dmean3D, dL_dcov3D, dL_dscale, dL_drot,
+                           scratch_e_first(scratch, R), scratch_part(scratch), o, shs, g.clamped, dL_dcolor, dL_dsh);
+    } else {
+        hipLaunchKernelGGL(gaussian_backward_kernel, dim3((a.P + 255) / 256), dim3(256), 0, s, a, g, radii, means3D,
+                           scales, rotations, cov3D, dL_dmean2D, dL_dconic, dL_dmean3D, dL_dcov3D,
+                           dL_dscale, dL_drot, scratch_e_first(scratch, R), scratch_part(scratch), o);
     }
     return hipGetLastError();
 }

@@ -14,7 +14,7 @@ import shutil
 import sys
 from collections import defaultdict
 
-KEYS = {"render_backward_kernel": "render_backward", "render_forward_kernel": "render",
+KEYS = {"gaussian_sh_backward_kernel": "gaussian_sh_backward", "render_backward_kernel": "render_backward", "render_forward_kernel": "render",
         "onesweep_kernel": "onesweep", "emit_instances_kernel": "emit_instances", "preprocess_kernel": "preprocess",
         "contrib_segments_kernel": "contrib_segments", "gaussian_backward_kernel": "gaussian_backward",
         "visible_scan_kernel": "visible_scan", "tile_ranges_kernel": "tile_ranges",
