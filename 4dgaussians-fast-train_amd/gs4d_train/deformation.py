@@ -268,8 +268,17 @@ class _Stacked(torch.autograd.Function):
         return tuple(g.split(ctx.rows, 0))
 
 
+_STACKED_OK = {}  # (ids of the tensors) -> (their data pointers and row counts) when last found stacked
+
+
 def _stacked(ts):
-    """cat(ts, 0) as a view when the tensors are contiguous and consecutive in one storage, else None."""
+    """cat(ts, 0) as a view when the tensors are contiguous and consecutive in one storage, else None.
+    The full check runs once per layout: the same tensor objects at the same addresses with the same row counts
+    (a moved or replaced .data changes the address) take the cached verdict -- host time every train step."""
+    key = tuple(map(id, ts))
+    sig = tuple((t.data_ptr(), t.shape[0]) for t in ts)
+    if _STACKED_OK.get(key) == sig:
+        return _Stacked.apply(*ts)
     t0 = ts[0]
     if not t0.is_contiguous():
         return None
@@ -279,6 +288,9 @@ def _stacked(ts):
                 or t.untyped_storage().data_ptr() != t0.untyped_storage().data_ptr() or t.storage_offset() != off:
             return None
         off += t.numel()
+    if len(_STACKED_OK) > 64:
+        _STACKED_OK.clear()
+    _STACKED_OK[key] = sig
     return _Stacked.apply(*ts)
 
 

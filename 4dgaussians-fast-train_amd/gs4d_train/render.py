@@ -7,6 +7,8 @@ returns {render, viewspace_points, visibility_filter = radii > 0, radii, depth} 
 """
 import math
 
+import numpy as np
+
 import torch
 
 import diff_gaussian_rasterization as dgr
@@ -24,6 +26,14 @@ def _time_value(t, dev):
             _TIMES.clear()
         v = _TIMES[key] = torch.full((1, 1), t, dtype=torch.float32, device=dev)
     return v
+
+
+def _time_float(t):
+    """float(torch.tensor(t)): a Python float becomes float32 on the way (torch's default dtype), without building a
+    CPU tensor per call; anything else takes torch.tensor as the reference does"""
+    if type(t) is float:
+        return float(np.float32(t))
+    return float(torch.tensor(t))
 
 
 _ZERO_POINTS = {}
@@ -108,7 +118,7 @@ def render(viewpoint_camera, pc, pipe_debug, bg_color, scaling_modifier=1.0, sta
         sh_degree=pc.active_sh_degree, campos=cam_c, prefiltered=False, debug=pipe_debug)
     # torch.tensor(time).to(dev).repeat(P, 1) (:52): the same float32 column, as one device value broadcast
     # over the P rows (made once per (device, time); no fill per call)
-    time = _time_value(float(torch.tensor(viewpoint_camera.time)), dev).expand(xyz.shape[0], 1)
+    time = _time_value(_time_float(viewpoint_camera.time), dev).expand(xyz.shape[0], 1)
     rasterizer = dgr.GaussianRasterizer(raster_settings=settings)
     if "coarse" not in stage and "fine" not in stage:
         raise NotImplementedError(stage)
