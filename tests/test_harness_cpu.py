@@ -481,3 +481,18 @@ def test_lr_schedule_matches_reference():
         np.testing.assert_array_equal(got, v[f"lr_{i}"])
         i += 1
     assert i == 5
+
+
+def test_splitk_chunk_rows_divides_p_or_falls_back():
+    """deformation._chunk_rows: the largest multiple of 8 in [3/4, 2] x kChunk that divides P (no remainder GEMM),
+    else kChunk (the remainder path)."""
+    from gs4d_train.deformation import _LinearSplitK, _chunk_rows
+    c0 = _LinearSplitK.kChunk
+    for P in (100_000, 300_000, 1_000_000, 4096, 65_536, 100_003, 50_001, 7, 0):
+        c = _chunk_rows(P)
+        if c != c0 or P % c0 == 0:
+            assert P % c == 0 and c % 8 == 0 and (3 * c0) // 4 <= c <= 2 * c0, (P, c)
+            assert not any(P % d == 0 for d in range(c + 8, 2 * c0 + 1, 8) if d % 8 == 0), (P, c)
+        else:
+            assert not any(P % d == 0 for d in range((3 * c0) // 4, 2 * c0 + 1) if d % 8 == 0), (P, c)
+    assert _chunk_rows(100_000) == 2000

@@ -397,7 +397,8 @@ def test_heads_backward_matches_fp64(P, W, ns):
 def test_mlp_gemms_match_fp64(P, N, K, col0):
     """The deformation MLP's GPU GEMMs on rocBLAS (deformation._splitk_dw: split-K chunk partials + their
     remainder + gs4d_sum_slices; deformation._mm_dx: dy @ W) vs fp64 torch, to 1e-5 of each result's largest
-    |term| sum; P a multiple of the 1024-row chunk and not, x a column block of a wider matrix (col0 > 0),
+    |term| sum; P with a chunk that divides it (100k: 2000 rows, _chunk_rows) and P with a remainder, x a column
+    block of a wider matrix (col0 > 0),
     W 64/128/256.  The tuned kernel of each shape class is the one that runs (gemm_tuned), rocBLAS's own
     pick (tune=False) computes the same product, and gs4d_sum_slices' scalar form."""
     from gs4d_train import _C, deformation as D
