@@ -386,7 +386,8 @@ def hexplane_regulation_accumulate_grad(ms_grids, time_smoothness_weight, l1_tim
         v = hexplane_regulation_accumulate_grad(ms_grids, time_smoothness_weight, l1_time_planes_weight,
                                                 plane_tv_weight, scale, with_value)
         return base.detach().reshape(()) + v if with_value else v
-    v = _C.hexplane_reg_accumulate([p.detach() for p in planes], [p.grad for p in planes], ws, wl, dloss,
+    # the planes go to the extension as they are (it only reads their storage: no detach per plane per step)
+    v = _C.hexplane_reg_accumulate(planes, [p.grad for p in planes], ws, wl, dloss,
                                    with_value=with_value,
                                    base=base.detach().contiguous() if (with_value and base is not None) else None)
     return v if with_value else None
