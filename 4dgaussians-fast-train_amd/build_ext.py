@@ -68,8 +68,11 @@ def module_path(pkg="diff_gaussian_rasterization"):
     return os.path.join(HERE, pkg, "_C" + ext_suffix())
 
 
-def build(force=False, verbose=False):
+def build(force=False, verbose=False, report=True):
+    """Compile what is out of date; report=True prints one line per object / library / module saying whether it
+    was compiled or reused (mtimes of its sources, the headers and this script)."""
     os.makedirs(OBJ, exist_ok=True)
+    done = []  # (artifact, "compiled" | "reused")
     headers = [os.path.join(CSRC, h) for h in ("gs4d_math.h", "gs4d_internal.h", "radix_sort.h")] + [os.path.join(INCLUDE, h) for h in ("gs4d.h", "gs4d_train.h")]
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
@@ -80,13 +83,19 @@ def build(force=False, verbose=False):
             extra = (["-ffp-contract=off"] if src in NO_CONTRACT else []) + (["-fno-slp-vectorize"] if src in NO_SLP else []) \
                 + (["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"] if src in SCHED_ILP else [])
             _run([hipcc, *HIPCC_FLAGS, *extra, "-c", s, "-o", o], verbose)
-        return o
+            return o, "compiled"
+        return o, "reused"
 
     with cf.ThreadPoolExecutor(max_workers=min(8, len(HIP_SOURCES))) as ex:
-        objs = list(ex.map(compile_one, HIP_SOURCES))
+        res = list(ex.map(compile_one, HIP_SOURCES))
+    objs = [o for o, _ in res]
+    done += res
     lib = lib_path()
     if force or _newer(lib, objs):
         _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", lib], verbose)
+        done.append((lib, "compiled"))
+    else:
+        done.append((lib, "reused"))
 
     # torch bindings: (package dir, glue source); each links libgs4d from diff_gaussian_rasterization/
     import torch
@@ -111,7 +120,13 @@ def build(force=False, verbose=False):
                 "-Wl,-rpath,$ORIGIN" + ("" if rel == "." else "/" + rel), "-Wl,-rpath," + os.path.join(tdir, "lib"),
                 "-Wl,-rpath,/opt/rocm/lib"]
             _run(cmd, verbose)
+            done.append((mod, "compiled"))
+        else:
+            done.append((mod, "reused"))
         mods.append(mod)
+    if report:
+        for path, how in done:
+            print(f"gs4d build: {how:8s} {os.path.relpath(path, HERE)}", flush=True)
     return lib, mods
 
 

@@ -25,11 +25,11 @@
 //     and added into an LDS window over the plane's anchor box (ds_add_u64), whose nonzero cells go to the
 //     packed gradient's 64-bit accumulators by one no-return integer atomic each.  Integer sums are
 //     exact, so no schedule changes a bit: the backward is deterministic by construction (there is no
-//     float-atomic mode).  The per-plane scale bounds every cell's sum: |term| <= max|dfeat| times the
-//     product of the other five planes' max|param| (each bilinear sample is a convex combination of its
-//     plane's parameters), a cell takes at most one tap per point, so |sum| <= N |term|max < 2^62 at the
-//     chosen scale (hex_plane_scale; details at hexplane_backward_kernel).  One launch unpacks the
-//     accumulators to floats in the (1, F, H, W) parameter layout.
+//     float-atomic mode).  The per-plane scale bounds every cell's sum: point i's terms are at most m_i =
+//     max_f |dfeat_{i,l,f}| times the product of the other five planes' max|param| (each bilinear sample is a
+//     convex combination of its plane's parameters), a cell takes at most one tap per point, so |sum| <=
+//     sum_i m_i prod_q max|param_q| < 2^61 at the chosen scale (hex_plane_scale; details at
+//     hexplane_backward_kernel).  One launch unpacks the accumulators to floats in the (1, F, H, W) layout.
 #include <algorithm>
 #include <climits>
 
@@ -160,7 +160,12 @@ __global__ __launch_bounds__(kHexThreads) void hexplane_forward_kernel(int N, co
 // ~300 us against 225).
 constexpr int kHexDvFloats = 2048;   // NPW * F
 constexpr int kHexLdsWords = 20480;  // 80 KiB: two workgroups per CU, as the registers allow
-constexpr int kHexNanWord = 63;      // scale words: [0] max|dfeat|, [1 + p] max|param| of plane p, [63] non-finite flag
+// scale words: [0] max|dfeat|, [1 + p] max|param| of plane p, [32 + p] the scale of plane p (written by the
+// backward's workgroup 0 for the conversion launches), [63] non-finite flag; then kHexHistWords words: per
+// level, the histogram of the points' m_i = max_f |dfeat_{i,l,f}| by binary exponent (bin e counts the m_i
+// in (2^(e-128), 2^(e-127)]: an upper bound of sum_i m_i that integer atomics build the same in every run)
+constexpr int kHexNanWord = 63, kHexScaleWord = 32, kHexMxWords = 64;
+constexpr int kHexHistBins = 256, kHexHistWords = GS4D_HEXPLANE_MAX_LEVELS * kHexHistBins;
 
 __host__ __device__ __forceinline__ int hex_points_per_wg(int F) {
     const int ppc = kHexThreads / (F / 4);
@@ -172,19 +177,23 @@ __host__ __device__ __forceinline__ int hex_points_per_wg(int F) {
 // 64-bit window
 __host__ __device__ __forceinline__ int hex_bwd_fixed_words(int F) {
     const int npw = hex_points_per_wg(F);
-    return (6 * npw * F + 6 * npw * 3 + 6 * 4 + 4 * 6 * 4 + 8 + 1) & ~1;
+    // (+ 2 GS4D_HEXPLANE_MAX_LEVELS words: the per-level bound sums, doubles just below the window)
+    return (6 * npw * F + 6 * npw * 3 + 6 * 4 + 4 * 6 * 4 + 8 + 1 + 2 * GS4D_HEXPLANE_MAX_LEVELS) & ~1;
 }
 __host__ __device__ __forceinline__ int hex_bwd_window(int F) { return (kHexLdsWords - hex_bwd_fixed_words(F)) / 2; }
 
 // The fixed-point scale of plane p (of level l): 2^e with e chosen so that the largest possible cell sum fits
 // 2^61.  A term is w dv with w <= 1 and dv = dfeat * the product of the level's 5 other plane values, each a
 // convex combination of its plane's parameters, and a cell takes at most one tap per point, so
-//   |sum| <= N max|dfeat| prod_{q != p} max|param_q|
-// (computed in double: no overflow).  A zero bound (every term is 0) takes 1; a bound beyond the float
-// exponent range clamps e to its minimum, -126 (the largest term is a float, < 2^128, so N of them scaled by
-// 2^-126 still fit); non-finite inputs are flagged separately (kHexNanWord).
-__device__ __forceinline__ float hex_plane_scale(int N, const uint32_t *mx, int l, int p) {
-    double b = (double)N * (double)__uint_as_float(mx[0]);
+//   |sum| <= sum_i m_i prod_{q != p} max|param_q|,   m_i = max_f |dfeat_{i,l,f}|
+// with sum_i m_i bounded from above by msum = sum_e hist[l][e] 2^(e-127) (each m_i rounded up to a power of
+// two; computed in double: no overflow).  Round 5 used N max|dfeat| in its place: with heavy-tailed dfeat
+// (a few points' gradients far above the rest) that wasted up to log2(max/mean) bits of every cell's
+// resolution.  A zero bound (every term is 0) takes 1; a bound beyond the float exponent range clamps e to its
+// minimum, -126 (the largest term is a float, < 2^128, so N of them scaled by 2^-126 still fit); non-finite
+// inputs are flagged separately (kHexNanWord).
+__device__ __forceinline__ float hex_plane_scale(double msum, const uint32_t *mx, int l, int p) {
+    double b = msum;
     for (int q = 0; q < 6; q++)
         if (q != p) b *= (double)__uint_as_float(mx[1 + 6 * l + q]);
     if (!(b > 0.0)) return 1.f;
@@ -192,6 +201,8 @@ __device__ __forceinline__ float hex_plane_scale(int N, const uint32_t *mx, int 
     (void)frexp(b, &ex);  // b < 2^ex
     return ldexpf(1.f, max(-126, min(127, 61 - ex)));
 }
+// the scale of plane pg as the backward's workgroup 0 stored it (the conversion launches run after it)
+__device__ __forceinline__ float hex_stored_scale(const uint32_t *mx, int pg) { return __uint_as_float(mx[kHexScaleWord + pg]); }
 __device__ __forceinline__ unsigned long long hex_fix(float v, float scale) {
     return (unsigned long long)__float2ll_rn(v * scale);  // scale is a power of two: v * scale is exact
 }
@@ -203,15 +214,50 @@ struct HexMaxRanges {
     int64_t n[1 + 6 * GS4D_HEXPLANE_MAX_LEVELS];
     int first[2 + 6 * GS4D_HEXPLANE_MAX_LEVELS];  // first block of each range (blocks in proportion to its size)
     int nr;
+    int N, levels, F;  // range 0 is dfeat, (N, levels F)
 };
+// Range 0 (dfeat): one (point, level) row of F floats per thread item: its m_i = max_f |dfeat| goes to the
+// level's exponent histogram (LDS, then one global integer add per nonzero bin) and to the maximum.
+__device__ __forceinline__ void hex_dfeat_pass(const HexMaxRanges &rg, int b, int nb, uint32_t *__restrict__ mx,
+                                               float &m, bool &bad) {
+    __shared__ uint32_t s_hist[GS4D_HEXPLANE_MAX_LEVELS][kHexHistBins];
+    for (int e = threadIdx.x; e < rg.levels * kHexHistBins; e += 256) (&s_hist[0][0])[e] = 0u;
+    __syncthreads();
+    const int G = rg.F / 4;
+    const float4 *x = reinterpret_cast<const float4 *>(rg.x[0]);
+    const int64_t rows = (int64_t)rg.N * rg.levels;
+    for (int64_t i = (int64_t)b * 256 + threadIdx.x; i < rows; i += (int64_t)nb * 256) {
+        float a = 0.f;
+        for (int k = 0; k < G; k++) {
+            const float4 v = x[i * G + k];
+            const float t = fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
+            bad |= !(t <= 3.4028235e38f) || v.x != v.x || v.y != v.y || v.z != v.z || v.w != v.w;
+            a = fmaxf(a, t);
+        }
+        m = fmaxf(m, a);
+        if (a > 0.f && a <= 3.4028235e38f) {
+            // bin: the smallest e with a <= 2^(e-127) (denormals in bin 1: 2^-126)
+            const uint32_t u = __float_as_uint(a), ex = u >> 23;
+            const uint32_t e = ex == 0u ? 1u : ex + ((u & 0x7FFFFFu) != 0u ? 1u : 0u);
+            atomicAdd(&s_hist[(int)(i % rg.levels)][min(e, (uint32_t)kHexHistBins - 1u)], 1u);
+        }
+    }
+    __syncthreads();
+    uint32_t *hist = mx + kHexMxWords;
+    for (int e = threadIdx.x; e < rg.levels * kHexHistBins; e += 256) {
+        const uint32_t c = (&s_hist[0][0])[e];
+        if (c) atomicAdd(hist + e, c);
+    }
+}
 __global__ __launch_bounds__(256) void hex_max_kernel(HexMaxRanges rg, uint32_t *__restrict__ mx) {
     int r = 0;
     while (r + 1 < rg.nr && (int)blockIdx.x >= rg.first[r + 1]) r++;
     const float4 *x = reinterpret_cast<const float4 *>(rg.x[r]);  // every range is float4-aligned, n % 4 == 0
-    const int64_t n = rg.n[r] / 4;
+    const int64_t n = r == 0 ? 0 : rg.n[r] / 4;
     const int b = (int)blockIdx.x - rg.first[r], nb = rg.first[r + 1] - rg.first[r];
     float m = 0.f;
     bool bad = false;
+    if (r == 0) hex_dfeat_pass(rg, b, nb, mx, m, bad);  // uniform over the block
     // sixteen 16-byte loads in flight per thread per round (the range is split over few blocks: each block's
     // maximum is one atomicMax on the range's word, and those serialise; so the rounds must be few and wide)
     constexpr int kU = 16;
@@ -252,7 +298,8 @@ __global__ __launch_bounds__(256) void hex_fix_to_packed_kernel(gs4d_hexplane_la
     const int pg = blockIdx.y, l = pg / 6, p = pg - 6 * l;
     const gs4d_hexplane_plane pl = lay.plane[pg];
     const int64_t n = (int64_t)pl.W * pl.H * lay.F;
-    const float inv = 1.f / hex_plane_scale(N, mx, l, p);
+    (void)l, (void)p, (void)N;
+    const float inv = 1.f / hex_stored_scale(mx, pg);
     const bool nan = mx[kHexNanWord] != 0;
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
         out[pl.offset + i] = nan ? __builtin_nanf("") : (float)acc[pl.offset + i] * inv;
@@ -263,7 +310,7 @@ __global__ __launch_bounds__(kHexThreads) void hexplane_backward_kernel(int N, c
                                                                         gs4d_hexplane_layout lay,
                                                                         const float *__restrict__ packed,
                                                                         const float *__restrict__ dfeat,
-                                                                        const uint32_t *__restrict__ mx,
+                                                                        uint32_t *__restrict__ mx,
                                                                         unsigned long long *__restrict__ dfix,
                                                                         float *__restrict__ dpts) {
     __shared__ unsigned long long smem64[kHexLdsWords / 2];
@@ -280,7 +327,32 @@ __global__ __launch_bounds__(kHexThreads) void hexplane_backward_kernel(int N, c
     const int q = threadIdx.x % G, slot = threadIdx.x / G;
     const int lane = threadIdx.x & 63, wv = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t first = (int64_t)blockIdx.x * npw;
+    // per level: msum = sum_e hist[l][e] 2^(e-127) (hex_plane_scale), the same fixed-order sum in every
+    // workgroup (thread t takes bin t; the wave tree; the waves in order).  The waves' partials use the
+    // window's first words before it is zeroed; the sums stay in the fixed region, just below the window.
+    double *const s_msum = reinterpret_cast<double *>(s_win) - GS4D_HEXPLANE_MAX_LEVELS;
+    {
+        double *s_part = reinterpret_cast<double *>(s_win);  // [level][wave]
+        const uint32_t *hist = mx + kHexMxWords;
+        for (int l = 0; l < lay.levels; l++) {
+            double v = ldexp((double)hist[l * kHexHistBins + threadIdx.x], (int)threadIdx.x - 127);
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+            if (lane == 0) s_part[l * (kHexThreads / 64) + wv] = v;
+        }
+        __syncthreads();
+        if ((int)threadIdx.x < lay.levels) {
+            double t = 0.0;
+            for (int w = 0; w < kHexThreads / 64; w++) t += s_part[threadIdx.x * (kHexThreads / 64) + w];
+            s_msum[threadIdx.x] = t;
+        }
+        __syncthreads();
+        if (blockIdx.x == 0 && (int)threadIdx.x < 6 * lay.levels)  // for the conversion launches after this one
+            mx[kHexScaleWord + threadIdx.x] = __float_as_uint(hex_plane_scale(s_msum[threadIdx.x / 6], mx,
+                                                                              threadIdx.x / 6, threadIdx.x % 6));
+    }
     for (int e = threadIdx.x; e < wcap; e += kHexThreads) s_win[e] = 0ull;  // flushes leave it zeroed
+    __syncthreads();
     for (int l = 0; l < lay.levels; l++) {
         // 1. reverse passes
         for (int c = 0; c < cpw; c++) {
@@ -403,7 +475,7 @@ __global__ __launch_bounds__(kHexThreads) void hexplane_backward_kernel(int N, c
             const gs4d_hexplane_plane pl = lay.plane[6 * l + p];
             const int ax0 = s_box[p * 4 + 0], ay0 = s_box[p * 4 + 1], aw = s_box[p * 4 + 2], ah = s_box[p * 4 + 3];
             if (aw * ah == 0) continue;  // uniform
-            const float scale = hex_plane_scale(N, mx, l, p);
+            const float scale = hex_plane_scale(s_msum[l], mx, l, p);
             const float *dvp = s_dv + p * npw * F;
             const int *ancp = s_anc + p * npw;
             const float2 *ixyp = s_ixy + p * npw;
@@ -431,6 +503,9 @@ __global__ __launch_bounds__(kHexThreads) void hexplane_backward_kernel(int N, c
                     if (in_y1) atomicAdd(b0 + (size_t)pl.W * F, hex_fix((xa * yb) * d, scale));
                     if (in_x1 && in_y1) atomicAdd(b0 + (size_t)(pl.W + 1) * F, hex_fix((xb * yb) * d, scale));
                 }
+                // every wave is done reading this plane's s_dv / s_anc / s_ixy before any starts the next
+                // level's step 1, which overwrites them (the branch is uniform: the barrier is reached by all)
+                __syncthreads();
                 continue;
             }
             const int gp = fp / 4, lg = __builtin_ctz(gp), lf = __builtin_ctz(fp);  // powers of two
@@ -545,7 +620,8 @@ __global__ __launch_bounds__(kRepackThreads) void hexplane_repack_kernel(gs4d_he
     float inv = 1.f;
     bool nan = false;
     if (FIX) {
-        inv = 1.f / hex_plane_scale(N, mx, p / 6, p % 6);
+        (void)N;
+        inv = 1.f / hex_stored_scale(mx, p);
         nan = mx[kHexNanWord] != 0;
     }
     auto src = [&](int64_t i) -> float {  // element i of the plane's packed block
@@ -716,7 +792,7 @@ int gs4d_hexplane_forward(int N, const float *pts, const uint32_t *order, const 
 size_t gs4d_hexplane_backward_scratch_bytes(int N, const gs4d_hexplane_layout *lay) {
     (void)N;
     if (!lay) return 256;
-    return 256 + 8 * (size_t)lay->total + 256;
+    return 4 * (size_t)(kHexMxWords + kHexHistWords) + 8 * (size_t)lay->total + 256;
 }
 
 int gs4d_hexplane_backward(int N, const float *pts, const uint32_t *order, const gs4d_hexplane_layout *lay,
@@ -744,10 +820,12 @@ int gs4d_hexplane_backward(int N, const float *pts, const uint32_t *order, const
     if (hex_bwd_window(lay->F) < 4 * 4) return 1;
     const int np = 6 * lay->levels;
     uint32_t *mx = (uint32_t *)align_up((size_t)scratch, 256);
-    unsigned long long *dfix = (unsigned long long *)(mx + 64);
-    if (hipMemsetAsync(mx, 0, 256 + 8 * (size_t)lay->total, s) != hipSuccess) return 3;
+    unsigned long long *dfix = (unsigned long long *)(mx + kHexMxWords + kHexHistWords);
+    if (hipMemsetAsync(mx, 0, 4 * (size_t)(kHexMxWords + kHexHistWords) + 8 * (size_t)lay->total, s) != hipSuccess)
+        return 3;
     HexMaxRanges rg;
     rg.nr = 1 + np;
+    rg.N = N, rg.levels = lay->levels, rg.F = lay->F;
     rg.x[0] = dfeat;
     rg.n[0] = (int64_t)N * lay->levels * lay->F;
     for (int p = 0; p < np; p++) {
@@ -757,6 +835,7 @@ int gs4d_hexplane_backward(int N, const float *pts, const uint32_t *order, const
     rg.first[0] = 0;
     for (int r = 0; r < rg.nr; r++)  // >= 16 float4 per thread, at most 128 blocks per range
         rg.first[r + 1] = rg.first[r] + (int)std::min<int64_t>(128, std::max<int64_t>(1, (rg.n[r] + 16383) / 16384));
+    static_assert(kHexScaleWord + 6 * GS4D_HEXPLANE_MAX_LEVELS <= kHexNanWord, "scale words overlap the flag");
     hipLaunchKernelGGL(hex_max_kernel, dim3(rg.first[rg.nr]), dim3(256), 0, s, rg, mx);
     hipLaunchKernelGGL(hexplane_backward_kernel, dim3((unsigned)nwg), dim3(kHexThreads), 0, s, N, pts, order, *lay,
                        packed, dfeat, mx, dfix, dpts);

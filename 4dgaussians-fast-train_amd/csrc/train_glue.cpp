@@ -676,6 +676,93 @@ torch::Tensor mlp_dw_bf16(const torch::Tensor &da, const torch::Tensor &hb) {
     return dw;
 }
 
+// ---- row surgery (gs4d_rows_assemble): every tensor rebuilt by one row plan in one launch.  srcs: the old (P, ...)
+// tensors (a ZERO tensor's gives only its shape and dtype); givens[i]: the last appended rows of a GATHER tensor
+// (or None); keep: (K) int32 old row indices; append: int32 old row indices of the gathered appended rows (empty
+// when none).  Returns the new (K + A, ...) tensors.
+std::vector<torch::Tensor> rows_assemble(const std::vector<torch::Tensor> &srcs,
+                                         const std::vector<c10::optional<torch::Tensor>> &givens,
+                                         const std::vector<int64_t> &modes, const torch::Tensor &keep,
+                                         const torch::Tensor &append, int64_t A) {
+    const int n = (int)srcs.size();
+    need(n >= 1 && n <= GS4D_ROWS_MAX_TENSORS && (int)givens.size() == n && (int)modes.size() == n,
+         "rows_assemble: 1-32 tensors, one given and one mode each");
+    need(keep.is_cuda() && keep.scalar_type() == torch::kInt32 && keep.dim() == 1 && keep.is_contiguous(),
+         "rows_assemble: keep must be a contiguous int32 GPU vector");
+    need(A >= 0, "rows_assemble: A >= 0");
+    const int64_t K = keep.size(0);
+    const bool has_append = append.defined() && append.numel() > 0;
+    if (has_append)
+        need(append.is_cuda() && append.scalar_type() == torch::kInt32 && append.dim() == 1 && append.is_contiguous() &&
+                 append.size(0) <= A,
+             "rows_assemble: append must be a contiguous int32 GPU vector of at most A indices");
+    c10::hip::HIPGuard guard(keep.device().index());
+    gs4d_rows_batch b{};
+    b.count = 0, b.K = K, b.A = A;
+    b.keep = keep.data_ptr<int32_t>();
+    b.append = has_append ? append.data_ptr<int32_t>() : nullptr;
+    std::vector<torch::Tensor> out, keepalive;
+    for (int i = 0; i < n; i++) {
+        const torch::Tensor &s = srcs[i];
+        need(s.is_cuda() && s.device() == keep.device() && s.dim() >= 1 && s.is_contiguous(),
+             "rows_assemble: sources are contiguous GPU tensors on keep's device");
+        const int es = (int)s.element_size();
+        need(es == 1 || es == 4, "rows_assemble: 1- or 4-byte elements");
+        const int64_t mode = modes[i];
+        need(mode >= GS4D_ROWS_GATHER && mode <= GS4D_ROWS_ZERO, "rows_assemble: mode");
+        std::vector<int64_t> shape(s.sizes().begin(), s.sizes().end());
+        int64_t width = 1;
+        for (size_t d = 1; d < shape.size(); d++) width *= shape[d];
+        shape[0] = K + A;
+        auto d = torch::empty(shape, s.options());
+        out.push_back(d);
+        if (width == 0) continue;  // rows without elements (e.g. SH rest at degree 0): nothing to copy
+        gs4d_rows_tensor &t = b.t[b.count++];
+        t.src = s.data_ptr(), t.dst = d.data_ptr(), t.width = width, t.esize = es, t.mode = (int)mode;
+        t.given_rows = 0;
+        if (mode == GS4D_ROWS_GATHER && givens[i].has_value() && givens[i]->defined()) {
+            auto g = givens[i]->to(s.scalar_type()).contiguous();
+            need(g.is_cuda() && g.device() == s.device() && g.dim() >= 1 && g.size(0) <= A && g.numel() == g.size(0) * width,
+                 "rows_assemble: given rows (<= A, ...) with the source's row width");
+            t.given = g.data_ptr();
+            t.given_rows = g.size(0);
+            keepalive.push_back(g);
+        }
+        if (mode == GS4D_ROWS_GATHER)
+            need(A - t.given_rows <= (has_append ? append.size(0) : 0), "rows_assemble: too few append indices");
+    }
+    if (K + A > 0) check(gs4d_rows_assemble(&b, (void *)stream_of(keep)), "rows_assemble");
+    return out;
+}
+
+// ---- the fp32 block's input gradient: dh (P, W) = da (P, KW) @ W1 (KW, W), f32 MFMA, fixed order
+torch::Tensor mlp_dx_f32(const torch::Tensor &da, const torch::Tensor &w1) {
+    gpu_f32(da, "mlp_dx_f32: da");
+    gpu_f32(w1, "mlp_dx_f32: W1");
+    need(da.dim() == 2 && w1.dim() == 2 && w1.size(0) == da.size(1), "mlp_dx_f32: da (P, KW), W1 (KW, W)");
+    c10::hip::HIPGuard guard(da.device().index());
+    auto dh = torch::empty({da.size(0), w1.size(1)}, da.options());
+    check(gs4d_mlp_dx_f32((int)da.size(0), (int)da.size(1), (int)w1.size(1), da.data_ptr<float>(), w1.data_ptr<float>(),
+                          dh.data_ptr<float>(), (void *)stream_of(da)),
+          "mlp_dx_f32");
+    return dh;
+}
+
+// ---- the fp32 block's first-layer weight gradient: dW1 (KW, W) = da^T h, f32 MFMA, fixed order
+torch::Tensor mlp_dw_f32(const torch::Tensor &da, const torch::Tensor &h) {
+    gpu_f32(da, "mlp_dw_f32: da");
+    gpu_f32(h, "mlp_dw_f32: h");
+    need(da.dim() == 2 && h.dim() == 2 && da.size(0) == h.size(0), "mlp_dw_f32: da (P, KW), h (P, W)");
+    c10::hip::HIPGuard guard(da.device().index());
+    const int P = (int)da.size(0), KW = (int)da.size(1), W = (int)h.size(1);
+    auto dw = torch::empty({KW, W}, da.options());
+    auto scratch = torch::empty({(int64_t)gs4d_mlp_dw_f32_scratch_bytes(P, KW, W)}, da.options().dtype(torch::kUInt8));
+    check(gs4d_mlp_dw_f32(P, KW, W, da.data_ptr<float>(), h.data_ptr<float>(), dw.data_ptr<float>(), scratch.data_ptr(),
+                          (void *)stream_of(da)),
+          "mlp_dw_f32");
+    return dw;
+}
+
 // ---- first deformation layer forward: h = relu(x W^T + b)
 // with_hb: also h rounded to bf16 ((P, W) view of a (ceil(P/16)*16, W) buffer) for the bf16 heads block
 std::vector<torch::Tensor> feature_relu_forward(const torch::Tensor &x, const torch::Tensor &w, const torch::Tensor &b,
@@ -1021,6 +1108,9 @@ PYBIND11_MODULE(_C, m) {
           py::arg("w2"), py::arg("b2"), py::arg("hb") = py::none());
     m.def("mlp_dx_bf16", &mlp_dx_bf16);
     m.def("mlp_dw_bf16", &mlp_dw_bf16);
+    m.def("rows_assemble", &rows_assemble);
+    m.def("mlp_dx_f32", &mlp_dx_f32);
+    m.def("mlp_dw_f32", &mlp_dw_f32);
     m.def("feature_relu_backward", &feature_relu_backward);
     m.def("heads_backward", &heads_backward);
     m.def("linear_dw", &linear_dw);

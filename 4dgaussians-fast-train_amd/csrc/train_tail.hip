@@ -1987,6 +1987,204 @@ __global__ __launch_bounds__(kDwbThreads) void mlp_dw_bf16_kernel(int P, int KW,
                 o[(size_t)(16 * (wv * MW + m) + 4 * g + r) * W + 16 * n + li] = acc[m][n][r];
 }
 
+// ---- the fp32 heads block's input gradient: dh (P x W) = da (P x KW) W1 (KW x W) on v_mfma_f32_16x16x4_f32
+// (f32 products and sums in one fixed order per element: the same bits in every process, where the library
+// GEMM this replaces was picked per process by timing).  Computed transposed as mlp_dx_bf16_kernel does:
+// dh^T = W1^T da^T.  In the 16-wide k slice kk, lane (q = l >> 4, c = l & 15) supplies k = 16 kk + 4 q + s in
+// MFMA step s, so one float4 load of da row c gives the lane's 4 steps of the B operand, and the A operand
+// W1^T[16 m + c][16 kk + 4 q .. + 3] is one 16-byte LDS read (row stride 68 floats: conflict-free).
+// A workgroup is 4 waves on ONE 64-feature group of dh (4 m tiles) and 64 rows (16 per wave): small units of
+// work (3136 workgroups at P = 100k, W = 128) keep the per-CU share even.  W1's 64 x 64 block of the group is
+// staged per 64-wide k chunk, transposed as it is stored, double-buffered (34 KiB per workgroup); da is
+// prefetched a chunk ahead.  Workgroups b and b + 8 (same XCD) take the two feature groups of the same rows,
+// so the second read of those da rows is an L2 hit.
+constexpr int kDxfThreads = 256, kDxfChunk = 64, kDxfStride = kDxfChunk + 4;  // floats
+template <int W>
+__global__ __launch_bounds__(kDxfThreads) void mlp_dx_f32_kernel(int P, int KW, int nrg, const float *__restrict__ da,
+                                                                 const float *__restrict__ w1, float *__restrict__ dh) {
+    constexpr int NG = W / 64;  // feature groups
+    __shared__ __attribute__((aligned(16))) float s_a[2][64 * kDxfStride];
+    int rg = blockIdx.x, fg = 0;
+    if (NG == 2) {
+        const int i = blockIdx.x & 15;
+        fg = i >> 3;
+        rg = (int)(blockIdx.x >> 4) * 8 + (i & 7);
+    }
+    if (rg >= nrg) return;  // the grid is padded to whole groups of 8 row groups (uniform over the workgroup)
+    const int lane = threadIdx.x & 63, wv = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6), q = lane >> 4,
+              c = lane & 15;
+    const int64_t row = (int64_t)rg * 64 + wv * 16 + c;
+    // rows past P read row P - 1 (unconditional loads; not stored)
+    const float *brow = da + (size_t)min(row, (int64_t)P - 1) * KW + 4 * q;
+    f4v acc[4];
+#pragma unroll
+    for (int m = 0; m < 4; m++) acc[m] = f4v{0.f, 0.f, 0.f, 0.f};
+    const int nch = KW / kDxfChunk;
+    // staging: piece e = t + 256 i is W1 row (64 ch + e / 16), features 64 fg + 4 (e % 16) .. + 3 (coalesced
+    // 256-byte row segments), stored to the LDS image's rows 4 (e % 16) .. + 3 at column e / 16
+    float4 ga[4];
+    auto load_a = [&](int ch) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int e = (int)threadIdx.x + kDxfThreads * i;
+            ga[i] = *reinterpret_cast<const float4 *>(w1 + (size_t)(ch * kDxfChunk + (e >> 4)) * W + 64 * fg + 4 * (e & 15));
+        }
+    };
+    auto store_a = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int e = (int)threadIdx.x + kDxfThreads * i;
+            float *d = &s_a[buf][4 * (e & 15) * kDxfStride + (e >> 4)];
+            d[0] = ga[i].x;
+            d[kDxfStride] = ga[i].y;
+            d[2 * kDxfStride] = ga[i].z;
+            d[3 * kDxfStride] = ga[i].w;
+        }
+    };
+    float4 bn[4];
+    auto load_b = [&](int ch) {
+#pragma unroll
+        for (int kk = 0; kk < 4; kk++) bn[kk] = *reinterpret_cast<const float4 *>(brow + ch * kDxfChunk + 16 * kk);
+    };
+    load_a(0);
+    load_b(0);
+    store_a(0);
+    __syncthreads();
+    for (int ch = 0; ch < nch; ch++) {
+        float4 b[4];
+#pragma unroll
+        for (int kk = 0; kk < 4; kk++) b[kk] = bn[kk];
+        const int nx = min(ch + 1, nch - 1);  // the last chunk re-loads itself: loads stay unconditional
+        load_a(nx);
+        load_b(nx);
+        const float *sa = s_a[ch & 1];
+#pragma unroll
+        for (int kk = 0; kk < 4; kk++)
+#pragma unroll
+            for (int m = 0; m < 4; m++) {
+                const float4 av = *reinterpret_cast<const float4 *>(sa + (16 * m + c) * kDxfStride + 16 * kk + 4 * q);
+                acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, b[kk].x, acc[m], 0, 0, 0);
+                acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, b[kk].y, acc[m], 0, 0, 0);
+                acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, b[kk].z, acc[m], 0, 0, 0);
+                acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, b[kk].w, acc[m], 0, 0, 0);
+            }
+        if (ch + 1 < nch) store_a((ch + 1) & 1);  // the other buffer: read by nobody since the last barrier
+        __syncthreads();
+    }
+    // D[feature 16 m + 4 q + r][row c]
+    if (row < P)
+#pragma unroll
+        for (int m = 0; m < 4; m++)
+            *reinterpret_cast<float4 *>(dh + (size_t)row * W + 64 * fg + 16 * m + 4 * q) =
+                make_float4(acc[m][0], acc[m][1], acc[m][2], acc[m][3]);
+}
+
+// ---- the fp32 heads block's first-layer weight gradient: dW1 (KW x W) = da^T h reduced over the P rows, on
+// v_mfma_f32_16x16x4_f32 with K = rows.  In the MFMA k-step over rows r .. r + 3, lane (q, c) supplies
+// A[feature c][row q] = da[r + q][64 mb + 16 mt + c] and B[row q][feature c] = h[r + q][16 nt + c], each one
+// dword load (16 lanes read 64 contiguous bytes of a row).  Workgroup (row chunk s, 64-row block mb of dW1): its
+// 4 waves take interleaved 8-row steps of the chunk (two MFMA k-steps, 24 loads in flight a step ahead of the
+// MFMAs), each accumulating the whole 64 x W block (W = 128: 32 tiles, 128 accumulator registers), and are
+// summed in LDS in the fixed order (w0 + w2) + (w1 + w3) into parts[s]; gs4d_sum_slices then adds the chunks
+// in order.  Deterministic by construction.  The m blocks of one chunk sit on one XCD (they share its h rows).
+constexpr int kDwfThreads = 256, kDwfStepRows = 8;
+template <int W>
+__global__ __launch_bounds__(kDwfThreads, 2) void mlp_dw_f32_kernel(int P, int KW, int S, int chunk_rows,
+                                                                    const float *__restrict__ da,
+                                                                    const float *__restrict__ h,
+                                                                    float *__restrict__ parts) {
+    constexpr int NT = W / 16, MT = 4, NACC = MT * NT * 4;  // accumulator floats per lane
+    __shared__ __attribute__((aligned(16))) float s_red[2][NACC * 64];
+    const int nmb = KW / 64;
+    // b = 8 (nmb j + mb) + x: chunk s = 8 j + x, so the nmb blocks of a chunk share b % 8 (the XCD)
+    const int b = blockIdx.x, x = b & 7, jm = b >> 3, mb = jm % nmb, s = 8 * (jm / nmb) + x;
+    if (s >= S) return;  // padding of the grid to whole groups of 8 chunks (uniform over the workgroup)
+    const int lane = threadIdx.x & 63, wv = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6), q = lane >> 4,
+              c = lane & 15;
+    const int64_t r0 = (int64_t)s * chunk_rows, r1 = min((int64_t)P, r0 + chunk_rows);
+    f4v acc[MT][NT];
+#pragma unroll
+    for (int mt = 0; mt < MT; mt++)
+#pragma unroll
+        for (int nt = 0; nt < NT; nt++) acc[mt][nt] = f4v{0.f, 0.f, 0.f, 0.f};
+    // step t of wave w: rows r0 + 32 t + 8 w .. + 7 (the workgroup reads 32 consecutive rows per step)
+    const int nst = (int)((r1 - r0 + 31) / 32);
+    float an[2][MT], hn[2][NT];
+    auto load = [&](int t) {
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const int64_t r = r0 + 32 * (int64_t)t + 8 * wv + 4 * u + q;
+            const bool ok = r < r1;
+            const int64_t rc = ok ? r : r1 - 1;
+            const float *pa = da + (size_t)rc * KW + 64 * mb + c;
+            const float *ph = h + (size_t)rc * W + c;
+#pragma unroll
+            for (int mt = 0; mt < MT; mt++) {
+                const float v = pa[16 * mt];
+                an[u][mt] = ok ? v : 0.f;
+            }
+#pragma unroll
+            for (int nt = 0; nt < NT; nt++) {
+                const float v = ph[16 * nt];
+                hn[u][nt] = ok ? v : 0.f;
+            }
+        }
+    };
+    if (nst > 0) load(0);
+    for (int t = 0; t < nst; t++) {
+        float av[2][MT], hv[2][NT];
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+#pragma unroll
+            for (int mt = 0; mt < MT; mt++) av[u][mt] = an[u][mt];
+#pragma unroll
+            for (int nt = 0; nt < NT; nt++) hv[u][nt] = hn[u][nt];
+        }
+        load(min(t + 1, nst - 1));  // the last step re-loads itself: loads stay unconditional
+#pragma unroll
+        for (int u = 0; u < 2; u++)
+#pragma unroll
+            for (int mt = 0; mt < MT; mt++)
+#pragma unroll
+                for (int nt = 0; nt < NT; nt++)
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u][mt], hv[u][nt], acc[mt][nt], 0, 0, 0);
+    }
+    // (w0 + w2) + (w1 + w3), lane-major LDS image (conflict-free): float i of lane l at i * 64 + l
+    auto put = [&](float *dst) {
+#pragma unroll
+        for (int mt = 0; mt < MT; mt++)
+#pragma unroll
+            for (int nt = 0; nt < NT; nt++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) dst[((mt * NT + nt) * 4 + r) * 64 + lane] = acc[mt][nt][r];
+    };
+    auto add = [&](const float *src) {
+#pragma unroll
+        for (int mt = 0; mt < MT; mt++)
+#pragma unroll
+            for (int nt = 0; nt < NT; nt++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) acc[mt][nt][r] += src[((mt * NT + nt) * 4 + r) * 64 + lane];
+    };
+    if (wv >= 2) put(s_red[wv - 2]);
+    __syncthreads();
+    if (wv < 2) add(s_red[wv]);
+    __syncthreads();
+    if (wv == 1) put(s_red[0]);
+    __syncthreads();
+    if (wv == 0) {
+        add(s_red[0]);
+        // D[feature 16 mt + 4 q + r][feature 16 nt + c] of rows 64 mb .. of dW1
+        float *o = parts + (size_t)s * KW * W + (size_t)64 * mb * W;
+#pragma unroll
+        for (int mt = 0; mt < MT; mt++)
+#pragma unroll
+            for (int nt = 0; nt < NT; nt++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) o[(size_t)(16 * mt + 4 * q + r) * W + 16 * nt + c] = acc[mt][nt][r];
+    }
+}
+
 // ---- the wide head's second-layer backward on the bf16 path (n = 48, W = 128): heads_bwd_wide_mfma_kernel's
 // products on v_mfma_f32_16x16x32_bf16 with g rounded to bf16 (the bf16 leg's operands), sums in fp32.  A
 // workgroup takes 32-row steps (grid-stride): the a tile (32 x 128 bf16) and the g tile (32 x 48 -> bf16,
@@ -2231,6 +2429,38 @@ using namespace gs4d;
 // 64-thread workgroups: a column per thread, so the (P / 1024)-slice sums of the MLP's 128 x 640 weight
 // gradient (20480 float4 columns) spread over 320 workgroups, every CU, where 256-thread ones filled 80 CUs
 constexpr int kSumThreads = 64;
+// ---- row surgery of densification / pruning (gs4d_rows_assemble, scene/gaussian_model.py:316-506): tensor
+// blockIdx.y, its output elements grid-strided over blockIdx.x.  Element c of output row r: r < K takes old
+// row keep[r]; r = K + j takes, by the tensor's mode, old row append[j] or (the last given_rows) given rows,
+// or zero.  Pure copies
+// (4-byte words or bytes): bitwise the reference's cat / boolean-index results.  The batch is passed by value.
+constexpr int64_t kRowsPerBlock = (int64_t)kTailThreads * 8;
+template <class T>
+__device__ __forceinline__ void rows_copy(const gs4d_rows_batch &b, const gs4d_rows_tensor &t) {
+    const int64_t w = t.width, n = (b.K + b.A) * w;
+    const T *__restrict__ src = (const T *)t.src;
+    const T *__restrict__ given = (const T *)t.given;
+    T *__restrict__ dst = (T *)t.dst;
+    for (int64_t e = (int64_t)blockIdx.x * kTailThreads + threadIdx.x; e < n; e += (int64_t)gridDim.x * kTailThreads) {
+        const int64_t r = e / w, c = e - r * w;
+        T v = T(0);
+        if (t.mode != GS4D_ROWS_ZERO) {
+            if (r < b.K) {
+                v = src[(int64_t)b.keep[r] * w + c];
+            } else if (t.mode == GS4D_ROWS_GATHER) {
+                const int64_t j = r - b.K, jg = j - (b.A - t.given_rows);
+                v = jg < 0 ? src[(int64_t)b.append[j] * w + c] : given[jg * w + c];
+            }
+        }
+        dst[e] = v;
+    }
+}
+__global__ __launch_bounds__(kTailThreads) void rows_assemble_kernel(gs4d_rows_batch b) {
+    const gs4d_rows_tensor &t = b.t[blockIdx.y];
+    if (t.esize == 4) rows_copy<uint32_t>(b, t);
+    else rows_copy<uint8_t>(b, t);
+}
+
 template <bool V4>
 __global__ __launch_bounds__(kSumThreads) void sum_slices_kernel(const float *__restrict__ parts, int S, int64_t n,
                                                                  float *__restrict__ out) {
@@ -2567,6 +2797,29 @@ int gs4d_deform_tail_backward(int P, int K, const float *scales, const float *r,
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
+int gs4d_rows_assemble(const gs4d_rows_batch *batch, void *stream) {
+    if (!batch || batch->count < 0 || batch->count > GS4D_ROWS_MAX_TENSORS || batch->K < 0 || batch->A < 0) return 1;
+    const gs4d_rows_batch &b = *batch;
+    const int64_t rows = b.K + b.A;
+    if (rows > INT32_MAX || (b.K > 0 && !b.keep)) return 1;
+    int64_t most = 0;
+    for (int i = 0; i < b.count; i++) {
+        const gs4d_rows_tensor &t = b.t[i];
+        if (t.width < 1 || (t.esize != 1 && t.esize != 4) || t.mode < GS4D_ROWS_GATHER || t.mode > GS4D_ROWS_ZERO) return 1;
+        if (rows > 0 && !t.dst) return 1;
+        if (t.mode != GS4D_ROWS_ZERO && b.K > 0 && !t.src) return 1;
+        if (t.mode == GS4D_ROWS_GATHER) {
+            if (t.given_rows < 0 || t.given_rows > b.A || (t.given_rows > 0 && !t.given)) return 1;
+            if (t.given_rows < b.A && (!b.append || !t.src)) return 1;
+        }
+        most = std::max(most, rows * t.width);
+    }
+    if (b.count == 0 || most == 0) return 0;
+    const unsigned gx = (unsigned)std::min<int64_t>((most + kRowsPerBlock - 1) / kRowsPerBlock, 4096);
+    hipLaunchKernelGGL(rows_assemble_kernel, dim3(gx, b.count), dim3(kTailThreads), 0, (hipStream_t)stream, b);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
 int gs4d_sum_slices(const float *parts, int S, int64_t n, float *out, void *stream) {
     if (S < 1 || n < 0 || (n > 0 && (!parts || !out))) return 1;
     if (n == 0) return 0;
@@ -2833,6 +3086,55 @@ int gs4d_mlp_dw_bf16(int P, int KW, int W, const uint16_t *da, const uint16_t *h
     float *parts = (float *)align_up((size_t)scratch, 256);
     hipLaunchKernelGGL(mlp_dw_bf16_kernel, dim3(S, KW / W), dim3(kDwbThreads), 0, s, P, KW, (const __bf16 *)da,
                        (const __bf16 *)hb, parts);
+    if (hipGetLastError() != hipSuccess) return 3;
+    return gs4d_sum_slices(parts, S, (int64_t)KW * W, dw, stream);
+}
+
+int gs4d_mlp_dx_f32(int P, int KW, int W, const float *da, const float *w1, float *dh, void *stream) {
+    if (P < 0 || KW < kDxfChunk || KW % kDxfChunk != 0 || (W != 64 && W != 128)) return 1;
+    if (P == 0) return 0;
+    if (!da || !w1 || !dh || (((size_t)da | (size_t)w1 | (size_t)dh) & 15) != 0) return 1;
+    const int nrg = (int)(((int64_t)P + 63) / 64);
+    hipStream_t s = (hipStream_t)stream;
+    if (W == 128)  // two feature groups per row group, the grid padded to whole groups of 8 row groups
+        hipLaunchKernelGGL(mlp_dx_f32_kernel<128>, dim3((unsigned)((nrg + 7) / 8 * 16)), dim3(kDxfThreads), 0, s, P, KW,
+                           nrg, da, w1, dh);
+    else
+        hipLaunchKernelGGL(mlp_dx_f32_kernel<64>, dim3((unsigned)nrg), dim3(kDxfThreads), 0, s, P, KW, nrg, da, w1, dh);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+// the row chunks of gs4d_mlp_dw_f32: about two rounds of two workgroups per CU over (chunk, m block), chunks
+// of a multiple of 32 rows and at least 256
+static void dwf_chunks(int P, int KW, int *S, int *rows) {
+    const int nmb = std::max(1, KW / 64);
+    const int64_t target = std::max<int64_t>(1, (4 * (int64_t)cu_count() + nmb / 2) / nmb);
+    int64_t c = ((int64_t)P + target - 1) / target;
+    c = std::max<int64_t>(256, (c + 31) / 32 * 32);
+    *rows = (int)c;
+    *S = (int)std::max<int64_t>(1, ((int64_t)P + c - 1) / c);
+}
+
+size_t gs4d_mlp_dw_f32_scratch_bytes(int P, int KW, int W) {
+    if (P <= 0 || KW <= 0 || W <= 0) return 256;
+    int S = 1, rows = 0;
+    dwf_chunks(P, KW, &S, &rows);
+    return 4 * (size_t)S * KW * W + 256;
+}
+
+int gs4d_mlp_dw_f32(int P, int KW, int W, const float *da, const float *h, float *dw, void *scratch, void *stream) {
+    if (P < 0 || (W != 64 && W != 128) || KW < 64 || KW % 64 != 0 || !dw) return 1;
+    hipStream_t s = (hipStream_t)stream;
+    if (P == 0) return hipMemsetAsync(dw, 0, 4 * (size_t)KW * W, s) == hipSuccess ? 0 : 3;
+    if (!da || !h || !scratch) return 1;
+    int S = 1, rows = 0;
+    dwf_chunks(P, KW, &S, &rows);
+    float *parts = (float *)align_up((size_t)scratch, 256);
+    const unsigned grid = (unsigned)(8 * (KW / 64) * ((S + 7) / 8));
+    if (W == 128)
+        hipLaunchKernelGGL(mlp_dw_f32_kernel<128>, dim3(grid), dim3(kDwfThreads), 0, s, P, KW, S, rows, da, h, parts);
+    else
+        hipLaunchKernelGGL(mlp_dw_f32_kernel<64>, dim3(grid), dim3(kDwfThreads), 0, s, P, KW, S, rows, da, h, parts);
     if (hipGetLastError() != hipSuccess) return 3;
     return gs4d_sum_slices(parts, S, (int64_t)KW * W, dw, stream);
 }

@@ -157,18 +157,18 @@ class Linear(nn.Linear):
         return F.linear(x, self.weight, self.bias)
 
 
-# The MLP's GEMMs run on rocBLAS kernels chosen at run time: gemm_f32(..., tune=True) times every solution
-# rocBLAS has for a shape class on its first call and keeps the fastest (train_glue.cpp).  On the r03 image
-# the chosen kernels took 121 (split-K dW, 97 chunks of 1024 rows), 8.7 (its 672-row remainder) and 126 us
-# (the input gradient da @ W1) where hipBLASLt's heuristic picks took 129, 14 and 158 us
-# (tools/tunableop_probe.sh, profiles/r03_tunableop_results.csv).  _C.gemm_tuned() lists the choices.
+# The heads block's two large GEMMs (W in {64, 128}) run on this library's f32-MFMA passes (gs4d_mlp_dw_f32,
+# gs4d_mlp_dx_f32): one fixed summation order, so a train step gives the same bits in every process.  The
+# shapes those do not serve (W = 256, the bf16 path's W = 64 weight gradient) go to rocBLAS through gemm_f32:
+# by default rocBLAS's own pick, which depends only on the shape (the same kernel in every process).
+# GS4D_GEMM_TUNE=1 opts into the run-time tuner instead (gemm_f32(..., tune=True) times every solution rocBLAS
+# has for a shape class on its first call and keeps the fastest, train_glue.cpp): faster on some shapes, but
+# the choice depends on timings, so two processes may run different kernels and round differently.
+# _C.gemm_tuned() lists the tuner's choices.
 
 
 _USE_ROCBLAS = os.environ.get("GS4D_MLP_ROCBLAS", "1") != "0"  # 0: torch's GEMMs (A/B runs)
-# The tuned choice depends on timings, so two processes may pick different kernels for a shape (and round
-# differently); a step is bitwise reproducible inside a process either way.  GS4D_GEMM_TUNE=0 keeps
-# rocBLAS's own pick, the same in every process (reproducible across runs, slower: ~+0.35 ms per fp32 step).
-_TUNE = os.environ.get("GS4D_GEMM_TUNE", "1") != "0"
+_TUNE = os.environ.get("GS4D_GEMM_TUNE", "0") == "1"
 
 
 def _rocblas_ok(*ts):
@@ -362,8 +362,14 @@ class _DeformHeads(torch.autograd.Function):
             from . import _C
             out = _C.heads_backward(a, list(douts), [x.contiguous() for x in w2])
             da, db1 = out[0], out[1]
-            dw1 = _splitk_dw(da, h)
-            dh = relu_in(_mm_dx(da, w1))
+            if W in (64, 128) and da.shape[1] % 64 == 0:
+                # the two large GEMMs on hand-written f32-MFMA passes: fixed summation order, the same bits in
+                # every process (gs4d_mlp_dw_f32 / gs4d_mlp_dx_f32)
+                dw1 = _C.mlp_dw_f32(da, h.contiguous())
+                dh = relu_in(_C.mlp_dx_f32(da, w1.contiguous()))
+            else:
+                dw1 = _splitk_dw(da, h)
+                dh = relu_in(_mm_dx(da, w1))
             return tuple([dh, dw1, db1] + out[2:])
         da = torch.empty_like(a)
         dw2, db2 = [None] * k, [None] * k

@@ -3,13 +3,14 @@
 Restates scene/gaussian_model.py of the reference (the train-step tail) for the
 fine-stage training path: the same parameter tensors and activations (:29-45), the Adam parameter
 groups and learning-rate schedules (:165-212), the densification statistics (:521-523), the
-clone / split / prune tensor surgery on the optimizer state (:316-505), opacity reset (:269-272),
+clone / split / prune events (:316-506, as row plans: gs4d_train/surgery.py), opacity reset (:269-272),
 the HexPlane regularisers (:538-566) and the PLY layout (:214-226, 250-314; see gs4d_train/ply.py).
 
-Three places run libgs4d HIP kernels when `fused=True` (the default on a GPU): the optimizer step
+Four places run libgs4d HIP kernels when `fused=True` (the default on a GPU): the optimizer step
 (one multi-tensor Adam launch, kernels.FusedAdam), the densification statistics
-(kernels.densify_stats) and the HexPlane regularisers (kernels.hexplane_regulation).  `fused=False` keeps the reference's torch formulation, which the parity
-tests compare against.
+(kernels.densify_stats), the HexPlane regularisers (kernels.hexplane_regulation) and the densify / prune
+row surgery (one gs4d_rows_assemble launch per event).  `fused=False` runs the torch formulations, which the
+parity tests compare against.
 """
 import math
 
@@ -17,6 +18,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
+from . import surgery
 from .deformation import DeformNetwork
 
 
@@ -230,135 +232,85 @@ class GaussianModel:
         self.xyz_gradient_accum[update_filter] += torch.norm(viewspace_grad[update_filter, :2], dim=-1, keepdim=True)
         self.denom[update_filter] += 1
 
-    # ---- optimizer-state surgery (gaussian_model.py:316-413)
-    def replace_tensor_to_optimizer(self, tensor, name):
-        out = {}
-        for group in self.optimizer.param_groups:
-            if group["name"] == name:
-                stored = self.optimizer.state.get(group["params"][0], None)
-                stored["exp_avg"] = torch.zeros_like(tensor)
-                stored["exp_avg_sq"] = torch.zeros_like(tensor)
-                del self.optimizer.state[group["params"][0]]
-                group["params"][0] = nn.Parameter(tensor.requires_grad_(True))
-                self.optimizer.state[group["params"][0]] = stored
-                out[group["name"]] = group["params"][0]
-        return out
-
-    def _prune_optimizer(self, mask):
-        out = {}
-        for group in self.optimizer.param_groups:
-            if len(group["params"]) > 1:
-                continue
-            stored = self.optimizer.state.get(group["params"][0], None)
-            if stored is not None:
-                stored["exp_avg"] = stored["exp_avg"][mask]
-                stored["exp_avg_sq"] = stored["exp_avg_sq"][mask]
-                del self.optimizer.state[group["params"][0]]
-                group["params"][0] = nn.Parameter(group["params"][0][mask].requires_grad_(True))
-                self.optimizer.state[group["params"][0]] = stored
-            else:
-                group["params"][0] = nn.Parameter(group["params"][0][mask].requires_grad_(True))
-            out[group["name"]] = group["params"][0]
-        return out
-
-    def _take(self, t):
-        self._xyz, self._features_dc, self._features_rest = t["xyz"], t["f_dc"], t["f_rest"]
-        self._opacity, self._scaling, self._rotation = t["opacity"], t["scaling"], t["rotation"]
+    # ---- densification and pruning (gaussian_model.py:316-506) as row plans over the old rows (surgery.py):
+    # every per-Gaussian tensor, its Adam moments and statistics rebuilt in one pass per event
+    def _row_ids(self, mask):
+        return torch.nonzero(mask, as_tuple=False).flatten()
 
     def prune_points(self, mask):
-        valid = ~mask
-        self._take(self._prune_optimizer(valid))
-        self._deformation_accum = self._deformation_accum[valid]
-        self.xyz_gradient_accum = self.xyz_gradient_accum[valid]
-        self._deformation_table = self._deformation_table[valid]
-        self.denom = self.denom[valid]
-        self.max_radii2D = self.max_radii2D[valid]
+        """Drop the rows where mask is True; surviving rows keep their moments and statistics."""
+        surgery.apply(self, surgery.RowPlan(keep=self._row_ids(~mask)))
 
-    def cat_tensors_to_optimizer(self, tensors_dict):
-        out = {}
-        for group in self.optimizer.param_groups:
-            if len(group["params"]) > 1:
-                continue
-            ext = tensors_dict[group["name"]]
-            stored = self.optimizer.state.get(group["params"][0], None)
-            if stored is not None:
-                stored["exp_avg"] = torch.cat((stored["exp_avg"], torch.zeros_like(ext)), dim=0)
-                stored["exp_avg_sq"] = torch.cat((stored["exp_avg_sq"], torch.zeros_like(ext)), dim=0)
-                del self.optimizer.state[group["params"][0]]
-                group["params"][0] = nn.Parameter(torch.cat((group["params"][0], ext), dim=0).requires_grad_(True))
-                self.optimizer.state[group["params"][0]] = stored
-            else:
-                group["params"][0] = nn.Parameter(torch.cat((group["params"][0], ext), dim=0).requires_grad_(True))
-            out[group["name"]] = group["params"][0]
-        return out
+    def _max_scale(self):
+        return torch.max(self.get_scaling, dim=1).values
 
-    def densification_postfix(self, new_xyz, new_features_dc, new_features_rest, new_opacities, new_scaling,
-                              new_rotation, new_deformation_table):
+    def _clone_rows(self, grads, grad_threshold, scene_extent):
+        """gaussian_model.py:443-457's choice: accumulated gradient at or above the threshold, small Gaussians."""
+        hot = torch.norm(grads, dim=-1) >= grad_threshold
+        return self._row_ids(hot & (self._max_scale() <= self.percent_dense * scene_extent))
+
+    def _split_rows(self, grads, grad_threshold, scene_extent):
+        """gaussian_model.py:415-423's choice: the same gradient test on large Gaussians.  (The reference pads the
+        gradient with zeros for rows cloned just before, which therefore never split: only old rows can.)"""
+        g = grads.reshape(-1)
+        return self._row_ids((g >= grad_threshold) & (self._max_scale() > self.percent_dense * scene_extent))
+
+    def _split_children(self, ids, N):
+        """Positions and scales of the N children of each row in ids (gaussian_model.py:424-431), children
+        ordered copy after copy; the sampling draws the same normals, in the same order, as the reference."""
         dev = self._xyz.device
-        self._take(self.cat_tensors_to_optimizer({"xyz": new_xyz, "f_dc": new_features_dc,
-                                                  "f_rest": new_features_rest, "opacity": new_opacities,
-                                                  "scaling": new_scaling, "rotation": new_rotation}))
-        self._deformation_table = torch.cat([self._deformation_table, new_deformation_table], -1)
-        P = self.get_xyz.shape[0]
-        self.xyz_gradient_accum = torch.zeros((P, 1), device=dev)
-        self._deformation_accum = torch.zeros((P, 3), device=dev)
-        self.denom = torch.zeros((P, 1), device=dev)
-        self.max_radii2D = torch.zeros((P), device=dev)
-
-    def densify_and_split(self, grads, grad_threshold, scene_extent, N=2):
-        """gaussian_model.py:415-441"""
-        dev = self._xyz.device
-        n_init = self.get_xyz.shape[0]
-        padded = torch.zeros((n_init), device=dev)
-        padded[:grads.shape[0]] = grads.squeeze()
-        sel = torch.where(padded >= grad_threshold, True, False)
-        sel = torch.logical_and(sel, torch.max(self.get_scaling, dim=1).values > self.percent_dense * scene_extent)
-        if not sel.any():
-            return
-        stds = self.get_scaling[sel].repeat(N, 1)
-        samples = torch.normal(mean=torch.zeros((stds.size(0), 3), device=dev), std=stds)
+        scale = self.get_scaling[ids].repeat(N, 1)
+        offsets = torch.normal(mean=torch.zeros((scale.size(0), 3), device=dev), std=scale)
         # data-parallel replicas select the same Gaussians (their statistics are all-reduced) but draw
         # from their own RNGs: rank 0's draws are the ones every replica uses
         from . import dp
         if getattr(self, "data_parallel_step", False) and dp.world() > 1:
-            torch.distributed.broadcast(samples, src=0)
-        rots = build_rotation(self._rotation[sel]).repeat(N, 1, 1)
-        new_xyz = torch.bmm(rots, samples.unsqueeze(-1)).squeeze(-1) + self.get_xyz[sel].repeat(N, 1)
-        new_scaling = self.scaling_inverse_activation(self.get_scaling[sel].repeat(N, 1) / (0.8 * N))
-        self.densification_postfix(new_xyz, self._features_dc[sel].repeat(N, 1, 1),
-                                   self._features_rest[sel].repeat(N, 1, 1), self._opacity[sel].repeat(N, 1),
-                                   new_scaling, self._rotation[sel].repeat(N, 1), self._deformation_table[sel].repeat(N))
-        prune_filter = torch.cat((sel, torch.zeros(N * sel.sum(), device=dev, dtype=bool)))
-        self.prune_points(prune_filter)
+            torch.distributed.broadcast(offsets, src=0)
+        rot = build_rotation(self._rotation[ids]).repeat(N, 1, 1)
+        xyz = torch.bmm(rot, offsets.unsqueeze(-1)).squeeze(-1) + self.get_xyz[ids].repeat(N, 1)
+        return xyz, self.scaling_inverse_activation(scale / (0.8 * N))
+
+    def _grow(self, clone_ids, split_ids, N=2):
+        """One plan for a clone pass followed by a split pass: the rows not split, the clones, the children.
+        Statistics restart at zero (densification_postfix)."""
+        dev = self._xyz.device
+        keep = torch.ones(self._xyz.shape[0], dtype=torch.bool, device=dev)
+        keep[split_ids] = False
+        computed, n_split = {}, split_ids.numel()
+        if n_split:
+            computed["xyz"], computed["scaling"] = self._split_children(split_ids, N)
+        plan = surgery.RowPlan(keep=self._row_ids(keep), append=torch.cat([clone_ids] + [split_ids] * N),
+                               computed=computed, n_new=clone_ids.numel() + N * n_split, stats="reset")
+        surgery.apply(self, plan)
 
     def densify_and_clone(self, grads, grad_threshold, scene_extent):
         """gaussian_model.py:443-457"""
-        mask = torch.where(torch.norm(grads, dim=-1) >= grad_threshold, True, False)
-        sel = torch.logical_and(mask, torch.max(self.get_scaling, dim=1).values <= self.percent_dense * scene_extent)
-        self.densification_postfix(self._xyz[sel], self._features_dc[sel], self._features_rest[sel],
-                                   self._opacity[sel], self._scaling[sel], self._rotation[sel],
-                                   self._deformation_table[sel])
+        empty = self._row_ids(torch.zeros(0, dtype=torch.bool, device=self._xyz.device))
+        self._grow(self._clone_rows(grads, grad_threshold, scene_extent), empty)
+
+    def densify_and_split(self, grads, grad_threshold, scene_extent, N=2):
+        """gaussian_model.py:415-441 (a no-op when nothing is selected, as there)"""
+        ids = self._split_rows(grads[:self._xyz.shape[0]], grad_threshold, scene_extent)
+        if ids.numel():
+            self._grow(ids[:0], ids, N)
 
     def prune(self, max_grad, min_opacity, extent, max_screen_size):
         """gaussian_model.py:489-499"""
-        prune_mask = (self.get_opacity < min_opacity).squeeze()
+        drop = (self.get_opacity < min_opacity).squeeze()
         if max_screen_size:
-            big_vs = self.max_radii2D > max_screen_size
-            big_ws = self.get_scaling.max(dim=1).values > 0.1 * extent
-            prune_mask = torch.logical_or(torch.logical_or(prune_mask, big_vs), big_ws)
-        self.prune_points(prune_mask)
+            drop = drop | (self.max_radii2D > max_screen_size) | (self._max_scale() > 0.1 * extent)
+        self.prune_points(drop)
 
     def densify(self, max_grad, min_opacity, extent, max_screen_size):
-        """gaussian_model.py:501-506"""
+        """gaussian_model.py:501-506: clone then split, as ONE row plan (the two passes' combined result)."""
         grads = self.xyz_gradient_accum / self.denom
         grads[grads.isnan()] = 0.0
-        self.densify_and_clone(grads, max_grad, extent)
-        self.densify_and_split(grads, max_grad, extent)
+        self._grow(self._clone_rows(grads, max_grad, extent), self._split_rows(grads, max_grad, extent))
 
     def reset_opacity(self):
         """gaussian_model.py:269-272"""
-        new = inverse_sigmoid(torch.min(self.get_opacity, torch.ones_like(self.get_opacity) * 0.01))
-        self._opacity = self.replace_tensor_to_optimizer(new, "opacity")["opacity"]
+        surgery.replace_param(self, "opacity",
+                              inverse_sigmoid(torch.min(self.get_opacity, torch.ones_like(self.get_opacity) * 0.01)))
 
     # ---- HexPlane regularisers (gaussian_model.py:538-566)
     def compute_regulation(self, time_smoothness_weight, l1_time_planes_weight, plane_tv_weight):

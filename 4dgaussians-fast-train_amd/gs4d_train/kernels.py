@@ -297,10 +297,15 @@ class _HexPointsAlias(torch.autograd.Function):
 
 
 def set_deterministic(flag=True):
-    """Kept for callers of the round-4 API: every kernel of the fused train step is now deterministic (the
-    HexPlane field's backward sums exact 64-bit fixed-point terms; the rasterizer reduces in fixed order),
-    so the step is bitwise reproducible whatever `flag` says."""
-    del flag
+    """The round-4 API for a bitwise-reproducible train step.  Every kernel of the fused step is deterministic by
+    default (the HexPlane field's backward sums exact 64-bit fixed-point terms, the rasterizer and the MLP's
+    f32-MFMA GEMMs reduce in a fixed order), and the GEMMs rocBLAS serves use its own shape-determined pick, so
+    two processes given the same inputs compute the same bits.  flag=True additionally switches off the opt-in
+    timing-based GEMM tuner (GS4D_GEMM_TUNE=1), whose choice can differ between processes; flag=False changes
+    nothing."""
+    if flag:
+        from . import deformation
+        deformation._TUNE = False
 
 
 def hexplane_points(xyz, t, aabb, alias=None):

@@ -90,6 +90,35 @@ typedef struct {
 int64_t gs4d_adam_chunks(int64_t n);
 int gs4d_adam_step(const gs4d_adam_batch *batch, void *stream);
 
+/* ---- Row surgery of densification and pruning: scene/gaussian_model.py:316-506 (prune_points,
+ * densification_postfix, densify_and_clone, densify_and_split, and the optimizer-state edits they make).
+ * One call rebuilds every per-Gaussian tensor (parameters, their Adam moments, statistics, the deformation
+ * table) by one ROW PLAN: output row r < K is old row keep[r]; the A appended rows K + j are, per tensor mode:
+ * GATHER -- old row append[j] for j < A - given_rows, then given[j - (A - given_rows)] (rows the caller
+ * computed, e.g. a split's children's positions); ZERO_NEW -- zero (the new rows' Adam moments).  ZERO makes
+ * every output row zero (the statistics the reference resets after densifying; src unused).  A copy is a copy:
+ * the result is bitwise the reference's cat / boolean-index sequence, in its row order.  Elements are 1 or 4
+ * bytes; rows are `width` elements, contiguous. */
+#define GS4D_ROWS_MAX_TENSORS 32
+enum { GS4D_ROWS_GATHER = 0, GS4D_ROWS_ZERO_NEW = 1, GS4D_ROWS_ZERO = 2 };
+typedef struct {
+    const void *src;    /* (P, width) old rows */
+    const void *given;  /* (given_rows, width): the last appended rows of a GATHER tensor */
+    void *dst;          /* (K + A, width) */
+    int64_t width;
+    int64_t given_rows; /* 0 <= given_rows <= A */
+    int esize;          /* 1 or 4 */
+    int mode;
+} gs4d_rows_tensor;
+typedef struct {
+    int count;
+    int64_t K, A;
+    const int32_t *keep;    /* K old row indices, in output order */
+    const int32_t *append;  /* old row indices of the gathered appended rows (A - given_rows of them per tensor) */
+    gs4d_rows_tensor t[GS4D_ROWS_MAX_TENSORS];
+} gs4d_rows_batch;
+int gs4d_rows_assemble(const gs4d_rows_batch *batch, void *stream);
+
 /* ---- HexPlane field: scene/hexplane.py:75-110 interpolate_ms_features (concat_features=True) over the
  * planes of init_grid_param (:50-72), each sampled with F.grid_sample(align_corners=True, bilinear,
  * padding_mode="border") (:22-48).  pts: (N, 4) normalised (x, y, z, t), 16-byte aligned.
@@ -240,6 +269,16 @@ int gs4d_mlp_dx_bf16(int P, int KW, int W, const uint16_t *da, const uint16_t *w
 size_t gs4d_mlp_dw_bf16_scratch_bytes(int P, int KW, int W);
 int gs4d_mlp_dw_bf16(int P, int KW, int W, const uint16_t *da, const uint16_t *hb, float *dw, void *scratch,
                      void *stream);
+/* The fp32 block's input gradient dh (P, W) = da (P, KW) @ W1 (KW, W) (the stacked first-layer weights as they
+ * lie: row-major, KW = k W), f32 MFMA with f32 products and sums in one fixed order: the same bits in every process
+ * (scene/deformation.py:73-78's heads, the input gradient autograd forms by one GEMM).  KW a multiple of 64, W in
+ * {64, 128}; rows 16-byte aligned. */
+int gs4d_mlp_dx_f32(int P, int KW, int W, const float *da, const float *w1, float *dh, void *stream);
+/* Its weight gradient dW1 (KW, W) = da^T h over the P rows (da (P, KW), h (P, W) row-major): per row chunk and
+ * 64-row block of dW1 an f32-MFMA block, its waves summed in a fixed order, the chunks summed in order (scratch:
+ * gs4d_mlp_dw_f32_scratch_bytes). */
+size_t gs4d_mlp_dw_f32_scratch_bytes(int P, int KW, int W);
+int gs4d_mlp_dw_f32(int P, int KW, int W, const float *da, const float *h, float *dw, void *scratch, void *stream);
 
 /* ---- The deformation field's first layer, backward, when feature_out is ONE Linear (defor_depth <= 1,
  * scene/deformation.py:51-55: hidden = x W^T + b) and every head begins with ReLU, so the heads read

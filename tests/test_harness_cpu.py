@@ -179,6 +179,89 @@ def test_densify_prune_keep_optimizer_state_aligned():
     assert float(st["exp_avg"].abs().sum()) == 0.0
 
 
+def _stepped_model(P=400, seed=0):
+    """A CPU model whose optimizer has state (one Adam step), with statistics set and a mixed deformation table."""
+    g, opt = _cpu_model(P=P, seed=seed)
+    g.training_setup(opt)
+    loss = sum((p ** 2).sum() for grp in g.optimizer.param_groups for p in grp["params"])
+    loss.backward()
+    g.optimizer.step()
+    gen = torch.Generator().manual_seed(seed + 1)
+    g.xyz_gradient_accum = torch.rand(P, 1, generator=gen) * 1e-3
+    g.denom = torch.ones(P, 1)
+    g.max_radii2D = torch.rand(P, generator=gen) * 10
+    g._deformation_accum = torch.rand(P, 3, generator=gen)
+    g._deformation_table = torch.rand(P, generator=gen) > 0.3
+    g.percent_dense = 0.05
+    return g
+
+
+def _rows(g):
+    names = {"xyz": "_xyz", "f_dc": "_features_dc", "f_rest": "_features_rest", "opacity": "_opacity",
+             "scaling": "_scaling", "rotation": "_rotation"}
+    out = {}
+    for n, a in names.items():
+        p = getattr(g, a)
+        st = g.optimizer.state[p]
+        out[n] = (p.detach().clone(), st["exp_avg"].clone(), st["exp_avg_sq"].clone(), st["step"])
+    return out
+
+
+def test_densify_rows_follow_reference_order():
+    """densify (gaussian_model.py:501-506 = clone :443-457 then split :415-441) as one row plan: checked element
+    by element against the row order the reference's two passes produce -- old rows not split (values and
+    moments kept), then clones (copies, zero moments), then the two children of each split row copy after
+    copy (copied attributes; scale log(s / 1.6); positions from the same normal draws); every statistic zero;
+    the table follows the rows; each optimizer state keeps its step."""
+    g = _stepped_model()
+    before = _rows(g)
+    P = before["xyz"][0].shape[0]
+    grads = g.xyz_gradient_accum / g.denom
+    smax = torch.exp(before["scaling"][0]).max(dim=1).values
+    hot = grads[:, 0] >= 5e-4
+    clone = torch.nonzero(hot & (smax <= 0.05)).flatten()
+    split = torch.nonzero(hot & (smax > 0.05)).flatten()
+    assert clone.numel() > 5 and split.numel() > 5
+    kept = torch.nonzero(~torch.isin(torch.arange(P), split)).flatten()
+    table0 = g._deformation_table.clone()
+    torch.manual_seed(9)
+    g.densify(5e-4, 0.005, 1.0, None)
+    torch.manual_seed(9)
+    s_split = torch.exp(before["scaling"][0][split]).repeat(2, 1)
+    draws = torch.normal(mean=torch.zeros((s_split.size(0), 3)), std=s_split)
+    K, C, S = kept.numel(), clone.numel(), split.numel()
+    after = _rows(g)
+    for n, (p0, m0, v0, step0) in before.items():
+        p1, m1, v1, step1 = after[n]
+        assert p1.shape[0] == K + C + 2 * S and step1 is step0
+        assert torch.equal(p1[:K], p0[kept]) and torch.equal(m1[:K], m0[kept]) and torch.equal(v1[:K], v0[kept])
+        assert torch.equal(p1[K:K + C], p0[clone])
+        assert not m1[K:].any() and not v1[K:].any()
+        if n not in ("xyz", "scaling"):
+            assert torch.equal(p1[K + C:], p0[split].repeat(2, *([1] * (p0.dim() - 1))))
+    sc = after["scaling"][0][K + C:]
+    assert torch.equal(sc, torch.log(s_split / (0.8 * 2)))
+    from gs4d_train.gaussians import build_rotation
+    rot = build_rotation(before["rotation"][0][split]).repeat(2, 1, 1)
+    xyz = torch.bmm(rot, draws.unsqueeze(-1)).squeeze(-1) + before["xyz"][0][split].repeat(2, 1)
+    assert torch.equal(after["xyz"][0][K + C:], xyz)
+    assert torch.equal(g._deformation_table, torch.cat([table0[kept], table0[clone], table0[split].repeat(2)]))
+    for name, shape in (("xyz_gradient_accum", (K + C + 2 * S, 1)), ("denom", (K + C + 2 * S, 1)),
+                        ("max_radii2D", (K + C + 2 * S,)), ("_deformation_accum", (K + C + 2 * S, 3))):
+        t = getattr(g, name)
+        assert t.shape == shape and not t.any(), name
+    # prune: surviving rows keep values, moments and statistics, in order
+    g.xyz_gradient_accum = torch.rand(K + C + 2 * S, 1)
+    acc0, before = g.xyz_gradient_accum.clone(), _rows(g)
+    live = (torch.sigmoid(before["opacity"][0]) >= 0.4).flatten()
+    g.prune(5e-4, 0.4, 1.0, None)
+    after = _rows(g)
+    for n, (p0, m0, v0, step0) in before.items():
+        p1, m1, v1, step1 = after[n]
+        assert torch.equal(p1, p0[live]) and torch.equal(m1, m0[live]) and torch.equal(v1, v0[live]) and step1 is step0
+    assert torch.equal(g.xyz_gradient_accum, acc0[live])
+
+
 def test_expon_lr_schedule():
     f = get_expon_lr_func(1.6e-4, 1.6e-6, lr_delay_mult=0.01, max_steps=20000)
     assert math.isclose(f(0), 1.6e-4)

@@ -5,6 +5,9 @@ statistics vs train.py:346-349 / gaussian_model.py:521-523, FusedAdam vs torch.o
 reference configures it, the fused HexPlane field vs scene/hexplane.py's F.grid_sample graph, and a
 whole train step fused vs unfused.  Tolerances are stated per test."""
 
+import copy
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -246,6 +249,57 @@ def test_hexplane_backward_nonfinite_and_scales():
         _, gm = _C.hexplane_backward(pts, planes, packed, dfeat * mag, order)
         for a, b in zip(ga, gm):
             torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-5 * a.abs().max().item())
+
+
+def test_row_surgery_hip_matches_torch_bitwise():
+    """Densify, prune and reset_opacity on the GPU: the one-launch row plans (gs4d_rows_assemble, fused=True)
+    against the same plans as torch index ops (fused=False) from the same state and RNG seed -- every
+    parameter, Adam moment, statistic and the deformation table bitwise equal, after a real train step made the
+    state (k-NN-initialised cloud, 20k Gaussians)."""
+    from gs4d_train import config, surgery
+    from gs4d_train.gaussians import GaussianModel
+    from gs4d_train.synthetic import make_point_cloud, make_training_views
+    from gs4d_train.train import train_step
+    hyper, opt = config.dynerf()
+    opt.iterations = 0
+    pts, cols = make_point_cloud(20000, seed=5)
+    views = make_training_views(1, 320, 240, seed=6)
+    bg = torch.ones(3, device="cuda")
+    torch.manual_seed(7)
+    g = GaussianModel(3, hyper, fused=True)
+    g.create_from_pcd(pts, cols, 1.0)
+    g.training_setup(opt)
+    g.active_sh_degree = 3
+    train_step(g, views, opt, hyper, 3001, bg)
+    gen = torch.Generator(device="cuda").manual_seed(3)
+    P = g._xyz.shape[0]
+    g.xyz_gradient_accum = torch.rand(P, 1, device="cuda", generator=gen) * 4e-4
+    g.denom = torch.ones(P, 1, device="cuda")
+    g._deformation_table = torch.rand(P, device="cuda", generator=gen) > 0.2
+
+    def state(m):
+        out = [m._deformation_table.clone()] + [getattr(m, n).clone() for n in surgery.STATS]
+        for name, attr in surgery.PARAMS.items():
+            p = getattr(m, attr)
+            st = m.optimizer.state[p]
+            out += [p.detach().clone(), st["exp_avg"].clone(), st["exp_avg_sq"].clone()]
+        return out
+
+    runs = []
+    for fused in (True, False):
+        m = copy.deepcopy(g)
+        m.fused = fused
+        torch.manual_seed(11)
+        m.densify(2e-4, 0.005, 0.5, None)
+        grown = state(m)
+        m.prune(2e-4, 0.12, 0.5, 20)
+        pruned = state(m)
+        m.reset_opacity()
+        runs.append((grown, pruned, state(m), m._xyz.shape[0]))
+    (a1, a2, a3, na), (b1, b2, b3, nb) = runs
+    assert na == nb and na != P
+    for x, y in zip(a1 + a2 + a3, b1 + b2 + b3):
+        assert x.dtype == y.dtype and torch.equal(x, y)
 
 
 def test_train_step_deterministic():
@@ -671,6 +725,65 @@ def test_mlp_dw_bf16_matches_fp64(P, KW):
     ref = da.double().t() @ hb.double()
     scale = da.double().abs().t() @ hb.double().abs()
     assert float(((dw.double() - ref).abs() - 1e-5 * scale).max().clamp_min(0)) == 0.0
+
+
+@pytest.mark.parametrize("P,KW,W", [(100_000, 640, 128), (100_003, 640, 128), (1, 640, 128), (0, 640, 128),
+                                     (2000, 192, 64), (777, 64, 128), (300, 1024, 64), (65, 128, 128)])
+def test_mlp_f32_gemms_match_fp64(P, KW, W):
+    """gs4d_mlp_dx_f32 (dh = da W1) and gs4d_mlp_dw_f32 (dW1 = da^T h), the fp32 heads block's two large GEMMs on
+    the f32 MFMA, vs fp64 torch: every element to 1e-5 of its |terms| sum (f32 products are exact in f64; the
+    bar covers fp32 accumulation over up to 1e5 terms).  Ragged P (partial 64-row groups, a partial last chunk
+    and 8-row step: rows past P read row P - 1 and are zeroed / not stored), P = 1 and 0 (dW1 all zeros), one
+    k chunk and sixteen, W 64 and 128.  A second call gives the same bits."""
+    from gs4d_train import _C
+    torch.manual_seed(P + KW + W)
+    da = torch.randn(P, KW, device="cuda")
+    h = torch.relu(torch.randn(P, W, device="cuda"))
+    w1 = torch.randn(KW, W, device="cuda") / KW ** 0.5
+    dh = _C.mlp_dx_f32(da, w1)
+    dw = _C.mlp_dw_f32(da, h)
+    assert dh.shape == (P, W) and dw.shape == (KW, W) and dh.dtype == dw.dtype == torch.float32
+    refw = da.double().t() @ h.double()
+    scw = da.double().abs().t() @ h.double().abs()
+    assert float(((dw.double() - refw).abs() - 1e-5 * scw).max().clamp_min(0)) == 0.0
+    if P == 0:
+        assert bool((dw == 0).all())
+        return
+    refx = da.double() @ w1.double()
+    scx = da.double().abs() @ w1.double().abs()
+    assert float(((dh.double() - refx).abs() - 1e-5 * scx).max().clamp_min(0)) == 0.0
+    assert torch.equal(_C.mlp_dx_f32(da, w1), dh) and torch.equal(_C.mlp_dw_f32(da, h), dw)
+    with pytest.raises(RuntimeError):  # a W the kernels are not built for is refused, not run
+        _C.mlp_dx_f32(da[:, :KW], torch.randn(KW, 96, device="cuda"))
+
+
+_CROSS_PROCESS = r"""
+import hashlib, sys, torch
+sys.path.insert(0, sys.argv[1])
+from gs4d_train import _C
+torch.manual_seed(5)
+P, KW, W = 100_003, 640, 128
+da = torch.randn(P, KW, device="cuda")
+h = torch.relu(torch.randn(P, W, device="cuda"))
+w1 = torch.randn(KW, W, device="cuda") / KW ** 0.5
+out = [_C.mlp_dx_f32(da, w1), _C.mlp_dw_f32(da, h)]
+torch.cuda.synchronize()
+print(hashlib.sha256(b"".join(t.cpu().numpy().tobytes() for t in out)).hexdigest())
+"""
+
+
+def test_mlp_f32_gemms_bitwise_across_processes():
+    """The fp32 heads-block GEMMs give the same bits in two separate processes (the round-5 rocBLAS kernels were
+    chosen per process by timing, and differently rounded kernels broke the fused-vs-unfused training pair)."""
+    import subprocess
+    import sys
+    pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "4dgaussians-fast-train_amd")
+    digests = []
+    for _ in range(2):
+        r = subprocess.run([sys.executable, "-c", _CROSS_PROCESS, pkg], capture_output=True, text=True, timeout=100)
+        assert r.returncode == 0, r.stderr[-2000:]
+        digests.append(r.stdout.strip().splitlines()[-1])
+    assert digests[0] == digests[1] and len(digests[0]) == 64, digests
 
 
 @pytest.mark.parametrize("P,N,K", [(100_003, 640, 128), (2048, 640, 128), (5000, 192, 64), (700, 640, 128)])
