@@ -548,7 +548,7 @@ std::vector<torch::Tensor> heads_forward(const torch::Tensor &a, const std::vect
     return out;
 }
 
-// ---- heads block forward, both layers: (a, [out_i]) for h (P, W), W1 (kW, W), b1 (kW), W2_i (n_i, W), b2_i (n_i)
+// ---- heads block forward, both layers: (a, W1^T, [out_i]) for h (P, W), W1 (kW, W), b1 (kW), W2_i (n_i, W), b2_i (n_i)
 std::vector<torch::Tensor> heads_block_forward(const torch::Tensor &h, const torch::Tensor &w1, const torch::Tensor &b1,
                                                const std::vector<torch::Tensor> &w2s,
                                                const std::vector<torch::Tensor> &b2s) {
@@ -565,8 +565,10 @@ std::vector<torch::Tensor> heads_block_forward(const torch::Tensor &h, const tor
     // whole 16-row blocks are stored (the ABI's padding rows); the caller sees the first P rows
     auto a_pad = torch::empty({(h.size(0) + 15) / 16 * 16, w1.size(0)}, h.options());
     auto a = a_pad.narrow(0, 0, h.size(0));
+    auto w1t = torch::empty({w1.size(1), w1.size(0)}, h.options());  // W1^T (W, kW), for the input gradient
     b.h = h.data_ptr<float>(), b.w1 = w1.data_ptr<float>(), b.b1 = b1.data_ptr<float>(), b.a = a_pad.data_ptr<float>();
-    std::vector<torch::Tensor> out{a}, keep;
+    b.w1t = w1t.data_ptr<float>();
+    std::vector<torch::Tensor> out{a, w1t}, keep;
     for (int i = 0; i < k; i++) {
         auto w2 = w2s[i].contiguous();
         auto b2 = b2s[i].contiguous();
@@ -735,14 +737,14 @@ std::vector<torch::Tensor> rows_assemble(const std::vector<torch::Tensor> &srcs,
     return out;
 }
 
-// ---- the fp32 block's input gradient: dh (P, W) = da (P, KW) @ W1 (KW, W), f32 MFMA, fixed order
-torch::Tensor mlp_dx_f32(const torch::Tensor &da, const torch::Tensor &w1) {
+// ---- the fp32 block's input gradient: dh (P, W) = da (P, KW) @ W1 from W1^T (W, KW), f32 MFMA, fixed order
+torch::Tensor mlp_dx_f32(const torch::Tensor &da, const torch::Tensor &w1t) {
     gpu_f32(da, "mlp_dx_f32: da");
-    gpu_f32(w1, "mlp_dx_f32: W1");
-    need(da.dim() == 2 && w1.dim() == 2 && w1.size(0) == da.size(1), "mlp_dx_f32: da (P, KW), W1 (KW, W)");
+    gpu_f32(w1t, "mlp_dx_f32: W1^T");
+    need(da.dim() == 2 && w1t.dim() == 2 && w1t.size(1) == da.size(1), "mlp_dx_f32: da (P, KW), W1^T (W, KW)");
     c10::hip::HIPGuard guard(da.device().index());
-    auto dh = torch::empty({da.size(0), w1.size(1)}, da.options());
-    check(gs4d_mlp_dx_f32((int)da.size(0), (int)da.size(1), (int)w1.size(1), da.data_ptr<float>(), w1.data_ptr<float>(),
+    auto dh = torch::empty({da.size(0), w1t.size(0)}, da.options());
+    check(gs4d_mlp_dx_f32((int)da.size(0), (int)da.size(1), (int)w1t.size(0), da.data_ptr<float>(), w1t.data_ptr<float>(),
                           dh.data_ptr<float>(), (void *)stream_of(da)),
           "mlp_dx_f32");
     return dh;

@@ -81,6 +81,7 @@ __device__ __forceinline__ bool publish_and_total(double t, TicketScratch ts, in
     // the slots in rounds of kRound per thread, all loads of a round in flight at once (then the rare waits)
     constexpr int kRound = 8;
     double s = 0.0;
+    bool lost = false;  // a slot still 0 after the bounded wait
     for (int i0 = 0; i0 < nblk; i0 += kRound * kTailThreads) {
         unsigned long long v[kRound];
 #pragma unroll
@@ -93,18 +94,25 @@ __device__ __forceinline__ bool publish_and_total(double t, TicketScratch ts, in
             const int i = i0 + k * kTailThreads + (int)threadIdx.x;
             for (uint32_t spins = 0; v[k] == 0ull && spins < (1u << 22); spins++)
                 v[k] = __hip_atomic_load(slot + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            lost |= v[k] == 0ull;
             if (i < nblk) __hip_atomic_store(slot + i, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (i < nblk) s += __longlong_as_double((long long)(v[k] - 1ull));
+            if (i < nblk && v[k] != 0ull) s += __longlong_as_double((long long)(v[k] - 1ull));
         }
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
     if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = s;
-    __syncthreads();
+    // A slot that never arrived (the wait gave up: never seen, but possible in principle) leaves its late store
+    // behind in the kept scratch, which would corrupt a later call's total silently.  Instead the scratch is
+    // poisoned (word 1 of the top counter's line, sticky): this total and every later one with this scratch
+    // are NaN, until the caller zeroes the scratch again.
+    const bool any_lost = __syncthreads_or(lost);
+    if (any_lost && threadIdx.x == 0) __hip_atomic_store(ts.ticket + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool poisoned = any_lost || __hip_atomic_load(ts.ticket + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
     double sum = 0.0;
 #pragma unroll
     for (int w = 0; w < kTailThreads / 64; w++) sum += s_w[w];
-    *total = sum;
+    *total = poisoned ? __builtin_nan("") : sum;
     if (threadIdx.x == 0) __hip_atomic_store(ts.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return true;
 }
@@ -1535,8 +1543,9 @@ __global__ __launch_bounds__(kHfThreads) void heads_fwd_kernel(HfArgs A, const f
 // (features along the MFMA rows, the 16 points along its columns), so the first layer's accumulators are
 // already the second layer's B operand: in k-step (t, v) lane l supplies feature 16 t + 4 (l >> 4) + v of
 // point l & 15 -- the v-th register of its t-th accumulator (D[4 (l >> 4) + v][l & 15]) -- and the A operand
-// (w1 / w2 rows from LDS, one 16-byte read per 4 MFMAs) uses the same feature order; 16 waves per
-// workgroup, one workgroup per CU.  h is read as that
+// (w1 / w2 rows from LDS, one 16-byte read per 4 MFMAs; row stride W + 8 floats, conflict-free for ds_read_b128's
+// four 16-lane groups -- round 5's W + 4 put two lanes of a group on one bank slot: 9.4M conflict cycles per
+// launch) uses the same feature order; 16 waves per workgroup, one workgroup per CU.  h is read as that
 // B operand directly (one float4 per lane per 16 features); a = relu(z + b1) is written once, for the
 // backward, and never read back.
 constexpr int kHbfThreads = 512;
@@ -1544,8 +1553,9 @@ template <int W>
 __global__ __launch_bounds__(kHbfThreads) void heads_block_fwd_kernel(HfArgs A, const float *__restrict__ h,
                                                                       const float *__restrict__ w1,
                                                                       const float *__restrict__ b1,
-                                                                      float *__restrict__ a) {
-    constexpr int NT = W / 16, WS = W + 4, NW = kHbfThreads / 64;
+                                                                      float *__restrict__ a,
+                                                                      float *__restrict__ w1t) {
+    constexpr int NT = W / 16, WS = W + 8, NW = kHbfThreads / 64;
     extern __shared__ float4 s_v[];
     float *s_w1 = reinterpret_cast<float *>(s_v);  // W rows x WS
     float *s_b1 = s_w1 + W * WS;                   // W
@@ -1567,6 +1577,16 @@ __global__ __launch_bounds__(kHbfThreads) void heads_block_fwd_kernel(HfArgs A, 
     }
     for (int e = threadIdx.x; e < npad; e += kHbfThreads) s_b2[e] = e < n ? A.b2[head][e] : 0.f;
     __syncthreads();
+    if (w1t && blockIdx.x == 0) {
+        // workgroup 0 of each head also writes W1_i^T for the backward's input gradient (gs4d_mlp_dx_f32): 4 rows
+        // of one column of the LDS image per 16-byte store
+        for (int e = threadIdx.x; e < W * W / 4; e += kHbfThreads) {
+            const int col = e / (W / 4), r4 = e % (W / 4);
+            *reinterpret_cast<float4 *>(w1t + (size_t)col * A.kW + head * W + 4 * r4) =
+                make_float4(s_w1[(4 * r4) * WS + col], s_w1[(4 * r4 + 1) * WS + col], s_w1[(4 * r4 + 2) * WS + col],
+                            s_w1[(4 * r4 + 3) * WS + col]);
+        }
+    }
     const int lane = threadIdx.x & 63, wv = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6), q = lane >> 4, c = lane & 15;
     const int nblk = (A.P + 15) / 16;
     const int stride = gridDim.x * NW;
@@ -1992,18 +2012,24 @@ __global__ __launch_bounds__(kDwbThreads) void mlp_dw_bf16_kernel(int P, int KW,
 // GEMM this replaces was picked per process by timing).  Computed transposed as mlp_dx_bf16_kernel does:
 // dh^T = W1^T da^T.  In the 16-wide k slice kk, lane (q = l >> 4, c = l & 15) supplies k = 16 kk + 4 q + s in
 // MFMA step s, so one float4 load of da row c gives the lane's 4 steps of the B operand, and the A operand
-// W1^T[16 m + c][16 kk + 4 q .. + 3] is one 16-byte LDS read (row stride 68 floats: conflict-free).
+// W1^T[16 m + c][16 kk + 4 q .. + 3] is one 16-byte LDS read.  The operand is W1^T (W x KW, written by the heads
+// block forward): its k-runs are staged with coalesced 16-byte loads and 16-byte LDS stores, row stride KC + 8
+// floats, which is conflict-free for both (ds_read_b128's four 16-lane groups; 8-lane store groups).  (Round 6
+// first staged W1 itself, transposing with scalar stores at stride KC + 4: 2-way conflicts on every read, 38M
+// conflict cycles per launch, 63 % MFMA busy.)
 // A workgroup is 4 waves on ONE 64-feature group of dh (4 m tiles) and 64 rows (16 per wave): small units of
-// work (3136 workgroups at P = 100k, W = 128) keep the per-CU share even.  W1's 64 x 64 block of the group is
-// staged per 64-wide k chunk, transposed as it is stored, double-buffered (34 KiB per workgroup); da is
-// prefetched a chunk ahead.  Workgroups b and b + 8 (same XCD) take the two feature groups of the same rows,
-// so the second read of those da rows is an L2 hit.
-constexpr int kDxfThreads = 256, kDxfChunk = 64, kDxfStride = kDxfChunk + 4;  // floats
-template <int W>
+// work (3136 workgroups at P = 100k, W = 128) keep the per-CU share even.  The group's 64 x KC block of W1^T is
+// staged per k chunk, double-buffered; da is prefetched a chunk ahead.  Workgroups b and b + 8 (same XCD) take the
+// two feature groups of the same rows, so the second read of those da rows is an L2 hit.
+// KC: the k chunk, 64, or 32 when KW / 64 is odd (the loop runs chunks in pairs: an even count keeps both halves
+// unconditional, so the compiler cannot sink the second half's loads into a branch).
+constexpr int kDxfThreads = 256;
+template <int W, int KC>
 __global__ __launch_bounds__(kDxfThreads) void mlp_dx_f32_kernel(int P, int KW, int nrg, const float *__restrict__ da,
-                                                                 const float *__restrict__ w1, float *__restrict__ dh) {
+                                                                 const float *__restrict__ w1t, float *__restrict__ dh) {
     constexpr int NG = W / 64;  // feature groups
-    __shared__ __attribute__((aligned(16))) float s_a[2][64 * kDxfStride];
+    constexpr int S = KC + 8, KK = KC / 16, NP = KC / 16, Q = KC / 4;  // NP: staging float4 per thread; Q per row
+    __shared__ __attribute__((aligned(16))) float s_a[2][64 * S];
     int rg = blockIdx.x, fg = 0;
     if (NG == 2) {
         const int i = blockIdx.x & 15;
@@ -2019,57 +2045,58 @@ __global__ __launch_bounds__(kDxfThreads) void mlp_dx_f32_kernel(int P, int KW, 
     f4v acc[4];
 #pragma unroll
     for (int m = 0; m < 4; m++) acc[m] = f4v{0.f, 0.f, 0.f, 0.f};
-    const int nch = KW / kDxfChunk;
-    // staging: piece e = t + 256 i is W1 row (64 ch + e / 16), features 64 fg + 4 (e % 16) .. + 3 (coalesced
-    // 256-byte row segments), stored to the LDS image's rows 4 (e % 16) .. + 3 at column e / 16
-    float4 ga[4];
+    const int nch = KW / KC;
+    // staging: piece e = t + 256 i is W1^T row 64 fg + e / Q (a feature), k 4 (e % Q) .. + 3 of the chunk
+    float4 ga[NP];
     auto load_a = [&](int ch) {
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
+        for (int i = 0; i < NP; i++) {
             const int e = (int)threadIdx.x + kDxfThreads * i;
-            ga[i] = *reinterpret_cast<const float4 *>(w1 + (size_t)(ch * kDxfChunk + (e >> 4)) * W + 64 * fg + 4 * (e & 15));
+            ga[i] = *reinterpret_cast<const float4 *>(w1t + (size_t)(64 * fg + e / Q) * KW + ch * KC + 4 * (e % Q));
         }
     };
     auto store_a = [&](int buf) {
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
+        for (int i = 0; i < NP; i++) {
             const int e = (int)threadIdx.x + kDxfThreads * i;
-            float *d = &s_a[buf][4 * (e & 15) * kDxfStride + (e >> 4)];
-            d[0] = ga[i].x;
-            d[kDxfStride] = ga[i].y;
-            d[2 * kDxfStride] = ga[i].z;
-            d[3 * kDxfStride] = ga[i].w;
+            *reinterpret_cast<float4 *>(&s_a[buf][(e / Q) * S + 4 * (e % Q)]) = ga[i];
         }
     };
-    float4 bn[4];
-    auto load_b = [&](int ch) {
+    auto load_b = [&](int ch, float4 (&b)[KK]) {
 #pragma unroll
-        for (int kk = 0; kk < 4; kk++) bn[kk] = *reinterpret_cast<const float4 *>(brow + ch * kDxfChunk + 16 * kk);
+        for (int kk = 0; kk < KK; kk++) b[kk] = *reinterpret_cast<const float4 *>(brow + ch * KC + 16 * kk);
     };
-    load_a(0);
-    load_b(0);
-    store_a(0);
-    __syncthreads();
-    for (int ch = 0; ch < nch; ch++) {
-        float4 b[4];
-#pragma unroll
-        for (int kk = 0; kk < 4; kk++) b[kk] = bn[kk];
+    // one chunk: the next chunk's loads first (into the other register set: no copies, whose waits the compiler
+    // placed mid-chunk), then this chunk's MFMAs, then the next chunk's W1^T block into the other LDS buffer
+    auto step = [&](int ch, const float4 (&b)[KK], float4 (&bnext)[KK]) {
         const int nx = min(ch + 1, nch - 1);  // the last chunk re-loads itself: loads stay unconditional
         load_a(nx);
-        load_b(nx);
+        load_b(nx, bnext);
+        __builtin_amdgcn_sched_barrier(0);  // left to itself the scheduler sank the loads below the MFMAs
         const float *sa = s_a[ch & 1];
 #pragma unroll
-        for (int kk = 0; kk < 4; kk++)
+        for (int kk = 0; kk < KK; kk++)
 #pragma unroll
             for (int m = 0; m < 4; m++) {
-                const float4 av = *reinterpret_cast<const float4 *>(sa + (16 * m + c) * kDxfStride + 16 * kk + 4 * q);
+                const float4 av = *reinterpret_cast<const float4 *>(sa + (16 * m + c) * S + 16 * kk + 4 * q);
                 acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, b[kk].x, acc[m], 0, 0, 0);
                 acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, b[kk].y, acc[m], 0, 0, 0);
                 acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, b[kk].z, acc[m], 0, 0, 0);
                 acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, b[kk].w, acc[m], 0, 0, 0);
             }
-        if (ch + 1 < nch) store_a((ch + 1) & 1);  // the other buffer: read by nobody since the last barrier
+        // the other buffer: read by nobody since the last barrier (after the last chunk, by nobody at all; the
+        // store is unconditional so that the loads feeding it stay where they are issued)
+        store_a((ch + 1) & 1);
         __syncthreads();
+    };
+    float4 b0[KK], b1[KK];
+    load_a(0);
+    load_b(0, b0);
+    store_a(0);
+    __syncthreads();
+    for (int ch = 0; ch < nch; ch += 2) {  // nch is even (KC)
+        step(ch, b0, b1);
+        step(ch + 1, b1, b0);
     }
     // D[feature 16 m + 4 q + r][row c]
     if (row < P)
@@ -2080,21 +2107,26 @@ __global__ __launch_bounds__(kDxfThreads) void mlp_dx_f32_kernel(int P, int KW, 
 }
 
 // ---- the fp32 heads block's first-layer weight gradient: dW1 (KW x W) = da^T h reduced over the P rows, on
-// v_mfma_f32_16x16x4_f32 with K = rows.  In the MFMA k-step over rows r .. r + 3, lane (q, c) supplies
-// A[feature c][row q] = da[r + q][64 mb + 16 mt + c] and B[row q][feature c] = h[r + q][16 nt + c], each one
-// dword load (16 lanes read 64 contiguous bytes of a row).  Workgroup (row chunk s, 64-row block mb of dW1): its
-// 4 waves take interleaved 8-row steps of the chunk (two MFMA k-steps, 24 loads in flight a step ahead of the
-// MFMAs), each accumulating the whole 64 x W block (W = 128: 32 tiles, 128 accumulator registers), and are
-// summed in LDS in the fixed order (w0 + w2) + (w1 + w3) into parts[s]; gs4d_sum_slices then adds the chunks
-// in order.  Deterministic by construction.  The m blocks of one chunk sit on one XCD (they share its h rows).
-constexpr int kDwfThreads = 256, kDwfStepRows = 8;
+// v_mfma_f32_16x16x4_f32 with K = rows.  Workgroup (row chunk s, 64-row block mb of dW1): 4 waves, wave w owning
+// the 64 x (W / 4) block of columns w W/4 ..; the chunk's rows pass through LDS in 16-row stages (da's 64 columns
+// and h's W columns of each row, coalesced 16-byte loads and stores, double-buffered, the next stage's loads
+// issued ahead of this stage's MFMAs).  In the MFMA k-step over stage rows r .. r + 3, lane (q, c) reads
+// A[feature c][row q] = da[r + q][64 mb + 16 mt + c] and B[row q][feature c] = h[r + q][16 nt + c] as single
+// dwords (row strides of 80 and W + 16 floats: the two rows a 32-lane half reads fall on opposite bank halves,
+// conflict-free).  Rows past P are staged as zeros.  Each wave writes its block of parts[s]; gs4d_sum_slices adds
+// the chunks in order.  Deterministic by construction.  The m blocks of one chunk sit on one XCD (they share its
+// h rows).  (Round 6 first read both operands straight from HBM as dwords at 2 waves/SIMD: 50 % MFMA busy.)
+constexpr int kDwfThreads = 256, kDwfStage = 16;
 template <int W>
-__global__ __launch_bounds__(kDwfThreads, 2) void mlp_dw_f32_kernel(int P, int KW, int S, int chunk_rows,
-                                                                    const float *__restrict__ da,
-                                                                    const float *__restrict__ h,
-                                                                    float *__restrict__ parts) {
-    constexpr int NT = W / 16, MT = 4, NACC = MT * NT * 4;  // accumulator floats per lane
-    __shared__ __attribute__((aligned(16))) float s_red[2][NACC * 64];
+__global__ __launch_bounds__(kDwfThreads) void mlp_dw_f32_kernel(int P, int KW, int S, int chunk_rows,
+                                                                 const float *__restrict__ da,
+                                                                 const float *__restrict__ h,
+                                                                 float *__restrict__ parts) {
+    constexpr int NTW = W / 64, MT = 4;  // n tiles per wave, m tiles
+    constexpr int SD = 64 + 16, SH = W + 16;
+    constexpr int PD = kDwfStage * 16 / kDwfThreads, PH = kDwfStage * (W / 4) / kDwfThreads;  // float4 per thread
+    __shared__ __attribute__((aligned(16))) float s_d[2][kDwfStage * SD];
+    __shared__ __attribute__((aligned(16))) float s_h[2][kDwfStage * SH];
     const int nmb = KW / 64;
     // b = 8 (nmb j + mb) + x: chunk s = 8 j + x, so the nmb blocks of a chunk share b % 8 (the XCD)
     const int b = blockIdx.x, x = b & 7, jm = b >> 3, mb = jm % nmb, s = 8 * (jm / nmb) + x;
@@ -2102,87 +2134,81 @@ __global__ __launch_bounds__(kDwfThreads, 2) void mlp_dw_f32_kernel(int P, int K
     const int lane = threadIdx.x & 63, wv = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6), q = lane >> 4,
               c = lane & 15;
     const int64_t r0 = (int64_t)s * chunk_rows, r1 = min((int64_t)P, r0 + chunk_rows);
-    f4v acc[MT][NT];
+    f4v acc[MT][NTW];
 #pragma unroll
     for (int mt = 0; mt < MT; mt++)
 #pragma unroll
-        for (int nt = 0; nt < NT; nt++) acc[mt][nt] = f4v{0.f, 0.f, 0.f, 0.f};
-    // step t of wave w: rows r0 + 32 t + 8 w .. + 7 (the workgroup reads 32 consecutive rows per step)
-    const int nst = (int)((r1 - r0 + 31) / 32);
-    float an[2][MT], hn[2][NT];
-    auto load = [&](int t) {
+        for (int nt = 0; nt < NTW; nt++) acc[mt][nt] = f4v{0.f, 0.f, 0.f, 0.f};
+    // staging: da piece e: stage row e / 16, float4 e % 16; h piece e: stage row e / (W / 4), float4 e % (W / 4)
+    float4 gd[PD], gh[PH];
+    auto load = [&](int st) {  // rows past r1 read row r1 - 1 (zeroed at the store)
 #pragma unroll
-        for (int u = 0; u < 2; u++) {
-            const int64_t r = r0 + 32 * (int64_t)t + 8 * wv + 4 * u + q;
-            const bool ok = r < r1;
-            const int64_t rc = ok ? r : r1 - 1;
-            const float *pa = da + (size_t)rc * KW + 64 * mb + c;
-            const float *ph = h + (size_t)rc * W + c;
+        for (int i = 0; i < PD; i++) {
+            const int e = (int)threadIdx.x + kDwfThreads * i;
+            const int64_t r = min(r0 + (int64_t)kDwfStage * st + e / 16, r1 - 1);
+            gd[i] = *reinterpret_cast<const float4 *>(da + (size_t)r * KW + 64 * mb + 4 * (e % 16));
+        }
 #pragma unroll
-            for (int mt = 0; mt < MT; mt++) {
-                const float v = pa[16 * mt];
-                an[u][mt] = ok ? v : 0.f;
-            }
-#pragma unroll
-            for (int nt = 0; nt < NT; nt++) {
-                const float v = ph[16 * nt];
-                hn[u][nt] = ok ? v : 0.f;
-            }
+        for (int i = 0; i < PH; i++) {
+            const int e = (int)threadIdx.x + kDwfThreads * i;
+            const int64_t r = min(r0 + (int64_t)kDwfStage * st + e / (W / 4), r1 - 1);
+            gh[i] = *reinterpret_cast<const float4 *>(h + (size_t)r * W + 4 * (e % (W / 4)));
         }
     };
-    if (nst > 0) load(0);
-    for (int t = 0; t < nst; t++) {
-        float av[2][MT], hv[2][NT];
+    auto store = [&](int st, int buf) {
+        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-        for (int u = 0; u < 2; u++) {
-#pragma unroll
-            for (int mt = 0; mt < MT; mt++) av[u][mt] = an[u][mt];
-#pragma unroll
-            for (int nt = 0; nt < NT; nt++) hv[u][nt] = hn[u][nt];
+        for (int i = 0; i < PD; i++) {
+            const int e = (int)threadIdx.x + kDwfThreads * i;
+            const bool ok = r0 + (int64_t)kDwfStage * st + e / 16 < r1;
+            *reinterpret_cast<float4 *>(&s_d[buf][(e / 16) * SD + 4 * (e % 16)]) = ok ? gd[i] : z;
         }
-        load(min(t + 1, nst - 1));  // the last step re-loads itself: loads stay unconditional
 #pragma unroll
-        for (int u = 0; u < 2; u++)
+        for (int i = 0; i < PH; i++) {
+            const int e = (int)threadIdx.x + kDwfThreads * i;
+            const bool ok = r0 + (int64_t)kDwfStage * st + e / (W / 4) < r1;
+            *reinterpret_cast<float4 *>(&s_h[buf][(e / (W / 4)) * SH + 4 * (e % (W / 4))]) = ok ? gh[i] : z;
+        }
+    };
+    // one stage: the next stage's loads first, then this stage's MFMAs from LDS, then the next stage into the other
+    // buffer (unconditional, as in mlp_dx_f32_kernel: stages run in pairs, so both halves are straight-line)
+    const int nst = (int)((r1 - r0 + 2 * kDwfStage - 1) / (2 * kDwfStage)) * 2;
+    auto step = [&](int st) {
+        load(min(st + 1, nst - 1));
+        __builtin_amdgcn_sched_barrier(0);
+        const float *sd = s_d[st & 1], *sh = s_h[st & 1];
+#pragma unroll
+        for (int u = 0; u < kDwfStage / 4; u++) {
+            float av[MT], hv[NTW];
+#pragma unroll
+            for (int mt = 0; mt < MT; mt++) av[mt] = sd[(4 * u + q) * SD + 16 * mt + c];
+#pragma unroll
+            for (int nt = 0; nt < NTW; nt++) hv[nt] = sh[(4 * u + q) * SH + 16 * (NTW * wv + nt) + c];
 #pragma unroll
             for (int mt = 0; mt < MT; mt++)
 #pragma unroll
-                for (int nt = 0; nt < NT; nt++)
-                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u][mt], hv[u][nt], acc[mt][nt], 0, 0, 0);
-    }
-    // (w0 + w2) + (w1 + w3), lane-major LDS image (conflict-free): float i of lane l at i * 64 + l
-    auto put = [&](float *dst) {
-#pragma unroll
-        for (int mt = 0; mt < MT; mt++)
-#pragma unroll
-            for (int nt = 0; nt < NT; nt++)
-#pragma unroll
-                for (int r = 0; r < 4; r++) dst[((mt * NT + nt) * 4 + r) * 64 + lane] = acc[mt][nt][r];
+                for (int nt = 0; nt < NTW; nt++)
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[mt], hv[nt], acc[mt][nt], 0, 0, 0);
+        }
+        store(st + 1, (st + 1) & 1);  // past the last stage: a padding stage, zeros, read by nobody
+        __syncthreads();
     };
-    auto add = [&](const float *src) {
-#pragma unroll
-        for (int mt = 0; mt < MT; mt++)
-#pragma unroll
-            for (int nt = 0; nt < NT; nt++)
-#pragma unroll
-                for (int r = 0; r < 4; r++) acc[mt][nt][r] += src[((mt * NT + nt) * 4 + r) * 64 + lane];
-    };
-    if (wv >= 2) put(s_red[wv - 2]);
+    load(0);
+    store(0, 0);
     __syncthreads();
-    if (wv < 2) add(s_red[wv]);
-    __syncthreads();
-    if (wv == 1) put(s_red[0]);
-    __syncthreads();
-    if (wv == 0) {
-        add(s_red[0]);
-        // D[feature 16 mt + 4 q + r][feature 16 nt + c] of rows 64 mb .. of dW1
-        float *o = parts + (size_t)s * KW * W + (size_t)64 * mb * W;
-#pragma unroll
-        for (int mt = 0; mt < MT; mt++)
-#pragma unroll
-            for (int nt = 0; nt < NT; nt++)
-#pragma unroll
-                for (int r = 0; r < 4; r++) o[(size_t)(16 * mt + 4 * q + r) * W + 16 * nt + c] = acc[mt][nt][r];
+    for (int st = 0; st < nst; st += 2) {
+        step(st);
+        step(st + 1);
     }
+    // D[feature 16 mt + 4 q + r][column 16 (NTW wv + nt) + c] of rows 64 mb .. of dW1
+    float *o = parts + (size_t)s * KW * W + (size_t)64 * mb * W;
+#pragma unroll
+    for (int mt = 0; mt < MT; mt++)
+#pragma unroll
+        for (int nt = 0; nt < NTW; nt++)
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+                o[(size_t)(16 * mt + 4 * q + r) * W + 16 * (NTW * wv + nt) + c] = acc[mt][nt][r];
 }
 
 // ---- the wide head's second-layer backward on the bf16 path (n = 48, W = 128): heads_bwd_wide_mfma_kernel's
@@ -2995,8 +3021,8 @@ int gs4d_heads_block_forward(const gs4d_heads_block_fwd *args, void *stream) {
     }
     if (((size_t)b.w1 & 15) != 0 || ((size_t)b.b1 & 15) != 0) return 1;
     if (b.P == 0) return 0;
-    if (!b.h || !b.a || (((size_t)b.h | (size_t)b.a) & 15) != 0) return 1;
-    const size_t lds = 4 * ((size_t)(b.W + npad_max) * (b.W + 4) + b.W + npad_max);
+    if (!b.h || !b.a || (((size_t)b.h | (size_t)b.a | (size_t)b.w1t) & 15) != 0) return 1;
+    const size_t lds = 4 * ((size_t)(b.W + npad_max) * (b.W + 8) + b.W + npad_max);
     const int nblk = (b.P + 15) / 16;
     // ~1024 workgroups over the heads, one resident per CU (LDS): each stages its head's weights once and
     // takes a few blocks per wave (measured at P = 100k, k = 5: 237 / 218 / 207 us for 256 / 512 / 1024)
@@ -3009,10 +3035,10 @@ int gs4d_heads_block_forward(const gs4d_heads_block_fwd *args, void *stream) {
         return kErrLds;
     if (b.W == 128)
         hipLaunchKernelGGL(heads_block_fwd_kernel<128>, dim3(per_head, b.k), dim3(kHbfThreads), lds, s, A, b.h, b.w1,
-                           b.b1, b.a);
+                           b.b1, b.a, b.w1t);
     else
         hipLaunchKernelGGL(heads_block_fwd_kernel<64>, dim3(per_head, b.k), dim3(kHbfThreads), lds, s, A, b.h, b.w1,
-                           b.b1, b.a);
+                           b.b1, b.a, b.w1t);
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
@@ -3090,25 +3116,28 @@ int gs4d_mlp_dw_bf16(int P, int KW, int W, const uint16_t *da, const uint16_t *h
     return gs4d_sum_slices(parts, S, (int64_t)KW * W, dw, stream);
 }
 
-int gs4d_mlp_dx_f32(int P, int KW, int W, const float *da, const float *w1, float *dh, void *stream) {
-    if (P < 0 || KW < kDxfChunk || KW % kDxfChunk != 0 || (W != 64 && W != 128)) return 1;
+int gs4d_mlp_dx_f32(int P, int KW, int W, const float *da, const float *w1t, float *dh, void *stream) {
+    if (P < 0 || KW < 64 || KW % 64 != 0 || (W != 64 && W != 128)) return 1;
     if (P == 0) return 0;
-    if (!da || !w1 || !dh || (((size_t)da | (size_t)w1 | (size_t)dh) & 15) != 0) return 1;
+    if (!da || !w1t || !dh || (((size_t)da | (size_t)w1t | (size_t)dh) & 15) != 0) return 1;
     const int nrg = (int)(((int64_t)P + 63) / 64);
     hipStream_t s = (hipStream_t)stream;
-    if (W == 128)  // two feature groups per row group, the grid padded to whole groups of 8 row groups
-        hipLaunchKernelGGL(mlp_dx_f32_kernel<128>, dim3((unsigned)((nrg + 7) / 8 * 16)), dim3(kDxfThreads), 0, s, P, KW,
-                           nrg, da, w1, dh);
-    else
-        hipLaunchKernelGGL(mlp_dx_f32_kernel<64>, dim3((unsigned)nrg), dim3(kDxfThreads), 0, s, P, KW, nrg, da, w1, dh);
+    const bool k64 = KW % 128 == 0;  // an even number of 64-wide chunks, else 32-wide ones
+    // W = 128: two feature groups per row group, the grid padded to whole groups of 8 row groups
+    const dim3 grid((unsigned)(W == 128 ? (nrg + 7) / 8 * 16 : nrg));
+    auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(kDxfThreads), 0, s, P, KW, nrg, da, w1t, dh); };
+    if (W == 128) k64 ? go(mlp_dx_f32_kernel<128, 64>) : go(mlp_dx_f32_kernel<128, 32>);
+    else k64 ? go(mlp_dx_f32_kernel<64, 64>) : go(mlp_dx_f32_kernel<64, 32>);
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
-// the row chunks of gs4d_mlp_dw_f32: about two rounds of two workgroups per CU over (chunk, m block), chunks
-// of a multiple of 32 rows and at least 256
+// the row chunks of gs4d_mlp_dw_f32: one resident round of workgroups over (chunk, m block) -- four per CU (126
+// registers: a wave per SIMD each) -- so that every workgroup runs once and all finish together; chunks a multiple of
+// 32 rows, at
+// least 256
 static void dwf_chunks(int P, int KW, int *S, int *rows) {
     const int nmb = std::max(1, KW / 64);
-    const int64_t target = std::max<int64_t>(1, (4 * (int64_t)cu_count() + nmb / 2) / nmb);
+    const int64_t target = std::max<int64_t>(1, (4 * (int64_t)cu_count()) / nmb);
     int64_t c = ((int64_t)P + target - 1) / target;
     c = std::max<int64_t>(256, (c + 31) / 32 * 32);
     *rows = (int)c;

@@ -321,17 +321,19 @@ class _DeformHeads(torch.autograd.Function):
             # both layers in one MFMA pass (gs4d_heads_block_forward): a is written once, for the backward
             from . import _C
             try:
-                a, *outs = _C.heads_block_forward(h.contiguous(), w1.contiguous(), b1.contiguous(),
-                                                  [t.contiguous() for t in second[0::2]], list(second[1::2]))
+                a, w1t, *outs = _C.heads_block_forward(h.contiguous(), w1.contiguous(), b1.contiguous(),
+                                                       [t.contiguous() for t in second[0::2]], list(second[1::2]))
             except RuntimeError as e:
                 if "status 4" not in str(e):
                     raise
                 _block_forward_unavailable(h.device, e)
             else:
                 ctx.save_for_backward(h, a, w1, *second[0::2])
+                ctx.w1t = w1t  # W1^T (W, kW), written by the same pass, for the input gradient
                 ctx.W = W
                 ctx.relu_done = relu_done
                 return tuple(outs)
+        ctx.w1t = None
         a = torch._addmm_activation(b1, h, w1.t())  # bias + ReLU in the GEMM epilogue where supported
         if a.is_cuda and W in (64, 128, 256) and k <= 8 and all(t.shape[0] <= 64 for t in second[0::2]) and \
                 sum(t.shape[0] for t in second[0::2]) * (W + 4) * 4 <= 64 * 1024:
@@ -366,7 +368,8 @@ class _DeformHeads(torch.autograd.Function):
                 # the two large GEMMs on hand-written f32-MFMA passes: fixed summation order, the same bits in
                 # every process (gs4d_mlp_dw_f32 / gs4d_mlp_dx_f32)
                 dw1 = _C.mlp_dw_f32(da, h.contiguous())
-                dh = relu_in(_C.mlp_dx_f32(da, w1.contiguous()))
+                w1t = ctx.w1t if ctx.w1t is not None else w1.t().contiguous()
+                dh = relu_in(_C.mlp_dx_f32(da, w1t))
             else:
                 dw1 = _splitk_dw(da, h)
                 dh = relu_in(_mm_dx(da, w1))
@@ -617,13 +620,11 @@ class Deformation(nn.Module):
         second = [t for hd in heads for t in (hd[3].weight, hd[3].bias)]
         return dict(zip(active, _DeformHeadsBF16.apply(h.contiguous(), hb, w1, b1, *second)))
 
-    def _pack_heads(self):
-        """Lay the heads' first-layer weights (and biases) back to back in one storage, each parameter a view
-        of its slice (same Parameter objects, so optimizers and state dicts are untouched): the heads block then
-        takes them as one (kW x W) operand with no per-step cat (_stacked).  Re-done whenever a move, load or
-        surgery has given a parameter its own storage again."""
-        heads = [getattr(self, name) for name in ("pos_deform", "scales_deform", "rotations_deform",
-                                                  "opacity_deform", "shs_deform")]
+    def _pack_heads(self, heads):
+        """Lay the given (active) heads' first-layer weights (and biases) back to back in one storage, in that
+        order, each parameter a view of its slice (same Parameter objects, so optimizers and state dicts are
+        untouched): the heads block then takes them as one (kW x W) operand with no per-step cat (_stacked).
+        Re-done whenever a move, load or surgery has given a parameter its own storage again."""
         for attr in ("weight", "bias"):
             ps = [hd[1].__getattr__(attr) for hd in heads]
             with torch.no_grad():
@@ -640,7 +641,9 @@ class Deformation(nn.Module):
         bs = [hd[1].bias for hd in heads]
         w1, b1 = _stacked(ws), _stacked(bs)
         if (w1 is None or b1 is None) and ws[0].is_cuda:
-            self._pack_heads()
+            # only the active heads, in their order: any subset then stacks (packing all five left a
+            # non-contiguous subset, e.g. no_do without no_dshs, re-packing and falling back to cat every step)
+            self._pack_heads(heads)
             w1, b1 = _stacked(ws), _stacked(bs)
         if w1 is None or b1 is None:
             return torch.cat(ws, 0), torch.cat(bs, 0)

@@ -269,11 +269,11 @@ int gs4d_mlp_dx_bf16(int P, int KW, int W, const uint16_t *da, const uint16_t *w
 size_t gs4d_mlp_dw_bf16_scratch_bytes(int P, int KW, int W);
 int gs4d_mlp_dw_bf16(int P, int KW, int W, const uint16_t *da, const uint16_t *hb, float *dw, void *scratch,
                      void *stream);
-/* The fp32 block's input gradient dh (P, W) = da (P, KW) @ W1 (KW, W) (the stacked first-layer weights as they
- * lie: row-major, KW = k W), f32 MFMA with f32 products and sums in one fixed order: the same bits in every process
+/* The fp32 block's input gradient dh (P, W) = da (P, KW) @ W1 (KW, W), given W1^T (W, KW) (the block forward's
+ * w1t), f32 MFMA with f32 products and sums in one fixed order: the same bits in every process
  * (scene/deformation.py:73-78's heads, the input gradient autograd forms by one GEMM).  KW a multiple of 64, W in
  * {64, 128}; rows 16-byte aligned. */
-int gs4d_mlp_dx_f32(int P, int KW, int W, const float *da, const float *w1, float *dh, void *stream);
+int gs4d_mlp_dx_f32(int P, int KW, int W, const float *da, const float *w1t, float *dh, void *stream);
 /* Its weight gradient dW1 (KW, W) = da^T h over the P rows (da (P, KW), h (P, W) row-major): per row chunk and
  * 64-row block of dW1 an f32-MFMA block, its waves summed in a fixed order, the chunks summed in order (scratch:
  * gs4d_mlp_dw_f32_scratch_bytes). */
@@ -324,6 +324,7 @@ typedef struct gs4d_heads_block_fwd {
     const float *w1;
     const float *b1;
     float *a;
+    float *w1t;  /* nullable: W1^T (W, kW), written for the backward's input gradient (gs4d_mlp_dx_f32) */
     int n[GS4D_HEADS_MAX];
     const float *w2[GS4D_HEADS_MAX];
     const float *b2[GS4D_HEADS_MAX];

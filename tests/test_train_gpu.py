@@ -251,6 +251,24 @@ def test_hexplane_backward_nonfinite_and_scales():
             torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-5 * a.abs().max().item())
 
 
+def test_heads_pack_any_active_subset():
+    """The heads' first-layer weights are packed back to back for the ACTIVE heads only: a
+    non-contiguous subset of the five (no_do=True, no_dshs=False: pos, scales, rotations, shs) stacks as one view
+    without a copy, and a second call reuses the packing (no re-pack: the parameters' storage stays put)."""
+    from gs4d_train import config
+    from gs4d_train.deformation import DeformNetwork
+    hyper, _ = config.dynerf()
+    hyper.no_do, hyper.no_dshs = True, False
+    net = DeformNetwork(hyper).cuda().deformation_net
+    heads = [getattr(net, n) for n in ("pos_deform", "scales_deform", "rotations_deform", "shs_deform")]
+    w1, b1 = net._first_layers(heads)
+    assert w1.shape == (4 * net.W, net.W) and w1.data_ptr() == heads[0][1].weight.data_ptr()
+    ptrs = [h[1].weight.data_ptr() for h in heads]
+    w1b, _ = net._first_layers(heads)
+    assert w1b.data_ptr() == w1.data_ptr() and ptrs == [h[1].weight.data_ptr() for h in heads]
+    assert torch.equal(w1b, torch.cat([h[1].weight for h in heads], 0))
+
+
 def test_row_surgery_hip_matches_torch_bitwise():
     """Densify, prune and reset_opacity on the GPU: the one-launch row plans (gs4d_rows_assemble, fused=True)
     against the same plans as torch index ops (fused=False) from the same state and RNG seed -- every
@@ -273,6 +291,13 @@ def test_row_surgery_hip_matches_torch_bitwise():
     train_step(g, views, opt, hyper, 3001, bg)
     gen = torch.Generator(device="cuda").manual_seed(3)
     P = g._xyz.shape[0]
+    with torch.no_grad():  # opacities spread around the prune threshold below
+        g._opacity.copy_(torch.randn(P, 1, device="cuda", generator=gen))
+    # every per-Gaussian parameter gets Adam moments (one more optimizer step with random gradients)
+    for name, attr in surgery.PARAMS.items():
+        p = getattr(g, attr)
+        p.grad = torch.randn(p.shape, device="cuda", generator=gen)
+    g.optimizer.step()
     g.xyz_gradient_accum = torch.rand(P, 1, device="cuda", generator=gen) * 4e-4
     g.denom = torch.ones(P, 1, device="cuda")
     g._deformation_table = torch.rand(P, device="cuda", generator=gen) > 0.2
@@ -281,8 +306,8 @@ def test_row_surgery_hip_matches_torch_bitwise():
         out = [m._deformation_table.clone()] + [getattr(m, n).clone() for n in surgery.STATS]
         for name, attr in surgery.PARAMS.items():
             p = getattr(m, attr)
-            st = m.optimizer.state[p]
-            out += [p.detach().clone(), st["exp_avg"].clone(), st["exp_avg_sq"].clone()]
+            st = m.optimizer.state.get(p, {})
+            out += [p.detach().clone()] + [st[k].clone() for k in ("exp_avg", "exp_avg_sq") if k in st]
         return out
 
     runs = []
@@ -292,12 +317,14 @@ def test_row_surgery_hip_matches_torch_bitwise():
         torch.manual_seed(11)
         m.densify(2e-4, 0.005, 0.5, None)
         grown = state(m)
-        m.prune(2e-4, 0.12, 0.5, 20)
+        m.prune(2e-4, 0.4, 0.5, 20)
         pruned = state(m)
+        assert 0 < m._xyz.shape[0] < grown[5].shape[0]
         m.reset_opacity()
         runs.append((grown, pruned, state(m), m._xyz.shape[0]))
     (a1, a2, a3, na), (b1, b2, b3, nb) = runs
     assert na == nb and na != P
+    assert len(a1) == len(b1) == len(a2) == len(b2) == len(a3) == len(b3) == 5 + 3 * 6
     for x, y in zip(a1 + a2 + a3, b1 + b2 + b3):
         assert x.dtype == y.dtype and torch.equal(x, y)
 
@@ -585,10 +612,11 @@ def test_heads_block_forward_matches_fp64(P, W, ns):
     b1 = torch.randn(k * W, device="cuda") * 0.1
     w2 = [torch.randn(n, W, device="cuda") / W ** 0.5 for n in ns]
     b2 = [torch.randn(n, device="cuda") for n in ns]
-    a, *out = _C.heads_block_forward(h, w1, b1, w2, b2)
-    assert a.shape == (P, k * W) and len(out) == k
+    a, w1t, *out = _C.heads_block_forward(h, w1, b1, w2, b2)
+    assert a.shape == (P, k * W) and len(out) == k and w1t.shape == (W, k * W)
     if P == 0:
         return
+    assert torch.equal(w1t, w1.t())  # written by the same pass for the backward (gs4d_mlp_dx_f32)
     hd = h.double()
     z = hd @ w1.double().t() + b1.double()
     za = hd.abs() @ w1.double().abs().t() + b1.double().abs()
@@ -730,7 +758,7 @@ def test_mlp_dw_bf16_matches_fp64(P, KW):
 @pytest.mark.parametrize("P,KW,W", [(100_000, 640, 128), (100_003, 640, 128), (1, 640, 128), (0, 640, 128),
                                      (2000, 192, 64), (777, 64, 128), (300, 1024, 64), (65, 128, 128)])
 def test_mlp_f32_gemms_match_fp64(P, KW, W):
-    """gs4d_mlp_dx_f32 (dh = da W1) and gs4d_mlp_dw_f32 (dW1 = da^T h), the fp32 heads block's two large GEMMs on
+    """gs4d_mlp_dx_f32 (dh = da W1, from W1^T) and gs4d_mlp_dw_f32 (dW1 = da^T h), the fp32 heads block's two large GEMMs on
     the f32 MFMA, vs fp64 torch: every element to 1e-5 of its |terms| sum (f32 products are exact in f64; the
     bar covers fp32 accumulation over up to 1e5 terms).  Ragged P (partial 64-row groups, a partial last chunk
     and 8-row step: rows past P read row P - 1 and are zeroed / not stored), P = 1 and 0 (dW1 all zeros), one
@@ -740,7 +768,8 @@ def test_mlp_f32_gemms_match_fp64(P, KW, W):
     da = torch.randn(P, KW, device="cuda")
     h = torch.relu(torch.randn(P, W, device="cuda"))
     w1 = torch.randn(KW, W, device="cuda") / KW ** 0.5
-    dh = _C.mlp_dx_f32(da, w1)
+    w1t = w1.t().contiguous()
+    dh = _C.mlp_dx_f32(da, w1t)
     dw = _C.mlp_dw_f32(da, h)
     assert dh.shape == (P, W) and dw.shape == (KW, W) and dh.dtype == dw.dtype == torch.float32
     refw = da.double().t() @ h.double()
@@ -752,9 +781,9 @@ def test_mlp_f32_gemms_match_fp64(P, KW, W):
     refx = da.double() @ w1.double()
     scx = da.double().abs() @ w1.double().abs()
     assert float(((dh.double() - refx).abs() - 1e-5 * scx).max().clamp_min(0)) == 0.0
-    assert torch.equal(_C.mlp_dx_f32(da, w1), dh) and torch.equal(_C.mlp_dw_f32(da, h), dw)
+    assert torch.equal(_C.mlp_dx_f32(da, w1t), dh) and torch.equal(_C.mlp_dw_f32(da, h), dw)
     with pytest.raises(RuntimeError):  # a W the kernels are not built for is refused, not run
-        _C.mlp_dx_f32(da[:, :KW], torch.randn(KW, 96, device="cuda"))
+        _C.mlp_dx_f32(da, torch.randn(96, KW, device="cuda"))
 
 
 _CROSS_PROCESS = r"""
@@ -766,7 +795,7 @@ P, KW, W = 100_003, 640, 128
 da = torch.randn(P, KW, device="cuda")
 h = torch.relu(torch.randn(P, W, device="cuda"))
 w1 = torch.randn(KW, W, device="cuda") / KW ** 0.5
-out = [_C.mlp_dx_f32(da, w1), _C.mlp_dw_f32(da, h)]
+out = [_C.mlp_dx_f32(da, w1.t().contiguous()), _C.mlp_dw_f32(da, h)]
 torch.cuda.synchronize()
 print(hashlib.sha256(b"".join(t.cpu().numpy().tobytes() for t in out)).hexdigest())
 """

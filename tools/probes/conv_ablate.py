@@ -1,5 +1,5 @@
 """Which fused piece changes the training trajectory?  The bouncing-balls convergence run of
-tests/test_convergence_gpu.py with the fused model but one piece swapped for its torch formulation
+tests/test_training_quality_gpu.py with the fused model but one piece swapped for its torch formulation
 (Adam, densification statistics, L1, deformation tail, HexPlane field, heads), or the reverse."""
 import copy
 import os
@@ -10,7 +10,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "4dgaussians-fast-train_amd"), os.path.
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-import test_convergence_gpu as T  # noqa: E402
+import test_training_quality_gpu as T  # noqa: E402
 from gs4d_train import config  # noqa: E402
 from gs4d_train.gaussians import GaussianModel  # noqa: E402
 from gs4d_train.train import train_step  # noqa: E402

@@ -1,11 +1,11 @@
 """Convergence diagnostics (GPU): fused vs unfused training of the bouncing-balls scene over seeds and
-lengths (tests/test_convergence_gpu.py), to separate trajectory noise from a systematic gap."""
+lengths (tests/test_training_quality_gpu.py), to separate trajectory noise from a systematic gap."""
 import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "4dgaussians-fast-train_amd"), os.path.join(ROOT, "tests")]
-import test_convergence_gpu as T  # noqa: E402
+import test_training_quality_gpu as T  # noqa: E402
 
 ds = T.make_dataset()
 kc, kf = int(sys.argv[1]), int(sys.argv[2])

@@ -1,4 +1,4 @@
-"""The short-horizon training pair of tests/test_convergence_gpu.py over many seeds, with the unfused (reference
+"""The short-horizon training pair of tests/test_training_quality_gpu.py over many seeds, with the unfused (reference
 torch formulation) arm run twice per seed: measures the unfused arm's own run-to-run spread (torch's grid_sample
 backward sums with float atomics) and the fused-vs-unfused gaps, to set the test's bars from measurements.
 Prints one JSON line per seed and a summary.  Usage: python tools/probes/conv_spread.py [n_seeds] [first_seed]"""
@@ -10,7 +10,7 @@ import numpy as np
 
 ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..")
 sys.path[:0] = [os.path.join(ROOT, "4dgaussians-fast-train_amd"), ROOT, os.path.join(ROOT, "tests")]
-from test_convergence_gpu import _train, make_dataset  # noqa: E402
+from test_training_quality_gpu import _train, make_dataset  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 12
 s0 = int(sys.argv[2]) if len(sys.argv) > 2 else 0

@@ -1,5 +1,5 @@
 """Fused vs unfused training drift (GPU diagnostic): the bouncing-balls setup of
-tests/test_convergence_gpu.py, both models stepped side by side on the same views; after each step the
+tests/test_training_quality_gpu.py, both models stepped side by side on the same views; after each step the
 largest relative parameter difference per group is printed, to tell rounding-level drift from a
 systematic difference in one of the fused kernels."""
 import copy
@@ -11,7 +11,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "4dgaussians-fast-train_amd"), os.path.
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-import test_convergence_gpu as T  # noqa: E402
+import test_training_quality_gpu as T  # noqa: E402
 from gs4d_train import config  # noqa: E402
 from gs4d_train.gaussians import GaussianModel  # noqa: E402
 from gs4d_train.train import train_step  # noqa: E402

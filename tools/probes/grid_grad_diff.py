@@ -12,7 +12,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import fused_drift as F  # noqa: E402
-import test_convergence_gpu as T  # noqa: E402
+import test_training_quality_gpu as T  # noqa: E402
 from gs4d_train import config  # noqa: E402
 from gs4d_train.train import train_step  # noqa: E402
 

@@ -33,7 +33,7 @@ def main():
     w2 = [torch.randn(n, W, device=dev) / W ** 0.5 for n in ns]
     b2 = [torch.randn(n, device=dev) for n in ns]
     gs = [torch.randn(P, n, device=dev) for n in ns]
-    a32, *_ = _C.heads_block_forward(h, w1, b1, w2, b2)
+    a32, _, *_ = _C.heads_block_forward(h, w1, b1, w2, b2)
     abf, hb, w1t, *_ = _C.heads_block_forward_bf16(h, w1, b1, w2, b2)
     da32 = _C.heads_backward(a32.contiguous(), gs, w2)[0]
     dabf = _C.heads_backward(abf.contiguous(), gs, w2)[0]

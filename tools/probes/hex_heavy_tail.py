@@ -28,7 +28,7 @@ for heavy in (False, True):
         rows = torch.randperm(N, device="cuda", generator=g)[: N // 100]
         dfeat[rows] *= 1e4
     _, gf = _C.hexplane_backward(pts, planes, packed, dfeat, order)
-    p64 = [p.double() for p in planes]
+    p64 = [p.double().requires_grad_(True) for p in planes]
     g64 = torch.autograd.grad(interpolate_ms_features(pts.double(), [p64[:6], p64[6:]]), p64, dfeat.double())
     g32 = torch.autograd.grad(interpolate_ms_features(pts, [list(f.grids[0]), list(f.grids[1])]),
                               [p for l in f.grids for p in l], dfeat)

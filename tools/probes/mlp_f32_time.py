@@ -26,7 +26,8 @@ for P, KW, W in [(100_000, 640, 128), (100_003, 640, 128), (2000, 192, 64), (300
     da = torch.randn(P, KW, device="cuda")
     h = torch.relu(torch.randn(P, W, device="cuda"))
     w1 = torch.randn(KW, W, device="cuda") / KW ** 0.5
-    dh = _C.mlp_dx_f32(da, w1)
+    w1t = w1.t().contiguous()
+    dh = _C.mlp_dx_f32(da, w1t)
     dw = _C.mlp_dw_f32(da, h)
     ref_x = da.double() @ w1.double()
     sc_x = da.double().abs() @ w1.double().abs()
@@ -35,7 +36,7 @@ for P, KW, W in [(100_000, 640, 128), (100_003, 640, 128), (2000, 192, 64), (300
     ex = float(((dh.double() - ref_x).abs() / sc_x.clamp_min(1e-30)).max())
     ew = float(((dw.double() - ref_w).abs() / sc_w.clamp_min(1e-30)).max())
     flops = 2.0 * P * KW * W
-    tx = timeit(lambda: _C.mlp_dx_f32(da, w1))
+    tx = timeit(lambda: _C.mlp_dx_f32(da, w1t))
     tw = timeit(lambda: _C.mlp_dw_f32(da, h))
     D._TUNE = False
     rx = timeit(lambda: D._mm_dx(da, w1))
@@ -44,7 +45,7 @@ for P, KW, W in [(100_000, 640, 128), (100_003, 640, 128), (2000, 192, 64), (300
     qx = timeit(lambda: D._mm_dx(da, w1))
     qw = timeit(lambda: D._splitk_dw(da, h))
     D._TUNE = False
-    same = torch.equal(_C.mlp_dx_f32(da, w1), dh) and torch.equal(_C.mlp_dw_f32(da, h), dw)
+    same = torch.equal(_C.mlp_dx_f32(da, w1t), dh) and torch.equal(_C.mlp_dw_f32(da, h), dw)
     print(f"P={P} KW={KW} W={W}: dx_f32 {tx:.1f} us ({flops / tx / 1e6:.1f} TF/s, rel err {ex:.2e}) | "
           f"dw_f32 {tw:.1f} us ({flops / tw / 1e6:.1f} TF/s, rel err {ew:.2e}) | rocBLAS own pick dx {rx:.1f} dw {rw:.1f} | "
           f"tuned dx {qx:.1f} dw {qw:.1f} | repeat bitwise {same}", flush=True)

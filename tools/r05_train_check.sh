@@ -4,7 +4,7 @@
 export TMPDIR=/tmp
 OUT=gpurun_out/tc_${TAG:-r05}
 mkdir -p $OUT
-timeout -k 10 600 python -u -m pytest tests/test_train_gpu.py tests/test_convergence_gpu.py -m gpu -x -q --timeout 400 --timeout-method thread -k "${TESTS_K:-not long_horizon}" > $OUT/tests.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_train_gpu.py tests/test_training_quality_gpu.py -m gpu -x -q --timeout 400 --timeout-method thread -k "${TESTS_K:-not long_horizon}" > $OUT/tests.log 2>&1
 rc=$?; grep -E "passed|failed|Error" $OUT/tests.log | tail -8; [ $rc -ne 0 ] && exit $rc
 TAG=${TAG}_f32 bash tools/train_seq.sh | tail -1 || exit 1
 PROBE_ARGS="metric --bf16" TAG=${TAG}_bf16 bash tools/train_seq.sh | tail -1 || exit 1
