@@ -2046,57 +2046,60 @@ __global__ __launch_bounds__(kDxfThreads) void mlp_dx_f32_kernel(int P, int KW, 
 #pragma unroll
     for (int m = 0; m < 4; m++) acc[m] = f4v{0.f, 0.f, 0.f, 0.f};
     const int nch = KW / KC;
-    // staging: piece e = t + 256 i is W1^T row 64 fg + e / Q (a feature), k 4 (e % Q) .. + 3 of the chunk
-    float4 ga[NP];
-    auto load_a = [&](int ch) {
+    // staging: piece e = t + 256 i is W1^T row 64 fg + e / Q (a feature), k 4 (e % Q) .. + 3 of the chunk.
+    // Chunks run in pairs, the pair's two halves unrolled with compile-time buffer and register-set indices (no
+    // lambdas: captured register arrays were left in scratch memory), each half issuing the next chunk's loads
+    // ahead of its own MFMAs.  nch is even (KC), so both halves are straight-line code.
+    float4 bb[2][KK];
+    {
+        float4 ga[NP];
 #pragma unroll
         for (int i = 0; i < NP; i++) {
             const int e = (int)threadIdx.x + kDxfThreads * i;
-            ga[i] = *reinterpret_cast<const float4 *>(w1t + (size_t)(64 * fg + e / Q) * KW + ch * KC + 4 * (e % Q));
+            ga[i] = *reinterpret_cast<const float4 *>(w1t + (size_t)(64 * fg + e / Q) * KW + 4 * (e % Q));
         }
-    };
-    auto store_a = [&](int buf) {
+#pragma unroll
+        for (int kk = 0; kk < KK; kk++) bb[0][kk] = *reinterpret_cast<const float4 *>(brow + 16 * kk);
 #pragma unroll
         for (int i = 0; i < NP; i++) {
             const int e = (int)threadIdx.x + kDxfThreads * i;
-            *reinterpret_cast<float4 *>(&s_a[buf][(e / Q) * S + 4 * (e % Q)]) = ga[i];
+            *reinterpret_cast<float4 *>(&s_a[0][(e / Q) * S + 4 * (e % Q)]) = ga[i];
         }
-    };
-    auto load_b = [&](int ch, float4 (&b)[KK]) {
-#pragma unroll
-        for (int kk = 0; kk < KK; kk++) b[kk] = *reinterpret_cast<const float4 *>(brow + ch * KC + 16 * kk);
-    };
-    // one chunk: the next chunk's loads first (into the other register set: no copies, whose waits the compiler
-    // placed mid-chunk), then this chunk's MFMAs, then the next chunk's W1^T block into the other LDS buffer
-    auto step = [&](int ch, const float4 (&b)[KK], float4 (&bnext)[KK]) {
-        const int nx = min(ch + 1, nch - 1);  // the last chunk re-loads itself: loads stay unconditional
-        load_a(nx);
-        load_b(nx, bnext);
-        __builtin_amdgcn_sched_barrier(0);  // left to itself the scheduler sank the loads below the MFMAs
-        const float *sa = s_a[ch & 1];
-#pragma unroll
-        for (int kk = 0; kk < KK; kk++)
-#pragma unroll
-            for (int m = 0; m < 4; m++) {
-                const float4 av = *reinterpret_cast<const float4 *>(sa + (16 * m + c) * S + 16 * kk + 4 * q);
-                acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, b[kk].x, acc[m], 0, 0, 0);
-                acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, b[kk].y, acc[m], 0, 0, 0);
-                acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, b[kk].z, acc[m], 0, 0, 0);
-                acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, b[kk].w, acc[m], 0, 0, 0);
-            }
-        // the other buffer: read by nobody since the last barrier (after the last chunk, by nobody at all; the
-        // store is unconditional so that the loads feeding it stay where they are issued)
-        store_a((ch + 1) & 1);
-        __syncthreads();
-    };
-    float4 b0[KK], b1[KK];
-    load_a(0);
-    load_b(0, b0);
-    store_a(0);
+    }
     __syncthreads();
-    for (int ch = 0; ch < nch; ch += 2) {  // nch is even (KC)
-        step(ch, b0, b1);
-        step(ch + 1, b1, b0);
+    for (int ch = 0; ch < nch; ch += 2) {
+#pragma unroll
+        for (int hf = 0; hf < 2; hf++) {
+            const int nx = min(ch + hf + 1, nch - 1);  // the last chunk re-loads itself: loads stay unconditional
+            float4 ga[NP];
+#pragma unroll
+            for (int i = 0; i < NP; i++) {
+                const int e = (int)threadIdx.x + kDxfThreads * i;
+                ga[i] = *reinterpret_cast<const float4 *>(w1t + (size_t)(64 * fg + e / Q) * KW + nx * KC + 4 * (e % Q));
+            }
+#pragma unroll
+            for (int kk = 0; kk < KK; kk++) bb[hf ^ 1][kk] = *reinterpret_cast<const float4 *>(brow + nx * KC + 16 * kk);
+            __builtin_amdgcn_sched_barrier(0);  // left to itself the scheduler sank the loads below the MFMAs
+            const float *sa = s_a[hf];
+#pragma unroll
+            for (int kk = 0; kk < KK; kk++)
+#pragma unroll
+                for (int m = 0; m < 4; m++) {
+                    const float4 av = *reinterpret_cast<const float4 *>(sa + (16 * m + c) * S + 16 * kk + 4 * q);
+                    const float4 bv = bb[hf][kk];
+                    acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv.x, acc[m], 0, 0, 0);
+                    acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv.y, acc[m], 0, 0, 0);
+                    acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv.z, acc[m], 0, 0, 0);
+                    acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv.w, acc[m], 0, 0, 0);
+                }
+            // the other buffer: read by nobody since the last barrier (after the last chunk, by nobody at all)
+#pragma unroll
+            for (int i = 0; i < NP; i++) {
+                const int e = (int)threadIdx.x + kDxfThreads * i;
+                *reinterpret_cast<float4 *>(&s_a[hf ^ 1][(e / Q) * S + 4 * (e % Q)]) = ga[i];
+            }
+            __syncthreads();
+        }
     }
     // D[feature 16 m + 4 q + r][row c]
     if (row < P)
@@ -2117,6 +2120,10 @@ __global__ __launch_bounds__(kDxfThreads) void mlp_dx_f32_kernel(int P, int KW, 
 // the chunks in order.  Deterministic by construction.  The m blocks of one chunk sit on one XCD (they share its
 // h rows).  (Round 6 first read both operands straight from HBM as dwords at 2 waves/SIMD: 50 % MFMA busy.)
 constexpr int kDwfThreads = 256, kDwfStage = 16;
+// v, or zeros: component selects (a select between two float4 values became a select of scratch addresses)
+__device__ __forceinline__ float4 keep4(bool ok, float4 v) {
+    return make_float4(ok ? v.x : 0.f, ok ? v.y : 0.f, ok ? v.z : 0.f, ok ? v.w : 0.f);
+}
 template <int W>
 __global__ __launch_bounds__(kDwfThreads) void mlp_dw_f32_kernel(int P, int KW, int S, int chunk_rows,
                                                                  const float *__restrict__ da,
@@ -2139,66 +2146,75 @@ __global__ __launch_bounds__(kDwfThreads) void mlp_dw_f32_kernel(int P, int KW, 
     for (int mt = 0; mt < MT; mt++)
 #pragma unroll
         for (int nt = 0; nt < NTW; nt++) acc[mt][nt] = f4v{0.f, 0.f, 0.f, 0.f};
-    // staging: da piece e: stage row e / 16, float4 e % 16; h piece e: stage row e / (W / 4), float4 e % (W / 4)
-    float4 gd[PD], gh[PH];
-    auto load = [&](int st) {  // rows past r1 read row r1 - 1 (zeroed at the store)
-#pragma unroll
-        for (int i = 0; i < PD; i++) {
-            const int e = (int)threadIdx.x + kDwfThreads * i;
-            const int64_t r = min(r0 + (int64_t)kDwfStage * st + e / 16, r1 - 1);
-            gd[i] = *reinterpret_cast<const float4 *>(da + (size_t)r * KW + 64 * mb + 4 * (e % 16));
-        }
-#pragma unroll
-        for (int i = 0; i < PH; i++) {
-            const int e = (int)threadIdx.x + kDwfThreads * i;
-            const int64_t r = min(r0 + (int64_t)kDwfStage * st + e / (W / 4), r1 - 1);
-            gh[i] = *reinterpret_cast<const float4 *>(h + (size_t)r * W + 4 * (e % (W / 4)));
-        }
-    };
-    auto store = [&](int st, int buf) {
-        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-        for (int i = 0; i < PD; i++) {
-            const int e = (int)threadIdx.x + kDwfThreads * i;
-            const bool ok = r0 + (int64_t)kDwfStage * st + e / 16 < r1;
-            *reinterpret_cast<float4 *>(&s_d[buf][(e / 16) * SD + 4 * (e % 16)]) = ok ? gd[i] : z;
-        }
-#pragma unroll
-        for (int i = 0; i < PH; i++) {
-            const int e = (int)threadIdx.x + kDwfThreads * i;
-            const bool ok = r0 + (int64_t)kDwfStage * st + e / (W / 4) < r1;
-            *reinterpret_cast<float4 *>(&s_h[buf][(e / (W / 4)) * SH + 4 * (e % (W / 4))]) = ok ? gh[i] : z;
-        }
-    };
-    // one stage: the next stage's loads first, then this stage's MFMAs from LDS, then the next stage into the other
-    // buffer (unconditional, as in mlp_dx_f32_kernel: stages run in pairs, so both halves are straight-line)
+    // staging: da piece e: stage row e / 16, float4 e % 16; h piece e: stage row e / (W / 4), float4 e % (W / 4).
+    // Stages run in pairs, each half unrolled with compile-time buffer indices (see mlp_dx_f32_kernel): the next
+    // stage's loads, this stage's MFMAs from LDS, then the next stage into the other buffer (rows past r1 read row
+    // r1 - 1 and are stored as zeros; past the last stage a padding stage, zeros, read by nobody).
     const int nst = (int)((r1 - r0 + 2 * kDwfStage - 1) / (2 * kDwfStage)) * 2;
-    auto step = [&](int st) {
-        load(min(st + 1, nst - 1));
-        __builtin_amdgcn_sched_barrier(0);
-        const float *sd = s_d[st & 1], *sh = s_h[st & 1];
 #pragma unroll
-        for (int u = 0; u < kDwfStage / 4; u++) {
-            float av[MT], hv[NTW];
+    for (int pre = 0; pre < 1; pre++) {  // stage 0 into buffer 0
+        float4 gd[PD], gh[PH];
 #pragma unroll
-            for (int mt = 0; mt < MT; mt++) av[mt] = sd[(4 * u + q) * SD + 16 * mt + c];
-#pragma unroll
-            for (int nt = 0; nt < NTW; nt++) hv[nt] = sh[(4 * u + q) * SH + 16 * (NTW * wv + nt) + c];
-#pragma unroll
-            for (int mt = 0; mt < MT; mt++)
-#pragma unroll
-                for (int nt = 0; nt < NTW; nt++)
-                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[mt], hv[nt], acc[mt][nt], 0, 0, 0);
+        for (int i = 0; i < PD; i++) {
+            const int e = (int)threadIdx.x + kDwfThreads * i;
+            const int64_t r = r0 + e / 16;
+            gd[i] = *reinterpret_cast<const float4 *>(da + (size_t)min(r, r1 - 1) * KW + 64 * mb + 4 * (e % 16));
+            *reinterpret_cast<float4 *>(&s_d[0][(e / 16) * SD + 4 * (e % 16)]) = keep4(r < r1, gd[i]);
         }
-        store(st + 1, (st + 1) & 1);  // past the last stage: a padding stage, zeros, read by nobody
-        __syncthreads();
-    };
-    load(0);
-    store(0, 0);
+#pragma unroll
+        for (int i = 0; i < PH; i++) {
+            const int e = (int)threadIdx.x + kDwfThreads * i;
+            const int64_t r = r0 + e / (W / 4);
+            gh[i] = *reinterpret_cast<const float4 *>(h + (size_t)min(r, r1 - 1) * W + 4 * (e % (W / 4)));
+            *reinterpret_cast<float4 *>(&s_h[0][(e / (W / 4)) * SH + 4 * (e % (W / 4))]) = keep4(r < r1, gh[i]);
+        }
+    }
     __syncthreads();
     for (int st = 0; st < nst; st += 2) {
-        step(st);
-        step(st + 1);
+#pragma unroll
+        for (int hf = 0; hf < 2; hf++) {
+            const int64_t rn = r0 + (int64_t)kDwfStage * (st + hf + 1);  // the next stage's first row
+            float4 gd[PD], gh[PH];
+#pragma unroll
+            for (int i = 0; i < PD; i++) {
+                const int e = (int)threadIdx.x + kDwfThreads * i;
+                gd[i] = *reinterpret_cast<const float4 *>(da + (size_t)min(rn + e / 16, r1 - 1) * KW + 64 * mb +
+                                                          4 * (e % 16));
+            }
+#pragma unroll
+            for (int i = 0; i < PH; i++) {
+                const int e = (int)threadIdx.x + kDwfThreads * i;
+                gh[i] = *reinterpret_cast<const float4 *>(h + (size_t)min(rn + e / (W / 4), r1 - 1) * W +
+                                                          4 * (e % (W / 4)));
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            const float *sd = s_d[hf], *sh = s_h[hf];
+#pragma unroll
+            for (int u = 0; u < kDwfStage / 4; u++) {
+                float av[MT], hv[NTW];
+#pragma unroll
+                for (int mt = 0; mt < MT; mt++) av[mt] = sd[(4 * u + q) * SD + 16 * mt + c];
+#pragma unroll
+                for (int nt = 0; nt < NTW; nt++) hv[nt] = sh[(4 * u + q) * SH + 16 * (NTW * wv + nt) + c];
+#pragma unroll
+                for (int mt = 0; mt < MT; mt++)
+#pragma unroll
+                    for (int nt = 0; nt < NTW; nt++)
+                        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[mt], hv[nt], acc[mt][nt], 0, 0, 0);
+            }
+#pragma unroll
+            for (int i = 0; i < PD; i++) {
+                const int e = (int)threadIdx.x + kDwfThreads * i;
+                *reinterpret_cast<float4 *>(&s_d[hf ^ 1][(e / 16) * SD + 4 * (e % 16)]) = keep4(rn + e / 16 < r1, gd[i]);
+            }
+#pragma unroll
+            for (int i = 0; i < PH; i++) {
+                const int e = (int)threadIdx.x + kDwfThreads * i;
+                *reinterpret_cast<float4 *>(&s_h[hf ^ 1][(e / (W / 4)) * SH + 4 * (e % (W / 4))]) =
+                    keep4(rn + e / (W / 4) < r1, gh[i]);
+            }
+            __syncthreads();
+        }
     }
     // D[feature 16 mt + 4 q + r][column 16 (NTW wv + nt) + c] of rows 64 mb .. of dW1
     float *o = parts + (size_t)s * KW * W + (size_t)64 * mb * W;

@@ -19,21 +19,28 @@ scene, and that the fused HIP kernels train it as the reference's own PyTorch fo
 
 Training is chaotic in the rounding: the two formulations agree per step to ~1e-7 (test_train_gpu.py),
 but Adam's first steps turn the sign of near-zero gradients into full-size updates and densification
-thresholds accumulated gradients, so long runs fan out -- and neither run is bitwise reproducible (the
-grid gradients of both are summed with float atomics).  Measured over seeds at K_COARSE + K_FINE =
-800 + 2500 iterations, test PSNR spreads by +-0.6 dB run to run for EITHER formulation
-(tools/probes/conv_diag.py, conv_ablate.py); at 300 + 300 iterations without densification the two
-runs already differ by ~0.1 dB.  Hence two tests:
-  * short horizon (no densification, 200 + 200 iterations, 6 seeds): the formulations' mean held-out
-    PSNR within 0.1 dB, each seed's two runs within 0.2 dB (single seeds measured 0.02-0.16 dB apart,
-    so one pair, or the mean of three, sits at the noise of a 0.1 dB bar) and their last-50-iteration
-    mean losses within 1 %;
+thresholds accumulated gradients, so the trajectories of two formulations that differ only in rounding fan out.
+What the tests can assert is therefore statistical, with bars set from measurements:
+  * the fused arm is bitwise reproducible across processes (round 6: every kernel of the fused step sums in a
+    fixed order, the MLP's large GEMMs included -- round 5's timing-tuned library GEMMs were not, and its
+    per-seed bar failed on the driver); the unfused arm is not (torch's grid_sample backward sums with float
+    atomics);
+  * measured over 12 seeds at 200 + 200 iterations, two processes (tools/probes/conv_spread.py,
+    profiles/r06/conv_spread_{a,b}.log): the unfused arm's run-to-run difference has sd 0.025-0.026 dB (so
+    one run's sd is ~0.018), the fused-minus-unfused per-seed gap sd 0.052-0.054 dB with mean -0.009 / -0.020 dB
+    and largest |gap| 0.136 dB;
+  * short horizon (no densification, 200 + 200 iterations, SHORT_SEEDS = 12): each seed's gap within
+    SHORT_RUN_DELTA = 0.25 dB (4.7 sigma of the measured gap: false failure ~3e-6 per seed, ~3e-5 over 12), the
+    12-seed mean gap within SHORT_DELTA = 0.07 dB (4.6 sigma of the mean, sigma = 0.053 / sqrt(12): ~4e-6),
+    and the last-50-iteration mean losses within 1 %;
   * long horizon (the full miniature schedule, 5 seeds each): every run converges (above RUN_FLOOR and
     PSNR_GAIN over its start), each formulation's median above PSNR_FLOOR, the median fused PSNR within
     PSNR_DELTA of the median unfused PSNR, and the same for the fused run with the opt-in bf16
     deformation MLP (3 seeds).  Medians, because a run now and then loses ~2 dB to an unlucky
     densification (an unfused run at 26.4 dB, train 31.9, among 28-29 dB runs): the claim is about the
     formulations, not one trajectory.
+This file sorts after the parity suites (test_gpu_parity, test_knn, test_train_gpu): a statistical failure here
+cannot hide their results under `pytest -x`.
 """
 import copy
 import math
@@ -52,13 +59,9 @@ RUN_FLOOR = 25.0      # dB, every run
 PSNR_GAIN = 15.0      # dB over the initial random point cloud (8.5-8.7 dB)
 PSNR_DELTA = 1.0      # dB between the medians of the fused and the unfused runs
 SEEDS = 5
-SHORT_DELTA = 0.1     # dB between the two formulations' mean short-horizon PSNR over SHORT_SEEDS seeds
-SHORT_RUN_DELTA = 0.35  # dB between the two runs of any one seed.  Measured (round 5, 6 seeds): per-seed gaps
-                        # 0.02-0.19 dB in one run and 0.33 dB at seed 2 in another -- the reference formulation
-                        # alone moved 0.17 dB at that seed between two runs (21.776 vs 21.943 dB: torch's
-                        # atomic-order backward), so one run of each formulation can differ by ~2x that.  The
-                        # 6-seed mean bar SHORT_DELTA (0.1 dB) is what holds the formulations together.
-SHORT_SEEDS = 6
+SHORT_DELTA = 0.07    # dB, |mean over SHORT_SEEDS seeds of (fused - unfused)|: 4.6 sigma of the measured mean (docstring)
+SHORT_RUN_DELTA = 0.25  # dB, |fused - unfused| at any one seed: 4.7 sigma of the measured per-seed gap (docstring)
+SHORT_SEEDS = 12
 
 
 def _cameras(n, seed, offset):
@@ -165,7 +168,8 @@ def test_short_horizon_fused_matches_unfused(dataset):
         assert abs(la - lb) <= 0.01 * lb, (seed, la, lb)
         assert abs(res[True][1] - res[False][1]) <= SHORT_RUN_DELTA, (seed, res[True][1], res[False][1])
     mf, mu = float(np.mean(test[True])), float(np.mean(test[False]))
-    print(f"short mean test PSNR: fused {mf:.3f} dB, unfused {mu:.3f} dB")
+    gaps = np.array(test[True]) - np.array(test[False])
+    print(f"short mean test PSNR: fused {mf:.3f} dB, unfused {mu:.3f} dB; per-seed gap sd {gaps.std(ddof=1):.3f} dB")
     assert abs(mf - mu) <= SHORT_DELTA, (mf, mu)
 
 
