@@ -2024,7 +2024,8 @@ __global__ __launch_bounds__(kDwbThreads) void mlp_dw_bf16_kernel(int P, int KW,
 // KC: the k chunk, 64, or 32 when KW / 64 is odd (the loop runs chunks in pairs: an even count keeps both halves
 // unconditional, so the compiler cannot sink the second half's loads into a branch).
 constexpr int kDxfThreads = 256;
-template <int W, int KC>
+// RB: 16-row blocks per wave (2: each W1^T LDS read feeds twice the MFMAs)
+template <int W, int KC, int RB>
 __global__ __launch_bounds__(kDxfThreads) void mlp_dx_f32_kernel(int P, int KW, int nrg, const float *__restrict__ da,
                                                                  const float *__restrict__ w1t, float *__restrict__ dh) {
     constexpr int NG = W / 64;  // feature groups
@@ -2039,18 +2040,25 @@ __global__ __launch_bounds__(kDxfThreads) void mlp_dx_f32_kernel(int P, int KW, 
     if (rg >= nrg) return;  // the grid is padded to whole groups of 8 row groups (uniform over the workgroup)
     const int lane = threadIdx.x & 63, wv = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6), q = lane >> 4,
               c = lane & 15;
-    const int64_t row = (int64_t)rg * 64 + wv * 16 + c;
-    // rows past P read row P - 1 (unconditional loads; not stored)
-    const float *brow = da + (size_t)min(row, (int64_t)P - 1) * KW + 4 * q;
-    f4v acc[4];
+    int64_t row[RB];
+    const float *brow[RB];
 #pragma unroll
-    for (int m = 0; m < 4; m++) acc[m] = f4v{0.f, 0.f, 0.f, 0.f};
+    for (int rb = 0; rb < RB; rb++) {
+        row[rb] = (int64_t)rg * 64 * RB + wv * 16 * RB + 16 * rb + c;
+        // rows past P read row P - 1 (unconditional loads; not stored)
+        brow[rb] = da + (size_t)min(row[rb], (int64_t)P - 1) * KW + 4 * q;
+    }
+    f4v acc[4][RB];
+#pragma unroll
+    for (int m = 0; m < 4; m++)
+#pragma unroll
+        for (int rb = 0; rb < RB; rb++) acc[m][rb] = f4v{0.f, 0.f, 0.f, 0.f};
     const int nch = KW / KC;
     // staging: piece e = t + 256 i is W1^T row 64 fg + e / Q (a feature), k 4 (e % Q) .. + 3 of the chunk.
     // Chunks run in pairs, the pair's two halves unrolled with compile-time buffer and register-set indices (no
     // lambdas: captured register arrays were left in scratch memory), each half issuing the next chunk's loads
     // ahead of its own MFMAs.  nch is even (KC), so both halves are straight-line code.
-    float4 bb[2][KK];
+    float4 bb[2][RB][KK];
     {
         float4 ga[NP];
 #pragma unroll
@@ -2059,7 +2067,9 @@ __global__ __launch_bounds__(kDxfThreads) void mlp_dx_f32_kernel(int P, int KW, 
             ga[i] = *reinterpret_cast<const float4 *>(w1t + (size_t)(64 * fg + e / Q) * KW + 4 * (e % Q));
         }
 #pragma unroll
-        for (int kk = 0; kk < KK; kk++) bb[0][kk] = *reinterpret_cast<const float4 *>(brow + 16 * kk);
+        for (int rb = 0; rb < RB; rb++)
+#pragma unroll
+            for (int kk = 0; kk < KK; kk++) bb[0][rb][kk] = *reinterpret_cast<const float4 *>(brow[rb] + 16 * kk);
 #pragma unroll
         for (int i = 0; i < NP; i++) {
             const int e = (int)threadIdx.x + kDxfThreads * i;
@@ -2078,7 +2088,10 @@ __global__ __launch_bounds__(kDxfThreads) void mlp_dx_f32_kernel(int P, int KW, 
                 ga[i] = *reinterpret_cast<const float4 *>(w1t + (size_t)(64 * fg + e / Q) * KW + nx * KC + 4 * (e % Q));
             }
 #pragma unroll
-            for (int kk = 0; kk < KK; kk++) bb[hf ^ 1][kk] = *reinterpret_cast<const float4 *>(brow + nx * KC + 16 * kk);
+            for (int rb = 0; rb < RB; rb++)
+#pragma unroll
+                for (int kk = 0; kk < KK; kk++)
+                    bb[hf ^ 1][rb][kk] = *reinterpret_cast<const float4 *>(brow[rb] + nx * KC + 16 * kk);
             __builtin_amdgcn_sched_barrier(0);  // left to itself the scheduler sank the loads below the MFMAs
             const float *sa = s_a[hf];
 #pragma unroll
@@ -2086,11 +2099,14 @@ __global__ __launch_bounds__(kDxfThreads) void mlp_dx_f32_kernel(int P, int KW, 
 #pragma unroll
                 for (int m = 0; m < 4; m++) {
                     const float4 av = *reinterpret_cast<const float4 *>(sa + (16 * m + c) * S + 16 * kk + 4 * q);
-                    const float4 bv = bb[hf][kk];
-                    acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv.x, acc[m], 0, 0, 0);
-                    acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv.y, acc[m], 0, 0, 0);
-                    acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv.z, acc[m], 0, 0, 0);
-                    acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv.w, acc[m], 0, 0, 0);
+#pragma unroll
+                    for (int rb = 0; rb < RB; rb++) {
+                        const float4 bv = bb[hf][rb][kk];
+                        acc[m][rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv.x, acc[m][rb], 0, 0, 0);
+                        acc[m][rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv.y, acc[m][rb], 0, 0, 0);
+                        acc[m][rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv.z, acc[m][rb], 0, 0, 0);
+                        acc[m][rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv.w, acc[m][rb], 0, 0, 0);
+                    }
                 }
             // the other buffer: read by nobody since the last barrier (after the last chunk, by nobody at all)
 #pragma unroll
@@ -2102,11 +2118,13 @@ __global__ __launch_bounds__(kDxfThreads) void mlp_dx_f32_kernel(int P, int KW, 
         }
     }
     // D[feature 16 m + 4 q + r][row c]
-    if (row < P)
 #pragma unroll
-        for (int m = 0; m < 4; m++)
-            *reinterpret_cast<float4 *>(dh + (size_t)row * W + 64 * fg + 16 * m + 4 * q) =
-                make_float4(acc[m][0], acc[m][1], acc[m][2], acc[m][3]);
+    for (int rb = 0; rb < RB; rb++)
+        if (row[rb] < P)
+#pragma unroll
+            for (int m = 0; m < 4; m++)
+                *reinterpret_cast<float4 *>(dh + (size_t)row[rb] * W + 64 * fg + 16 * m + 4 * q) =
+                    make_float4(acc[m][rb][0], acc[m][rb][1], acc[m][rb][2], acc[m][rb][3]);
 }
 
 // ---- the fp32 heads block's first-layer weight gradient: dW1 (KW x W) = da^T h reduced over the P rows, on
@@ -2124,29 +2142,32 @@ constexpr int kDwfThreads = 256, kDwfStage = 16;
 __device__ __forceinline__ float4 keep4(bool ok, float4 v) {
     return make_float4(ok ? v.x : 0.f, ok ? v.y : 0.f, ok ? v.z : 0.f, ok ? v.w : 0.f);
 }
-template <int W>
+// MB: dW1 rows per workgroup, 64 (waves side by side over the W columns) or 128 (waves 2 x 2, each a 64 x W/2
+// block: twice the MFMAs per stage and per LDS read)
+template <int W, int MB>
 __global__ __launch_bounds__(kDwfThreads) void mlp_dw_f32_kernel(int P, int KW, int S, int chunk_rows,
                                                                  const float *__restrict__ da,
                                                                  const float *__restrict__ h,
                                                                  float *__restrict__ parts) {
-    constexpr int NTW = W / 64, MT = 4;  // n tiles per wave, m tiles
-    constexpr int SD = 64 + 16, SH = W + 16;
-    constexpr int PD = kDwfStage * 16 / kDwfThreads, PH = kDwfStage * (W / 4) / kDwfThreads;  // float4 per thread
+    constexpr int MT = 4, NTW = MB == 64 ? W / 64 : W / 32;  // m tiles and n tiles per wave
+    constexpr int SD = MB + 16, SH = W + 16, QD = MB / 4;    // QD: float4 per staged da row
+    constexpr int PD = kDwfStage * QD / kDwfThreads, PH = kDwfStage * (W / 4) / kDwfThreads;  // float4 per thread
     __shared__ __attribute__((aligned(16))) float s_d[2][kDwfStage * SD];
     __shared__ __attribute__((aligned(16))) float s_h[2][kDwfStage * SH];
-    const int nmb = KW / 64;
+    const int nmb = KW / MB;
     // b = 8 (nmb j + mb) + x: chunk s = 8 j + x, so the nmb blocks of a chunk share b % 8 (the XCD)
     const int b = blockIdx.x, x = b & 7, jm = b >> 3, mb = jm % nmb, s = 8 * (jm / nmb) + x;
     if (s >= S) return;  // padding of the grid to whole groups of 8 chunks (uniform over the workgroup)
     const int lane = threadIdx.x & 63, wv = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6), q = lane >> 4,
               c = lane & 15;
+    const int wm = MB == 64 ? 0 : wv >> 1, wn = MB == 64 ? wv : wv & 1;  // the wave's m and n block
     const int64_t r0 = (int64_t)s * chunk_rows, r1 = min((int64_t)P, r0 + chunk_rows);
     f4v acc[MT][NTW];
 #pragma unroll
     for (int mt = 0; mt < MT; mt++)
 #pragma unroll
         for (int nt = 0; nt < NTW; nt++) acc[mt][nt] = f4v{0.f, 0.f, 0.f, 0.f};
-    // staging: da piece e: stage row e / 16, float4 e % 16; h piece e: stage row e / (W / 4), float4 e % (W / 4).
+    // staging: da piece e: stage row e / QD, float4 e % QD; h piece e: stage row e / (W / 4), float4 e % (W / 4).
     // Stages run in pairs, each half unrolled with compile-time buffer indices (see mlp_dx_f32_kernel): the next
     // stage's loads, this stage's MFMAs from LDS, then the next stage into the other buffer (rows past r1 read row
     // r1 - 1 and are stored as zeros; past the last stage a padding stage, zeros, read by nobody).
@@ -2157,9 +2178,9 @@ __global__ __launch_bounds__(kDwfThreads) void mlp_dw_f32_kernel(int P, int KW, 
 #pragma unroll
         for (int i = 0; i < PD; i++) {
             const int e = (int)threadIdx.x + kDwfThreads * i;
-            const int64_t r = r0 + e / 16;
-            gd[i] = *reinterpret_cast<const float4 *>(da + (size_t)min(r, r1 - 1) * KW + 64 * mb + 4 * (e % 16));
-            *reinterpret_cast<float4 *>(&s_d[0][(e / 16) * SD + 4 * (e % 16)]) = keep4(r < r1, gd[i]);
+            const int64_t r = r0 + e / QD;
+            gd[i] = *reinterpret_cast<const float4 *>(da + (size_t)min(r, r1 - 1) * KW + MB * mb + 4 * (e % QD));
+            *reinterpret_cast<float4 *>(&s_d[0][(e / QD) * SD + 4 * (e % QD)]) = keep4(r < r1, gd[i]);
         }
 #pragma unroll
         for (int i = 0; i < PH; i++) {
@@ -2178,8 +2199,8 @@ __global__ __launch_bounds__(kDwfThreads) void mlp_dw_f32_kernel(int P, int KW, 
 #pragma unroll
             for (int i = 0; i < PD; i++) {
                 const int e = (int)threadIdx.x + kDwfThreads * i;
-                gd[i] = *reinterpret_cast<const float4 *>(da + (size_t)min(rn + e / 16, r1 - 1) * KW + 64 * mb +
-                                                          4 * (e % 16));
+                gd[i] = *reinterpret_cast<const float4 *>(da + (size_t)min(rn + e / QD, r1 - 1) * KW + MB * mb +
+                                                          4 * (e % QD));
             }
 #pragma unroll
             for (int i = 0; i < PH; i++) {
@@ -2193,9 +2214,9 @@ __global__ __launch_bounds__(kDwfThreads) void mlp_dw_f32_kernel(int P, int KW, 
             for (int u = 0; u < kDwfStage / 4; u++) {
                 float av[MT], hv[NTW];
 #pragma unroll
-                for (int mt = 0; mt < MT; mt++) av[mt] = sd[(4 * u + q) * SD + 16 * mt + c];
+                for (int mt = 0; mt < MT; mt++) av[mt] = sd[(4 * u + q) * SD + 64 * wm + 16 * mt + c];
 #pragma unroll
-                for (int nt = 0; nt < NTW; nt++) hv[nt] = sh[(4 * u + q) * SH + 16 * (NTW * wv + nt) + c];
+                for (int nt = 0; nt < NTW; nt++) hv[nt] = sh[(4 * u + q) * SH + 16 * (NTW * wn + nt) + c];
 #pragma unroll
                 for (int mt = 0; mt < MT; mt++)
 #pragma unroll
@@ -2205,7 +2226,7 @@ __global__ __launch_bounds__(kDwfThreads) void mlp_dw_f32_kernel(int P, int KW, 
 #pragma unroll
             for (int i = 0; i < PD; i++) {
                 const int e = (int)threadIdx.x + kDwfThreads * i;
-                *reinterpret_cast<float4 *>(&s_d[hf ^ 1][(e / 16) * SD + 4 * (e % 16)]) = keep4(rn + e / 16 < r1, gd[i]);
+                *reinterpret_cast<float4 *>(&s_d[hf ^ 1][(e / QD) * SD + 4 * (e % QD)]) = keep4(rn + e / QD < r1, gd[i]);
             }
 #pragma unroll
             for (int i = 0; i < PH; i++) {
@@ -2216,15 +2237,15 @@ __global__ __launch_bounds__(kDwfThreads) void mlp_dw_f32_kernel(int P, int KW, 
             __syncthreads();
         }
     }
-    // D[feature 16 mt + 4 q + r][column 16 (NTW wv + nt) + c] of rows 64 mb .. of dW1
-    float *o = parts + (size_t)s * KW * W + (size_t)64 * mb * W;
+    // D[feature 64 wm + 16 mt + 4 q + r][column 16 (NTW wn + nt) + c] of rows MB mb .. of dW1
+    float *o = parts + (size_t)s * KW * W + (size_t)(MB * mb + 64 * wm) * W;
 #pragma unroll
     for (int mt = 0; mt < MT; mt++)
 #pragma unroll
         for (int nt = 0; nt < NTW; nt++)
 #pragma unroll
             for (int r = 0; r < 4; r++)
-                o[(size_t)(16 * mt + 4 * q + r) * W + 16 * (NTW * wv + nt) + c] = acc[mt][nt][r];
+                o[(size_t)(16 * mt + 4 * q + r) * W + 16 * (NTW * wn + nt) + c] = acc[mt][nt][r];
 }
 
 // ---- the wide head's second-layer backward on the bf16 path (n = 48, W = 128): heads_bwd_wide_mfma_kernel's
@@ -3132,27 +3153,44 @@ int gs4d_mlp_dw_bf16(int P, int KW, int W, const uint16_t *da, const uint16_t *h
     return gs4d_sum_slices(parts, S, (int64_t)KW * W, dw, stream);
 }
 
+// A/B switch of the kernels' shapes (development only; 0 = the kept shapes): GS4D_MLP_SHAPE bit 0 = one 16-row
+// block per wave in gs4d_mlp_dx_f32, bit 1 = 64-row m blocks in gs4d_mlp_dw_f32
+static int mlp_shape() {
+    static const int v = [] {
+        const char *e = getenv("GS4D_MLP_SHAPE");
+        return e ? atoi(e) : 0;
+    }();
+    return v;
+}
+
 int gs4d_mlp_dx_f32(int P, int KW, int W, const float *da, const float *w1t, float *dh, void *stream) {
     if (P < 0 || KW < 64 || KW % 64 != 0 || (W != 64 && W != 128)) return 1;
     if (P == 0) return 0;
     if (!da || !w1t || !dh || (((size_t)da | (size_t)w1t | (size_t)dh) & 15) != 0) return 1;
-    const int nrg = (int)(((int64_t)P + 63) / 64);
     hipStream_t s = (hipStream_t)stream;
     const bool k64 = KW % 128 == 0;  // an even number of 64-wide chunks, else 32-wide ones
+    const int RB = (mlp_shape() & 1) ? 1 : 2;
+    const int nrg = (int)(((int64_t)P + 64 * RB - 1) / (64 * RB));
     // W = 128: two feature groups per row group, the grid padded to whole groups of 8 row groups
     const dim3 grid((unsigned)(W == 128 ? (nrg + 7) / 8 * 16 : nrg));
     auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(kDxfThreads), 0, s, P, KW, nrg, da, w1t, dh); };
-    if (W == 128) k64 ? go(mlp_dx_f32_kernel<128, 64>) : go(mlp_dx_f32_kernel<128, 32>);
-    else k64 ? go(mlp_dx_f32_kernel<64, 64>) : go(mlp_dx_f32_kernel<64, 32>);
+    if (RB == 2) {  // 32-wide k chunks: two register sets of B for two row blocks fit 4 waves/SIMD
+        if (W == 128) go(mlp_dx_f32_kernel<128, 32, 2>);
+        else go(mlp_dx_f32_kernel<64, 32, 2>);
+    } else {
+        if (W == 128) k64 ? go(mlp_dx_f32_kernel<128, 64, 1>) : go(mlp_dx_f32_kernel<128, 32, 1>);
+        else k64 ? go(mlp_dx_f32_kernel<64, 64, 1>) : go(mlp_dx_f32_kernel<64, 32, 1>);
+    }
     return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
-// the row chunks of gs4d_mlp_dw_f32: one resident round of workgroups over (chunk, m block) -- four per CU (126
-// registers: a wave per SIMD each) -- so that every workgroup runs once and all finish together; chunks a multiple of
-// 32 rows, at
-// least 256
-static void dwf_chunks(int P, int KW, int *S, int *rows) {
-    const int nmb = std::max(1, KW / 64);
+// the m-block rows of gs4d_mlp_dw_f32's workgroups
+static int dwf_mb(int KW, int W) { return (KW % 128 == 0 && W == 128 && !(mlp_shape() & 2)) ? 128 : 64; }
+// the row chunks of gs4d_mlp_dw_f32: one resident round of workgroups over (chunk, m block) -- four per CU (a
+// wave per SIMD each, <= 128 registers) -- so that every workgroup runs once and all finish together; chunks a
+// multiple of 32 rows, at least 256
+static void dwf_chunks(int P, int KW, int W, int *S, int *rows) {
+    const int nmb = std::max(1, KW / dwf_mb(KW, W));
     const int64_t target = std::max<int64_t>(1, (4 * (int64_t)cu_count()) / nmb);
     int64_t c = ((int64_t)P + target - 1) / target;
     c = std::max<int64_t>(256, (c + 31) / 32 * 32);
@@ -3163,7 +3201,7 @@ static void dwf_chunks(int P, int KW, int *S, int *rows) {
 size_t gs4d_mlp_dw_f32_scratch_bytes(int P, int KW, int W) {
     if (P <= 0 || KW <= 0 || W <= 0) return 256;
     int S = 1, rows = 0;
-    dwf_chunks(P, KW, &S, &rows);
+    dwf_chunks(P, KW, W, &S, &rows);
     return 4 * (size_t)S * KW * W + 256;
 }
 
@@ -3173,13 +3211,15 @@ int gs4d_mlp_dw_f32(int P, int KW, int W, const float *da, const float *h, float
     if (P == 0) return hipMemsetAsync(dw, 0, 4 * (size_t)KW * W, s) == hipSuccess ? 0 : 3;
     if (!da || !h || !scratch) return 1;
     int S = 1, rows = 0;
-    dwf_chunks(P, KW, &S, &rows);
+    dwf_chunks(P, KW, W, &S, &rows);
     float *parts = (float *)align_up((size_t)scratch, 256);
-    const unsigned grid = (unsigned)(8 * (KW / 64) * ((S + 7) / 8));
-    if (W == 128)
-        hipLaunchKernelGGL(mlp_dw_f32_kernel<128>, dim3(grid), dim3(kDwfThreads), 0, s, P, KW, S, rows, da, h, parts);
-    else
-        hipLaunchKernelGGL(mlp_dw_f32_kernel<64>, dim3(grid), dim3(kDwfThreads), 0, s, P, KW, S, rows, da, h, parts);
+    const int MB = dwf_mb(KW, W);
+    const unsigned grid = (unsigned)(8 * (KW / MB) * ((S + 7) / 8));
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(kDwfThreads), 0, s, P, KW, S, rows, da, h, parts);
+    };
+    if (W == 128) MB == 128 ? go(mlp_dw_f32_kernel<128, 128>) : go(mlp_dw_f32_kernel<128, 64>);
+    else go(mlp_dw_f32_kernel<64, 64>);
     if (hipGetLastError() != hipSuccess) return 3;
     return gs4d_sum_slices(parts, S, (int64_t)KW * W, dw, stream);
 }
