@@ -1,6 +1,5 @@
 #!/bin/bash
-# A/B of the fp32 heads GEMM shapes (GS4D_MLP_SHAPE: 0 kept, 1 dx register-staged one row block, 2 dw 64-row m blocks,
-# 4 register-staged dx, 32 register-staged dW)
+# A/B of the fp32 heads GEMM shapes (GS4D_MLP_SHAPE: 0 kept, 1 dx one row block per wave, 2 dw 64-row m blocks)
 set -o pipefail
 O=gpurun_out/r06_gemm_ab
 mkdir -p $O
