@@ -2555,6 +2555,42 @@ __global__ __launch_bounds__(kSumThreads) void sum_slices_kernel(const float *__
     }
 }
 
+// Many slices (S >= 16) over few outputs (the split-K weight gradients: 200 slices of 82k floats): a wave per
+// 16 float4 outputs, its four 16-lane groups summing a quarter of the slices each in slice order, then the
+// quarters as (q0 + q1) + (q2 + q3) through two lane swaps -- a fixed tree, so every run gives the same bits, and
+// four times the loads in flight of one thread per output (which left most CUs idle: 80 workgroups).
+__global__ __launch_bounds__(kSumThreads) void sum_slices_quarters_kernel(const float *__restrict__ parts, int S,
+                                                                          int64_t m, float4 *__restrict__ out) {
+    const int lane = threadIdx.x & 63, g = lane >> 4;
+    const int64_t i = (((int64_t)blockIdx.x * kSumThreads + threadIdx.x) >> 6) * 16 + (lane & 15);
+    const int s0 = g * S / 4, s1 = (g + 1) * S / 4;
+    const float4 *p = reinterpret_cast<const float4 *>(parts) + (i < m ? i : 0);
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    int s = s0;
+    for (; s + 7 < s1; s += 8) {  // eight slices' loads issued together, added in order
+        float4 v[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) v[k] = p[(size_t)(s + k) * m];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            acc.x += v[k].x; acc.y += v[k].y; acc.z += v[k].z; acc.w += v[k].w;
+        }
+    }
+    for (; s < s1; s++) {
+        const float4 a = p[(size_t)s * m];
+        acc.x += a.x; acc.y += a.y; acc.z += a.z; acc.w += a.w;
+    }
+    // (q0 + q1) + (q2 + q3): float addition commutes exactly, so both lanes of a swap hold the same bits
+#pragma unroll
+    for (int off = 16; off <= 32; off <<= 1) {
+        acc.x += __shfl_xor(acc.x, off);
+        acc.y += __shfl_xor(acc.y, off);
+        acc.z += __shfl_xor(acc.z, off);
+        acc.w += __shfl_xor(acc.w, off);
+    }
+    if (g == 0 && i < m) out[i] = acc;
+}
+
 extern "C" {
 
 // the launches: maximal runs of heads of one class (narrow: n <= 16; wide: n = 48)
@@ -2888,6 +2924,12 @@ int gs4d_sum_slices(const float *parts, int S, int64_t n, float *out, void *stre
     if (n == 0) return 0;
     const bool v4 = n % 4 == 0 && ((uintptr_t)parts % 16) == 0 && ((uintptr_t)out % 16) == 0;
     const int64_t m = v4 ? n / 4 : n;
+    if (v4 && S >= 16 && m <= ((int64_t)1 << 24)) {
+        const unsigned g4 = (unsigned)((m + 15) / 16 * 64 + kSumThreads - 1) / kSumThreads;
+        hipLaunchKernelGGL(sum_slices_quarters_kernel, dim3(g4), dim3(kSumThreads), 0, (hipStream_t)stream, parts, S,
+                           m, reinterpret_cast<float4 *>(out));
+        return hipGetLastError() == hipSuccess ? 0 : 3;
+    }
     const unsigned grid = (unsigned)std::min<int64_t>((m + kSumThreads - 1) / kSumThreads, 16384);
     if (v4)
         hipLaunchKernelGGL(sum_slices_kernel<true>, dim3(grid), dim3(kSumThreads), 0, (hipStream_t)stream, parts, S, n, out);
