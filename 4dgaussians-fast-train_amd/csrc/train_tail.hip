@@ -1231,6 +1231,13 @@ __global__ __launch_bounds__(256) void heads_bwd_reduce_kernel(HbRed R, HbOut O)
     if (i < per) {
         int w = q;
         constexpr int K = kHbRedSlices;
+        for (; w + 7 * K < nwg; w += 8 * K) {  // eight loads in flight per thread (the kernel is latency-bound)
+            float x[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) x[u] = part[(size_t)(w + u * K) * per + i];
+            v0 += x[0]; v1 += x[1]; v2 += x[2]; v3 += x[3];
+            v0 += x[4]; v1 += x[5]; v2 += x[6]; v3 += x[7];
+        }
         for (; w + 3 * K < nwg; w += 4 * K) {
             v0 += part[(size_t)w * per + i];
             v1 += part[(size_t)(w + K) * per + i];
@@ -1427,6 +1434,13 @@ __global__ __launch_bounds__(256) void feature_bwd_reduce_kernel(int nwg, int pe
     float acc = 0.f;
     if (i < per) {
         int k = sl;
+        for (; k + 112 < nwg; k += 128) {  // eight loads in flight per thread (the kernel is latency-bound)
+            float x[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) x[u] = part[(size_t)(k + 16 * u) * per + i];
+#pragma unroll
+            for (int u = 0; u < 8; u++) acc += x[u];
+        }
         for (; k + 48 < nwg; k += 64) {
             const float a0 = part[(size_t)k * per + i], a1 = part[(size_t)(k + 16) * per + i];
             const float a2 = part[(size_t)(k + 32) * per + i], a3 = part[(size_t)(k + 48) * per + i];
