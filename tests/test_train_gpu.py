@@ -635,6 +635,25 @@ def test_mlp_gemms_match_fp64(P, N, K, col0):
     assert torch.equal(_C.sum_slices(parts), (((parts[0] + parts[1]) + parts[2]) + parts[3]) + parts[4])
 
 
+def test_sum_slices_quarter_tree():
+    """gs4d_sum_slices with many slices (S >= 16, float4 rows): each quarter of the slices summed in slice order,
+    the quarters as (q0 + q1) + (q2 + q3) -- a fixed tree, checked bit for bit (float adds done the same way by
+    torch), with a ragged quarter split (S = 37) and a partial last wave (50 float4 outputs)."""
+    from gs4d_train import _C
+    torch.manual_seed(11)
+    S = 37
+    parts = torch.randn(S, 50, 4, device="cuda")
+
+    def seq(a, b):
+        acc = torch.zeros_like(parts[0])
+        for s in range(a, b):
+            acc = acc + parts[s]
+        return acc
+
+    q = [seq(g * S // 4, (g + 1) * S // 4) for g in range(4)]
+    assert torch.equal(_C.sum_slices(parts), (q[0] + q[1]) + (q[2] + q[3]))
+
+
 def test_hexplane_fused_matches_reference_module():
     """The fused HexPlane kernels (the field's input points, forward and backward in HIP) against vectors made
     by RUNNING the reference's scene/hexplane.py (tests/golden/ref_hexplane_vectors.npz; F = 4, two levels,
